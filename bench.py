@@ -1,0 +1,225 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mrays/s (primary+secondary) at 1920x1080x64spp on 1..8 MI355X.
+
+Workload (BASELINE.json configs[2]): scenes/scene5.json with its
+Mesh pointed at the deterministic dragon stand-in (327,680 triangles; the real
+meshes/dragon.stl is missing from the reference snapshot), 1920x1080,
+`-g path -n 64`, reference defaults otherwise (-b 10 -a 0.01 -l sqr -o 1 -s phong).
+A step = one full frame through the C-ABI (rtx_render_device) with the scene and
+BVH already resident in HBM; with N ranks the frame's 8x8 tiles are dealt
+round-robin (rank r renders tiles t % N == r) and every step ends with the
+RCCL all-gather of the packed tiles (16 B/px), so the image is complete on
+every rank.  Rays = cast_ray calls + is_light_blocked calls, exactly as the
+reference defines its work; counted by the kernel.
+
+Launch: python bench.py [--gpus 1] [--steps K] [--warmup W]
+        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "c-raytracer_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+METRIC = "Mrays/s (primary+secondary) at 1920×1080×64spp; 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--scene", default="scene5", choices=["scene5", "scene5_l8", "scene6", "scene3", "scene1"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-count", action="store_true", help="skip the traversal-counting pass (roofline)")
+    ap.add_argument("--cpu-target-s", type=float, default=12.0)
+    ap.add_argument("--verbose", action="store_true")
+    return ap.parse_args()
+
+
+def scene_path(which):
+    import standins
+    if which.startswith("scene5") or which == "scene6":
+        return standins.ensure_scene(which)
+    return os.path.join(ROOT, "tests", "golden", "scenes", which + ".json")
+
+
+def flags_for(which, spp):
+    if which in ("scene1",):
+        return []
+    return ["-g", "path", "-n", str(spp)]
+
+
+def cpu_baseline(scene, frame, params, target_s, log):
+    """Our CPU restatement (oracle/restate.c, 'port') on a bounded, uniformly spaced sample of the
+    SAME frame's tiles, all host threads OpenMP.  Bit-exact with the reference built -O2 (tests)."""
+    from rtxpy import abi, oracle
+    import rtxpy
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    tx, ty = (frame.width + 7) // 8, (frame.height + 7) // 8
+    total = tx * ty
+    p = rtxpy.default_params(**{f: getattr(params, f) for f, _ in abi.Params._fields_})
+    # calibrate on ~4 tiles, then size the sample for ~target_s
+    stride = max(1, total // 4)
+    p.tile_offset, p.tile_stride = 0, stride
+    t0 = time.perf_counter()
+    _, _, (c0, s0) = oracle.render(scene, frame, p, threads)
+    dt = max(time.perf_counter() - t0, 1e-3)
+    n_tiles = (total + stride - 1) // stride
+    rate_tiles = n_tiles / dt
+    want = max(4, min(total, int(rate_tiles * target_s)))
+    stride = max(1, total // want)
+    p.tile_offset, p.tile_stride = stride // 2 if stride > 1 else 0, stride
+    t0 = time.perf_counter()
+    _, _, (c, s) = oracle.render(scene, frame, p, threads)
+    dt = time.perf_counter() - t0
+    n_tiles = len(range(p.tile_offset, total, stride))
+    log(f"cpu baseline: {n_tiles} tiles, {c}+{s} rays in {dt:.2f}s on {threads} threads")
+    return {"value": round((c + s) / dt / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{n_tiles} of {total} 8x8 tiles (every {stride}th) of the same {frame.width}x{frame.height} "
+                      f"frame and flags, counter RNG; oracle/restate.c is bit-exact with the reference built -O2",
+            "seconds": round(dt, 2), "rays": c + s}
+
+
+def main():
+    a = parse()
+    import numpy as np
+    import torch
+    import rtxpy
+    from rtxpy import abi
+    from rtxpy.dist import Gatherer
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    def log(msg):
+        if a.verbose or rank == 0:
+            print(f"[rank {rank}] {msg}", file=sys.stderr, flush=True)
+
+    path = scene_path(a.scene)
+    scene = rtxpy.Scene.load(path, base_dir=os.path.join(ROOT, "tests", "golden"))
+    frame = scene.frame(a.width, a.height)
+    flags = flags_for(a.scene, a.spp)
+    params = rtxpy.params_from_args(flags, seed=1)
+    params.tile_offset, params.tile_stride = rank, world
+
+    r = rtxpy.Renderer(local)
+    t0 = time.perf_counter()
+    r.upload(scene)
+    st = r.stats()
+    log(f"scene {os.path.basename(path)}: {scene.num_objects} objects, BVH {st.bvh_nodes} nodes depth {st.bvh_depth} "
+        f"({time.perf_counter() - t0:.2f}s build+upload)")
+
+    npx = a.width * a.height
+    d_rgb = torch.zeros((npx, 3), dtype=torch.float32, device=dev)
+    d_z = torch.zeros((npx,), dtype=torch.float32, device=dev)
+    gat = Gatherer(a.width, a.height, rank, world, dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        r.render_device(frame, params, d_rgb.data_ptr(), d_z.data_ptr(), stream.cuda_stream)
+        s = r.stats()
+        out = gat.gather(d_rgb, d_z)
+        return s, out
+
+    for i in range(a.warmup):
+        s, _ = step()
+        log(f"warmup {i}: {s.kernel_ms:.1f} ms, {s.closest_rays}+{s.shadow_rays} rays")
+
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    rays = 0
+    kms = []
+    for i in range(a.steps):
+        s, _ = step()
+        rays += s.closest_rays + s.shadow_rays
+        kms.append(s.kernel_ms)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    stats_closest, stats_shadow = s.closest_rays, s.shadow_rays
+
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+        rr = torch.tensor([rays], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(rr)
+        rays = int(rr.item())
+
+    kernel_ms = float(np.mean(kms))
+    roofline = None
+    if not a.no_count:
+        p2 = rtxpy.default_params(**{f: getattr(params, f) for f, _ in abi.Params._fields_})
+        p2.count_traversal = 1
+        r.render_device(frame, p2, d_rgb.data_ptr(), d_z.data_ptr(), stream.cuda_stream)
+        c = r.stats()
+        algo = (64 * c.node_visits + 48 * c.tri_tests + 32 * c.sphere_tests + 16 * c.plane_tests
+                + 48 * (c.closest_rays + c.shadow_rays))
+        achieved = algo / (kernel_ms * 1e-3) / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            try:
+                with open(pmc) as fh:
+                    tr = json.load(fh)
+                key = f"{a.scene}_{a.width}x{a.height}_n{a.spp}_g{world}"
+                if key in tr:
+                    traffic = tr[key]["hbm_bytes_per_launch"]
+            except (OSError, ValueError, KeyError):
+                traffic = None
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "algorithmic_bytes_per_launch": int(algo), "node_visits": int(c.node_visits),
+                    "tri_tests": int(c.tri_tests), "sphere_tests": int(c.sphere_tests),
+                    "plane_tests": int(c.plane_tests), "kernel_ms": round(kernel_ms, 3),
+                    "note": "B_ray = 64*node_visits + 48*tri_tests + 32*sphere_tests + 16*plane_tests + 48 "
+                            "(SURVEY §8(d)); visits counted per ray (lane) by a counting instance of the "
+                            "same kernel; duration = HIP events around rtx_render_device's launch"}
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(scene, frame, params, a.cpu_target_s, log)
+
+    if rank == 0:
+        value = rays / elapsed / 1e6
+        out = {"metric": METRIC, "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
+               "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
+               "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+               "data": "synthetic: reference scenes/%s.json with the SURVEY §8(d) deterministic stand-in mesh" % (
+                   a.scene.split("_")[0]),
+               "config": {"workload": f"{a.scene} {a.width}x{a.height} -g path -n {a.spp} (BASELINE configs[2])",
+                          "scene": os.path.basename(path), "width": a.width, "height": a.height, "spp": a.spp,
+                          "objects": int(scene.num_objects), "rays_per_frame_rank0": stats_closest + stats_shadow,
+                          "closest_rays_rank0": stats_closest, "shadow_rays_rank0": stats_shadow,
+                          "parallelism": f"tiles{world}", "kernel_ms_rank0": round(kernel_ms, 3)},
+               "roofline": roofline, "cpu_baseline": cpu}
+        if cpu:
+            out["config"]["gpu_over_cpu"] = round(value / cpu["value"], 1)
+        print(json.dumps(out), flush=True)
+    r.close()
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,490 @@
+/*
+ * C-ABI of include/rtx.h: device context, scene flattening + BVH upload
+ * (replaces accel_init, accel.c:266-315), render (replaces render_init +
+ * render, render.c:61-116 / 345-368), statistics, known-answer entry.
+ */
+#include <hip/hip_runtime.h>
+
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "bvh_build.h"
+#include "rtx.h"
+#include "rtx_device.h"
+#include "rtx_kat.h"
+
+extern "C" hipError_t rtx_launch_render(const DScene *S, const DFrame *F, const DParams *P, float *rgb, float *z,
+					 DTask *tasks, uint32_t task_cap, unsigned long long *ctr, uint32_t waves,
+					 int count, hipStream_t stream);
+extern "C" hipError_t rtx_launch_kat(int kind, uint32_t n, const float *in, float *out, int u32mode,
+				      hipStream_t stream);
+extern "C" hipError_t rtx_render_occupancy(uint32_t stack_size, int *blocks_per_cu);
+extern "C" size_t rtx_render_lds_bytes(uint32_t stack_size);
+
+static thread_local char g_err[512] = "";
+
+static int fail(int code, const char *fmt, ...)
+{
+	va_list ap;
+	va_start(ap, fmt);
+	vsnprintf(g_err, sizeof(g_err), fmt, ap);
+	va_end(ap);
+	return code;
+}
+
+#define HIP_TRY(expr)                                                                                   \
+	do {                                                                                            \
+		hipError_t e_ = (expr);                                                                 \
+		if (e_ != hipSuccess)                                                                   \
+			return fail(RTX_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));        \
+	} while (0)
+
+struct rtx_ctx {
+	int device = 0;
+	hipStream_t stream = nullptr;
+	hipEvent_t ev0 = nullptr, ev1 = nullptr;
+	int cus = 0;
+	/* scene */
+	DNode *d_nodes = nullptr;
+	DPrim *d_prims = nullptr;
+	DPlane *d_planes = nullptr;
+	DMaterial *d_mats = nullptr;
+	DEmitter *d_emitters = nullptr;
+	DScene scene{};
+	bool have_scene = false;
+	/* work buffers */
+	DTask *d_tasks = nullptr;
+	size_t task_bytes = 0;
+	unsigned long long *d_ctr = nullptr;
+	float *d_rgb = nullptr, *d_z = nullptr;
+	size_t fb_pixels = 0;
+	rtx_stats stats{};
+};
+
+extern "C" const char *rtx_last_error(void)
+{
+	return g_err;
+}
+
+extern "C" void rtx_params_default(rtx_params *p)
+{
+	memset(p, 0, sizeof(*p));
+	p->max_bounces = 10;
+	p->min_intensity_sqr = .01f * .01f;
+	p->reflection = RTX_PHONG;
+	p->gi = RTX_GI_AMBIENT;
+	p->samples = 1;
+	p->attenuation = RTX_ATT_SQR;
+	p->attenuation_offset = 1.f;
+	p->rng = RTX_RNG_COUNTER;
+	p->seed = 1;
+	p->u32conv = RTX_U32_SAT;
+	p->tile_offset = 0;
+	p->tile_stride = 1;
+	p->count_traversal = 0;
+}
+
+extern "C" int rtx_device_count(int *count)
+{
+	if (!count)
+		return fail(RTX_ERR_ARG, "null count");
+	int n = 0;
+	hipError_t e = hipGetDeviceCount(&n);
+	*count = (e == hipSuccess) ? n : 0;
+	return RTX_OK;
+}
+
+template <class T> static void dfree(T *&p)
+{
+	if (p)
+		(void)hipFree(p);
+	p = nullptr;
+}
+
+static void free_scene(rtx_ctx *c)
+{
+	dfree(c->d_nodes);
+	dfree(c->d_prims);
+	dfree(c->d_planes);
+	dfree(c->d_mats);
+	dfree(c->d_emitters);
+	c->have_scene = false;
+}
+
+extern "C" void rtx_close(rtx_ctx *c)
+{
+	if (!c)
+		return;
+	(void)hipSetDevice(c->device);
+	if (c->stream)
+		(void)hipStreamSynchronize(c->stream);
+	free_scene(c);
+	dfree(c->d_tasks);
+	dfree(c->d_ctr);
+	dfree(c->d_rgb);
+	dfree(c->d_z);
+	if (c->ev0)
+		(void)hipEventDestroy(c->ev0);
+	if (c->ev1)
+		(void)hipEventDestroy(c->ev1);
+	if (c->stream)
+		(void)hipStreamDestroy(c->stream);
+	delete c;
+}
+
+extern "C" int rtx_open(int device, rtx_ctx **out)
+{
+	if (!out)
+		return fail(RTX_ERR_ARG, "null out");
+	*out = nullptr;
+	int n = 0;
+	if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+		return fail(RTX_ERR_NODEV, "no HIP device available");
+	if (device < 0 || device >= n)
+		return fail(RTX_ERR_NODEV, "device %d out of range (%d devices)", device, n);
+	hipDeviceProp_t prop;
+	HIP_TRY(hipGetDeviceProperties(&prop, device));
+	if (!strstr(prop.gcnArchName, "gfx950"))
+		return fail(RTX_ERR_NODEV, "device %d is %s, this build targets gfx950 only", device, prop.gcnArchName);
+	rtx_ctx *c = new rtx_ctx();
+	c->device = device;
+	c->cus = prop.multiProcessorCount;
+	hipError_t e;
+	if ((e = hipSetDevice(device)) != hipSuccess || (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
+	    (e = hipEventCreate(&c->ev0)) != hipSuccess || (e = hipEventCreate(&c->ev1)) != hipSuccess ||
+	    (e = hipMalloc(&c->d_ctr, sizeof(unsigned long long) * RTX_C_N)) != hipSuccess) {
+		rtx_close(c);
+		return fail(RTX_ERR_HIP, "context setup failed: %s", hipGetErrorString(e));
+	}
+	*out = c;
+	return RTX_OK;
+}
+
+template <class T> static int upload(T *&dst, const std::vector<T> &v)
+{
+	dfree(dst);
+	size_t n = std::max<size_t>(v.size(), 1);
+	HIP_TRY(hipMalloc(&dst, n * sizeof(T)));
+	if (!v.empty())
+		HIP_TRY(hipMemcpy(dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+	return RTX_OK;
+}
+
+static inline float pad_lo(float x, float ext) { return x - (std::fabs(x) + ext) * 2e-6f - 1e-30f; }
+static inline float pad_hi(float x, float ext) { return x + (std::fabs(x) + ext) * 2e-6f + 1e-30f; }
+
+extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
+{
+	if (!c || !sc)
+		return fail(RTX_ERR_ARG, "null argument");
+	if (!sc->num_materials || !sc->materials)
+		return fail(RTX_ERR_SCENE, "scene has no materials");
+	if (sc->num_objects && !sc->objects)
+		return fail(RTX_ERR_ARG, "objects pointer is null");
+	if (sc->num_emitters && !sc->emitters)
+		return fail(RTX_ERR_ARG, "emitters pointer is null");
+	HIP_TRY(hipSetDevice(c->device));
+	free_scene(c);
+
+	std::vector<DMaterial> mats(sc->num_materials);
+	for (uint32_t i = 0; i < sc->num_materials; i++) {
+		const rtx_material &m = sc->materials[i];
+		DMaterial &d = mats[i];
+		memset(&d, 0, sizeof(d));
+		memcpy(d.ks, m.ks, 12);
+		memcpy(d.ka, m.ka, 12);
+		memcpy(d.kr, m.kr, 12);
+		memcpy(d.kt, m.kt, 12);
+		memcpy(d.ke, m.ke, 12);
+		d.shininess = m.shininess;
+		d.ior = m.refractive_index;
+		d.tex = m.texture;
+		d.periodic = m.periodic;
+		memcpy(d.color, m.color, sizeof(d.color));
+		d.scale = m.scale;
+		d.mortar = m.mortar_width;
+		d.nfs = m.noise_feature_scale;
+		d.ns = m.noise_scale;
+		d.fs = m.frequency_scale;
+		d.flags = (m.emittant ? RTX_MF_EMITTANT : 0) | (m.reflective ? RTX_MF_REFLECTIVE : 0) |
+			  (m.transparent ? RTX_MF_TRANSPARENT : 0);
+	}
+
+	std::vector<uint32_t> bounded;
+	std::vector<DPlane> planes;
+	std::vector<uint32_t> plane_of(sc->num_objects, RTX_NONE);
+	for (uint32_t i = 0; i < sc->num_objects; i++) {
+		const rtx_object &o = sc->objects[i];
+		if (o.material < 0 || (uint32_t)o.material >= sc->num_materials)
+			return fail(RTX_ERR_SCENE, "object %u: material index %d out of range", i, o.material);
+		if (o.type == RTX_PLANE) {
+			DPlane p;
+			memset(&p, 0, sizeof(p));
+			memcpy(p.n, o.n, 12);
+			p.d = o.d;
+			p.eps = o.epsilon;
+			p.obj = i;
+			p.mat = (uint32_t)o.material;
+			plane_of[i] = (uint32_t)planes.size();
+			planes.push_back(p);
+		} else if (o.type == RTX_SPHERE || o.type == RTX_TRIANGLE) {
+			bounded.push_back(i);
+		} else {
+			return fail(RTX_ERR_SCENE, "object %u: unknown type %d", i, o.type);
+		}
+	}
+
+	/* leaf boxes (sphere_get_corners / triangle_get_corners), padded so the traversal's
+	 * FMA slab test is conservative */
+	const uint32_t nb = (uint32_t)bounded.size();
+	std::vector<float> lo(3 * (size_t)nb), hi(3 * (size_t)nb);
+	for (uint32_t k = 0; k < nb; k++) {
+		const rtx_object &o = sc->objects[bounded[k]];
+		float l[3], h[3];
+		if (o.type == RTX_SPHERE) {
+			for (int a = 0; a < 3; a++) {
+				l[a] = o.p0[a] - o.radius;
+				h[a] = o.p0[a] + o.radius;
+			}
+		} else {
+			for (int a = 0; a < 3; a++) {
+				l[a] = std::min(o.p0[a], std::min(o.p1[a], o.p2[a]));
+				h[a] = std::max(o.p0[a], std::max(o.p1[a], o.p2[a]));
+			}
+		}
+		float ext = std::max(h[0] - l[0], std::max(h[1] - l[1], h[2] - l[2]));
+		for (int a = 0; a < 3; a++) {
+			lo[3 * (size_t)k + a] = pad_lo(l[a], ext);
+			hi[3 * (size_t)k + a] = pad_hi(h[a], ext);
+		}
+	}
+	BvhOutput bvh;
+	BvhConfig cfg;
+	bvh_build(BvhInput{ nb, lo.data(), hi.data() }, cfg, bvh);
+
+	std::vector<DPrim> prims(nb);
+	std::vector<uint32_t> prim_of(sc->num_objects, RTX_NONE);
+	for (uint32_t k = 0; k < nb; k++) {
+		const uint32_t oi = bounded[bvh.order[k]];
+		const rtx_object &o = sc->objects[oi];
+		DPrim &p = prims[k];
+		memset(&p, 0, sizeof(p));
+		uint32_t meta = ((uint32_t)o.type << 24) | (uint32_t)o.material;
+		memcpy(p.a, o.p0, 12);
+		p.a[3] = o.epsilon;
+		if (o.type == RTX_SPHERE) {
+			p.b[0] = o.radius;
+		} else {
+			memcpy(p.b, o.e1, 12);
+			memcpy(p.c, o.e2, 12);
+			memcpy(p.d, o.n, 12);
+		}
+		memcpy(&p.b[3], &oi, 4);
+		memcpy(&p.c[3], &meta, 4);
+		prim_of[oi] = k;
+	}
+
+	std::vector<DEmitter> emit(sc->num_emitters);
+	for (uint32_t i = 0; i < sc->num_emitters; i++) {
+		uint32_t oi = sc->emitters[i];
+		if (oi >= sc->num_objects)
+			return fail(RTX_ERR_SCENE, "emitter %u: object %u out of range", i, oi);
+		const rtx_object &o = sc->objects[oi];
+		if (o.type == RTX_PLANE)
+			return fail(RTX_ERR_SCENE, "Plane cannot be emittant");
+		DEmitter &e = emit[i];
+		memset(&e, 0, sizeof(e));
+		e.obj = oi;
+		e.type = (uint32_t)o.type;
+		e.num_lights = o.num_lights;
+		const rtx_material &m = sc->materials[o.material];
+		float inv = 1.f / (float)o.num_lights; /* render.c:175 */
+		for (int a = 0; a < 3; a++)
+			e.li[a] = m.ke[a] * inv;
+		memcpy(e.p0, o.p0, 12);
+		memcpy(e.p1, o.p1, 12);
+		memcpy(e.p2, o.p2, 12);
+		e.radius = o.radius;
+	}
+
+	int rc;
+	if ((rc = upload(c->d_nodes, bvh.nodes)) || (rc = upload(c->d_prims, prims)) ||
+	    (rc = upload(c->d_planes, planes)) || (rc = upload(c->d_mats, mats)) || (rc = upload(c->d_emitters, emit)))
+		return rc;
+
+	DScene &S = c->scene;
+	memset(&S, 0, sizeof(S));
+	S.nodes = c->d_nodes;
+	S.prims = c->d_prims;
+	S.planes = c->d_planes;
+	S.mats = c->d_mats;
+	S.emitters = c->d_emitters;
+	S.root_ref = nb ? bvh.root_ref : RTX_EMPTY_REF;
+	S.num_prims = nb;
+	S.num_planes = (uint32_t)planes.size();
+	S.num_emitters = sc->num_emitters;
+	S.stack_size = std::max<uint32_t>(bvh.depth + 1, 4);
+	memcpy(S.ambient, sc->ambient, 12);
+	c->have_scene = true;
+	c->stats.bvh_nodes = (uint32_t)bvh.nodes.size();
+	c->stats.bvh_depth = bvh.depth;
+	c->stats.bvh_prims = nb;
+	return RTX_OK;
+}
+
+static int render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, float *d_rgb, float *d_z,
+			 hipStream_t stream)
+{
+	if (!c->have_scene)
+		return fail(RTX_ERR_STATE, "rtx_render before rtx_upload_scene");
+	if (!fr || !p)
+		return fail(RTX_ERR_ARG, "null frame/params");
+	if (!fr->width || !fr->height)
+		return fail(RTX_ERR_ARG, "empty frame %ux%u", fr->width, fr->height);
+	if (!p->tile_stride || p->tile_offset >= p->tile_stride)
+		return fail(RTX_ERR_ARG, "bad tile sharding %u/%u", p->tile_offset, p->tile_stride);
+	DFrame F;
+	F.width = fr->width;
+	F.height = fr->height;
+	memcpy(F.corner, fr->corner, 12);
+	memcpy(F.step_x, fr->step_x, 12);
+	memcpy(F.step_y, fr->step_y, 12);
+	memcpy(F.origin, fr->origin, 12);
+	DParams P;
+	memset(&P, 0, sizeof(P));
+	P.max_bounces = p->max_bounces;
+	P.min_intensity_sqr = p->min_intensity_sqr;
+	P.reflection = p->reflection;
+	P.gi = p->gi;
+	P.samples = p->samples;
+	P.attenuation = p->attenuation;
+	P.att_offset = p->attenuation_offset;
+	P.rng = p->rng;
+	P.seed = p->seed;
+	P.u32conv = p->u32conv;
+	P.tile_offset = p->tile_offset;
+	P.tile_stride = p->tile_stride;
+	P.tiles_x = (fr->width + RTX_TILE_W - 1) / RTX_TILE_W;
+	const uint64_t tiles_y = (fr->height + RTX_TILE_H - 1) / RTX_TILE_H;
+	const uint64_t total = (uint64_t)P.tiles_x * tiles_y;
+	P.ntiles = p->tile_offset < total ? (uint32_t)((total - p->tile_offset + p->tile_stride - 1) / p->tile_stride) : 0;
+
+	int per_cu = 0;
+	HIP_TRY(rtx_render_occupancy(c->scene.stack_size, &per_cu));
+	if (per_cu <= 0)
+		return fail(RTX_ERR_HIP, "render kernel does not fit (LDS %zu B)", rtx_render_lds_bytes(c->scene.stack_size));
+	uint32_t waves = (uint32_t)std::min<uint64_t>((uint64_t)per_cu * c->cus, std::max<uint32_t>(P.ntiles, 1));
+	/* LIFO task stack: each batch pops <= 64 and pushes <= 128, depth <= max_bounces */
+	uint32_t task_cap = 64u * (std::min<uint32_t>(P.max_bounces, 4096u) + 3u);
+	size_t need = (size_t)waves * task_cap * sizeof(DTask);
+	if (need > c->task_bytes) {
+		dfree(c->d_tasks);
+		HIP_TRY(hipMalloc(&c->d_tasks, need));
+		c->task_bytes = need;
+	}
+	HIP_TRY(hipMemsetAsync(c->d_ctr, 0, sizeof(unsigned long long) * RTX_C_N, stream));
+	HIP_TRY(hipEventRecord(c->ev0, stream));
+	if (P.ntiles)
+		HIP_TRY(rtx_launch_render(&c->scene, &F, &P, d_rgb, d_z, c->d_tasks, task_cap, c->d_ctr, waves,
+					  p->count_traversal, stream));
+	HIP_TRY(hipEventRecord(c->ev1, stream));
+	unsigned long long ctr[RTX_C_N];
+	HIP_TRY(hipMemcpyAsync(ctr, c->d_ctr, sizeof(ctr), hipMemcpyDeviceToHost, stream));
+	HIP_TRY(hipStreamSynchronize(stream));
+	float ms = 0.f;
+	HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+	c->stats.closest_rays = ctr[RTX_C_CLOSEST];
+	c->stats.shadow_rays = ctr[RTX_C_SHADOW];
+	c->stats.node_visits = ctr[RTX_C_NODES];
+	c->stats.tri_tests = ctr[RTX_C_TRIS];
+	c->stats.sphere_tests = ctr[RTX_C_SPHERES];
+	c->stats.plane_tests = ctr[RTX_C_PLANES];
+	c->stats.kernel_ms = ms;
+	c->stats.waves = waves;
+	if (ctr[RTX_C_OVERFLOW])
+		return fail(RTX_ERR_STATE, "secondary-ray task stack overflow in %llu waves", ctr[RTX_C_OVERFLOW]);
+	return RTX_OK;
+}
+
+extern "C" int rtx_render_device(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, void *d_rgb, void *d_z,
+				 void *stream)
+{
+	if (!c)
+		return fail(RTX_ERR_ARG, "null context");
+	HIP_TRY(hipSetDevice(c->device));
+	return render_common(c, fr, p, (float *)d_rgb, (float *)d_z, stream ? (hipStream_t)stream : c->stream);
+}
+
+extern "C" int rtx_render(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, float *rgb, float *z)
+{
+	if (!c || !fr || !p)
+		return fail(RTX_ERR_ARG, "null argument");
+	HIP_TRY(hipSetDevice(c->device));
+	const size_t px = (size_t)fr->width * fr->height;
+	if (px > c->fb_pixels) {
+		dfree(c->d_rgb);
+		dfree(c->d_z);
+		HIP_TRY(hipMalloc(&c->d_rgb, px * 3 * sizeof(float)));
+		HIP_TRY(hipMalloc(&c->d_z, px * sizeof(float)));
+		c->fb_pixels = px;
+	}
+	/* pixels of tiles outside this shard keep the caller's values */
+	if (p->tile_stride > 1) {
+		if (rgb)
+			HIP_TRY(hipMemcpyAsync(c->d_rgb, rgb, px * 12, hipMemcpyHostToDevice, c->stream));
+		if (z)
+			HIP_TRY(hipMemcpyAsync(c->d_z, z, px * 4, hipMemcpyHostToDevice, c->stream));
+	}
+	int rc = render_common(c, fr, p, rgb ? c->d_rgb : nullptr, z ? c->d_z : nullptr, c->stream);
+	if (rc)
+		return rc;
+	if (rgb)
+		HIP_TRY(hipMemcpy(rgb, c->d_rgb, px * 12, hipMemcpyDeviceToHost));
+	if (z)
+		HIP_TRY(hipMemcpy(z, c->d_z, px * 4, hipMemcpyDeviceToHost));
+	return RTX_OK;
+}
+
+extern "C" int rtx_get_stats(const rtx_ctx *c, rtx_stats *out)
+{
+	if (!c || !out)
+		return fail(RTX_ERR_ARG, "null argument");
+	*out = c->stats;
+	return RTX_OK;
+}
+
+extern "C" int rtx_kat(int kind, uint32_t n, const float *in, float *out, const rtx_params *params)
+{
+	if (kind < 0 || kind >= RTX_KAT_NKINDS)
+		return fail(RTX_ERR_ARG, "bad KAT kind %d", kind);
+	if (!n)
+		return RTX_OK;
+	if (!in || !out)
+		return fail(RTX_ERR_ARG, "null buffers");
+	int ndev = 0;
+	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+		return fail(RTX_ERR_NODEV, "no HIP device available");
+	const size_t bi = (size_t)n * rtx_kat_in_width[kind] * 4, bo = (size_t)n * rtx_kat_out_width[kind] * 4;
+	float *din = nullptr, *dout = nullptr;
+	HIP_TRY(hipMalloc(&din, bi));
+	if (hipMalloc(&dout, bo) != hipSuccess) {
+		(void)hipFree(din);
+		return fail(RTX_ERR_NOMEM, "KAT output allocation failed");
+	}
+	int rc = RTX_OK;
+	hipError_t e = hipMemcpy(din, in, bi, hipMemcpyHostToDevice);
+	if (e == hipSuccess)
+		e = rtx_launch_kat(kind, n, din, dout, params ? params->u32conv : RTX_U32_SAT, nullptr);
+	if (e == hipSuccess)
+		e = hipMemcpy(out, dout, bo, hipMemcpyDeviceToHost);
+	if (e != hipSuccess)
+		rc = fail(RTX_ERR_HIP, "KAT failed: %s", hipGetErrorString(e));
+	(void)hipFree(din);
+	(void)hipFree(dout);
+	return rc;
+}

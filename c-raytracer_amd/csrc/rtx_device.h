@@ -1,0 +1,140 @@
+/*
+ * Device-side scene layout in HBM (shared by the host uploader and the kernels).
+ *
+ *  DNode  64 B  BVH2 inner node: both children's AABBs + child refs.  A ref is
+ *               an inner-node index (>= 0) or a leaf: RTX_LEAF_BIT | first << 4 |
+ *               (count-1), count <= 16 primitives contiguous in `prims`.
+ *               Replaces the pointer-linked struct BVH + malloc'd BoundingCuboid
+ *               of accel.c:25-40.  Nodes are stored depth-first (left child
+ *               adjacent) so a traversal walks forward through memory.
+ *  DPrim  64 B  one bounded object (sphere / triangle) in BVH leaf order:
+ *               a = (v0 | centre, epsilon), b = (e1 | (r,0,0), object id bits),
+ *               c = (e2, meta bits = material | type << 24), d = (normal, 0).
+ *               Shadow tests read a..c (48 B); d only for the final closest hit.
+ *  DPlane 32 B  unbound objects (object.c:168-197), linear scan, never in the BVH.
+ *  DMaterial    material + texture parameters (material.c:27-53).
+ *  DEmitter     emittant_objects[] entry with ke/num_lights premultiplied
+ *               (render.c:175).
+ * Hit ids: prim index, or RTX_PLANE_BIT | plane index; RTX_NONE = no object.
+ */
+#ifndef RTX_DEVICE_H
+#define RTX_DEVICE_H
+
+#include <stdint.h>
+
+#define RTX_LEAF_BIT 0x80000000u
+#define RTX_PLANE_BIT 0x80000000u
+#define RTX_NONE 0xFFFFFFFFu
+#define RTX_EMPTY_REF 0xFFFFFFFFu /* BVH with no bounded objects */
+#define RTX_MAX_LEAF 16
+
+#define RTX_MF_EMITTANT 1
+#define RTX_MF_REFLECTIVE 2
+#define RTX_MF_TRANSPARENT 4
+
+#define RTX_TILE_W 8
+#define RTX_TILE_H 8
+
+typedef struct DNode {
+	float lo0x, hi0x, lo0y, hi0y;
+	float lo0z, hi0z, lo1x, hi1x;
+	float lo1y, hi1y, lo1z, hi1z;
+	uint32_t ref0, ref1, axis, pad;
+} DNode;
+
+typedef struct DPrim {
+	float a[4];
+	float b[4];
+	float c[4];
+	float d[4];
+} DPrim;
+
+typedef struct DPlane {
+	float n[3];
+	float d;
+	float eps;
+	uint32_t obj;
+	uint32_t mat;
+	uint32_t pad;
+} DPlane;
+
+typedef struct DMaterial {
+	float ks[3], ka[3], kr[3], kt[3], ke[3];
+	float shininess, ior;
+	int32_t tex, periodic;
+	float color[2][3];
+	float scale, mortar, nfs, ns, fs;
+	uint32_t flags;
+	float pad[2];
+} DMaterial;
+
+typedef struct DEmitter {
+	uint32_t obj;      /* reference object index (emittant_objects[i]) */
+	uint32_t type;     /* RTX_SPHERE / RTX_TRIANGLE */
+	uint32_t num_lights;
+	float li[3];       /* ke * (1 / num_lights) */
+	float p0[3], p1[3], p2[3];
+	float radius;
+} DEmitter;
+
+#define RTX_MAX_EMITTERS 64
+
+typedef struct DScene {
+	const DNode *nodes;
+	const DPrim *prims;
+	const DPlane *planes;
+	const DMaterial *mats;
+	const DEmitter *emitters;
+	uint32_t root_ref;
+	uint32_t num_prims;
+	uint32_t num_planes;
+	uint32_t num_emitters;
+	uint32_t stack_size;   /* per-lane closest-hit stack entries (>= BVH depth) */
+	float ambient[3];
+} DScene;
+
+typedef struct DFrame {
+	uint32_t width, height;
+	float corner[3], step_x[3], step_y[3], origin[3];
+} DFrame;
+
+typedef struct DParams {
+	uint32_t max_bounces;
+	float min_intensity_sqr;
+	int32_t reflection, gi;
+	uint32_t samples;
+	int32_t attenuation;
+	float att_offset;
+	int32_t rng;
+	uint64_t seed;
+	int32_t u32conv;
+	uint32_t tile_offset, tile_stride;
+	uint32_t ntiles;       /* tiles this launch renders */
+	uint32_t tiles_x;
+} DParams;
+
+/* secondary (reflection / refraction) ray waiting in a wave's task stack */
+typedef struct DTask {
+	float o[3];
+	float d[3];
+	float kr[3];
+	uint32_t rb;
+	uint32_t inside;
+	uint32_t key_lo, key_hi;
+	uint32_t slot;
+} DTask;
+
+/* global counters written by the render kernel */
+enum {
+	RTX_C_TILE = 0,   /* work queue head */
+	RTX_C_CLOSEST,
+	RTX_C_SHADOW,
+	RTX_C_NODES,
+	RTX_C_TRIS,
+	RTX_C_SPHERES,
+	RTX_C_PLANES,
+	RTX_C_OVERFLOW,
+	RTX_C_N
+};
+
+#endif

@@ -1,0 +1,227 @@
+"""rtxpy — Python (ctypes) driver for the rtx C-ABI (include/rtx.h, include/rtx_scene.h).
+
+Host plumbing for tests and bench.py.  The product is the C-ABI library
+``c-raytracer_amd/lib/librtx.so`` (HIP kernels for gfx950) and the C host glue
+``librtxscene.so``; this module only loads them.  There is no CPU fallback:
+``Renderer`` raises if librtx.so is missing or no gfx950 device is usable.
+
+The CPU oracle (``oracle/librtx_oracle.so``) is test infrastructure and is
+reached only through ``rtxpy.oracle`` by tests/, ``__graft_entry__.smoke()``
+and bench.py's cpu_baseline leg.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+from .abi import (Frame, Params, SceneDesc, Stats, RTX_OK)  # noqa: F401
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO_ROOT = os.path.dirname(PKG_DIR)
+LIB_DIR = os.path.join(PKG_DIR, "lib")
+LIBRTX = os.path.join(LIB_DIR, "librtx.so")
+LIBSCENE = os.path.join(LIB_DIR, "librtxscene.so")
+ENGINE = os.path.join(LIB_DIR, "engine")
+
+_scene_lib = None
+_rtx_lib = None
+
+
+class RtxError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"rtx error {code}: {msg}")
+        self.code = code
+
+
+def scene_lib():
+    global _scene_lib
+    if _scene_lib is None:
+        if not os.path.exists(LIBSCENE):
+            raise RtxError(abi.RTX_ERR_STATE, f"{LIBSCENE} not built (run __graft_entry__.build())")
+        lib = C.CDLL(LIBSCENE)
+        abi.declare_scene(lib)
+        _scene_lib = lib
+    return _scene_lib
+
+
+def rtx_lib():
+    """Load librtx.so (the HIP path).  Raises when it is missing: no fallback."""
+    global _rtx_lib
+    if _rtx_lib is None:
+        if not os.path.exists(LIBRTX):
+            raise RtxError(abi.RTX_ERR_STATE, f"{LIBRTX} not built (run __graft_entry__.build())")
+        lib = C.CDLL(LIBRTX)
+        abi.declare_rtx(lib)
+        _rtx_lib = lib
+    return _rtx_lib
+
+
+def _check_scene(rc):
+    if rc != RTX_OK:
+        raise RtxError(rc, scene_lib().rtx_scene_last_error().decode(errors="replace"))
+
+
+def _check(rc):
+    if rc != RTX_OK:
+        raise RtxError(rc, rtx_lib().rtx_last_error().decode(errors="replace"))
+
+
+class Scene:
+    """A loaded scene (owner of the C rtx_scene)."""
+
+    def __init__(self, handle):
+        self._h = handle
+        self.desc = scene_lib().rtx_scene_desc_of(handle).contents
+
+    @classmethod
+    def load(cls, path, scale=None, base_dir=None):
+        h = C.c_void_p()
+        _check_scene(scene_lib().rtx_scene_load(os.fsencode(path), scale.encode() if scale else None,
+                                                os.fsencode(base_dir) if base_dir else None, C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def parse(cls, text, name="<memory>", scale=None, base_dir=None):
+        data = text.encode() if isinstance(text, str) else text
+        h = C.c_void_p()
+        _check_scene(scene_lib().rtx_scene_parse(data, len(data), name.encode(), scale.encode() if scale else None,
+                                                 os.fsencode(base_dir) if base_dir else None, C.byref(h)))
+        return cls(h)
+
+    def frame(self, width, height):
+        fr = Frame()
+        _check_scene(scene_lib().rtx_frame_setup(C.byref(self.desc.camera), width, height, C.byref(fr)))
+        return fr
+
+    @property
+    def num_objects(self):
+        return self.desc.num_objects
+
+    def objects(self):
+        return [self.desc.objects[i] for i in range(self.desc.num_objects)]
+
+    def materials(self):
+        return [self.desc.materials[i] for i in range(self.desc.num_materials)]
+
+    def emitters(self):
+        return [self.desc.emitters[i] for i in range(self.desc.num_emitters)]
+
+    def close(self):
+        if self._h:
+            scene_lib().rtx_scene_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def default_params(**kw):
+    """rtx_params_default (render.c:53-60 defaults) plus overrides."""
+    p = Params()
+    p.max_bounces = 10
+    p.min_intensity_sqr = 0.01 * 0.01
+    p.reflection = abi.RTX_PHONG
+    p.gi = abi.RTX_GI_AMBIENT
+    p.samples = 1
+    p.attenuation = abi.RTX_ATT_SQR
+    p.attenuation_offset = 1.0
+    p.rng = abi.RTX_RNG_COUNTER
+    p.seed = 1
+    p.u32conv = abi.RTX_U32_SAT
+    p.tile_offset = 0
+    p.tile_stride = 1
+    p.count_traversal = 0
+    # float32 rounding of .01f*.01f like the C default
+    p.min_intensity_sqr = float(np.float32(np.float32(0.01) * np.float32(0.01)))
+    for k, v in kw.items():
+        if not hasattr(p, k):
+            raise AttributeError(k)
+        setattr(p, k, v)
+    return p
+
+
+def params_from_args(args, **kw):
+    """render_init (render.c:61-116) over a reference-style argument list."""
+    p = default_params(**kw)
+    argv = [b"engine"] + [a.encode() for a in args]
+    arr = (C.c_char_p * len(argv))(*argv)
+    scene_lib().rtx_params_from_argv(len(argv), arr, C.byref(p))
+    return p
+
+
+def hash_djb(s):
+    return scene_lib().rtx_hash_djb(s.encode())
+
+
+def write_tiff(path, rgb, z=None, raw=False):
+    rgb = np.ascontiguousarray(rgb, dtype=np.float32)
+    h, w = rgb.shape[:2]
+    zz = None
+    if raw:
+        zz = np.ascontiguousarray(z, dtype=np.float32)
+    rc = scene_lib().rtx_tiff_write(os.fsencode(path), w, h, rgb.ctypes.data,
+                                    zz.ctypes.data if zz is not None else None, 1 if raw else 0)
+    if rc != RTX_OK:
+        raise RtxError(rc, f"tiff write failed: {path}")
+
+
+def write_stl(path, tris):
+    tris = np.ascontiguousarray(tris, dtype=np.float32).reshape(-1, 9)
+    _check_scene(scene_lib().rtx_stl_write(os.fsencode(path), tris.shape[0], tris.ctypes.data))
+
+
+class Renderer:
+    """One rtx context on one HIP device (rtx_open .. rtx_close)."""
+
+    def __init__(self, device=0):
+        self.lib = rtx_lib()
+        self._ctx = C.c_void_p()
+        _check(self.lib.rtx_open(device, C.byref(self._ctx)))
+        self.device = device
+
+    def upload(self, scene):
+        _check(self.lib.rtx_upload_scene(self._ctx, C.byref(scene.desc)))
+
+    def render(self, frame, params, rgb=None, z=None):
+        w, h = frame.width, frame.height
+        if rgb is None:
+            rgb = np.zeros((h, w, 3), np.float32)
+        if z is None:
+            z = np.zeros((h, w), np.float32)
+        assert rgb.dtype == np.float32 and rgb.flags.c_contiguous and rgb.size == w * h * 3
+        assert z.dtype == np.float32 and z.flags.c_contiguous and z.size == w * h
+        _check(self.lib.rtx_render(self._ctx, C.byref(frame), C.byref(params), rgb.ctypes.data, z.ctypes.data))
+        return rgb, z
+
+    def render_device(self, frame, params, d_rgb, d_z, stream=None):
+        """d_rgb / d_z: device pointers (ints), stream: hipStream_t as int or None."""
+        _check(self.lib.rtx_render_device(self._ctx, C.byref(frame), C.byref(params), C.c_void_p(d_rgb),
+                                          C.c_void_p(d_z), C.c_void_p(stream) if stream else None))
+
+    def stats(self):
+        s = Stats()
+        _check(self.lib.rtx_get_stats(self._ctx, C.byref(s)))
+        return s
+
+    def close(self):
+        if self._ctx:
+            self.lib.rtx_close(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def gpu_kat(kind, records, params=None):
+    records = np.ascontiguousarray(records, dtype=np.float32).reshape(-1, abi.KAT_IN[kind])
+    out = np.zeros((records.shape[0], abi.KAT_OUT[kind]), np.float32)
+    p = params or default_params()
+    _check(rtx_lib().rtx_kat(kind, records.shape[0], records.ctypes.data, out.ctypes.data, C.byref(p)))
+    return out

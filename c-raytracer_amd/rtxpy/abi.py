@@ -1,0 +1,139 @@
+"""ctypes mirror of include/rtx.h, include/rtx_scene.h and include/rtx_kat.h.
+
+Test / bench plumbing only: the product boundary is the C-ABI in include/.
+"""
+import ctypes as C
+
+RTX_OK = 0
+RTX_ERR_ARG, RTX_ERR_HIP, RTX_ERR_NOMEM, RTX_ERR_SCENE, RTX_ERR_NODEV, RTX_ERR_STATE, RTX_ERR_IO = (
+    -1, -2, -3, -4, -5, -6, -7)
+
+RTX_SPHERE, RTX_TRIANGLE, RTX_PLANE = 0, 1, 2
+RTX_TEX_UNIFORM, RTX_TEX_CHECKERBOARD, RTX_TEX_BRICK, RTX_TEX_NOISY_PERIODIC = 0, 1, 2, 3
+RTX_PHONG, RTX_BLINN = 0, 1
+RTX_GI_AMBIENT, RTX_GI_PATH = 0, 1
+RTX_ATT_NONE, RTX_ATT_LIN, RTX_ATT_SQR = 0, 1, 2
+RTX_RNG_COUNTER, RTX_RNG_CONST = 0, 1
+RTX_U32_SAT, RTX_U32_WRAP = 0, 1
+
+F3 = C.c_float * 3
+
+
+class Material(C.Structure):
+    _fields_ = [("id", C.c_int32), ("ks", F3), ("ka", F3), ("kr", F3), ("kt", F3), ("ke", F3),
+                ("shininess", C.c_float), ("refractive_index", C.c_float), ("texture", C.c_int32),
+                ("periodic", C.c_int32), ("color", F3 * 2), ("scale", C.c_float), ("mortar_width", C.c_float),
+                ("noise_feature_scale", C.c_float), ("noise_scale", C.c_float), ("frequency_scale", C.c_float),
+                ("emittant", C.c_int32), ("reflective", C.c_int32), ("transparent", C.c_int32)]
+
+
+class Object(C.Structure):
+    _fields_ = [("type", C.c_int32), ("material", C.c_int32), ("num_lights", C.c_uint32), ("epsilon", C.c_float),
+                ("p0", F3), ("p1", F3), ("p2", F3), ("e1", F3), ("e2", F3), ("n", F3), ("radius", C.c_float),
+                ("d", C.c_float)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("position", F3), ("vectors", F3 * 3), ("fov", C.c_float), ("focal_length", C.c_float)]
+
+
+class SceneDesc(C.Structure):
+    _fields_ = [("num_materials", C.c_uint32), ("materials", C.POINTER(Material)), ("num_objects", C.c_uint32),
+                ("objects", C.POINTER(Object)), ("num_emitters", C.c_uint32), ("emitters", C.POINTER(C.c_uint32)),
+                ("ambient", F3), ("camera", Camera)]
+
+
+class Frame(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("corner", F3), ("step_x", F3), ("step_y", F3),
+                ("origin", F3)]
+
+
+class Params(C.Structure):
+    _fields_ = [("max_bounces", C.c_uint32), ("min_intensity_sqr", C.c_float), ("reflection", C.c_int32),
+                ("gi", C.c_int32), ("samples", C.c_uint32), ("attenuation", C.c_int32),
+                ("attenuation_offset", C.c_float), ("rng", C.c_int32), ("seed", C.c_uint64),
+                ("u32conv", C.c_int32), ("tile_offset", C.c_uint32), ("tile_stride", C.c_uint32),
+                ("count_traversal", C.c_int32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("closest_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("node_visits", C.c_uint64),
+                ("tri_tests", C.c_uint64), ("sphere_tests", C.c_uint64), ("plane_tests", C.c_uint64),
+                ("kernel_ms", C.c_double), ("bvh_nodes", C.c_uint32), ("bvh_depth", C.c_uint32),
+                ("bvh_prims", C.c_uint32), ("waves", C.c_uint32)]
+
+
+# include/rtx_kat.h
+KAT_MOLLER, KAT_SPHERE, KAT_PLANE, KAT_SLAB, KAT_NOISE, KAT_TEXTURE, KAT_SPH_LIGHT, KAT_TRI_LIGHT, \
+    KAT_MORTON, KAT_U32, KAT_GI_DIR, KAT_REFRACT = range(12)
+KAT_IN = [16, 11, 11, 13, 3, 16, 9, 11, 3, 1, 6, 7]
+KAT_OUT = [2, 5, 5, 3, 1, 3, 3, 3, 1, 2, 3, 3]
+KAT_NAMES = ["moller", "sphere", "plane", "slab", "noise", "texture", "sph_light", "tri_light", "morton", "u32",
+             "gi_dir", "refract"]
+
+# symbols include/rtx.h declares (checked by tests/test_abi.py)
+RTX_SYMBOLS = ["rtx_params_default", "rtx_device_count", "rtx_open", "rtx_upload_scene", "rtx_render",
+               "rtx_render_device", "rtx_get_stats", "rtx_close", "rtx_last_error", "rtx_kat"]
+RTX_SCENE_SYMBOLS = ["rtx_scene_load", "rtx_scene_parse", "rtx_scene_desc_of", "rtx_scene_num_json_objects",
+                     "rtx_scene_free", "rtx_scene_last_error", "rtx_frame_setup", "rtx_tiff_write", "rtx_hash_djb",
+                     "rtx_params_from_argv", "rtx_stl_write"]
+
+
+def declare_scene(lib):
+    lib.rtx_scene_load.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.POINTER(C.c_void_p)]
+    lib.rtx_scene_load.restype = C.c_int
+    lib.rtx_scene_parse.argtypes = [C.c_char_p, C.c_size_t, C.c_char_p, C.c_char_p, C.c_char_p,
+                                    C.POINTER(C.c_void_p)]
+    lib.rtx_scene_parse.restype = C.c_int
+    lib.rtx_scene_desc_of.argtypes = [C.c_void_p]
+    lib.rtx_scene_desc_of.restype = C.POINTER(SceneDesc)
+    lib.rtx_scene_num_json_objects.argtypes = [C.c_void_p]
+    lib.rtx_scene_num_json_objects.restype = C.c_uint32
+    lib.rtx_scene_free.argtypes = [C.c_void_p]
+    lib.rtx_scene_free.restype = None
+    lib.rtx_scene_last_error.argtypes = []
+    lib.rtx_scene_last_error.restype = C.c_char_p
+    lib.rtx_frame_setup.argtypes = [C.POINTER(Camera), C.c_uint32, C.c_uint32, C.POINTER(Frame)]
+    lib.rtx_frame_setup.restype = C.c_int
+    lib.rtx_tiff_write.argtypes = [C.c_char_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_int]
+    lib.rtx_tiff_write.restype = C.c_int
+    lib.rtx_hash_djb.argtypes = [C.c_char_p]
+    lib.rtx_hash_djb.restype = C.c_uint32
+    lib.rtx_params_from_argv.argtypes = [C.c_int, C.POINTER(C.c_char_p), C.POINTER(Params)]
+    lib.rtx_params_from_argv.restype = None
+    lib.rtx_stl_write.argtypes = [C.c_char_p, C.c_uint32, C.c_void_p]
+    lib.rtx_stl_write.restype = C.c_int
+
+
+def declare_rtx(lib):
+    lib.rtx_params_default.argtypes = [C.POINTER(Params)]
+    lib.rtx_params_default.restype = None
+    lib.rtx_device_count.argtypes = [C.POINTER(C.c_int)]
+    lib.rtx_device_count.restype = C.c_int
+    lib.rtx_open.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+    lib.rtx_open.restype = C.c_int
+    lib.rtx_upload_scene.argtypes = [C.c_void_p, C.POINTER(SceneDesc)]
+    lib.rtx_upload_scene.restype = C.c_int
+    lib.rtx_render.argtypes = [C.c_void_p, C.POINTER(Frame), C.POINTER(Params), C.c_void_p, C.c_void_p]
+    lib.rtx_render.restype = C.c_int
+    lib.rtx_render_device.argtypes = [C.c_void_p, C.POINTER(Frame), C.POINTER(Params), C.c_void_p, C.c_void_p,
+                                      C.c_void_p]
+    lib.rtx_render_device.restype = C.c_int
+    lib.rtx_get_stats.argtypes = [C.c_void_p, C.POINTER(Stats)]
+    lib.rtx_get_stats.restype = C.c_int
+    lib.rtx_close.argtypes = [C.c_void_p]
+    lib.rtx_close.restype = None
+    lib.rtx_last_error.argtypes = []
+    lib.rtx_last_error.restype = C.c_char_p
+    lib.rtx_kat.argtypes = [C.c_int, C.c_uint32, C.c_void_p, C.c_void_p, C.POINTER(Params)]
+    lib.rtx_kat.restype = C.c_int
+
+
+def declare_oracle(lib):
+    lib.rtx_oracle_params_default.argtypes = [C.POINTER(Params)]
+    lib.rtx_oracle_params_default.restype = None
+    lib.rtx_oracle_render.argtypes = [C.POINTER(SceneDesc), C.POINTER(Frame), C.POINTER(Params), C.c_void_p,
+                                      C.c_void_p, C.POINTER(C.c_uint64), C.c_int]
+    lib.rtx_oracle_render.restype = C.c_int
+    lib.rtx_oracle_kat.argtypes = [C.c_int, C.c_uint32, C.c_void_p, C.c_void_p, C.POINTER(Params)]
+    lib.rtx_oracle_kat.restype = C.c_int

@@ -1,0 +1,86 @@
+"""Tile sharding across ranks and the framebuffer gather.
+
+Tiles are 8x8 pixels, row-major over the frame; rank r of N renders the tiles
+t with t % N == r (rtx_params.tile_offset / tile_stride).  Interleaving deals
+the expensive centre of the frame to every rank.  After rendering, each rank
+packs its tiles (rgb + z = 16 B per pixel) into one contiguous buffer and the
+buffers are all-gathered (RCCL over xGMI with the "nccl" backend on GPUs, gloo in
+the CPU tests); rank 0 unpacks.  The only collective is this exchange: pixels
+are independent, so there is no reduction.
+"""
+import numpy as np
+import torch
+
+TILE = 8
+
+
+def tile_grid(width, height):
+    return (width + TILE - 1) // TILE, (height + TILE - 1) // TILE
+
+
+def rank_tiles(width, height, rank, world):
+    tx, ty = tile_grid(width, height)
+    return np.arange(rank, tx * ty, world, dtype=np.int64)
+
+
+def tile_pixel_index(width, height, tiles):
+    """(len(tiles), 64) flat pixel indices (-1 for pixels outside the frame)."""
+    tx, _ = tile_grid(width, height)
+    tiles = np.asarray(tiles, np.int64)
+    lx = np.arange(64) % TILE
+    ly = np.arange(64) // TILE
+    x = (tiles % tx)[:, None] * TILE + lx[None, :]
+    y = (tiles // tx)[:, None] * TILE + ly[None, :]
+    idx = y * width + x
+    idx[(x >= width) | (y >= height)] = -1
+    return idx
+
+
+class Gatherer:
+    """Packs / all-gathers / unpacks one rank's tiles.  Works on any device torch supports."""
+
+    def __init__(self, width, height, rank, world, device):
+        self.w, self.h, self.rank, self.world = width, height, rank, world
+        self.device = device
+        counts = [len(rank_tiles(width, height, r, world)) for r in range(world)]
+        self.max_tiles = max(counts) if counts else 0
+        idx = np.full((self.max_tiles, 64), -1, np.int64)
+        mine = tile_pixel_index(width, height, rank_tiles(width, height, rank, world))
+        idx[:mine.shape[0]] = mine
+        self.mine = torch.from_numpy(idx.reshape(-1)).to(device)
+        self.valid = self.mine >= 0
+        self.safe = torch.where(self.valid, self.mine, torch.zeros_like(self.mine))
+        all_idx = []
+        for r in range(world):
+            a = np.full((self.max_tiles, 64), -1, np.int64)
+            t = tile_pixel_index(width, height, rank_tiles(width, height, r, world))
+            a[:t.shape[0]] = t
+            all_idx.append(a.reshape(-1))
+        self.all_idx = torch.from_numpy(np.concatenate(all_idx)).to(device)
+        self.all_valid = self.all_idx >= 0
+        self.packed = torch.empty((self.max_tiles * 64, 4), dtype=torch.float32, device=device)
+        self.gathered = torch.empty((world * self.max_tiles * 64, 4), dtype=torch.float32, device=device)
+
+    def pack(self, rgb_flat, z_flat):
+        """rgb_flat: (W*H, 3), z_flat: (W*H,) tensors on self.device."""
+        self.packed[:, :3] = rgb_flat[self.safe]
+        self.packed[:, 3] = z_flat[self.safe]
+        self.packed[~self.valid] = 0.0
+        return self.packed
+
+    def gather(self, rgb_flat, z_flat, group=None):
+        """All-gather every rank's tiles; returns full (W*H,3), (W*H,) on every rank."""
+        packed = self.pack(rgb_flat, z_flat)
+        if self.world == 1:
+            self.gathered.copy_(packed)
+        else:
+            torch.distributed.all_gather_into_tensor(self.gathered, packed, group=group)
+        return self.unpack(self.gathered)
+
+    def unpack(self, gathered):
+        rgb = torch.zeros((self.w * self.h, 3), dtype=torch.float32, device=self.device)
+        z = torch.zeros((self.w * self.h,), dtype=torch.float32, device=self.device)
+        sel = self.all_valid
+        rgb[self.all_idx[sel]] = gathered[sel, :3]
+        z[self.all_idx[sel]] = gathered[sel, 3]
+        return rgb, z

@@ -1,0 +1,218 @@
+/*
+ * rtx.h — C-ABI of the MI355X-native trace/intersect/shade path.
+ *
+ * Drop-in boundary for C-Raytracer's hot path.  The reference
+ * enters the path at src/raytracer/main.c:76-79:
+ *
+ *     accel_init();   // accel.c:266-315   BVH build over objects[]
+ *     render_init();  // render.c:61-116   CLI -> render globals
+ *     render();       // render.c:345-368  per-pixel cast_ray() recursion
+ *     ...
+ *     accel_deinit(); // accel.c:100-103
+ *
+ * with all inputs passed through globals (objects[], emittant_objects[],
+ * unbound_objects[], materials[], camera, image, global_ambient_light_intensity)
+ * and the outputs image.raster / image.z_buffer.  Here every input crosses the
+ * boundary explicitly as plain structs and pointers:
+ *
+ *     rtx_open()          replaces nothing (device context; owns device memory)
+ *     rtx_upload_scene()  replaces accel_init()           accel.c:266
+ *     rtx_render()        replaces render_init()+render() render.c:61, 345
+ *     rtx_close()         replaces accel_deinit()         accel.c:100
+ *
+ * Host glue that the reference keeps outside the path (scene.c JSON loader,
+ * object.c STL ingest, image.c image-plane setup and TIFF writer, argv.c CLI)
+ * lives in librtxscene and is declared in rtx_scene.h.
+ *
+ * Conventions: every int-returning call returns RTX_OK (0) or a negative
+ * RTX_ERR_* code and sets a thread-local message readable with
+ * rtx_last_error().  The library never calls exit().  Buffers passed in are
+ * caller-owned and copied; the library owns device memory only.
+ */
+#ifndef RTX_H
+#define RTX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTX_ABI_VERSION 1
+
+enum rtx_status {
+	RTX_OK = 0,
+	RTX_ERR_ARG = -1,     /* bad argument / shape */
+	RTX_ERR_HIP = -2,     /* HIP runtime failure */
+	RTX_ERR_NOMEM = -3,   /* host or device allocation failed */
+	RTX_ERR_SCENE = -4,   /* scene rejected (reference would error()/exit(1)) */
+	RTX_ERR_NODEV = -5,   /* no usable gfx950 device */
+	RTX_ERR_STATE = -6,   /* call order (e.g. render before upload) */
+	RTX_ERR_IO = -7,      /* file I/O (scene / mesh / TIFF) */
+};
+
+/* object.h:17-23 enum ObjectType (UNBOUND_OBJECTS build) */
+enum rtx_object_type { RTX_SPHERE = 0, RTX_TRIANGLE = 1, RTX_PLANE = 2 };
+
+/* material.c:27-53 texture kinds, material.h:17-22 enum PeriodicFunction */
+enum rtx_texture_type {
+	RTX_TEX_UNIFORM = 0,
+	RTX_TEX_CHECKERBOARD = 1,
+	RTX_TEX_BRICK = 2,
+	RTX_TEX_NOISY_PERIODIC = 3,
+};
+enum rtx_periodic { RTX_PERIODIC_SIN = 0, RTX_PERIODIC_SAW = 1, RTX_PERIODIC_TRIANGLE = 2, RTX_PERIODIC_SQUARE = 3 };
+
+/* struct Material (material.h:30-44) + its texture, flattened. */
+typedef struct rtx_material {
+	int32_t id;
+	float ks[3], ka[3], kr[3], kt[3], ke[3];
+	float shininess;
+	float refractive_index;
+	int32_t texture;        /* enum rtx_texture_type */
+	int32_t periodic;       /* enum rtx_periodic (noisy periodic only) */
+	/* uniform: color[0]; checkerboard/brick: colors[0], colors[1];
+	 * noisy periodic: color[0] = color, color[1] = color gradient */
+	float color[2][3];
+	float scale;            /* checkerboard, brick */
+	float mortar_width;     /* brick */
+	float noise_feature_scale, noise_scale, frequency_scale; /* noisy periodic */
+	/* material_init (material.c:81-83): ‖k‖ > 1e-6 */
+	int32_t emittant, reflective, transparent;
+} rtx_material;
+
+/*
+ * One object of the reference's objects[] array (object.c:25-44), in load
+ * order, with the values its *_postinit / *_scale produced:
+ *   sphere   : p0 = position, radius                                (object.c:25-29)
+ *   triangle : p0,p1,p2 = vertices, e1 = v1-v0, e2 = v2-v0,
+ *              n = norm(e1 x e2)                                    (object.c:31-36, 327-340)
+ *   plane    : n = unit normal, d = n . position                    (object.c:39-43, 457-466)
+ * epsilon is resolved (per-type default applied), num_lights as loaded.
+ */
+typedef struct rtx_object {
+	int32_t type;           /* enum rtx_object_type */
+	int32_t material;       /* index into rtx_scene_desc.materials */
+	uint32_t num_lights;
+	float epsilon;
+	float p0[3], p1[3], p2[3];
+	float e1[3], e2[3];
+	float n[3];
+	float radius;
+	float d;
+} rtx_object;
+
+/* struct Camera (camera.h:17-22) after camera_init/camera_scale. */
+typedef struct rtx_camera {
+	float position[3];
+	float vectors[3][3];    /* v0, v1 normalised; v2 = v0 x v1 (camera.c:29-32) */
+	float fov;
+	float focal_length;
+} rtx_camera;
+
+/* Everything accel_init() + render() read from globals. */
+typedef struct rtx_scene_desc {
+	uint32_t num_materials;
+	const rtx_material *materials;
+	uint32_t num_objects;
+	const rtx_object *objects;       /* reference order */
+	uint32_t num_emitters;
+	const uint32_t *emitters;        /* object indices, emittant_objects[] order */
+	float ambient[3];                /* global_ambient_light_intensity */
+	rtx_camera camera;
+} rtx_scene_desc;
+
+/* struct Image's plane (image.h:17-26) as image_init (image.c:34-56) built it. */
+typedef struct rtx_frame {
+	uint32_t width, height;
+	float corner[3];        /* image.corner */
+	float step_x[3];        /* image.vectors[X] */
+	float step_y[3];        /* image.vectors[Y] */
+	float origin[3];        /* camera.position */
+} rtx_frame;
+
+enum rtx_reflection { RTX_PHONG = 0, RTX_BLINN = 1 };                       /* render.c:32-35 */
+enum rtx_gi { RTX_GI_AMBIENT = 0, RTX_GI_PATH = 1 };                        /* render.c:37-40 */
+enum rtx_attenuation { RTX_ATT_NONE = 0, RTX_ATT_LIN = 1, RTX_ATT_SQR = 2 }; /* render.c:42-46 */
+/* rand_flt (system.c:93-96) replacement */
+enum rtx_rng {
+	RTX_RNG_COUNTER = 0,  /* counter-based hash of (seed, pixel, ray-tree node, draw) */
+	RTX_RNG_CONST = 1,    /* every draw == 0.5f (the oracle's REF_CONST_RNG) */
+};
+/* (uint32_t)float in texture_get_color_checkerboard/brick (material.c:164,173)
+ * is UB for negatives; its result depends on the host ISA. */
+enum rtx_u32conv {
+	RTX_U32_SAT = 0,      /* x86 AVX-512 vcvttss2usi: x <= -1 or >= 2^32 or NaN -> 0xFFFFFFFF */
+	RTX_U32_WRAP = 1,     /* 64-bit cvttss2si truncated to 32 bits (generic x86-64) */
+};
+
+/* render_init() globals (render.c:53-60) + library extensions. */
+typedef struct rtx_params {
+	uint32_t max_bounces;        /* -b, default 10 */
+	float min_intensity_sqr;     /* -a squared, default 1e-4 */
+	int32_t reflection;          /* -s, enum rtx_reflection, default phong */
+	int32_t gi;                  /* -g, enum rtx_gi, default ambient */
+	uint32_t samples;            /* -n, default 1 (path GI samples at the primary hit) */
+	int32_t attenuation;         /* -l, enum rtx_attenuation, default sqr */
+	float attenuation_offset;    /* -o, default 1.0 */
+	int32_t rng;                 /* enum rtx_rng */
+	uint64_t seed;
+	int32_t u32conv;             /* enum rtx_u32conv */
+	/* sharding: render only tiles t with t % tile_stride == tile_offset
+	 * (1 tile = 8x8 pixels, row-major over the frame).  Pixels of other tiles are
+	 * left untouched in the output.  Defaults 0 / 1 = whole frame. */
+	uint32_t tile_offset, tile_stride;
+	/* count BVH node visits and primitive tests (slower kernel instance) */
+	int32_t count_traversal;
+} rtx_params;
+
+/* Defaults of render.c:53-60 (+ counter RNG, seed 1, SAT conversion, whole frame). */
+void rtx_params_default(rtx_params *p);
+
+typedef struct rtx_stats {
+	uint64_t closest_rays;       /* cast_ray() calls (render.c:136) */
+	uint64_t shadow_rays;        /* is_light_blocked() calls (render.c:126) */
+	/* only with count_traversal: */
+	uint64_t node_visits;        /* BVH internal nodes fetched per ray, summed */
+	uint64_t tri_tests;
+	uint64_t sphere_tests;
+	uint64_t plane_tests;
+	double kernel_ms;            /* device time of the last rtx_render*, HIP events */
+	uint32_t bvh_nodes;
+	uint32_t bvh_depth;
+	uint32_t bvh_prims;
+	uint32_t waves;              /* persistent waves launched */
+} rtx_stats;
+
+typedef struct rtx_ctx rtx_ctx;
+
+int rtx_device_count(int *count);
+/* Open a context on HIP device `device` (must be gfx950). */
+int rtx_open(int device, rtx_ctx **out);
+/* Flatten + copy the scene to the device, build the BVH (replaces accel_init). */
+int rtx_upload_scene(rtx_ctx *ctx, const rtx_scene_desc *scene);
+/* Render into caller-owned HOST buffers rgb[W*H*3] (row-major, row 0 = top,
+ * overwritten, not accumulated) and z[W*H] (primary-hit distance, 0 on miss);
+ * either may be NULL.  Replaces render_init()+render(). */
+int rtx_render(rtx_ctx *ctx, const rtx_frame *frame, const rtx_params *params, float *rgb, float *z);
+/* Same into DEVICE buffers on the context's device, enqueued on `stream`
+ * (hipStream_t, NULL = the context's own stream); synchronises the stream. */
+int rtx_render_device(rtx_ctx *ctx, const rtx_frame *frame, const rtx_params *params, void *d_rgb, void *d_z,
+		      void *stream);
+int rtx_get_stats(const rtx_ctx *ctx, rtx_stats *out);
+void rtx_close(rtx_ctx *ctx);
+const char *rtx_last_error(void);
+
+/*
+ * Known-answer entry: evaluates one device function over n inputs on the GPU
+ * (used by the -m gpu parity tests against the oracle's KAT fixtures).
+ * kind / record layouts are listed in rtx_kat.h.
+ */
+int rtx_kat(int kind, uint32_t n, const float *in, float *out, const rtx_params *params);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RTX_H */

@@ -1,0 +1,95 @@
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "c-raytracer_amd")
+for p in (PKG, os.path.join(ROOT, "tools")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+SCENES = os.path.join(GOLDEN, "scenes")
+FRAMES = os.path.join(GOLDEN, "frames")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a gfx950 GPU (run with -m gpu on the MI355X box)")
+    config.addinivalue_line("markers", "slow: long-running")
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _built():
+    """Native libraries are built in-tree by __graft_entry__.build(); build on demand if missing."""
+    import rtxpy
+    from rtxpy import oracle
+    need = [rtxpy.LIBSCENE, oracle.LIBORACLE]
+    if not all(os.path.exists(p) for p in need):
+        sys.path.insert(0, ROOT)
+        import __graft_entry__
+        __graft_entry__.build()
+    yield
+
+
+def manifest():
+    with open(os.path.join(FRAMES, "manifest.json")) as fh:
+        return json.load(fh)
+
+
+def golden_frame(name):
+    d = np.load(os.path.join(FRAMES, name + ".npz"))
+    return d["rgb"], d["z"]
+
+
+def load_config(name):
+    """(scene, frame, params) for a golden frame config."""
+    import rtxpy
+    import standins
+    m = manifest()[name]
+    if "standin" in m["scene"]:
+        standins.ensure_scene(m["scene"].split("_standin")[0])
+    flags = m["flags"]
+    scale = None
+    if "-r" in flags:
+        scale = flags[flags.index("-r") + 1]
+    scene = rtxpy.Scene.load(os.path.join(SCENES, m["scene"]), scale=scale, base_dir=GOLDEN)
+    frame = scene.frame(m["width"], m["height"])
+    params = rtxpy.params_from_args(flags)
+    params.rng = rtxpy.abi.RTX_RNG_CONST if m["rng"] == "const" else rtxpy.abi.RTX_RNG_COUNTER
+    return scene, frame, params, m
+
+
+def compare_const(rgb, z, ref_rgb, ref_z, px_frac=0.995, rel_l1=1e-2):
+    """SURVEY.md §8(c) tolerances for constant-RNG frames (from the reference's own -Ofast vs -O2 noise floor):
+    hit mask <= 0.01 % of pixels; |dz| <= 1e-4*max(z,1) on >= 99.9 % of hit pixels;
+    per-channel |d rgb| <= 1e-4*max(ref) on >= px_frac of pixels; image relL1 <= rel_l1."""
+    out = {}
+    hit, ref_hit = z > 0, ref_z > 0
+    out["hit_mismatch"] = float((hit != ref_hit).mean())
+    both = hit & ref_hit
+    zr = np.abs(z - ref_z) / np.maximum(ref_z, 1.0)
+    out["z_ok"] = float((zr[both] <= 1e-4).mean()) if both.any() else 1.0
+    tol = 1e-4 * float(np.abs(ref_rgb).max())
+    out["px_ok"] = float(((np.abs(rgb - ref_rgb) <= tol).all(axis=2)).mean())
+    out["rel_l1"] = float(np.abs(rgb - ref_rgb).sum() / max(float(np.abs(ref_rgb).sum()), 1e-30))
+    ok = (out["hit_mismatch"] <= 1e-4 + 1.0 / z.size and out["z_ok"] >= 0.999 and out["px_ok"] >= px_frac
+          and out["rel_l1"] <= rel_l1)
+    return ok, out
+
+
+def floor_tolerance(m):
+    """Colour tolerance for a const-RNG config: SURVEY §8(c) defaults, widened to the reference's
+    own Ofast-vs-O2 difference where that is larger (e.g. scene5's checkerboard wall sits exactly
+    on an integer checker boundary, so float->uint32 of 5*z flips with the last bit of z)."""
+    f = m.get("floor", {"px_ok": 1.0, "rel_l1": 0.0})
+    return {"px_frac": min(0.995, f["px_ok"] - 0.01), "rel_l1": max(1e-2, 1.5 * f["rel_l1"] + 2e-3)}
+
+
+def box_filter(img, k=8):
+    h, w = img.shape[:2]
+    h2, w2 = h // k * k, w // k * k
+    x = img[:h2, :w2]
+    return x.reshape(h2 // k, k, w2 // k, k, -1).mean(axis=(1, 3))

@@ -1,0 +1,36 @@
+#!/bin/bash
+# One GPU-box session: smoke -> gpu tests -> bench -> rocprof.  Each GPU step has its own
+# time limit; a fault/timeout (exit >= 124 or signal) stops the script before the next GPU step.
+# Usage: tools/gpu_round.sh <tag> [steps...]   steps: smoke tests bench prof pmc
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${1:-r01}; shift || true
+STEPS=${*:-"smoke tests bench"}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+run() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "=== $name ($(date +%T))" | tee -a "$OUT/steps.log"
+  timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a "$OUT/steps.log"
+  tail -5 "$OUT/$name.log"
+  if [ $rc -ge 124 ] || [ $rc -gt 128 ]; then echo "GPU step $name ended with $rc: stopping"; exit $rc; fi
+  return 0
+}
+python3 tools/standins.py scene5 scene6 > /dev/null
+for s in $STEPS; do
+  case $s in
+    smoke) run smoke 240 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) run tests 1500 python3 -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    testsall) run testsall 1500 python3 -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    bench) run bench 900 python3 bench.py --verbose ;;
+    benchq) run benchq 600 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --verbose ;;
+    prof) run prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-count ;;
+    pmcf) run pmcf 900 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count ;;
+    pmcw) run pmcw 900 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count ;;
+    pmcv) run pmcv 900 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES -d "$OUT/pmc_valu" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count ;;
+  esac
+done
+echo done
