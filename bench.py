@@ -58,35 +58,99 @@ def flags_for(which, spp):
     return ["-g", "path", "-n", str(spp)]
 
 
-def cpu_baseline(scene, frame, params, target_s, log):
-    """Our CPU restatement (oracle/restate.c, 'port') on a bounded, uniformly spaced sample of the
-    SAME frame's tiles, all host threads OpenMP.  Bit-exact with the reference built -O2 (tests)."""
+def _omp_threads():
+    return int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+
+
+def cpu_port(scene, frame, params, target_s, log):
+    """Our CPU restatement (oracle/restate.c, 'port') on an evenly spaced sample of the SAME frame's
+    tiles, all host threads.  Bit-exact with the reference built -O2, but ~10x faster than the
+    reference binary (flat BVH arrays, counter RNG without glibc's rand() lock)."""
     from rtxpy import abi, oracle
     import rtxpy
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = _omp_threads()
     tx, ty = (frame.width + 7) // 8, (frame.height + 7) // 8
     total = tx * ty
     p = rtxpy.default_params(**{f: getattr(params, f) for f, _ in abi.Params._fields_})
-    # calibrate on ~4 tiles, then size the sample for ~target_s
     stride = max(1, total // 4)
     p.tile_offset, p.tile_stride = 0, stride
     t0 = time.perf_counter()
-    _, _, (c0, s0) = oracle.render(scene, frame, p, threads)
+    oracle.render(scene, frame, p, threads)
     dt = max(time.perf_counter() - t0, 1e-3)
-    n_tiles = (total + stride - 1) // stride
-    rate_tiles = n_tiles / dt
-    want = max(4, min(total, int(rate_tiles * target_s)))
+    want = max(4, min(total, int(((total + stride - 1) // stride) / dt * target_s)))
     stride = max(1, total // want)
     p.tile_offset, p.tile_stride = stride // 2 if stride > 1 else 0, stride
     t0 = time.perf_counter()
     _, _, (c, s) = oracle.render(scene, frame, p, threads)
     dt = time.perf_counter() - t0
     n_tiles = len(range(p.tile_offset, total, stride))
-    log(f"cpu baseline: {n_tiles} tiles, {c}+{s} rays in {dt:.2f}s on {threads} threads")
+    log(f"cpu port: {n_tiles} tiles, {c}+{s} rays in {dt:.2f}s on {threads} threads")
     return {"value": round((c + s) / dt / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"{n_tiles} of {total} 8x8 tiles (every {stride}th) of the same {frame.width}x{frame.height} "
-                      f"frame and flags, counter RNG; oracle/restate.c is bit-exact with the reference built -O2",
-            "seconds": round(dt, 2), "rays": c + s}
+                      f"frame and flags, counter RNG", "seconds": round(dt, 2), "rays": c + s}
+
+
+def cpu_reference(scene_file, flags, width, height, target_s, log):
+    """The reference itself (oracle/_ref/engine_seed_*: /root/reference's sources built with its own
+    Makefile.rt flags + the determinism shim), timed on the host cores at a reduced resolution of the
+    same scene and flags (Mrays/s is intensive: scale the resolution, not the spp).
+    Rays are counted by the instrumented build (engine_count_*) on the same config."""
+    import subprocess
+    import tempfile
+    refdir = os.path.join(ROOT, "oracle", "_ref")
+    threads = _omp_threads()
+    golden = os.path.join(ROOT, "tests", "golden")
+    with tempfile.TemporaryDirectory() as wd:
+        os.symlink(os.path.join(golden, "meshes"), os.path.join(wd, "meshes"))
+        os.symlink(os.path.dirname(scene_file), os.path.join(wd, "scenes"))
+        rel = os.path.join("scenes", os.path.basename(scene_file))
+        env = dict(os.environ, RTX_REF_SEED="1", OMP_NUM_THREADS=str(threads))
+
+        def run(binary, w, h):
+            cmd = [binary, rel, os.path.join(wd, "o.tif"), str(w), str(h), "-m", "max"] + flags
+            t0 = time.perf_counter()
+            p = subprocess.run(cmd, cwd=wd, env=env, capture_output=True, text=True, timeout=600)
+            dt = time.perf_counter() - t0
+            if p.returncode != 0:
+                raise RuntimeError(f"{os.path.basename(binary)} rc={p.returncode}")
+            stamps = []
+            for line in p.stdout.splitlines():  # reference log: "[sss.mmm] file: func: line: msg"
+                if "Commencing raytracing." in line or "Saving image." in line:
+                    stamps.append(float(line[1:line.index("]")]))
+            t_render = (stamps[-1] - stamps[0]) if len(stamps) == 2 else dt
+            t_render = max(t_render, 1e-3)
+            counts = None
+            for line in p.stderr.splitlines():
+                if line.startswith("RTX_REF_COUNT"):
+                    kv = dict(x.split("=") for x in line.split()[1:])
+                    counts = int(kv["closest"]) + int(kv["shadow"])
+            return dt, t_render, counts
+
+        for arch in ("native", "v3"):
+            eng = os.path.join(refdir, f"engine_seed_{arch}")
+            cnt = os.path.join(refdir, f"engine_count_{arch}")
+            if not (os.path.exists(eng) and os.path.exists(cnt)):
+                continue
+            try:
+                # calibrate on a tiny frame, then size the frame for ~target_s of rendering
+                w, h = 16, 9
+                _, tr, _ = run(eng, w, h)
+                _, _, rays = run(cnt, w, h)
+                rate = rays / max(tr, 0.05)
+                scale = min(64.0, max(1.0, rate * target_s / rays) ** 0.5)
+                w, h = max(16, int(w * scale)), max(9, int(h * scale))
+                _, tr, _ = run(eng, w, h)
+                _, _, rays = run(cnt, w, h)
+            except (RuntimeError, subprocess.TimeoutExpired, OSError) as e:
+                log(f"reference {arch} unusable here: {e}")
+                continue
+            log(f"cpu reference ({arch}): {w}x{h} {' '.join(flags)}: {rays} rays in {tr:.2f}s on {threads} threads")
+            return {"value": round(rays / tr / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "reference",
+                    "sample": f"reference engine (Makefile.rt flags, -march={'native' if arch == 'native' else 'x86-64-v3'}"
+                              f", -m max) on the same scene and flags at {w}x{h}; render window = its own "
+                              f"'Commencing raytracing' -> 'Saving image' log stamps; rays from the instrumented "
+                              f"build on the same config", "seconds": round(tr, 2), "rays": rays}
+    return None
 
 
 def main():
@@ -157,6 +221,8 @@ def main():
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     stats_closest, stats_shadow = s.closest_rays, s.shadow_rays
+    split = {"trace_ms": round(s.trace_ms, 3), "shadow_ms": round(s.shadow_ms, 3), "accum_ms": round(s.accum_ms, 3),
+             "shade_points": int(s.shade_points), "chunks": int(s.chunks)}
 
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -196,9 +262,16 @@ def main():
                             "(SURVEY §8(d)); visits counted per ray (lane) by a counting instance of the "
                             "same kernel; duration = HIP events around rtx_render_device's launch"}
 
-    cpu = None
+    cpu = port = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(scene, frame, params, a.cpu_target_s, log)
+        try:
+            cpu = cpu_reference(path, flags, a.width, a.height, a.cpu_target_s, log)
+        except Exception as e:  # never let the baseline kill the measurement
+            log(f"reference baseline failed: {e}")
+        port = cpu_port(scene, frame, params, a.cpu_target_s / 2, log)
+        if cpu is None:
+            cpu = port
+            port = None
 
     if rank == 0:
         value = rays / elapsed / 1e6
@@ -211,10 +284,13 @@ def main():
                           "scene": os.path.basename(path), "width": a.width, "height": a.height, "spp": a.spp,
                           "objects": int(scene.num_objects), "rays_per_frame_rank0": stats_closest + stats_shadow,
                           "closest_rays_rank0": stats_closest, "shadow_rays_rank0": stats_shadow,
-                          "parallelism": f"tiles{world}", "kernel_ms_rank0": round(kernel_ms, 3)},
+                          "parallelism": f"tiles{world}", "kernel_ms_rank0": round(kernel_ms, 3),
+                          "kernels_rank0": split, "shadow_occ": os.environ.get("RTX_SHADOW_OCC", "default")},
                "roofline": roofline, "cpu_baseline": cpu}
         if cpu:
             out["config"]["gpu_over_cpu"] = round(value / cpu["value"], 1)
+        if port:
+            out["cpu_port"] = port
         print(json.dumps(out), flush=True)
     r.close()
     if world > 1:

@@ -18,13 +18,22 @@
 #include "rtx_device.h"
 #include "rtx_kat.h"
 
-extern "C" hipError_t rtx_launch_render(const DScene *S, const DFrame *F, const DParams *P, float *rgb, float *z,
-					 DTask *tasks, uint32_t task_cap, unsigned long long *ctr, uint32_t waves,
-					 int count, hipStream_t stream);
+extern "C" size_t rtx_trace_lds_bytes(uint32_t stack_size);
+extern "C" size_t rtx_shadow_lds_bytes(uint32_t stack_size);
+extern "C" hipError_t rtx_trace_occupancy(uint32_t stack_size, int *blocks_per_cu);
+extern "C" hipError_t rtx_launch_trace(const DScene *S, const DFrame *F, const DParams *P, float *rgb, float *z,
+				       DTask *tasks, uint32_t task_cap, float4 *staging, uint32_t staging_cap,
+				       float4 *sp_out, uint32_t sp_cap, uint2 *tile_rec, uint32_t tile_begin,
+				       uint32_t tile_end, unsigned long long *ctr, uint32_t waves, int count,
+				       hipStream_t stream);
+extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const float4 *sp, uint32_t n_sp,
+					uint32_t per_wave, uint32_t slot_b, float4 *contrib, unsigned long long *ctr,
+					int count, hipStream_t stream);
+extern "C" hipError_t rtx_launch_accum(const DFrame *F, const DParams *P, const uint2 *tile_rec,
+				       const float4 *contrib, uint32_t tile_begin, uint32_t ntiles, float *rgb,
+				       hipStream_t stream);
 extern "C" hipError_t rtx_launch_kat(int kind, uint32_t n, const float *in, float *out, int u32mode,
-				      hipStream_t stream);
-extern "C" hipError_t rtx_render_occupancy(uint32_t stack_size, int *blocks_per_cu);
-extern "C" size_t rtx_render_lds_bytes(uint32_t stack_size);
+				     hipStream_t stream);
 
 static thread_local char g_err[512] = "";
 
@@ -57,9 +66,19 @@ struct rtx_ctx {
 	DEmitter *d_emitters = nullptr;
 	DScene scene{};
 	bool have_scene = false;
-	/* work buffers */
+	/* work buffers (grow-only) */
 	DTask *d_tasks = nullptr;
 	size_t task_bytes = 0;
+	float4 *d_staging = nullptr;
+	size_t staging_bytes = 0;
+	float4 *d_sp = nullptr;
+	size_t sp_bytes = 0;
+	float4 *d_contrib = nullptr;
+	size_t contrib_bytes = 0;
+	uint2 *d_tile_rec = nullptr;
+	size_t tile_rec_bytes = 0;
+	hipEvent_t ev[4] = { nullptr, nullptr, nullptr, nullptr };
+	uint32_t total_lights = 0;
 	unsigned long long *d_ctr = nullptr;
 	float *d_rgb = nullptr, *d_z = nullptr;
 	size_t fb_pixels = 0;
@@ -125,6 +144,13 @@ extern "C" void rtx_close(rtx_ctx *c)
 		(void)hipStreamSynchronize(c->stream);
 	free_scene(c);
 	dfree(c->d_tasks);
+	dfree(c->d_staging);
+	dfree(c->d_sp);
+	dfree(c->d_contrib);
+	dfree(c->d_tile_rec);
+	for (auto &e : c->ev)
+		if (e)
+			(void)hipEventDestroy(e);
 	dfree(c->d_ctr);
 	dfree(c->d_rgb);
 	dfree(c->d_z);
@@ -157,6 +183,8 @@ extern "C" int rtx_open(int device, rtx_ctx **out)
 	hipError_t e;
 	if ((e = hipSetDevice(device)) != hipSuccess || (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
 	    (e = hipEventCreate(&c->ev0)) != hipSuccess || (e = hipEventCreate(&c->ev1)) != hipSuccess ||
+	    (e = hipEventCreate(&c->ev[0])) != hipSuccess || (e = hipEventCreate(&c->ev[1])) != hipSuccess ||
+	    (e = hipEventCreate(&c->ev[2])) != hipSuccess || (e = hipEventCreate(&c->ev[3])) != hipSuccess ||
 	    (e = hipMalloc(&c->d_ctr, sizeof(unsigned long long) * RTX_C_N)) != hipSuccess) {
 		rtx_close(c);
 		return fail(RTX_ERR_HIP, "context setup failed: %s", hipGetErrorString(e));
@@ -329,6 +357,9 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 	S.num_planes = (uint32_t)planes.size();
 	S.num_emitters = sc->num_emitters;
 	S.stack_size = std::max<uint32_t>(bvh.depth + 1, 4);
+	c->total_lights = 0;
+	for (const DEmitter &e : emit)
+		c->total_lights += e.num_lights;
 	memcpy(S.ambient, sc->ambient, 12);
 	c->have_scene = true;
 	c->stats.bvh_nodes = (uint32_t)bvh.nodes.size();
@@ -375,39 +406,118 @@ static int render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, f
 	P.ntiles = p->tile_offset < total ? (uint32_t)((total - p->tile_offset + p->tile_stride - 1) / p->tile_stride) : 0;
 
 	int per_cu = 0;
-	HIP_TRY(rtx_render_occupancy(c->scene.stack_size, &per_cu));
+	HIP_TRY(rtx_trace_occupancy(c->scene.stack_size, &per_cu));
 	if (per_cu <= 0)
-		return fail(RTX_ERR_HIP, "render kernel does not fit (LDS %zu B)", rtx_render_lds_bytes(c->scene.stack_size));
-	uint32_t waves = (uint32_t)std::min<uint64_t>((uint64_t)per_cu * c->cus, std::max<uint32_t>(P.ntiles, 1));
+		return fail(RTX_ERR_HIP, "trace kernel does not fit (LDS %zu B)", rtx_trace_lds_bytes(c->scene.stack_size));
+	const uint32_t waves = (uint32_t)std::min<uint64_t>((uint64_t)per_cu * c->cus, std::max<uint32_t>(P.ntiles, 1));
 	/* LIFO task stack: each batch pops <= 64 and pushes <= 128, depth <= max_bounces */
-	uint32_t task_cap = 64u * (std::min<uint32_t>(P.max_bounces, 4096u) + 3u);
-	size_t need = (size_t)waves * task_cap * sizeof(DTask);
-	if (need > c->task_bytes) {
-		dfree(c->d_tasks);
-		HIP_TRY(hipMalloc(&c->d_tasks, need));
-		c->task_bytes = need;
-	}
+	const uint32_t mb = std::min<uint32_t>(P.max_bounces, 4096u);
+	const uint32_t task_cap = 64u * (mb + 3u);
+	/* shade points per tile: 64 px x (primary + GI samples) + secondary-ray allowance */
+	const uint64_t gi_n = P.gi == RTX_GI_PATH ? (uint64_t)P.samples : 0u;
+	uint64_t staging_cap = 64ull * (1 + gi_n) + 64ull * 4 * std::min<uint32_t>(mb, 16u) * (gi_n ? 2 : 1) + 64;
+	const uint64_t avg_tile = 64ull * (1 + gi_n) * 5 / 4 + 64;
+	size_t free_b = 0, total_b = 0;
+	HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+	const uint64_t budget = std::min<uint64_t>(24ull << 30, free_b / 3);
+	uint32_t chunk_tiles = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(P.ntiles, budget / (avg_tile * 112)));
+
+	auto grow = [](auto *&ptr, size_t &have, size_t need) -> hipError_t {
+		if (need <= have)
+			return hipSuccess;
+		dfree(ptr);
+		have = 0;
+		hipError_t e = hipMalloc(&ptr, need);
+		if (e == hipSuccess)
+			have = need;
+		return e;
+	};
+	HIP_TRY(grow(c->d_tasks, c->task_bytes, (size_t)waves * task_cap * sizeof(DTask)));
+
 	HIP_TRY(hipMemsetAsync(c->d_ctr, 0, sizeof(unsigned long long) * RTX_C_N, stream));
 	HIP_TRY(hipEventRecord(c->ev0, stream));
-	if (P.ntiles)
-		HIP_TRY(rtx_launch_render(&c->scene, &F, &P, d_rgb, d_z, c->d_tasks, task_cap, c->d_ctr, waves,
-					  p->count_traversal, stream));
+	double t_trace = 0, t_shadow = 0, t_accum = 0;
+	uint64_t shade_points = 0;
+	uint32_t chunks = 0;
+	/* shadow kernel: lane slots of slot_b = pow2ceil(lights) (<= 64) lanes per point; ~16 packets per wave */
+	uint32_t slot_b = 1;
+	while (slot_b < 64 && slot_b < c->total_lights)
+		slot_b <<= 1;
+	const uint32_t slots_per_point = (std::max<uint32_t>(c->total_lights, 1) + slot_b - 1) / slot_b;
+	const uint32_t per_wave = std::max<uint32_t>(1, std::min<uint32_t>(64, 1024 / (slot_b * slots_per_point)));
+	for (uint32_t begin = 0; begin < P.ntiles;) {
+		const uint32_t end = std::min<uint32_t>(P.ntiles, begin + chunk_tiles);
+		const uint64_t sp_cap64 = std::min<uint64_t>((uint64_t)(end - begin) * avg_tile + staging_cap, 0xFFFFFFF0ull);
+		const uint32_t sp_cap = (uint32_t)sp_cap64;
+		HIP_TRY(grow(c->d_staging, c->staging_bytes, (size_t)waves * staging_cap * 6 * sizeof(float4)));
+		HIP_TRY(grow(c->d_sp, c->sp_bytes, (size_t)sp_cap * 6 * sizeof(float4)));
+		HIP_TRY(grow(c->d_contrib, c->contrib_bytes, (size_t)sp_cap * sizeof(float4)));
+		HIP_TRY(grow(c->d_tile_rec, c->tile_rec_bytes, (size_t)(end - begin) * sizeof(uint2)));
+		HIP_TRY(hipMemsetAsync(c->d_ctr, 0, sizeof(unsigned long long) * RTX_C_CHUNK_N, stream));
+		HIP_TRY(hipEventRecord(c->ev[0], stream));
+		HIP_TRY(rtx_launch_trace(&c->scene, &F, &P, d_rgb, d_z, c->d_tasks, task_cap, c->d_staging,
+					 (uint32_t)staging_cap, c->d_sp, sp_cap, c->d_tile_rec, begin, end, c->d_ctr,
+					 std::min<uint32_t>(waves, end - begin), p->count_traversal, stream));
+		HIP_TRY(hipEventRecord(c->ev[1], stream));
+		unsigned long long head[RTX_C_CHUNK_N];
+		HIP_TRY(hipMemcpyAsync(head, c->d_ctr, sizeof(head), hipMemcpyDeviceToHost, stream));
+		HIP_TRY(hipStreamSynchronize(stream));
+		if (head[RTX_C_OVERFLOW]) {
+			if (staging_cap >= (1ull << 26))
+				return fail(RTX_ERR_STATE, "secondary-ray storage overflow (task stack or %llu shade points per tile)",
+					    (unsigned long long)staging_cap);
+			staging_cap *= 2; /* retry the chunk with room for larger ray trees */
+			continue;
+		}
+		if (head[RTX_C_SPOVERFLOW]) {
+			if (end - begin == 1)
+				return fail(RTX_ERR_STATE, "shade-point array overflow on a single tile");
+			chunk_tiles = std::max<uint32_t>(1, (end - begin) / 2);
+			continue;
+		}
+		const uint32_t n_sp = (uint32_t)head[RTX_C_SPCOUNT];
+		shade_points += n_sp;
+		HIP_TRY(rtx_launch_shadow(&c->scene, &P, c->d_sp, n_sp, per_wave, slot_b, c->d_contrib, c->d_ctr, p->count_traversal,
+					  stream));
+		HIP_TRY(hipEventRecord(c->ev[2], stream));
+		HIP_TRY(rtx_launch_accum(&F, &P, c->d_tile_rec, c->d_contrib, begin, end - begin, d_rgb, stream));
+		HIP_TRY(hipEventRecord(c->ev[3], stream));
+		HIP_TRY(hipEventSynchronize(c->ev[3]));
+		float a = 0, b = 0, cc = 0;
+		HIP_TRY(hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
+		HIP_TRY(hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
+		HIP_TRY(hipEventElapsedTime(&cc, c->ev[2], c->ev[3]));
+		t_trace += a;
+		t_shadow += b;
+		t_accum += cc;
+		chunks++;
+		begin = end;
+	}
 	HIP_TRY(hipEventRecord(c->ev1, stream));
 	unsigned long long ctr[RTX_C_N];
 	HIP_TRY(hipMemcpyAsync(ctr, c->d_ctr, sizeof(ctr), hipMemcpyDeviceToHost, stream));
 	HIP_TRY(hipStreamSynchronize(stream));
 	float ms = 0.f;
 	HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
-	c->stats.closest_rays = ctr[RTX_C_CLOSEST];
-	c->stats.shadow_rays = ctr[RTX_C_SHADOW];
-	c->stats.node_visits = ctr[RTX_C_NODES];
-	c->stats.tri_tests = ctr[RTX_C_TRIS];
-	c->stats.sphere_tests = ctr[RTX_C_SPHERES];
-	c->stats.plane_tests = ctr[RTX_C_PLANES];
-	c->stats.kernel_ms = ms;
-	c->stats.waves = waves;
-	if (ctr[RTX_C_OVERFLOW])
-		return fail(RTX_ERR_STATE, "secondary-ray task stack overflow in %llu waves", ctr[RTX_C_OVERFLOW]);
+	rtx_stats &st = c->stats;
+	st.closest_rays = ctr[RTX_C_CLOSEST];
+	st.shadow_rays = ctr[RTX_C_SHADOW];
+	st.shadow_node_visits = ctr[RTX_C_SNODES];
+	st.shadow_tri_tests = ctr[RTX_C_STRIS];
+	st.shadow_sphere_tests = ctr[RTX_C_SSPHERES];
+	st.shadow_plane_tests = ctr[RTX_C_SPLANES];
+	st.node_visits = ctr[RTX_C_NODES] + ctr[RTX_C_SNODES];
+	st.tri_tests = ctr[RTX_C_TRIS] + ctr[RTX_C_STRIS];
+	st.sphere_tests = ctr[RTX_C_SPHERES] + ctr[RTX_C_SSPHERES];
+	st.plane_tests = ctr[RTX_C_PLANES] + ctr[RTX_C_SPLANES];
+	st.shade_points = shade_points;
+	st.kernel_ms = t_trace + t_shadow + t_accum;
+	st.trace_ms = t_trace;
+	st.shadow_ms = t_shadow;
+	st.accum_ms = t_accum;
+	st.waves = waves;
+	st.chunks = chunks;
+	(void)ms;
 	return RTX_OK;
 }
 

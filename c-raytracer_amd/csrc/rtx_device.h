@@ -35,14 +35,14 @@
 #define RTX_TILE_W 8
 #define RTX_TILE_H 8
 
-typedef struct DNode {
+typedef struct __attribute__((aligned(64))) DNode {
 	float lo0x, hi0x, lo0y, hi0y;
 	float lo0z, hi0z, lo1x, hi1x;
 	float lo1y, hi1y, lo1z, hi1z;
 	uint32_t ref0, ref1, axis, pad;
 } DNode;
 
-typedef struct DPrim {
+typedef struct __attribute__((aligned(64))) DPrim {
 	float a[4];
 	float b[4];
 	float c[4];
@@ -124,17 +124,24 @@ typedef struct DTask {
 	uint32_t slot;
 } DTask;
 
-/* global counters written by the render kernel */
+/* global counters written by the kernels */
 enum {
-	RTX_C_TILE = 0,   /* work queue head */
+	RTX_C_TILE = 0,   /* k_trace work queue head (per chunk) */
+	RTX_C_SPCOUNT,    /* shade points emitted (per chunk) */
+	RTX_C_OVERFLOW,   /* task-stack / staging overflow (per chunk) */
+	RTX_C_SPOVERFLOW, /* chunk shade-point array overflow (per chunk) */
 	RTX_C_CLOSEST,
 	RTX_C_SHADOW,
-	RTX_C_NODES,
+	RTX_C_NODES,      /* closest-hit traversal counts (count mode) */
 	RTX_C_TRIS,
 	RTX_C_SPHERES,
 	RTX_C_PLANES,
-	RTX_C_OVERFLOW,
+	RTX_C_SNODES,     /* shadow traversal counts (count mode) */
+	RTX_C_STRIS,
+	RTX_C_SSPHERES,
+	RTX_C_SPLANES,
 	RTX_C_N
 };
+#define RTX_C_CHUNK_N 4 /* counters reset per chunk */
 
 #endif

@@ -1,44 +1,51 @@
 /*
  * MI355X (gfx950) kernels for C-Raytracer's trace/intersect/shade hot path.
  *
- * One persistent kernel, one wavefront per workgroup.  Each wave pulls 8x8
- * pixel tiles from a device-wide queue (one returning atomic per tile) and
- * evaluates the reference's cast_ray() ray tree (render.c:136-343) for all 64
- * pixels of the tile, iteratively instead of recursively:
+ * The reference's cast_ray() recursion (render.c:136-343) is evaluated as three
+ * kernels per chunk of 8x8 pixel tiles, one wavefront per workgroup:
  *
- *   batch   = up to 64 closest-hit rays, one per lane (primaries of the tile,
- *             then reflection/refraction children popped from the wave's task
- *             stack in HBM; __ballot/mbcnt compaction on push)
- *   trace   = per-lane BVH2 traversal, stack in LDS ([entry][lane], conflict-free)
- *   shade   = per-lane hit setup; local terms (ke, ambient) routed to the
- *             owning pixel's accumulator; children pushed; shade points (SP)
- *             written to an LDS table
- *   light   = the (SP, light sample) pairs of the batch flattened and processed
- *             64 at a time; each group of 64 shadow rays traverses the BVH as a
- *             PACKET: node/primitive indices are wave-uniform, so node records
- *             come in through scalar loads, every lane tests its own ray and
- *             __ballot picks the children to descend (the shadow rays of one
- *             hit all aim at the same emitter, so the packet is coherent).
- *             Per-SP sums by a deterministic segmented wave reduction.
- *   GI      = (SP, sample) pairs flattened the same way, traced per lane,
- *             their hits shaded and lit like any other batch.
+ *  k_trace  (persistent; tiles from a device queue, one returning atomic each)
+ *           every closest-hit query of the tile's ray trees: primaries, then
+ *           reflection/refraction children from a per-wave LIFO task stack in
+ *           HBM (__ballot/mbcnt compaction on push), and the path-GI samples
+ *           of each batch flattened over (hit, sample) 64 at a time.  Per-lane
+ *           BVH2 traversal with the stack in LDS ([entry][lane]).  Local terms
+ *           (ke, ambient) go straight to the tile's pixels; every hit that sees
+ *           lights becomes a 96-byte shade point, appended in a fixed order to
+ *           a per-wave staging region and moved to the chunk's contiguous
+ *           array at tile end.
+ *  k_shadow (one wave per few shade points) direct lighting, the dominant
+ *           work (95.9-99.6 % of all rays): (point, light) pairs flattened and
+ *           traced 64 at a time as a PACKET - node and primitive indices are
+ *           wave-uniform, every lane tests its own shadow ray, __ballot picks
+ *           the children.  Shadow rays of one hit all aim at one small emitter,
+ *           so packets stay coherent.  Per-point sums by deterministic
+ *           segmented wave reductions.
+ *  k_accum  (one wave per tile) adds the points' light terms to their pixels
+ *           in emission order.
  *
- * Everything a pixel receives is summed in a fixed order inside one wave, so
- * the image is bit-identical whichever wave, GPU or tile order renders it.
+ * No float atomics anywhere: a pixel's value is bit-identical whichever wave,
+ * GPU or tile order renders it.
  */
 #include <hip/hip_runtime.h>
 #include <float.h>
+#include <stdlib.h>
 
 #include "rtx_kat.h"
 #include "rtx_math.h"
 #include "rtx_rng.h"
 
 #define WAVE 64
+#ifndef RTX_SHADOW_OCC_DEFAULT
+#define RTX_SHADOW_OCC_DEFAULT 0
+#endif
+
 
 /* ------------------------------------------------------------------------ */
 /* wave helpers                                                             */
 /* ------------------------------------------------------------------------ */
 typedef unsigned long long u64;
+typedef uint32_t v16u __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ u64 ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ uint32_t popc64(u64 m) { return (uint32_t)__popcll(m); }
@@ -48,12 +55,12 @@ __device__ __forceinline__ uint32_t mbcnt(u64 m)
 	return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ float unif(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
 __device__ __forceinline__ uint32_t readlane(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
 __device__ __forceinline__ float readlanef(float v, uint32_t l)
 {
 	return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
+__device__ __forceinline__ bool lane_in(u64 m) { return (m >> lane_id()) & 1ull; }
 
 /* deterministic butterfly sum: every lane gets the same total */
 __device__ __forceinline__ float wave_sum(float v)
@@ -64,7 +71,7 @@ __device__ __forceinline__ float wave_sum(float v)
 	return v;
 }
 
-/* exclusive prefix sum of v over the wave; total returned via *tot (uniform) */
+/* exclusive prefix sum over the wave; *tot = total (uniform) */
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t *tot)
 {
 	uint32_t x = v;
@@ -78,427 +85,28 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t *tot)
 	return x - v;
 }
 
-/* ------------------------------------------------------------------------ */
-/* kernel-wide context                                                      */
-/* ------------------------------------------------------------------------ */
-struct Ctx {
-	DScene S;
-	DFrame F;
-	DParams P;
-	float *lds_sp_a;   /* 64 SP records */
-	float *lds_sp_b;   /* 64 SP records (aliases the traversal stack) */
-	uint32_t *off_a;   /* 65 offsets */
-	uint32_t *off_b;
-	uint32_t *pstk;    /* packet stack (wave-uniform) */
-	uint32_t *stk;     /* per-lane stack [entry][lane] */
-	uint32_t total_lights;
-	/* counters (wave-uniform) */
-	u64 n_closest, n_shadow, n_nodes, n_tris, n_spheres, n_planes;
-};
-
-#define SPW 24 /* floats per shade-point record (6 x float4) */
-
-struct SP {
-	f3 p;
-	float eps;
-	f3 n;
-	uint32_t obj;
-	f3 d;
-	uint32_t mat;
-	f3 w;
-	uint32_t slot;
-	f3 tex;
-	uint32_t key_lo;
-	float delta;
-	uint32_t ngi;
-	uint32_t nl;
-	uint32_t key_hi;
-};
-
-__device__ __forceinline__ void sp_store(float *tab, uint32_t k, const SP &s)
+/* largest k in [0,64) with off[k] <= idx, for off[0] = 0 <= idx < off[64] */
+__device__ __forceinline__ uint32_t owner_of(const uint32_t *off, uint32_t idx)
 {
-	float4 *q = (float4 *)(tab + k * SPW);
-	q[0] = make_float4(s.p.x, s.p.y, s.p.z, s.eps);
-	q[1] = make_float4(s.n.x, s.n.y, s.n.z, __uint_as_float(s.obj));
-	q[2] = make_float4(s.d.x, s.d.y, s.d.z, __uint_as_float(s.mat));
-	q[3] = make_float4(s.w.x, s.w.y, s.w.z, __uint_as_float(s.slot));
-	q[4] = make_float4(s.tex.x, s.tex.y, s.tex.z, __uint_as_float(s.key_lo));
-	q[5] = make_float4(s.delta, __uint_as_float(s.ngi), __uint_as_float(s.nl), __uint_as_float(s.key_hi));
+	uint32_t lo = 0, hi = WAVE;
+	while (hi - lo > 1) {
+		uint32_t mid = (lo + hi) >> 1;
+		if (off[mid] <= idx)
+			lo = mid;
+		else
+			hi = mid;
+	}
+	return lo;
 }
 
-__device__ __forceinline__ SP sp_load(const float *tab, uint32_t k)
+__device__ __forceinline__ void lds_sync()
 {
-	const float4 *q = (const float4 *)(tab + k * SPW);
-	float4 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4], f = q[5];
-	SP s;
-	s.p = mk3(a.x, a.y, a.z);
-	s.eps = a.w;
-	s.n = mk3(b.x, b.y, b.z);
-	s.obj = __float_as_uint(b.w);
-	s.d = mk3(c.x, c.y, c.z);
-	s.mat = __float_as_uint(c.w);
-	s.w = mk3(d.x, d.y, d.z);
-	s.slot = __float_as_uint(d.w);
-	s.tex = mk3(e.x, e.y, e.z);
-	s.key_lo = __float_as_uint(e.w);
-	s.delta = f.x;
-	s.ngi = __float_as_uint(f.y);
-	s.nl = __float_as_uint(f.z);
-	s.key_hi = __float_as_uint(f.w);
-	return s;
-}
-
-__device__ __forceinline__ uint64_t key_of(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
-
-__device__ __forceinline__ void draw(const DParams &P, uint64_t key, uint32_t stream, uint32_t idx, float &u1, float &u2)
-{
-	if (P.rng == RTX_RNG_CONST) {
-		u1 = 0.5f;
-		u2 = 0.5f;
-	} else {
-		rtx_draw2(key, stream, idx, &u1, &u2);
-	}
-}
-
-__device__ __forceinline__ float att_factor(const DParams &P, float dist)
-{
-	if (P.attenuation == RTX_ATT_LIN)
-		return 1.f / (P.att_offset + dist);
-	if (P.attenuation == RTX_ATT_SQR) {
-		float q = P.att_offset + dist;
-		return 1.f / (q * q);
-	}
-	return 1.f;
-}
-
-/* lights an SP on object `obj` samples: sum of num_lights of the emitters != obj */
-__device__ __forceinline__ uint32_t lights_for(const Ctx &C, uint32_t obj)
-{
-	uint32_t n = C.total_lights;
-	for (uint32_t e = 0; e < C.S.num_emitters; e++)
-		if (C.S.emitters[e].obj == obj)
-			n -= C.S.emitters[e].num_lights;
-	return n;
-}
-
-/* ------------------------------------------------------------------------ */
-/* closest hit: planes, then BVH (render.c:118-124); per-lane traversal     */
-/* ------------------------------------------------------------------------ */
-template <bool COUNT>
-__device__ void trace_closest(Ctx &C, bool act, f3 o, f3 d, uint32_t inside, float &t_out, uint32_t &hid_out,
-			      uint32_t &nodes, uint32_t &tris, uint32_t &sph, uint32_t &pln)
-{
-	const DScene &S = C.S;
-	float tbest = FLT_MAX;
-	uint32_t hid = RTX_NONE;
-	if (act && isnan3(d)) /* TIR / degenerate directions: no hit */
-		act = false;
-	/* inside-object shortcut (render.c:143-144) */
-	if (act && inside != RTX_NONE) {
-		float t;
-		bool h;
-		if (inside & RTX_PLANE_BIT) {
-			const DPlane &pl = S.planes[inside & ~RTX_PLANE_BIT];
-			h = hit_plane(ld3(pl.n), pl.d, o, d, pl.eps, t);
-		} else {
-			const DPrim &pr = S.prims[inside];
-			uint32_t type = __float_as_uint(pr.c[3]) >> 24;
-			if (type == RTX_SPHERE)
-				h = hit_sphere(mk3(pr.a[0], pr.a[1], pr.a[2]), pr.b[0], o, d, pr.a[3], t);
-			else
-				h = hit_triangle(mk3(pr.a[0], pr.a[1], pr.a[2]), mk3(pr.b[0], pr.b[1], pr.b[2]),
-						 mk3(pr.c[0], pr.c[1], pr.c[2]), o, d, pr.a[3], t);
-		}
-		if (h) {
-			tbest = t;
-			hid = inside;
-			act = false;
-		}
-	}
-	if (act) {
-		for (uint32_t i = 0; i < S.num_planes; i++) {
-			const DPlane &pl = S.planes[i];
-			float t;
-			if (COUNT)
-				pln++;
-			if (hit_plane(ld3(pl.n), pl.d, o, d, pl.eps, t) && t < tbest) {
-				tbest = t;
-				hid = RTX_PLANE_BIT | i;
-			}
-		}
-	}
-	if (act && S.root_ref != RTX_EMPTY_REF) {
-		const f3 inv = safe_inv(d);
-		const f3 oi = mul3v(o, inv);
-		uint32_t ref = S.root_ref;
-		uint32_t sp = 0;
-		uint32_t *stk = C.stk + lane_id();
-		for (;;) {
-			if (ref & RTX_LEAF_BIT) {
-				uint32_t first = (ref >> 4) & 0x7FFFFFFu, cnt = (ref & 15u) + 1;
-				for (uint32_t k = 0; k < cnt; k++) {
-					const DPrim &pr = S.prims[first + k];
-					float4 a = *(const float4 *)pr.a, b = *(const float4 *)pr.b, c = *(const float4 *)pr.c;
-					uint32_t type = __float_as_uint(c.w) >> 24;
-					float t;
-					bool h;
-					if (type == RTX_SPHERE) {
-						if (COUNT)
-							sph++;
-						h = hit_sphere(mk3(a.x, a.y, a.z), b.x, o, d, a.w, t);
-					} else {
-						if (COUNT)
-							tris++;
-						h = hit_triangle(mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z), mk3(c.x, c.y, c.z), o, d,
-								 a.w, t);
-					}
-					if (h && t < tbest) {
-						tbest = t;
-						hid = first + k;
-					}
-				}
-				if (sp == 0)
-					break;
-				ref = stk[--sp * WAVE];
-			} else {
-				const float4 *nd = (const float4 *)(S.nodes + ref);
-				float4 n0 = nd[0], n1 = nd[1], n2 = nd[2];
-				uint4 n3 = *(const uint4 *)(nd + 3);
-				if (COUNT)
-					nodes++;
-				float tn0, tn1;
-				bool h0 = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, oi, inv, tbest, tn0) && tn0 < tbest;
-				bool h1 = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, oi, inv, tbest, tn1) && tn1 < tbest;
-				if (h0 && h1) {
-					/* nearer child first; tie -> right first (accel.c:341-345) */
-					uint32_t nr = tn0 < tn1 ? n3.x : n3.y, fr = tn0 < tn1 ? n3.y : n3.x;
-					stk[sp++ * WAVE] = fr;
-					ref = nr;
-				} else if (h0) {
-					ref = n3.x;
-				} else if (h1) {
-					ref = n3.y;
-				} else {
-					if (sp == 0)
-						break;
-					ref = stk[--sp * WAVE];
-				}
-			}
-		}
-	}
-	t_out = tbest;
-	hid_out = hid;
-}
-
-/* ------------------------------------------------------------------------ */
-/* shadow any-hit with transmittance (render.c:126-134, object.c:183-197,   */
-/* accel.c:360-387) for one group of <= 64 rays, BVH walked as a packet.    */
-/* ------------------------------------------------------------------------ */
-template <bool COUNT>
-__device__ void shadow_packet(Ctx &C, bool act, f3 o, f3 d, float dist, uint32_t emit_obj, f3 &li, bool &blocked)
-{
-	const DScene &S = C.S;
-	blocked = false;
-	if (act) {
-		for (uint32_t i = 0; i < S.num_planes; i++) {
-			const DPlane &pl = S.planes[i];
-			float t;
-			if (hit_plane(ld3(pl.n), pl.d, o, d, pl.eps, t) && t < dist) {
-				const DMaterial &m = S.mats[pl.mat];
-				if (m.flags & RTX_MF_TRANSPARENT)
-					li = mul3v(li, ld3(m.kt));
-				else {
-					blocked = true;
-					break;
-				}
-			}
-		}
-	}
-	if (COUNT)
-		C.n_planes += (u64)popc64(ballot(act)) * S.num_planes;
-	u64 live = ballot(act && !blocked);
-	if (!live || S.root_ref == RTX_EMPTY_REF)
-		return;
-	const f3 inv = safe_inv(d);
-	const f3 oi = mul3v(o, inv);
-	/* near-first order from the first live ray's direction signs */
-	const uint32_t lead = (uint32_t)__ffsll((long long)live) - 1;
-	const uint32_t dsign = uni(((d.x >= 0.f) ? 1u : 0u) | ((d.y >= 0.f) ? 2u : 0u) | ((d.z >= 0.f) ? 4u : 0u));
-	const uint32_t dsgn = readlane(dsign, lead);
-	uint32_t ref = S.root_ref;
-	uint32_t sp = 0;
-	for (;;) {
-		if (ref & RTX_LEAF_BIT) {
-			const uint32_t first = (ref >> 4) & 0x7FFFFFFu, cnt = (ref & 15u) + 1;
-			for (uint32_t k = 0; k < cnt; k++) {
-				const DPrim &pr = S.prims[first + k];
-				const uint32_t meta = __float_as_uint(pr.c[3]);
-				const uint32_t type = meta >> 24;
-				const uint32_t obj = __float_as_uint(pr.b[3]);
-				const bool mine = ((live >> lane_id()) & 1ull) && obj != emit_obj;
-				float t;
-				bool h = false;
-				if (type == RTX_SPHERE) {
-					if (COUNT)
-						C.n_spheres += popc64(live);
-					if (mine)
-						h = hit_sphere(mk3(pr.a[0], pr.a[1], pr.a[2]), pr.b[0], o, d, pr.a[3], t);
-				} else {
-					if (COUNT)
-						C.n_tris += popc64(live);
-					if (mine)
-						h = hit_triangle(mk3(pr.a[0], pr.a[1], pr.a[2]), mk3(pr.b[0], pr.b[1], pr.b[2]),
-								 mk3(pr.c[0], pr.c[1], pr.c[2]), o, d, pr.a[3], t);
-				}
-				h = h && t < dist;
-				if (ballot(h)) {
-					const DMaterial &m = S.mats[meta & 0xFFFFFFu];
-					if (m.flags & RTX_MF_TRANSPARENT) {
-						if (h)
-							li = mul3v(li, mk3(m.kt[0], m.kt[1], m.kt[2]));
-					} else if (h) {
-						blocked = true;
-					}
-				}
-			}
-			live = ballot(((live >> lane_id()) & 1ull) && !blocked);
-			if (!live || sp == 0)
-				break;
-			ref = uni(C.pstk[--sp]);
-		} else {
-			const DNode &nd = S.nodes[ref];
-			const bool me = (live >> lane_id()) & 1ull;
-			float tn0, tn1;
-			bool h0 = me && slab(nd.lo0x, nd.hi0x, nd.lo0y, nd.hi0y, nd.lo0z, nd.hi0z, oi, inv, dist, tn0);
-			bool h1 = me && slab(nd.lo1x, nd.hi1x, nd.lo1y, nd.hi1y, nd.lo1z, nd.hi1z, oi, inv, dist, tn1);
-			if (COUNT)
-				C.n_nodes += popc64(live);
-			const u64 b0 = ballot(h0), b1 = ballot(h1);
-			if (b0 && b1) {
-				const uint32_t ax = nd.axis & 3u;
-				const bool pos = (dsgn >> ax) & 1u;
-				const bool lg = (nd.axis >> 2) & 1u;
-				const uint32_t nr = (pos != lg) ? nd.ref0 : nd.ref1;
-				const uint32_t fr = (pos != lg) ? nd.ref1 : nd.ref0;
-				if (lane_id() == 0)
-					C.pstk[sp] = fr;
-				sp++;
-				ref = nr;
-			} else if (b0) {
-				ref = nd.ref0;
-			} else if (b1) {
-				ref = nd.ref1;
-			} else {
-				if (sp == 0)
-					break;
-				ref = uni(C.pstk[--sp]);
-			}
-		}
-	}
-}
-
-/* ------------------------------------------------------------------------ */
-/* direct lighting (render.c:170-229) for the shade points in `tab`:        */
-/* returns, in the owner lane k, L_k = sum over its light samples of        */
-/* (diffuse + specular) before the SP weight is applied.                    */
-/* ------------------------------------------------------------------------ */
-template <bool COUNT>
-__device__ f3 direct_light(Ctx &C, const float *tab, uint32_t *off, uint32_t nl_mine)
-{
-	const DParams &P = C.P;
-	f3 L = mk3(0.f, 0.f, 0.f);
-	uint32_t total;
-	uint32_t ex = wave_excl_scan(nl_mine, &total);
-	if (total == 0)
-		return L;
-	off[lane_id()] = ex;
-	if (lane_id() == 0)
-		off[WAVE] = total;
 	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
 	__builtin_amdgcn_wave_barrier();
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-	C.n_shadow += total;
-	for (uint32_t base = 0; base < total; base += WAVE) {
-		const uint32_t idx = base + lane_id();
-		const bool act = idx < total;
-		/* owner SP: largest k with off[k] <= idx */
-		uint32_t k = 0;
-		if (act) {
-			uint32_t lo = 0, hi = WAVE; /* off[lo] <= idx < off[hi] */
-			while (hi - lo > 1) {
-				uint32_t mid = (lo + hi) >> 1;
-				if (off[mid] <= idx)
-					lo = mid;
-				else
-					hi = mid;
-			}
-			k = lo;
-		}
-		f3 contrib = mk3(0.f, 0.f, 0.f);
-		const SP s = sp_load(tab, k);
-		uint32_t j = idx - off[k];
-		/* (emitter, light) of this sample, emitters in scene order, skipping the hit object */
-		uint32_t e = 0;
-		for (; e < C.S.num_emitters; e++) {
-			const DEmitter &E = C.S.emitters[e];
-			if (E.obj == s.obj)
-				continue;
-			if (j < E.num_lights)
-				break;
-			j -= E.num_lights;
-		}
-		if (e >= C.S.num_emitters)
-			e = 0;
-		const DEmitter &E = C.S.emitters[e];
-		float u1, u2;
-		draw(P, key_of(s.key_lo, s.key_hi), e, j, u1, u2);
-		const f3 lp = light_point(E, s.p, u1, u2);
-		const f3 dv = sub3(lp, s.p);
-		const float ldist = mag3(dv);
-		const f3 ldir = mul3s(dv, 1.f / ldist);
-		const float a = dot3(ldir, s.n);
-		f3 li = ld3(E.li);
-		bool blocked;
-		shadow_packet<COUNT>(C, act, s.p, ldir, ldist, E.obj, li, blocked);
-		if (act && !blocked) {
-			if (P.attenuation == RTX_ATT_LIN)
-				li = mul3s(li, 1.f / (P.att_offset + ldist));
-			else if (P.attenuation == RTX_ATT_SQR)
-				li = mul3s(li, 1.f / (P.att_offset + magsqr3(dv)));
-			const DMaterial &m = C.S.mats[s.mat];
-			f3 diff = mul3s(mul3v(s.tex, li), fmaxf(0.f, a));
-			float sm;
-			if (P.reflection == RTX_BLINN) {
-				f3 h = norm3(add3(mul3s(ldir, -1.f), s.d));
-				sm = -dot3(s.n, h);
-			} else {
-				f3 r = sub3(mul3s(s.n, 2.f * a), ldir);
-				sm = -dot3(r, s.d);
-			}
-			f3 spec = mul3s(mul3v(ld3(m.ks), li), fmaxf(0.f, powf(sm, m.shininess)));
-			contrib = add3(diff, spec);
-		}
-		/* segmented reduction: lanes are ordered by k */
-		const uint32_t last = min(total - base, (uint32_t)WAVE) - 1;
-		const uint32_t k0 = readlane(k, 0), k1 = readlane(k, last);
-		for (uint32_t kk = k0; kk <= k1; kk++) {
-			const bool in = act && k == kk;
-			if (!ballot(in))
-				continue;
-			float sx = wave_sum(in ? contrib.x : 0.f);
-			float sy = wave_sum(in ? contrib.y : 0.f);
-			float sz = wave_sum(in ? contrib.z : 0.f);
-			if (lane_id() == kk) {
-				L.x += sx;
-				L.y += sy;
-				L.z += sz;
-			}
-		}
-	}
-	return L;
 }
 
-/* add c (per lane) into the accumulator of pixel slot `slot` (owned by lane slot), fixed order */
+/* add c (per lane) into the accumulator of pixel slot `slot` (owned by lane `slot`), fixed order */
 __device__ __forceinline__ void route_add(f3 &acc, bool valid, uint32_t slot, f3 c)
 {
 	u64 m = ballot(valid);
@@ -526,11 +134,147 @@ __device__ __forceinline__ void route_add(f3 &acc, bool valid, uint32_t slot, f3
 	}
 }
 
-__device__ __forceinline__ void lds_sync()
+__device__ __forceinline__ uint64_t key_of(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+
+__device__ __forceinline__ void draw(const DParams &P, uint64_t key, uint32_t stream, uint32_t idx, float &u1, float &u2)
 {
-	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-	__builtin_amdgcn_wave_barrier();
-	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+	if (P.rng == RTX_RNG_CONST) {
+		u1 = 0.5f;
+		u2 = 0.5f;
+	} else {
+		rtx_draw2(key, stream, idx, &u1, &u2);
+	}
+}
+
+__device__ __forceinline__ float att_factor(const DParams &P, float dist)
+{
+	if (P.attenuation == RTX_ATT_LIN)
+		return 1.f / (P.att_offset + dist);
+	if (P.attenuation == RTX_ATT_SQR) {
+		float q = P.att_offset + dist;
+		return 1.f / (q * q);
+	}
+	return 1.f;
+}
+
+/* lights a shade point on object `obj` samples: num_lights summed over emitters != obj (render.c:172-174) */
+__device__ __forceinline__ uint32_t lights_for(const DScene &S, uint32_t total, uint32_t obj)
+{
+	uint32_t n = total;
+	for (uint32_t e = 0; e < S.num_emitters; e++)
+		if (S.emitters[e].obj == obj)
+			n -= S.emitters[e].num_lights;
+	return n;
+}
+
+/* ------------------------------------------------------------------------ */
+/* closest hit: inside-object shortcut, planes, then BVH (render.c:118-147)  */
+/* per-lane traversal, stack in LDS laid out [entry][lane]                  */
+/* ------------------------------------------------------------------------ */
+struct TraceCount {
+	uint32_t nodes, tris, sph, pln;
+};
+
+template <bool COUNT>
+__device__ void trace_closest(const DScene &S, uint32_t *stk, bool act, f3 o, f3 d, uint32_t inside, float &t_out,
+			      uint32_t &hid_out, TraceCount &tc)
+{
+	float tbest = FLT_MAX;
+	uint32_t hid = RTX_NONE;
+	if (act && isnan3(d)) /* TIR / degenerate directions hit nothing */
+		act = false;
+	if (act && inside != RTX_NONE) {
+		float t;
+		bool h;
+		if (inside & RTX_PLANE_BIT) {
+			const DPlane &pl = S.planes[inside & ~RTX_PLANE_BIT];
+			h = hit_plane(ld3(pl.n), pl.d, o, d, pl.eps, t);
+		} else {
+			const DPrim &pr = S.prims[inside];
+			if ((__float_as_uint(pr.c[3]) >> 24) == RTX_SPHERE)
+				h = hit_sphere(mk3(pr.a[0], pr.a[1], pr.a[2]), pr.b[0], o, d, pr.a[3], t);
+			else
+				h = hit_triangle(mk3(pr.a[0], pr.a[1], pr.a[2]), mk3(pr.b[0], pr.b[1], pr.b[2]),
+						 mk3(pr.c[0], pr.c[1], pr.c[2]), o, d, pr.a[3], t);
+		}
+		if (h) {
+			tbest = t;
+			hid = inside;
+			act = false;
+		}
+	}
+	if (act) {
+		for (uint32_t i = 0; i < S.num_planes; i++) {
+			const DPlane &pl = S.planes[i];
+			float t;
+			if (COUNT)
+				tc.pln++;
+			if (hit_plane(ld3(pl.n), pl.d, o, d, pl.eps, t) && t < tbest) {
+				tbest = t;
+				hid = RTX_PLANE_BIT | i;
+			}
+		}
+	}
+	if (act && S.root_ref != RTX_EMPTY_REF) {
+		const f3 inv = safe_inv(d);
+		const f3 oi = mul3v(o, inv);
+		uint32_t ref = S.root_ref;
+		uint32_t sp = 0;
+		stk += lane_id();
+		for (;;) {
+			if (ref & RTX_LEAF_BIT) {
+				const uint32_t first = (ref >> 4) & 0x7FFFFFFu, cnt = (ref & 15u) + 1;
+				for (uint32_t k = 0; k < cnt; k++) {
+					const float4 *pr = (const float4 *)(S.prims + first + k);
+					const float4 a = pr[0], b = pr[1], c = pr[2];
+					float t;
+					bool h;
+					if ((__float_as_uint(c.w) >> 24) == RTX_SPHERE) {
+						if (COUNT)
+							tc.sph++;
+						h = hit_sphere(mk3(a.x, a.y, a.z), b.x, o, d, a.w, t);
+					} else {
+						if (COUNT)
+							tc.tris++;
+						h = hit_triangle(mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z), mk3(c.x, c.y, c.z), o, d,
+								 a.w, t);
+					}
+					if (h && t < tbest) {
+						tbest = t;
+						hid = first + k;
+					}
+				}
+				if (sp == 0)
+					break;
+				ref = stk[--sp * WAVE];
+			} else {
+				const float4 *nd = (const float4 *)(S.nodes + ref);
+				const float4 n0 = nd[0], n1 = nd[1], n2 = nd[2];
+				const uint4 n3 = *(const uint4 *)(nd + 3);
+				if (COUNT)
+					tc.nodes++;
+				float tn0, tn1;
+				const bool h0 = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, oi, inv, tbest, tn0) && tn0 < tbest;
+				const bool h1 = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, oi, inv, tbest, tn1) && tn1 < tbest;
+				if (h0 && h1) {
+					/* nearer child first; tie -> right first (accel.c:341-345) */
+					const bool l_first = tn0 < tn1;
+					stk[sp++ * WAVE] = l_first ? n3.y : n3.x;
+					ref = l_first ? n3.x : n3.y;
+				} else if (h0) {
+					ref = n3.x;
+				} else if (h1) {
+					ref = n3.y;
+				} else {
+					if (sp == 0)
+						break;
+					ref = stk[--sp * WAVE];
+				}
+			}
+		}
+	}
+	t_out = tbest;
+	hid_out = hid;
 }
 
 struct HitInfo {
@@ -541,14 +285,14 @@ struct HitInfo {
 	float eps;
 };
 
-/* hit record of hid for ray (o,d) at t: point, normal (object.c sphere 254-265, triangle 356-365, plane 473-488) */
+/* hit record of hid for ray (o,d) at t (object.c sphere 254-265, triangle 356-365, plane 473-488) */
 __device__ __forceinline__ HitInfo hit_info(const DScene &S, uint32_t hid, f3 o, f3 d, float t)
 {
 	HitInfo h;
 	h.p = add3(mul3s(d, t), o);
 	if (hid & RTX_PLANE_BIT) {
 		const DPlane &pl = S.planes[hid & ~RTX_PLANE_BIT];
-		f3 n = ld3(pl.n);
+		const f3 n = ld3(pl.n);
 		h.n = signbit(dot3(n, d)) ? n : mul3s(n, -1.f);
 		h.obj = pl.obj;
 		h.mat = pl.mat;
@@ -556,12 +300,10 @@ __device__ __forceinline__ HitInfo hit_info(const DScene &S, uint32_t hid, f3 o,
 	} else {
 		const DPrim &pr = S.prims[hid];
 		const uint32_t meta = __float_as_uint(pr.c[3]);
-		if ((meta >> 24) == RTX_SPHERE) {
-			f3 c = mk3(pr.a[0], pr.a[1], pr.a[2]);
-			h.n = mul3s(sub3(add3(mul3s(d, t), o), c), 1.f / pr.b[0]);
-		} else {
+		if ((meta >> 24) == RTX_SPHERE)
+			h.n = mul3s(sub3(add3(mul3s(d, t), o), mk3(pr.a[0], pr.a[1], pr.a[2])), 1.f / pr.b[0]);
+		else
 			h.n = mk3(pr.d[0], pr.d[1], pr.d[2]);
-		}
 		h.obj = __float_as_uint(pr.b[3]);
 		h.mat = meta & 0xFFFFFFu;
 		h.eps = pr.a[3];
@@ -572,137 +314,194 @@ __device__ __forceinline__ HitInfo hit_info(const DScene &S, uint32_t hid, f3 o,
 }
 
 /* ------------------------------------------------------------------------ */
-/* GI for the shade points of tab_a with ngi > 0 (render.c:238-288)         */
+/* shade points                                                             */
+/*  - GI parents live in an LDS table inside k_trace (SPW floats each)      */
+/*  - every shade point with lights is emitted as a 96-byte record          */
+/*    (6 x float4) for k_shadow:                                            */
+/*      q0 = P, W.x   q1 = n, W.y   q2 = d, W.z   q3 = tex, mat             */
+/*      q4 = obj, key_lo, key_hi, nl   q5 = slot, -, -, -                   */
 /* ------------------------------------------------------------------------ */
-template <bool COUNT>
-__device__ void gi_batch(Ctx &C, uint32_t ngi_mine, f3 &acc, uint32_t &lane_nodes, uint32_t &lane_tris,
-			 uint32_t &lane_sph, uint32_t &lane_pln)
+#define SPW 16
+
+struct GiParent {
+	f3 p;
+	float eps;
+	f3 n;
+	float delta;
+	f3 w;
+	uint32_t slot;
+	uint32_t key_lo, key_hi, ngi, pad;
+};
+
+__device__ __forceinline__ void gp_store(float *tab, uint32_t k, const GiParent &g)
 {
-	const DParams &P = C.P;
+	float4 *q = (float4 *)(tab + k * SPW);
+	q[0] = make_float4(g.p.x, g.p.y, g.p.z, g.eps);
+	q[1] = make_float4(g.n.x, g.n.y, g.n.z, g.delta);
+	q[2] = make_float4(g.w.x, g.w.y, g.w.z, __uint_as_float(g.slot));
+	q[3] = make_float4(__uint_as_float(g.key_lo), __uint_as_float(g.key_hi), __uint_as_float(g.ngi), 0.f);
+}
+
+__device__ __forceinline__ GiParent gp_load(const float *tab, uint32_t k)
+{
+	const float4 *q = (const float4 *)(tab + k * SPW);
+	const float4 a = q[0], b = q[1], c = q[2], e = q[3];
+	GiParent g;
+	g.p = mk3(a.x, a.y, a.z);
+	g.eps = a.w;
+	g.n = mk3(b.x, b.y, b.z);
+	g.delta = b.w;
+	g.w = mk3(c.x, c.y, c.z);
+	g.slot = __float_as_uint(c.w);
+	g.key_lo = __float_as_uint(e.x);
+	g.key_hi = __float_as_uint(e.y);
+	g.ngi = __float_as_uint(e.z);
+	return g;
+}
+
+struct ShadePt {
+	f3 p, n, d, w, tex;
+	uint32_t mat, obj, key_lo, key_hi, nl, slot;
+};
+
+__device__ __forceinline__ void spr_store(float4 *rec, const ShadePt &s)
+{
+	rec[0] = make_float4(s.p.x, s.p.y, s.p.z, s.w.x);
+	rec[1] = make_float4(s.n.x, s.n.y, s.n.z, s.w.y);
+	rec[2] = make_float4(s.d.x, s.d.y, s.d.z, s.w.z);
+	rec[3] = make_float4(s.tex.x, s.tex.y, s.tex.z, __uint_as_float(s.mat));
+	rec[4] = make_float4(__uint_as_float(s.obj), __uint_as_float(s.key_lo), __uint_as_float(s.key_hi),
+			     __uint_as_float(s.nl));
+	rec[5] = make_float4(__uint_as_float(s.slot), 0.f, 0.f, 0.f);
+}
+
+#define SPREC 6 /* float4 per shade-point record */
+
+/* ------------------------------------------------------------------------ */
+/* k_trace: per 8x8 tile, every cast_ray() of the tile's ray trees          */
+/* ------------------------------------------------------------------------ */
+struct TraceOut {
+	float4 *staging; /* this wave's staging region */
+	uint32_t cap;    /* records */
+	uint32_t n;      /* records written for the current tile (uniform) */
+	bool overflow;
+};
+
+/* append the lanes' shade points (has) to the staging region, order = lane order */
+__device__ __forceinline__ void emit_sp(TraceOut &T, bool has, const ShadePt &s)
+{
+	const u64 m = ballot(has);
+	if (!m)
+		return;
+	const uint32_t pos = T.n + mbcnt(m);
+	if (has && pos < T.cap)
+		spr_store(T.staging + (size_t)pos * SPREC, s);
+	T.n += popc64(m);
+	if (T.n > T.cap)
+		T.overflow = true;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void gi_batch(const DScene &S, const DParams &P, uint32_t total_lights, uint32_t *stk,
+					 float *gp_tab, uint32_t *off, uint32_t ngi_mine, f3 &acc, TraceOut &T,
+					 TraceCount &tc, u64 &n_closest)
+{
 	uint32_t total;
-	uint32_t ex = wave_excl_scan(ngi_mine, &total);
+	const uint32_t ex = wave_excl_scan(ngi_mine, &total);
 	if (total == 0)
 		return;
 	lds_sync();
-	C.off_a[lane_id()] = ex;
+	off[lane_id()] = ex;
 	if (lane_id() == 0)
-		C.off_a[WAVE] = total;
+		off[WAVE] = total;
 	lds_sync();
 	for (uint32_t base = 0; base < total; base += WAVE) {
 		const uint32_t idx = base + lane_id();
 		const bool act = idx < total;
-		uint32_t h = 0;
-		if (act) {
-			uint32_t lo = 0, hi = WAVE;
-			while (hi - lo > 1) {
-				uint32_t mid = (lo + hi) >> 1;
-				if (C.off_a[mid] <= idx)
-					lo = mid;
-				else
-					hi = mid;
-			}
-			h = lo;
-		}
-		const SP par = sp_load(C.lds_sp_a, h);
-		const uint32_t s = idx - C.off_a[h];
+		const uint32_t h = act ? owner_of(off, idx) : 0u;
+		const GiParent par = gp_load(gp_tab, h);
+		const uint32_t s = idx - off[h];
 		const uint64_t pkey = key_of(par.key_lo, par.key_hi);
 		float u1, u2;
 		draw(P, pkey, RTX_STREAM_GI, s, u1, u2);
+		/* render.c:270-286: uniform hemisphere sample about n, weight delta * (n . dir) */
 		const f3 dir = gi_direction(par.n, par.eps, u1, u2);
 		const f3 kr = mul3s(par.w, par.delta * dot3(par.n, dir));
 		const uint64_t ckey = rtx_key_child(pkey, RTX_CHILD_GI0 + s);
-		/* child cast_ray(.., 0 bounces, no inside object) */
 		float t;
 		uint32_t hid;
-		lds_sync();
-		trace_closest<COUNT>(C, act, par.p, dir, RTX_NONE, t, hid, lane_nodes, lane_tris, lane_sph, lane_pln);
-		C.n_closest += popc64(ballot(act));
+		trace_closest<COUNT>(S, stk, act, par.p, dir, RTX_NONE, t, hid, tc);
+		n_closest += popc64(ballot(act));
 		const bool hit = act && hid != RTX_NONE;
-		SP cs = SP();
+		ShadePt cs = ShadePt();
 		f3 cc = mk3(0.f, 0.f, 0.f);
-		uint32_t nl = 0;
+		bool has = false;
 		if (hit) {
-			HitInfo hi = hit_info(C.S, hid, par.p, dir, t);
-			const DMaterial &m = C.S.mats[hi.mat];
+			/* child cast_ray(..., 0 bounces): ke + direct light only (path mode has no ambient term) */
+			const HitInfo hi = hit_info(S, hid, par.p, dir, t);
+			const DMaterial &m = S.mats[hi.mat];
 			const f3 w = mul3s(kr, att_factor(P, t));
-			cc = mul3v(w, ld3(m.ke)); /* path mode: no ambient term */
-			nl = hi.outside ? lights_for(C, hi.obj) : 0u;
+			cc = mul3v(w, ld3(m.ke));
+			cs.nl = hi.outside ? lights_for(S, total_lights, hi.obj) : 0u;
+			has = cs.nl != 0;
 			cs.p = hi.p;
-			cs.eps = hi.eps;
 			cs.n = hi.n;
-			cs.obj = hi.obj;
 			cs.d = dir;
-			cs.mat = hi.mat;
 			cs.w = w;
+			cs.mat = hi.mat;
+			cs.obj = hi.obj;
 			cs.slot = par.slot;
-			cs.tex = nl ? texture_color(m, hi.p, P.u32conv) : mk3(0.f, 0.f, 0.f);
+			cs.tex = has ? texture_color(m, hi.p, P.u32conv) : mk3(0.f, 0.f, 0.f);
 			cs.key_lo = (uint32_t)ckey;
 			cs.key_hi = (uint32_t)(ckey >> 32);
-			cs.delta = 0.f;
-			cs.ngi = 0;
-			cs.nl = nl;
 		}
 		route_add(acc, hit, par.slot, cc);
-		lds_sync();
-		if (hit)
-			sp_store(C.lds_sp_b, lane_id(), cs);
-		lds_sync();
-		f3 L = direct_light<COUNT>(C, C.lds_sp_b, C.off_b, nl);
-		route_add(acc, nl != 0, cs.slot, mul3v(cs.w, L));
+		emit_sp(T, has, cs);
 		lds_sync();
 	}
 }
 
-/* ------------------------------------------------------------------------ */
-/* the persistent render kernel                                             */
-/* ------------------------------------------------------------------------ */
 template <bool COUNT>
-__global__ __launch_bounds__(WAVE) void k_render(DScene S, DFrame F, DParams P, float *__restrict__ rgb,
-						 float *__restrict__ zbuf, DTask *__restrict__ tasks, uint32_t task_cap,
-						 unsigned long long *__restrict__ ctr)
+__global__ __launch_bounds__(WAVE) void k_trace(DScene S, DFrame F, DParams P, float *__restrict__ rgb,
+						float *__restrict__ zbuf, DTask *__restrict__ tasks, uint32_t task_cap,
+						float4 *__restrict__ staging, uint32_t staging_cap,
+						float4 *__restrict__ sp_out, uint32_t sp_cap, uint2 *__restrict__ tile_rec,
+						uint32_t tile_begin, uint32_t tile_end, unsigned long long *__restrict__ ctr)
 {
 	extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-	Ctx C;
-	C.S = S;
-	C.F = F;
-	C.P = P;
-	{
-		unsigned char *p = lds_raw;
-		C.lds_sp_a = (float *)p;
-		p += WAVE * SPW * 4;
-		C.off_a = (uint32_t *)p;
-		p += 80 * 4;
-		C.off_b = (uint32_t *)p;
-		p += 80 * 4;
-		C.pstk = (uint32_t *)p;
-		p += ((S.stack_size + 3) & ~3u) * 4;
-		C.stk = (uint32_t *)p;
-		C.lds_sp_b = (float *)p;
-	}
-	C.total_lights = 0;
+	float *gp_tab = (float *)lds_raw;
+	uint32_t *off = (uint32_t *)(lds_raw + WAVE * SPW * 4);
+	uint32_t *stk = (uint32_t *)(lds_raw + WAVE * SPW * 4 + 80 * 4);
+
+	uint32_t total_lights = 0;
 	for (uint32_t e = 0; e < S.num_emitters; e++)
-		C.total_lights += S.emitters[e].num_lights;
-	C.n_closest = C.n_shadow = C.n_nodes = C.n_tris = C.n_spheres = C.n_planes = 0;
-	uint32_t lane_nodes = 0, lane_tris = 0, lane_sph = 0, lane_pln = 0;
+		total_lights += S.emitters[e].num_lights;
+	u64 n_closest = 0;
+	TraceCount tc = { 0, 0, 0, 0 };
 	DTask *my_tasks = tasks + (size_t)blockIdx.x * task_cap;
-	uint32_t overflow = 0;
+	TraceOut T;
+	T.staging = staging + (size_t)blockIdx.x * staging_cap * SPREC;
+	T.cap = staging_cap;
+	bool overflow = false, sp_overflow = false;
 
 	for (;;) {
 		uint32_t tile = 0;
 		if (lane_id() == 0)
 			tile = (uint32_t)atomicAdd(&ctr[RTX_C_TILE], 1ull);
-		tile = uni(__shfl(tile, 0, WAVE));
-		if (tile >= P.ntiles)
+		tile = uni(__shfl(tile, 0, WAVE)) + tile_begin;
+		if (tile >= tile_end)
 			break;
 		const uint32_t g = P.tile_offset + tile * P.tile_stride;
 		const uint32_t tx = g % P.tiles_x, ty = g / P.tiles_x;
 		const uint32_t px = tx * RTX_TILE_W + (lane_id() & 7), py = ty * RTX_TILE_H + (lane_id() >> 3);
 		const bool valid_px = px < F.width && py < F.height;
+		T.n = 0;
+		T.overflow = false;
 
 		f3 acc = mk3(0.f, 0.f, 0.f);
 		float zval = 0.f;
 
-		/* primary rays (render.c:353-363): P = corner + row*vy, then += vx (col+1) times */
+		/* primary ray (render.c:353-363): P = corner + row*vy, then += vx (col+1) times, sequentially */
 		bool act = valid_px;
 		f3 o = ld3(F.origin), d = mk3(0.f, 0.f, 1.f), kr = mk3(1.f, 1.f, 1.f);
 		uint32_t rb = P.max_bounces, inside = RTX_NONE, slot = lane_id();
@@ -710,29 +509,27 @@ __global__ __launch_bounds__(WAVE) void k_render(DScene S, DFrame F, DParams P, 
 		bool primary = true;
 		if (act) {
 			f3 pp = add3(mul3s(ld3(F.step_y), (float)py), ld3(F.corner));
+			const f3 sx = ld3(F.step_x);
 			for (uint32_t c = 0; c <= px; c++)
-				pp = add3(pp, ld3(F.step_x));
+				pp = add3(pp, sx);
 			d = norm3(sub3(pp, o));
 			key = rtx_key_pixel(P.seed, py * F.width + px);
 		}
 		uint32_t top = 0;
 		for (;;) {
-			/* ---- trace the batch ---- */
 			float t;
 			uint32_t hid;
 			lds_sync();
-			trace_closest<COUNT>(C, act, o, d, inside, t, hid, lane_nodes, lane_tris, lane_sph, lane_pln);
-			C.n_closest += popc64(ballot(act));
+			trace_closest<COUNT>(S, stk, act, o, d, inside, t, hid, tc);
+			n_closest += popc64(ballot(act));
 			const bool hit = act && hid != RTX_NONE;
-			/* ---- shade setup ---- */
-			SP sp = SP();
+			ShadePt sp = ShadePt();
+			GiParent gp = GiParent();
 			f3 cc = mk3(0.f, 0.f, 0.f);
-			uint32_t nl = 0, ngi = 0;
-			bool want_refl = false, want_refr = false;
-			f3 rkr = mk3(0.f, 0.f, 0.f), rkt = mk3(0.f, 0.f, 0.f), rdir = mk3(0.f, 0.f, 0.f),
-			   tdir = mk3(0.f, 0.f, 0.f);
+			bool has = false, want_refl = false, want_refr = false;
+			f3 rkr = mk3(0.f, 0.f, 0.f), rkt = rkr, rdir = rkr, tdir = rkr;
 			if (hit) {
-				HitInfo h = hit_info(S, hid, o, d, t);
+				const HitInfo h = hit_info(S, hid, o, d, t);
 				const DMaterial &m = S.mats[h.mat];
 				const f3 w = mul3s(kr, att_factor(P, t));
 				f3 local = ld3(m.ke);
@@ -740,16 +537,16 @@ __global__ __launch_bounds__(WAVE) void k_render(DScene S, DFrame F, DParams P, 
 					local = add3(local, mul3v(ld3(m.ka), ld3(S.ambient)));
 				cc = mul3v(w, local);
 				if (primary)
-					zval = rb ? t : 0.f;
+					zval = rb ? t : 0.f; /* render.c:304-305, 342 */
 				if (rb) {
-					if (inside != hid && (m.flags & RTX_MF_REFLECTIVE)) {
+					if (inside != hid && (m.flags & RTX_MF_REFLECTIVE)) { /* render.c:308-317 */
 						rkr = mul3v(kr, ld3(m.kr));
 						if (P.min_intensity_sqr < magsqr3(rkr)) {
 							want_refl = true;
 							rdir = sub3(d, mul3s(h.n, 2.f * h.b));
 						}
 					}
-					if (m.flags & RTX_MF_TRANSPARENT) {
+					if (m.flags & RTX_MF_TRANSPARENT) { /* render.c:320-340 */
 						rkt = mul3v(kr, ld3(m.kt));
 						if (P.min_intensity_sqr < magsqr3(rkt)) {
 							want_refr = true;
@@ -757,58 +554,62 @@ __global__ __launch_bounds__(WAVE) void k_render(DScene S, DFrame F, DParams P, 
 						}
 					}
 				}
-				nl = h.outside ? lights_for(C, h.obj) : 0u;
-				ngi = (P.gi == RTX_GI_PATH && rb && h.outside) ? (rb == P.max_bounces ? P.samples : 1u) : 0u;
+				sp.nl = h.outside ? lights_for(S, total_lights, h.obj) : 0u;
+				has = sp.nl != 0;
 				sp.p = h.p;
-				sp.eps = h.eps;
 				sp.n = h.n;
-				sp.obj = h.obj;
 				sp.d = d;
-				sp.mat = h.mat;
 				sp.w = w;
+				sp.mat = h.mat;
+				sp.obj = h.obj;
 				sp.slot = slot;
-				sp.tex = nl ? texture_color(m, h.p, P.u32conv) : mk3(0.f, 0.f, 0.f);
+				sp.tex = has ? texture_color(m, h.p, P.u32conv) : mk3(0.f, 0.f, 0.f);
 				sp.key_lo = (uint32_t)key;
 				sp.key_hi = (uint32_t)(key >> 32);
-				sp.delta = (rb == P.max_bounces) ? 1.f / (float)P.samples : 1.f;
-				sp.ngi = ngi;
-				sp.nl = nl;
+				gp.p = h.p;
+				gp.eps = h.eps;
+				gp.n = h.n;
+				gp.w = w;
+				gp.slot = slot;
+				gp.key_lo = sp.key_lo;
+				gp.key_hi = sp.key_hi;
+				gp.ngi = (P.gi == RTX_GI_PATH && rb && h.outside) ? (rb == P.max_bounces ? P.samples : 1u) : 0u;
+				gp.delta = (rb == P.max_bounces) ? 1.f / (float)P.samples : 1.f;
 			}
 			route_add(acc, hit, slot, cc);
-			if (primary && act)
-				zval = hit ? zval : 0.f;
-			/* ---- push reflection / refraction children (compacted) ---- */
+			emit_sp(T, has, sp);
+			/* push reflection / refraction children (compacted, LIFO) */
 			{
 				const u64 mr = ballot(want_refl), mt = ballot(want_refr);
 				const uint32_t nr = popc64(mr), nt = popc64(mt);
 				if (nr + nt) {
 					if (top + nr + nt > task_cap) {
-						overflow = 1;
+						overflow = true;
 					} else {
-						uint32_t pos_r = top + mbcnt(mr), pos_t = top + nr + mbcnt(mt);
-						const uint64_t kref = rtx_key_child(key, RTX_CHILD_REFLECT);
-						const uint64_t krft = rtx_key_child(key, RTX_CHILD_REFRACT);
+						const uint32_t pos_r = top + mbcnt(mr), pos_t = top + nr + mbcnt(mt);
 						if (want_refl) {
+							const uint64_t k2 = rtx_key_child(key, RTX_CHILD_REFLECT);
 							DTask tk;
 							tk.o[0] = sp.p.x; tk.o[1] = sp.p.y; tk.o[2] = sp.p.z;
 							tk.d[0] = rdir.x; tk.d[1] = rdir.y; tk.d[2] = rdir.z;
 							tk.kr[0] = rkr.x; tk.kr[1] = rkr.y; tk.kr[2] = rkr.z;
 							tk.rb = rb - 1;
 							tk.inside = RTX_NONE;
-							tk.key_lo = (uint32_t)kref;
-							tk.key_hi = (uint32_t)(kref >> 32);
+							tk.key_lo = (uint32_t)k2;
+							tk.key_hi = (uint32_t)(k2 >> 32);
 							tk.slot = slot;
 							my_tasks[pos_r] = tk;
 						}
 						if (want_refr) {
+							const uint64_t k2 = rtx_key_child(key, RTX_CHILD_REFRACT);
 							DTask tk;
 							tk.o[0] = sp.p.x; tk.o[1] = sp.p.y; tk.o[2] = sp.p.z;
 							tk.d[0] = tdir.x; tk.d[1] = tdir.y; tk.d[2] = tdir.z;
 							tk.kr[0] = rkt.x; tk.kr[1] = rkt.y; tk.kr[2] = rkt.z;
 							tk.rb = rb - 1;
 							tk.inside = hid;
-							tk.key_lo = (uint32_t)krft;
-							tk.key_hi = (uint32_t)(krft >> 32);
+							tk.key_lo = (uint32_t)k2;
+							tk.key_hi = (uint32_t)(k2 >> 32);
 							tk.slot = slot;
 							my_tasks[pos_t] = tk;
 						}
@@ -816,21 +617,17 @@ __global__ __launch_bounds__(WAVE) void k_render(DScene S, DFrame F, DParams P, 
 					}
 				}
 			}
-			/* ---- direct light of the batch's shade points ---- */
-			lds_sync();
-			if (hit)
-				sp_store(C.lds_sp_a, lane_id(), sp);
-			lds_sync();
-			{
-				f3 L = direct_light<COUNT>(C, C.lds_sp_a, C.off_b, nl);
-				route_add(acc, nl != 0, slot, mul3v(sp.w, L));
+			/* path-traced GI children of this batch's hits (render.c:238-288) */
+			if (P.gi == RTX_GI_PATH) {
+				lds_sync();
+				if (hit)
+					gp_store(gp_tab, lane_id(), gp);
+				gi_batch<COUNT>(S, P, total_lights, stk, gp_tab, off, hit ? gp.ngi : 0u, acc, T, tc,
+						n_closest);
 			}
-			/* ---- path-traced GI children ---- */
-			if (P.gi == RTX_GI_PATH)
-				gi_batch<COUNT>(C, ngi, acc, lane_nodes, lane_tris, lane_sph, lane_pln);
-			/* ---- next batch: pop up to 64 tasks (LIFO) ---- */
 			if (top == 0)
 				break;
+			/* next batch: pop up to 64 tasks */
 			__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
 			const uint32_t n = min(top, (uint32_t)WAVE);
 			top -= n;
@@ -848,7 +645,7 @@ __global__ __launch_bounds__(WAVE) void k_render(DScene S, DFrame F, DParams P, 
 			}
 			__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
 		}
-		/* ---- write the tile ---- */
+		/* local terms + z of the tile; light terms are added by k_accum */
 		if (valid_px) {
 			const size_t pix = (size_t)py * F.width + px;
 			if (rgb) {
@@ -859,39 +656,315 @@ __global__ __launch_bounds__(WAVE) void k_render(DScene S, DFrame F, DParams P, 
 			if (zbuf)
 				zbuf[pix] = zval;
 		}
+		/* move the tile's shade points to the chunk's contiguous array */
+		uint32_t n = T.n;
+		uint32_t start = 0;
+		if (T.overflow) {
+			overflow = true;
+			n = 0;
+		}
+		if (lane_id() == 0)
+			start = n ? (uint32_t)atomicAdd(&ctr[RTX_C_SPCOUNT], (unsigned long long)n) : 0u;
+		start = uni(__shfl(start, 0, WAVE));
+		if ((uint64_t)start + n > sp_cap) {
+			sp_overflow = true;
+			n = 0;
+		}
+		__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+		for (uint32_t i = lane_id(); i < n * SPREC; i += WAVE)
+			sp_out[(size_t)start * SPREC + i] = T.staging[i];
+		if (lane_id() == 0)
+			tile_rec[tile - tile_begin] = make_uint2(start, n);
 	}
-	/* ---- counters ---- */
 	if (COUNT) {
-		u64 ln = lane_nodes, lt = lane_tris, ls = lane_sph, lp = lane_pln;
+		u64 a = tc.nodes, b = tc.tris, c = tc.sph, d2 = tc.pln;
 #pragma unroll
 		for (int o2 = 32; o2 > 0; o2 >>= 1) {
-			ln += __shfl_xor(ln, o2, WAVE);
-			lt += __shfl_xor(lt, o2, WAVE);
-			ls += __shfl_xor(ls, o2, WAVE);
-			lp += __shfl_xor(lp, o2, WAVE);
+			a += __shfl_xor(a, o2, WAVE);
+			b += __shfl_xor(b, o2, WAVE);
+			c += __shfl_xor(c, o2, WAVE);
+			d2 += __shfl_xor(d2, o2, WAVE);
 		}
-		C.n_nodes += ln;
-		C.n_tris += lt;
-		C.n_spheres += ls;
-		C.n_planes += lp;
+		if (lane_id() == 0) {
+			atomicAdd(&ctr[RTX_C_NODES], a);
+			atomicAdd(&ctr[RTX_C_TRIS], b);
+			atomicAdd(&ctr[RTX_C_SPHERES], c);
+			atomicAdd(&ctr[RTX_C_PLANES], d2);
+		}
 	}
 	if (lane_id() == 0) {
-		atomicAdd(&ctr[RTX_C_CLOSEST], C.n_closest);
-		atomicAdd(&ctr[RTX_C_SHADOW], C.n_shadow);
-		if (COUNT) {
-			atomicAdd(&ctr[RTX_C_NODES], C.n_nodes);
-			atomicAdd(&ctr[RTX_C_TRIS], C.n_tris);
-			atomicAdd(&ctr[RTX_C_SPHERES], C.n_spheres);
-			atomicAdd(&ctr[RTX_C_PLANES], C.n_planes);
-		}
+		atomicAdd(&ctr[RTX_C_CLOSEST], n_closest);
 		if (overflow)
 			atomicAdd(&ctr[RTX_C_OVERFLOW], 1ull);
+		if (sp_overflow)
+			atomicAdd(&ctr[RTX_C_SPOVERFLOW], 1ull);
 	}
 }
 
 /* ------------------------------------------------------------------------ */
-/* known-answer kernel (include/rtx_kat.h)                                  */
+/* k_shadow: direct lighting (render.c:170-229) of shade points.            */
+/* A wave takes `per_wave` consecutive shade points, flattens their         */
+/* (point, light sample) pairs and walks the BVH with 64 shadow rays at a   */
+/* time as a packet: node / primitive indices are wave-uniform (scalar      */
+/* loads), each lane tests its own ray, __ballot picks the children.        */
 /* ------------------------------------------------------------------------ */
+struct ShadowCount {
+	u64 nodes, tris, sph, pln;
+};
+
+template <bool COUNT>
+__device__ __forceinline__ void shadow_packet(const DNode *__restrict__ nodes, const DPrim *__restrict__ prims,
+					      const DMaterial *__restrict__ mats, const DPlane *__restrict__ planes,
+					      uint32_t num_planes, uint32_t root_ref, uint32_t *pstk, bool act, f3 o, f3 d,
+					      float dist, uint32_t emit_obj, f3 &li, bool &blocked, ShadowCount &sc)
+{
+	/* unbound_objects_is_light_blocked (object.c:183-197): planes first */
+	blocked = false;
+	if (act) {
+		for (uint32_t i = 0; i < num_planes; i++) {
+			const DPlane &pl = planes[i];
+			float t;
+			if (hit_plane(ld3(pl.n), pl.d, o, d, pl.eps, t) && t < dist) {
+				const DMaterial &m = mats[pl.mat];
+				if (m.flags & RTX_MF_TRANSPARENT) {
+					li = mul3v(li, ld3(m.kt));
+				} else {
+					blocked = true;
+					break;
+				}
+			}
+		}
+	}
+	if (COUNT)
+		sc.pln += (u64)popc64(ballot(act)) * num_planes;
+	u64 live = ballot(act && !blocked);
+	if (!live || root_ref == RTX_EMPTY_REF)
+		return;
+	const f3 inv = safe_inv(d);
+	const f3 oi = mul3v(o, inv);
+	/* near-first order from the first live ray's direction signs (any order is correct) */
+	const uint32_t lead = (uint32_t)__ffsll((long long)live) - 1;
+	const uint32_t dsgn = readlane(((d.x >= 0.f) ? 1u : 0u) | ((d.y >= 0.f) ? 2u : 0u) | ((d.z >= 0.f) ? 4u : 0u), lead);
+	uint32_t ref = root_ref;
+	uint32_t sp = 0;
+	for (;;) {
+		if (ref & RTX_LEAF_BIT) {
+			/* accel.c:362-373: skip the emitter, opaque -> blocked, transparent -> Li *= kt */
+			const uint32_t first = (ref >> 4) & 0x7FFFFFFu, cnt = (ref & 15u) + 1;
+			for (uint32_t k = 0; k < cnt; k++) {
+				/* the whole 64-byte record in one scalar load */
+				const v16u pr = *(const v16u *)(prims + first + k);
+				const uint32_t meta = pr[11], obj = pr[7];
+				const bool mine = lane_in(live) & (obj != emit_obj);
+				const f3 a = mk3(__uint_as_float(pr[0]), __uint_as_float(pr[1]), __uint_as_float(pr[2]));
+				float t = 0.f;
+				bool h;
+				if ((meta >> 24) == RTX_SPHERE) {
+					if (COUNT)
+						sc.sph += popc64(live);
+					h = hit_sphere(a, __uint_as_float(pr[4]), o, d, __uint_as_float(pr[3]), t);
+				} else {
+					if (COUNT)
+						sc.tris += popc64(live);
+					h = hit_triangle(a, mk3(__uint_as_float(pr[4]), __uint_as_float(pr[5]), __uint_as_float(pr[6])),
+							 mk3(__uint_as_float(pr[8]), __uint_as_float(pr[9]), __uint_as_float(pr[10])),
+							 o, d, __uint_as_float(pr[3]), t);
+				}
+				h = h & mine & (t < dist);
+				if (ballot(h)) {
+					const DMaterial &m = mats[meta & 0xFFFFFFu];
+					if (m.flags & RTX_MF_TRANSPARENT) {
+						const f3 kt = mk3(m.kt[0], m.kt[1], m.kt[2]);
+						if (h)
+							li = mul3v(li, kt);
+					} else {
+						blocked = blocked | h;
+					}
+				}
+			}
+			live = ballot(lane_in(live) & !blocked);
+			if (!live || sp == 0)
+				break;
+			ref = uni(pstk[--sp]);
+		} else {
+			/* both child boxes + refs in one scalar load */
+			const v16u nd = *(const v16u *)(nodes + ref);
+			const bool me = lane_in(live);
+			float tn0, tn1;
+			const bool h0 = slab(__uint_as_float(nd[0]), __uint_as_float(nd[1]), __uint_as_float(nd[2]),
+					     __uint_as_float(nd[3]), __uint_as_float(nd[4]), __uint_as_float(nd[5]), oi, inv, dist,
+					     tn0) & me;
+			const bool h1 = slab(__uint_as_float(nd[6]), __uint_as_float(nd[7]), __uint_as_float(nd[8]),
+					     __uint_as_float(nd[9]), __uint_as_float(nd[10]), __uint_as_float(nd[11]), oi, inv,
+					     dist, tn1) & me;
+			if (COUNT)
+				sc.nodes += popc64(live);
+			const u64 b0 = ballot(h0), b1 = ballot(h1);
+			const uint32_t r0 = nd[12], r1 = nd[13], axis = nd[14];
+			if (b0 && b1) {
+				const bool left_first = ((dsgn >> (axis & 3u)) & 1u) != ((axis >> 2) & 1u);
+				if (lane_id() == 0)
+					pstk[sp] = left_first ? r1 : r0;
+				sp++;
+				ref = left_first ? r0 : r1;
+			} else if (b0) {
+				ref = r0;
+			} else if (b1) {
+				ref = r1;
+			} else {
+				if (sp == 0)
+					break;
+				ref = uni(pstk[--sp]);
+			}
+		}
+	}
+}
+
+template <bool COUNT, int OCC>
+__global__ __launch_bounds__(WAVE, OCC) void k_shadow(DScene S, const DNode *__restrict__ nodes,
+						 const DPrim *__restrict__ prims, const DMaterial *__restrict__ mats,
+						 const DPlane *__restrict__ planes, const DEmitter *__restrict__ emitters,
+						 DParams P, const float4 *__restrict__ sp, uint32_t n_sp, uint32_t per_wave,
+						 uint32_t slot_b, float4 *__restrict__ contrib,
+						 unsigned long long *__restrict__ ctr)
+{
+	extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+	uint32_t *off = (uint32_t *)lds_raw;
+	uint32_t *pstk = off + 80;
+	const uint32_t j0 = blockIdx.x * per_wave;
+	if (j0 >= n_sp)
+		return;
+	const uint32_t cnt = min(per_wave, n_sp - j0);
+	const bool own = lane_id() < cnt;
+	const float4 *my = sp + (size_t)(j0 + (own ? lane_id() : 0)) * SPREC;
+	const uint32_t nl_mine = own ? __float_as_uint(my[4].w) : 0u;
+	/* each point's samples occupy whole lane slots of B lanes (B = power of two), so a point's
+	 * packet partial sums never depend on which other points share its wave: deterministic */
+	uint32_t total;
+	const uint32_t ex = wave_excl_scan((nl_mine + slot_b - 1) / slot_b, &total);
+	off[lane_id()] = ex;
+	if (lane_id() == 0)
+		off[WAVE] = total;
+	lds_sync();
+	f3 L = mk3(0.f, 0.f, 0.f);
+	ShadowCount sc = { 0, 0, 0, 0 };
+	u64 n_rays = 0;
+	const uint32_t slots_per_packet = WAVE / slot_b;
+	for (uint32_t base = 0; base < total; base += slots_per_packet) {
+		const uint32_t slot = base + lane_id() / slot_b;
+		const uint32_t k = slot < total ? owner_of(off, slot) : 0u;
+		const uint32_t idx = (slot - off[k]) * slot_b + lane_id() % slot_b;
+		const bool act = slot < total && idx < __shfl(nl_mine, k, WAVE);
+		n_rays += popc64(ballot(act));
+		const float4 *rec = sp + (size_t)(j0 + k) * SPREC;
+		const float4 q0 = rec[0], q4 = rec[4];
+		const f3 p = mk3(q0.x, q0.y, q0.z);
+		const uint32_t obj = __float_as_uint(q4.x);
+		uint32_t j = idx;
+		/* (emitter, light) of this sample: emitters in scene order, the hit object skipped */
+		uint32_t e = 0;
+		for (; e < S.num_emitters; e++) {
+			const uint32_t eo = emitters[e].obj, enl = emitters[e].num_lights;
+			if (eo == obj)
+				continue;
+			if (j < enl)
+				break;
+			j -= enl;
+		}
+		if (e >= S.num_emitters)
+			e = 0;
+		const DEmitter &E = emitters[e];
+		float u1, u2;
+		draw(P, key_of(__float_as_uint(q4.y), __float_as_uint(q4.z)), e, j, u1, u2);
+		const f3 lp = light_point(E, p, u1, u2);
+		const f3 dv = sub3(lp, p);
+		const float ldist = mag3(dv);
+		const float dsq = magsqr3(dv);
+		const f3 ldir = mul3s(dv, 1.f / ldist);
+		f3 li = ld3(E.li);
+		bool blocked;
+		shadow_packet<COUNT>(nodes, prims, mats, planes, S.num_planes, S.root_ref, pstk, act, p, ldir, ldist,
+				     E.obj, li, blocked, sc);
+		f3 contribution = mk3(0.f, 0.f, 0.f);
+		if (act && !blocked) {
+			/* shading terms re-read after the traversal to keep them out of its registers */
+			const float4 q1 = rec[1], q2 = rec[2], q3 = rec[3];
+			const f3 n = mk3(q1.x, q1.y, q1.z), dir = mk3(q2.x, q2.y, q2.z);
+			const float a = dot3(ldir, n);
+			if (P.attenuation == RTX_ATT_LIN)
+				li = mul3s(li, 1.f / (P.att_offset + ldist));
+			else if (P.attenuation == RTX_ATT_SQR)
+				li = mul3s(li, 1.f / (P.att_offset + dsq));
+			const DMaterial &m = mats[__float_as_uint(q3.w)];
+			const f3 diff = mul3s(mul3v(mk3(q3.x, q3.y, q3.z), li), fmaxf(0.f, a));
+			float sm;
+			if (P.reflection == RTX_BLINN) {
+				sm = -dot3(n, norm3(add3(mul3s(ldir, -1.f), dir)));
+			} else {
+				sm = -dot3(sub3(mul3s(n, 2.f * a), ldir), dir);
+			}
+			const f3 spec = mul3s(mul3v(ld3(m.ks), li), fmaxf(0.f, powf(sm, m.shininess)));
+			contribution = add3(diff, spec);
+		}
+		/* per-shade-point sums; lanes are ordered by k */
+		const uint32_t last_slot_lane = (min(total - base, slots_per_packet) - 1) * slot_b;
+		const uint32_t k0 = readlane(k, 0), k1 = readlane(k, last_slot_lane);
+		for (uint32_t kk = k0; kk <= k1; kk++) {
+			const bool in = act && k == kk;
+			if (!ballot(in))
+				continue;
+			const float sx = wave_sum(in ? contribution.x : 0.f);
+			const float sy = wave_sum(in ? contribution.y : 0.f);
+			const float sz = wave_sum(in ? contribution.z : 0.f);
+			if (lane_id() == kk)
+				L = add3(L, mk3(sx, sy, sz));
+		}
+	}
+	if (own) {
+		const float4 q0 = my[0], q1 = my[1], q2 = my[2], q5 = my[5];
+		const f3 w = mk3(q0.w, q1.w, q2.w);
+		const f3 c = mul3v(w, L);
+		contrib[j0 + lane_id()] = make_float4(c.x, c.y, c.z, q5.x);
+	}
+	if (lane_id() == 0) {
+		atomicAdd(&ctr[RTX_C_SHADOW], n_rays);
+		if (COUNT) {
+			atomicAdd(&ctr[RTX_C_SNODES], sc.nodes);
+			atomicAdd(&ctr[RTX_C_STRIS], sc.tris);
+			atomicAdd(&ctr[RTX_C_SSPHERES], sc.sph);
+			atomicAdd(&ctr[RTX_C_SPLANES], sc.pln);
+		}
+	}
+}
+
+/* ------------------------------------------------------------------------ */
+/* k_accum: one wave per tile adds its shade points' light terms to the     */
+/* tile's pixels in emission order (deterministic, no float atomics)        */
+/* ------------------------------------------------------------------------ */
+__global__ __launch_bounds__(WAVE) void k_accum(DFrame F, DParams P, const uint2 *__restrict__ tile_rec,
+						 const float4 *__restrict__ contrib, uint32_t tile_begin,
+						 float *__restrict__ rgb)
+{
+	const uint32_t t = blockIdx.x;
+	const uint2 rec = tile_rec[t];
+	f3 acc = mk3(0.f, 0.f, 0.f);
+	for (uint32_t base = 0; base < rec.y; base += WAVE) {
+		const bool valid = base + lane_id() < rec.y;
+		float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
+		if (valid)
+			c = contrib[rec.x + base + lane_id()];
+		route_add(acc, valid, valid ? __float_as_uint(c.w) : 0u, mk3(c.x, c.y, c.z));
+	}
+	const uint32_t g = P.tile_offset + (tile_begin + t) * P.tile_stride;
+	const uint32_t px = (g % P.tiles_x) * RTX_TILE_W + (lane_id() & 7), py = (g / P.tiles_x) * RTX_TILE_H + (lane_id() >> 3);
+	if (px < F.width && py < F.height) {
+		const size_t pix = (size_t)py * F.width + px;
+		rgb[pix * 3 + 0] += acc.x;
+		rgb[pix * 3 + 1] += acc.y;
+		rgb[pix * 3 + 2] += acc.z;
+	}
+}
+
 __global__ void k_kat(int kind, uint32_t n, const float *__restrict__ in, float *__restrict__ out, int u32mode)
 {
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1025,40 +1098,84 @@ __global__ void k_kat(int kind, uint32_t n, const float *__restrict__ in, float 
 	}
 }
 
+
 /* ------------------------------------------------------------------------ */
 /* launchers (called from rtx_api.cpp)                                      */
 /* ------------------------------------------------------------------------ */
-extern "C" size_t rtx_render_lds_bytes(uint32_t stack_size)
+extern "C" size_t rtx_trace_lds_bytes(uint32_t stack_size)
 {
-	size_t sp = (size_t)WAVE * SPW * 4;
-	size_t stk = (size_t)stack_size * WAVE * 4;
-	return sp + 2 * 80 * 4 + (((size_t)stack_size + 3) & ~3ull) * 4 + (stk > sp ? stk : sp);
+	return (size_t)WAVE * SPW * 4 + 80 * 4 + (size_t)stack_size * WAVE * 4;
 }
 
-extern "C" hipError_t rtx_launch_render(const DScene *S, const DFrame *F, const DParams *P, float *rgb, float *z,
-					 DTask *tasks, uint32_t task_cap, unsigned long long *ctr, uint32_t waves,
-					 int count, hipStream_t stream)
+extern "C" size_t rtx_shadow_lds_bytes(uint32_t stack_size)
 {
-	size_t lds = rtx_render_lds_bytes(S->stack_size);
-	if (count) {
-		hipLaunchKernelGGL(k_render<true>, dim3(waves), dim3(WAVE), lds, stream, *S, *F, *P, rgb, z, tasks,
-				   task_cap, ctr);
-	} else {
-		hipLaunchKernelGGL(k_render<false>, dim3(waves), dim3(WAVE), lds, stream, *S, *F, *P, rgb, z, tasks,
-				   task_cap, ctr);
+	return 80 * 4 + (((size_t)stack_size + 3) & ~3ull) * 4;
+}
+
+extern "C" hipError_t rtx_trace_occupancy(uint32_t stack_size, int *blocks_per_cu)
+{
+	return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_trace<false>, WAVE,
+							     rtx_trace_lds_bytes(stack_size));
+}
+
+extern "C" hipError_t rtx_launch_trace(const DScene *S, const DFrame *F, const DParams *P, float *rgb, float *z,
+				       DTask *tasks, uint32_t task_cap, float4 *staging, uint32_t staging_cap,
+				       float4 *sp_out, uint32_t sp_cap, uint2 *tile_rec, uint32_t tile_begin,
+				       uint32_t tile_end, unsigned long long *ctr, uint32_t waves, int count,
+				       hipStream_t stream)
+{
+	const size_t lds = rtx_trace_lds_bytes(S->stack_size);
+	if (count)
+		hipLaunchKernelGGL(k_trace<true>, dim3(waves), dim3(WAVE), lds, stream, *S, *F, *P, rgb, z, tasks, task_cap,
+				   staging, staging_cap, sp_out, sp_cap, tile_rec, tile_begin, tile_end, ctr);
+	else
+		hipLaunchKernelGGL(k_trace<false>, dim3(waves), dim3(WAVE), lds, stream, *S, *F, *P, rgb, z, tasks,
+				   task_cap, staging, staging_cap, sp_out, sp_cap, tile_rec, tile_begin, tile_end, ctr);
+	return hipGetLastError();
+}
+
+extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const float4 *sp, uint32_t n_sp,
+					uint32_t per_wave, uint32_t slot_b, float4 *contrib, unsigned long long *ctr,
+					int count, hipStream_t stream)
+{
+	const size_t lds = rtx_shadow_lds_bytes(S->stack_size);
+	const uint32_t grid = (n_sp + per_wave - 1) / per_wave;
+	if (!grid)
+		return hipSuccess;
+	/* occupancy variant: RTX_SHADOW_OCC = 0 (compiler's choice), 7 or 8 waves/SIMD (register caps) */
+	static int occ = -1;
+	if (occ < 0) {
+		const char *e = getenv("RTX_SHADOW_OCC");
+		occ = e ? atoi(e) : RTX_SHADOW_OCC_DEFAULT;
 	}
+#define RTX_LAUNCH_SHADOW(C, O)                                                                                  \
+	hipLaunchKernelGGL((k_shadow<C, O>), dim3(grid), dim3(WAVE), lds, stream, *S, S->nodes, S->prims, S->mats,     \
+			   S->planes, S->emitters, *P, sp, n_sp, per_wave, slot_b, contrib, ctr)
+	if (count)
+		RTX_LAUNCH_SHADOW(true, 1);
+	else if (occ == 8)
+		RTX_LAUNCH_SHADOW(false, 8);
+	else if (occ == 7)
+		RTX_LAUNCH_SHADOW(false, 7);
+	else
+		RTX_LAUNCH_SHADOW(false, 1);
+#undef RTX_LAUNCH_SHADOW
+	return hipGetLastError();
+}
+
+extern "C" hipError_t rtx_launch_accum(const DFrame *F, const DParams *P, const uint2 *tile_rec,
+				       const float4 *contrib, uint32_t tile_begin, uint32_t ntiles, float *rgb,
+				       hipStream_t stream)
+{
+	if (!ntiles || !rgb)
+		return hipSuccess;
+	hipLaunchKernelGGL(k_accum, dim3(ntiles), dim3(WAVE), 0, stream, *F, *P, tile_rec, contrib, tile_begin, rgb);
 	return hipGetLastError();
 }
 
 extern "C" hipError_t rtx_launch_kat(int kind, uint32_t n, const float *in, float *out, int u32mode,
-				      hipStream_t stream)
+				     hipStream_t stream)
 {
 	hipLaunchKernelGGL(k_kat, dim3((n + 255) / 256), dim3(256), 0, stream, kind, n, in, out, u32mode);
 	return hipGetLastError();
-}
-
-extern "C" hipError_t rtx_render_occupancy(uint32_t stack_size, int *blocks_per_cu)
-{
-	size_t lds = rtx_render_lds_bytes(stack_size);
-	return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_render<false>, WAVE, lds);
 }

@@ -173,16 +173,27 @@ void rtx_params_default(rtx_params *p);
 typedef struct rtx_stats {
 	uint64_t closest_rays;       /* cast_ray() calls (render.c:136) */
 	uint64_t shadow_rays;        /* is_light_blocked() calls (render.c:126) */
-	/* only with count_traversal: */
-	uint64_t node_visits;        /* BVH internal nodes fetched per ray, summed */
+	/* only with count_traversal: per-ray work summed over all rays (closest + shadow) */
+	uint64_t node_visits;        /* BVH inner nodes fetched (2 child boxes tested) */
 	uint64_t tri_tests;
 	uint64_t sphere_tests;
 	uint64_t plane_tests;
-	double kernel_ms;            /* device time of the last rtx_render*, HIP events */
+	/* ... of which by shadow rays */
+	uint64_t shadow_node_visits;
+	uint64_t shadow_tri_tests;
+	uint64_t shadow_sphere_tests;
+	uint64_t shadow_plane_tests;
+	uint64_t shade_points;       /* hits whose direct lighting was evaluated */
+	double kernel_ms;            /* device time of the last rtx_render*, HIP events, all kernels */
+	double trace_ms;             /* ... closest-hit / shading kernel */
+	double shadow_ms;            /* ... shadow-ray kernel */
+	double accum_ms;             /* ... per-tile accumulation kernel */
 	uint32_t bvh_nodes;
 	uint32_t bvh_depth;
 	uint32_t bvh_prims;
-	uint32_t waves;              /* persistent waves launched */
+	uint32_t waves;              /* persistent waves of the closest-hit kernel */
+	uint32_t chunks;             /* tile chunks the frame was split into */
+	uint32_t pad;
 } rtx_stats;
 
 typedef struct rtx_ctx rtx_ctx;
