@@ -252,7 +252,10 @@ struct Flattener {
 				ax = a;
 			}
 		}
-		d.axis = (uint32_t)ax | (((L.box.lo[ax] + L.box.hi[ax]) > (R.box.lo[ax] + R.box.hi[ax])) ? 4u : 0u);
+		const bool lcg = (L.box.lo[ax] + L.box.hi[ax]) > (R.box.lo[ax] + R.box.hi[ax]);
+		d.order = 0;
+		for (uint32_t o = 0; o < 8; o++) /* left first when the ray moves from the left centroid's side */
+			d.order |= ((((o >> ax) & 1u) != 0) != lcg) ? 1u << o : 0u;
 		d.pad = 0;
 		return me;
 	}

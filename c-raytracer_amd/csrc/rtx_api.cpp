@@ -60,7 +60,6 @@ struct rtx_ctx {
 	int cus = 0;
 	/* scene */
 	DNode *d_nodes = nullptr;
-	DPrim *d_prims = nullptr;
 	DPlane *d_planes = nullptr;
 	DMaterial *d_mats = nullptr;
 	DEmitter *d_emitters = nullptr;
@@ -128,7 +127,6 @@ template <class T> static void dfree(T *&p)
 static void free_scene(rtx_ctx *c)
 {
 	dfree(c->d_nodes);
-	dfree(c->d_prims);
 	dfree(c->d_planes);
 	dfree(c->d_mats);
 	dfree(c->d_emitters);
@@ -219,6 +217,8 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 	HIP_TRY(hipSetDevice(c->device));
 	free_scene(c);
 
+	if (sc->num_materials > RTX_META_MAT)
+		return fail(RTX_ERR_SCENE, "too many materials (%u)", sc->num_materials);
 	std::vector<DMaterial> mats(sc->num_materials);
 	for (uint32_t i = 0; i < sc->num_materials; i++) {
 		const rtx_material &m = sc->materials[i];
@@ -303,6 +303,8 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 		DPrim &p = prims[k];
 		memset(&p, 0, sizeof(p));
 		uint32_t meta = ((uint32_t)o.type << 24) | (uint32_t)o.material;
+		if (mats[o.material].flags & RTX_MF_TRANSPARENT)
+			meta |= RTX_META_TRANSPARENT;
 		memcpy(p.a, o.p0, 12);
 		p.a[3] = o.epsilon;
 		if (o.type == RTX_SPHERE) {
@@ -340,23 +342,47 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 		e.radius = o.radius;
 	}
 
+	/* nodes and primitives in one array of 64-byte records: the shadow walk addresses both
+	 * through one base pointer (record num_nodes + i = primitive i) */
+	const uint32_t nnodes = (uint32_t)bvh.nodes.size();
+	if (((uint64_t)nnodes + nb) * sizeof(DNode) > 0xFFFFFFC0ull)
+		return fail(RTX_ERR_SCENE, "scene too large: %u BVH nodes + %u primitives exceed 4 GB of records", nnodes, nb);
+	/* builder refs (node index | RTX_LEAF_BIT leaf) -> device refs (record byte offset | leaf bits) */
+	auto dref = [nnodes](uint32_t r) -> uint32_t {
+		if (r == RTX_EMPTY_REF)
+			return r;
+		if (r & RTX_LEAF_BIT)
+			return (nnodes + ((r >> 4) & 0x7FFFFFFu)) * (uint32_t)sizeof(DNode) | RTX_REF_LEAF | (r & 15u);
+		return r * (uint32_t)sizeof(DNode);
+	};
+	std::vector<DNode> recs(nnodes + (size_t)nb);
+	for (uint32_t i = 0; i < nnodes; i++) {
+		recs[i] = bvh.nodes[i];
+		recs[i].ref0 = dref(recs[i].ref0);
+		recs[i].ref1 = dref(recs[i].ref1);
+	}
+	if (nb)
+		memcpy(recs.data() + nnodes, prims.data(), nb * sizeof(DPrim));
 	int rc;
-	if ((rc = upload(c->d_nodes, bvh.nodes)) || (rc = upload(c->d_prims, prims)) ||
+	if ((rc = upload(c->d_nodes, recs)) ||
 	    (rc = upload(c->d_planes, planes)) || (rc = upload(c->d_mats, mats)) || (rc = upload(c->d_emitters, emit)))
 		return rc;
 
 	DScene &S = c->scene;
 	memset(&S, 0, sizeof(S));
 	S.nodes = c->d_nodes;
-	S.prims = c->d_prims;
+	S.num_nodes = nnodes;
+	S.prims = (const DPrim *)(c->d_nodes + nnodes);
 	S.planes = c->d_planes;
 	S.mats = c->d_mats;
 	S.emitters = c->d_emitters;
-	S.root_ref = nb ? bvh.root_ref : RTX_EMPTY_REF;
+	S.root_ref = nb ? dref(bvh.root_ref) : RTX_EMPTY_REF;
 	S.num_prims = nb;
 	S.num_planes = (uint32_t)planes.size();
 	S.num_emitters = sc->num_emitters;
 	S.stack_size = std::max<uint32_t>(bvh.depth + 1, 4);
+	if (bvh.depth > 63) /* k_shadow keeps its packet stack in the 64 lanes of one VGPR */
+		return fail(RTX_ERR_SCENE, "BVH depth %u exceeds 63", bvh.depth);
 	c->total_lights = 0;
 	for (const DEmitter &e : emit)
 		c->total_lights += e.num_lights;

@@ -1,15 +1,21 @@
 /*
  * Device-side scene layout in HBM (shared by the host uploader and the kernels).
  *
- *  DNode  64 B  BVH2 inner node: both children's AABBs + child refs.  A ref is
- *               an inner-node index (>= 0) or a leaf: RTX_LEAF_BIT | first << 4 |
- *               (count-1), count <= 16 primitives contiguous in `prims`.
+ *  DNode  64 B  BVH2 inner node: both children's AABBs + child refs + the
+ *               child order per ray-direction octant.  A ref is the byte offset
+ *               of the child's 64-byte record from `nodes` (64-aligned), with
+ *               RTX_REF_LEAF | (count-1) in its low bits for a leaf of count
+ *               <= 16 primitives contiguous in the record array (primitive i
+ *               is record num_nodes + i).
  *               Replaces the pointer-linked struct BVH + malloc'd BoundingCuboid
  *               of accel.c:25-40.  Nodes are stored depth-first (left child
  *               adjacent) so a traversal walks forward through memory.
  *  DPrim  64 B  one bounded object (sphere / triangle) in BVH leaf order:
  *               a = (v0 | centre, epsilon), b = (e1 | (r,0,0), object id bits),
- *               c = (e2, meta bits = material | type << 24), d = (normal, 0).
+ *               c = (e2, meta bits = material | transparent << 23 | type << 24),
+ *               d = (normal, 0).  The primitives follow the nodes in one
+ *               allocation (record index nnodes + i), so the shadow walk
+ *               addresses both through one base pointer.
  *               Shadow tests read a..c (48 B); d only for the final closest hit.
  *  DPlane 32 B  unbound objects (object.c:168-197), linear scan, never in the BVH.
  *  DMaterial    material + texture parameters (material.c:27-53).
@@ -22,11 +28,18 @@
 
 #include <stdint.h>
 
-#define RTX_LEAF_BIT 0x80000000u
+#define RTX_LEAF_BIT 0x80000000u  /* builder-side leaf refs (bvh_build.cpp) */
+#define RTX_REF_LEAF 32u          /* device refs: byte offset | leaf flag | count-1 */
+#define RTX_REF_CNT 31u
+#define RTX_REF_OFF (~63u)
 #define RTX_PLANE_BIT 0x80000000u
 #define RTX_NONE 0xFFFFFFFFu
 #define RTX_EMPTY_REF 0xFFFFFFFFu /* BVH with no bounded objects */
 #define RTX_MAX_LEAF 16
+
+/* DPrim meta word (c[3]): material | transparent flag | type << 24 */
+#define RTX_META_MAT 0x7FFFFFu
+#define RTX_META_TRANSPARENT 0x800000u
 
 #define RTX_MF_EMITTANT 1
 #define RTX_MF_REFLECTIVE 2
@@ -39,7 +52,9 @@ typedef struct __attribute__((aligned(64))) DNode {
 	float lo0x, hi0x, lo0y, hi0y;
 	float lo0z, hi0z, lo1x, hi1x;
 	float lo1y, hi1y, lo1z, hi1z;
-	uint32_t ref0, ref1, axis, pad;
+	uint32_t ref0, ref1;
+	uint32_t order; /* bit o: left child first for direction octant o (bit a of o: dir[a] >= 0) */
+	uint32_t pad;
 } DNode;
 
 typedef struct __attribute__((aligned(64))) DPrim {
@@ -86,6 +101,7 @@ typedef struct DScene {
 	const DMaterial *mats;
 	const DEmitter *emitters;
 	uint32_t root_ref;
+	uint32_t num_nodes;    /* prims == (const DPrim *)(nodes + num_nodes) */
 	uint32_t num_prims;
 	uint32_t num_planes;
 	uint32_t num_emitters;

@@ -36,8 +36,18 @@
 #include "rtx_rng.h"
 
 #define WAVE 64
+/* shadow-walk build switches (measurement variants; defaults are the tuned choice) */
+#ifndef RTX_SH_PF
+#define RTX_SH_PF 1  /* touch the children's records before the current step's tests */
+#endif
+#ifndef RTX_SH_OCT
+#define RTX_SH_OCT 0 /* specialise the box test on a packet-uniform direction octant (measured slower) */
+#endif
+#ifndef RTX_SH_RCP
+#define RTX_SH_RCP 1 /* any-hit triangle test with v_rcp_f32 instead of IEEE 1/a */
+#endif
 #ifndef RTX_SHADOW_OCC_DEFAULT
-#define RTX_SHADOW_OCC_DEFAULT 0
+#define RTX_SHADOW_OCC_DEFAULT 8
 #endif
 
 
@@ -47,7 +57,7 @@
 typedef unsigned long long u64;
 typedef uint32_t v16u __attribute__((ext_vector_type(16)));
 
-__device__ __forceinline__ u64 ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ u64 ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ uint32_t popc64(u64 m) { return (uint32_t)__popcll(m); }
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 __device__ __forceinline__ uint32_t mbcnt(u64 m)
@@ -222,8 +232,9 @@ __device__ void trace_closest(const DScene &S, uint32_t *stk, bool act, f3 o, f3
 		uint32_t sp = 0;
 		stk += lane_id();
 		for (;;) {
-			if (ref & RTX_LEAF_BIT) {
-				const uint32_t first = (ref >> 4) & 0x7FFFFFFu, cnt = (ref & 15u) + 1;
+			if (ref & RTX_REF_LEAF) {
+				const uint32_t first = (ref & RTX_REF_OFF) / (uint32_t)sizeof(DNode) - S.num_nodes,
+					       cnt = (ref & RTX_REF_CNT) + 1;
 				for (uint32_t k = 0; k < cnt; k++) {
 					const float4 *pr = (const float4 *)(S.prims + first + k);
 					const float4 a = pr[0], b = pr[1], c = pr[2];
@@ -248,7 +259,7 @@ __device__ void trace_closest(const DScene &S, uint32_t *stk, bool act, f3 o, f3
 					break;
 				ref = stk[--sp * WAVE];
 			} else {
-				const float4 *nd = (const float4 *)(S.nodes + ref);
+				const float4 *nd = (const float4 *)((const char *)S.nodes + (ref & RTX_REF_OFF));
 				const float4 n0 = nd[0], n1 = nd[1], n2 = nd[2];
 				const uint4 n3 = *(const uint4 *)(nd + 3);
 				if (COUNT)
@@ -305,7 +316,7 @@ __device__ __forceinline__ HitInfo hit_info(const DScene &S, uint32_t hid, f3 o,
 		else
 			h.n = mk3(pr.d[0], pr.d[1], pr.d[2]);
 		h.obj = __float_as_uint(pr.b[3]);
-		h.mat = meta & 0xFFFFFFu;
+		h.mat = meta & RTX_META_MAT;
 		h.eps = pr.a[3];
 	}
 	h.b = dot3(h.n, d);
@@ -712,14 +723,184 @@ struct ShadowCount {
 	u64 nodes, tris, sph, pln;
 };
 
-template <bool COUNT>
-__device__ __forceinline__ void shadow_packet(const DNode *__restrict__ nodes, const DPrim *__restrict__ prims,
-					      const DMaterial *__restrict__ mats, const DPlane *__restrict__ planes,
-					      uint32_t num_planes, uint32_t root_ref, uint32_t *pstk, bool act, f3 o, f3 d,
-					      float dist, uint32_t emit_obj, f3 &li, bool &blocked, ShadowCount &sc)
+/* 64-byte BVH records are read through the constant address space: with a wave-uniform
+ * address that is one s_load_dwordx16 into SGPRs, whatever the compiler can prove about
+ * where the base pointer came from (the records are never written while a kernel runs) */
+typedef const v16u __attribute__((address_space(4))) *crec_t;
+
+__device__ __forceinline__ v16u rec_load(const char *recs, uint32_t off) { return *(crec_t)(recs + off); }
+
+/* prefetch: one dword of a record (s_load_dword), which brings its 64-byte line into the
+ * scalar cache and L2 while this step computes.  Issued by inline asm so the compiler neither
+ * sinks it nor waits for it; its destination SGPR stays live (hence untouched) until
+ * consume(), which takes a field of the next record as an input and so sits behind that
+ * record's lgkmcnt(0) wait, which has drained the touch too. */
+__device__ __forceinline__ uint32_t touch(const char *recs, uint32_t off)
 {
-	/* unbound_objects_is_light_blocked (object.c:183-197): planes first */
-	blocked = false;
+	uint32_t v;
+	asm volatile("s_load_dword %0, %1, %2" : "=s"(v) : "s"(recs), "s"(off));
+	return v;
+}
+__device__ __forceinline__ void consume(uint32_t a, uint32_t b, uint32_t dep)
+{
+	asm volatile("; consume %0 %1 %2" ::"s"(a), "s"(b), "s"(dep));
+}
+/* drain outstanding touches before their registers can be reused (walk exit) */
+__device__ __forceinline__ void drain(uint32_t a, uint32_t b)
+{
+	asm volatile("s_waitcnt lgkmcnt(0)\n\t; drained %0 %1" ::"s"(a), "s"(b));
+}
+
+/* child-box test of the packet walk (the slab test of accel.c:112-158 on padded boxes).
+ * OCT < 8: every live ray's direction lies in octant OCT (bit a set = inv[a] >= 0), so each
+ * axis' entry plane is known at compile time and the per-axis min/max of `slab` drop out;
+ * fma is monotone in the plane coordinate, so the answer is the same as slab()'s. */
+template <int OCT>
+__device__ __forceinline__ bool box_hit(const v16u &nd, const uint32_t b, f3 oi, f3 inv, float tlim)
+{
+	if (OCT == 8) {
+		float tn;
+		return slab(__uint_as_float(nd[b]), __uint_as_float(nd[b + 1]), __uint_as_float(nd[b + 2]),
+			    __uint_as_float(nd[b + 3]), __uint_as_float(nd[b + 4]), __uint_as_float(nd[b + 5]), oi, inv, tlim,
+			    tn);
+	}
+	const float nx = __uint_as_float(nd[b + ((OCT & 1) ? 0 : 1)]), fx = __uint_as_float(nd[b + ((OCT & 1) ? 1 : 0)]);
+	const float ny = __uint_as_float(nd[b + ((OCT & 2) ? 2 : 3)]), fy = __uint_as_float(nd[b + ((OCT & 2) ? 3 : 2)]);
+	const float nz = __uint_as_float(nd[b + ((OCT & 4) ? 4 : 5)]), fz = __uint_as_float(nd[b + ((OCT & 4) ? 5 : 4)]);
+	const float tn = fmaxf(fmaxf(fmaf(nx, inv.x, -oi.x), fmaf(ny, inv.y, -oi.y)), fmaxf(fmaf(nz, inv.z, -oi.z), 0.f));
+	const float tf =
+		fminf(fminf(fmaf(fx, inv.x, -oi.x), fmaf(fy, inv.y, -oi.y)), fminf(fmaf(fz, inv.z, -oi.z), tlim));
+	return tn <= tf;
+}
+
+/* moller_trumbore (object.c:422-441) as a branch-free any-hit test on (eps, tlim): same
+ * accept conditions; 1/a by v_rcp_f32 (1 ulp) since only the hit/miss decision is used */
+__device__ __forceinline__ bool any_tri(f3 v0, f3 e1, f3 e2, f3 o, f3 d, float eps, float tlim)
+{
+	const f3 h = cross3(d, e2);
+	const float a = dot3(e1, h);
+	const float f = RTX_SH_RCP ? __builtin_amdgcn_rcpf(a) : 1.f / a;
+	const f3 s = sub3(o, v0);
+	const float u = f * dot3(s, h);
+	const f3 q = cross3(s, e1);
+	const float v = f * dot3(d, q);
+	const float t = f * dot3(e2, q);
+	return !(a < eps && a > -eps) & !(u < 0.f || u > 1.f) & !(v < 0.f || u + v > 1.f) & (t > eps) & (t < tlim);
+}
+
+/* one primitive of a leaf against the packet (accel.c:362-373): the target emitter skipped,
+ * opaque hit -> the lane is blocked (tl = -1: no later test can hit it), transparent hit ->
+ * li *= kt.  Returns true when a lane was blocked. */
+template <bool COUNT>
+__device__ __forceinline__ bool shadow_prim(const v16u &pr, const DMaterial *__restrict__ mats, f3 o, f3 d, float &tl,
+					    uint32_t emit_u, uint32_t emit_obj, f3 &li, ShadowCount &sc)
+{
+	const uint32_t meta = pr[11], obj = pr[7];
+	if (obj == emit_u)
+		return false;
+	const f3 a = mk3(__uint_as_float(pr[0]), __uint_as_float(pr[1]), __uint_as_float(pr[2]));
+	bool h;
+	if ((meta >> 24) == RTX_SPHERE) {
+		if (COUNT)
+			sc.sph += popc64(ballot(tl >= 0.f));
+		float t = 0.f;
+		h = hit_sphere(a, __uint_as_float(pr[4]), o, d, __uint_as_float(pr[3]), t) & (t < tl);
+	} else {
+		if (COUNT)
+			sc.tris += popc64(ballot(tl >= 0.f));
+		h = any_tri(a, mk3(__uint_as_float(pr[4]), __uint_as_float(pr[5]), __uint_as_float(pr[6])),
+			    mk3(__uint_as_float(pr[8]), __uint_as_float(pr[9]), __uint_as_float(pr[10])), o, d,
+			    __uint_as_float(pr[3]), tl);
+	}
+	if (emit_u == RTX_NONE) /* the packet's rays aim at different emitters */
+		h = h & (obj != emit_obj);
+	if (!ballot(h))
+		return false;
+	if (meta & RTX_META_TRANSPARENT) {
+		const DMaterial &m = mats[meta & RTX_META_MAT];
+		const f3 kt = mk3(m.kt[0], m.kt[1], m.kt[2]);
+		if (h)
+			li = mul3v(li, kt);
+		return false;
+	}
+	if (h)
+		tl = -1.f;
+	return true;
+}
+
+/* is_light_blocked for one packet of shadow rays (accel.c:317-387): the 64 rays walk the BVH
+ * together.  Node and primitive records are wave-uniform (one 64-byte s_load_dwordx16 each),
+ * each lane tests its own ray, the ballots pick the children.  A lane's liveness is its
+ * segment end tl (< 0: inactive or blocked), so no lane masks are carried; control stays on
+ * a few scalar registers: the ref (record byte offset | leaf bits), the stack depth, and the
+ * stack itself, one ref per lane of a VGPR (depth <= 63, checked at upload). */
+template <bool COUNT, int OCT>
+__device__ __forceinline__ void shadow_walk(const char *__restrict__ recs, const DMaterial *__restrict__ mats,
+					    uint32_t root_ref, f3 o, f3 d, f3 inv, float &tl, uint32_t emit_u,
+					    uint32_t emit_obj, uint32_t lead_oct, f3 &li, ShadowCount &sc)
+{
+	const f3 oi = mul3v(o, inv);
+	const uint32_t oct = OCT < 8 ? (uint32_t)OCT : lead_oct;
+	uint32_t ref = root_ref, sp = 0, stk = 0, pf0 = 0, pf1 = 0;
+	for (;;) {
+		const v16u rec = rec_load(recs, ref & RTX_REF_OFF);
+		if (RTX_SH_PF)
+			consume(pf0, pf1, rec[15]);
+		if (!(ref & RTX_REF_LEAF)) {
+			if (RTX_SH_PF) {
+				pf0 = touch(recs, rec[12] & RTX_REF_OFF);
+				pf1 = touch(recs, rec[13] & RTX_REF_OFF);
+			}
+			if (COUNT)
+				sc.nodes += popc64(ballot(tl >= 0.f));
+			const u64 b0 = ballot(box_hit<OCT>(rec, 0, oi, inv, tl));
+			const u64 b1 = ballot(box_hit<OCT>(rec, 6, oi, inv, tl));
+			/* near child first for the packet's direction octant (any order is correct) */
+			const bool lf = (rec[14] >> oct) & 1u;
+			const uint32_t rn = lf ? rec[12] : rec[13], rf = lf ? rec[13] : rec[12];
+			const u64 bn = lf ? b0 : b1, bf = lf ? b1 : b0;
+			if (bn) {
+				if (bf) {
+					stk = lane_id() == sp ? rf : stk;
+					sp++;
+				}
+				ref = rn;
+				continue;
+			}
+			if (bf) {
+				ref = rf;
+				continue;
+			}
+		} else {
+			const uint32_t off = ref & RTX_REF_OFF, cnt = (ref & RTX_REF_CNT) + 1;
+			if (RTX_SH_PF) { /* the leaf's second primitive and the stack top (next pop) */
+				pf0 = touch(recs, off + (cnt > 1 ? (uint32_t)sizeof(DNode) : 0u));
+				pf1 = touch(recs, sp ? readlane(stk, sp - 1) & RTX_REF_OFF : off);
+			}
+			bool blk = shadow_prim<COUNT>(rec, mats, o, d, tl, emit_u, emit_obj, li, sc);
+			for (uint32_t k = 1; k < cnt; k++)
+				blk |= shadow_prim<COUNT>(rec_load(recs, off + k * (uint32_t)sizeof(DNode)), mats, o, d, tl, emit_u,
+							 emit_obj, li, sc);
+			if (blk && !ballot(tl >= 0.f))
+				break; /* every ray of the packet is blocked */
+		}
+		if (sp == 0)
+			break;
+		ref = readlane(stk, --sp);
+	}
+	if (RTX_SH_PF)
+		drain(pf0, pf1);
+}
+
+/* planes first (unbound_objects_is_light_blocked, object.c:183-197), then the BVH walk,
+ * specialised on the packet's direction octant when all live rays share it.  Returns the
+ * lane's blocked flag; li carries the transmittance product. */
+template <bool COUNT>
+__device__ __forceinline__ bool shadow_packet(const char *__restrict__ recs, const DMaterial *__restrict__ mats,
+					      const DPlane *__restrict__ planes, uint32_t num_planes, uint32_t root_ref,
+					      bool act, f3 o, f3 d, float dist, uint32_t emit_obj, f3 &li, ShadowCount &sc)
+{
+	float tl = act ? dist : -1.f;
 	if (act) {
 		for (uint32_t i = 0; i < num_planes; i++) {
 			const DPlane &pl = planes[i];
@@ -729,7 +910,7 @@ __device__ __forceinline__ void shadow_packet(const DNode *__restrict__ nodes, c
 				if (m.flags & RTX_MF_TRANSPARENT) {
 					li = mul3v(li, ld3(m.kt));
 				} else {
-					blocked = true;
+					tl = -1.f;
 					break;
 				}
 			}
@@ -737,133 +918,107 @@ __device__ __forceinline__ void shadow_packet(const DNode *__restrict__ nodes, c
 	}
 	if (COUNT)
 		sc.pln += (u64)popc64(ballot(act)) * num_planes;
-	u64 live = ballot(act && !blocked);
+	const bool alive = tl >= 0.f;
+	const u64 live = ballot(alive);
 	if (!live || root_ref == RTX_EMPTY_REF)
-		return;
+		return act && !alive;
 	const f3 inv = safe_inv(d);
-	const f3 oi = mul3v(o, inv);
-	/* near-first order from the first live ray's direction signs (any order is correct) */
-	const uint32_t lead = (uint32_t)__ffsll((long long)live) - 1;
-	const uint32_t dsgn = readlane(((d.x >= 0.f) ? 1u : 0u) | ((d.y >= 0.f) ? 2u : 0u) | ((d.z >= 0.f) ? 4u : 0u), lead);
-	uint32_t ref = root_ref;
-	uint32_t sp = 0;
-	for (;;) {
-		if (ref & RTX_LEAF_BIT) {
-			/* accel.c:362-373: skip the emitter, opaque -> blocked, transparent -> Li *= kt */
-			const uint32_t first = (ref >> 4) & 0x7FFFFFFu, cnt = (ref & 15u) + 1;
-			for (uint32_t k = 0; k < cnt; k++) {
-				/* the whole 64-byte record in one scalar load */
-				const v16u pr = *(const v16u *)(prims + first + k);
-				const uint32_t meta = pr[11], obj = pr[7];
-				const bool mine = lane_in(live) & (obj != emit_obj);
-				const f3 a = mk3(__uint_as_float(pr[0]), __uint_as_float(pr[1]), __uint_as_float(pr[2]));
-				float t = 0.f;
-				bool h;
-				if ((meta >> 24) == RTX_SPHERE) {
-					if (COUNT)
-						sc.sph += popc64(live);
-					h = hit_sphere(a, __uint_as_float(pr[4]), o, d, __uint_as_float(pr[3]), t);
-				} else {
-					if (COUNT)
-						sc.tris += popc64(live);
-					h = hit_triangle(a, mk3(__uint_as_float(pr[4]), __uint_as_float(pr[5]), __uint_as_float(pr[6])),
-							 mk3(__uint_as_float(pr[8]), __uint_as_float(pr[9]), __uint_as_float(pr[10])),
-							 o, d, __uint_as_float(pr[3]), t);
-				}
-				h = h & mine & (t < dist);
-				if (ballot(h)) {
-					const DMaterial &m = mats[meta & 0xFFFFFFu];
-					if (m.flags & RTX_MF_TRANSPARENT) {
-						const f3 kt = mk3(m.kt[0], m.kt[1], m.kt[2]);
-						if (h)
-							li = mul3v(li, kt);
-					} else {
-						blocked = blocked | h;
-					}
-				}
-			}
-			live = ballot(lane_in(live) & !blocked);
-			if (!live || sp == 0)
-				break;
-			ref = uni(pstk[--sp]);
-		} else {
-			/* both child boxes + refs in one scalar load */
-			const v16u nd = *(const v16u *)(nodes + ref);
-			const bool me = lane_in(live);
-			float tn0, tn1;
-			const bool h0 = slab(__uint_as_float(nd[0]), __uint_as_float(nd[1]), __uint_as_float(nd[2]),
-					     __uint_as_float(nd[3]), __uint_as_float(nd[4]), __uint_as_float(nd[5]), oi, inv, dist,
-					     tn0) & me;
-			const bool h1 = slab(__uint_as_float(nd[6]), __uint_as_float(nd[7]), __uint_as_float(nd[8]),
-					     __uint_as_float(nd[9]), __uint_as_float(nd[10]), __uint_as_float(nd[11]), oi, inv,
-					     dist, tn1) & me;
-			if (COUNT)
-				sc.nodes += popc64(live);
-			const u64 b0 = ballot(h0), b1 = ballot(h1);
-			const uint32_t r0 = nd[12], r1 = nd[13], axis = nd[14];
-			if (b0 && b1) {
-				const bool left_first = ((dsgn >> (axis & 3u)) & 1u) != ((axis >> 2) & 1u);
-				if (lane_id() == 0)
-					pstk[sp] = left_first ? r1 : r0;
-				sp++;
-				ref = left_first ? r0 : r1;
-			} else if (b0) {
-				ref = r0;
-			} else if (b1) {
-				ref = r1;
-			} else {
-				if (sp == 0)
-					break;
-				ref = uni(pstk[--sp]);
-			}
-		}
+	const uint32_t oct = ((~__float_as_uint(inv.x)) >> 31) | (((~__float_as_uint(inv.y)) >> 31) << 1) |
+			     (((~__float_as_uint(inv.z)) >> 31) << 2);
+	const uint32_t lead_lane = (uint32_t)__ffsll((long long)live) - 1;
+	const uint32_t lead = readlane(oct, lead_lane), lead_emit = readlane(emit_obj, lead_lane);
+	const uint32_t emit_u = ballot(alive & (emit_obj != lead_emit)) ? RTX_NONE : lead_emit;
+	const uint32_t sel = (!RTX_SH_OCT || ballot(alive & (oct != lead))) ? 8u : lead;
+	switch (sel) {
+#define RTX_WALK(K)                                                                                                   \
+	case K:                                                                                                           \
+		shadow_walk<COUNT, K>(recs, mats, root_ref, o, d, inv, tl, emit_u, emit_obj, K, li, sc);                     \
+		break;
+#if RTX_SH_OCT
+	RTX_WALK(0) RTX_WALK(1) RTX_WALK(2) RTX_WALK(3) RTX_WALK(4) RTX_WALK(5) RTX_WALK(6) RTX_WALK(7)
+#endif
+	default:
+		shadow_walk<COUNT, 8>(recs, mats, root_ref, o, d, inv, tl, emit_u, emit_obj, lead, li, sc);
+		break;
+#undef RTX_WALK
 	}
+	return act && tl < 0.f;
+}
+
+/* k_shadow arguments.  Lane 0 copies them to LDS; the packet loop re-reads them from there
+ * after each walk (behind a compiler memory barrier), so none stays live in registers across
+ * the traversal, which needs every SGPR it can get at 8 waves/SIMD. */
+struct KShadow {
+	const DNode *recs; /* BVH nodes, then primitives from record nnodes */
+	const DMaterial *mats;
+	const DPlane *planes;
+	const DEmitter *emitters;
+	const float4 *sp;
+	float4 *contrib;
+	unsigned long long *ctr;
+	uint32_t nnodes, root_ref, num_planes, num_emitters;
+	uint32_t n_sp, per_wave, slot_b, slot_lg;
+	int32_t rng, attenuation, reflection;
+	float att_offset;
+};
+
+__device__ __forceinline__ void reread_barrier() { asm volatile("" ::: "memory"); }
+
+/* a pointer read from LDS, made wave-uniform (SGPRs) so accesses through it stay scalar */
+template <typename T> __device__ __forceinline__ T *unip(T *p)
+{
+	const uint64_t v = (uint64_t)p;
+	return (T *)(((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v));
 }
 
 template <bool COUNT, int OCC>
-__global__ __launch_bounds__(WAVE, OCC) void k_shadow(DScene S, const DNode *__restrict__ nodes,
-						 const DPrim *__restrict__ prims, const DMaterial *__restrict__ mats,
-						 const DPlane *__restrict__ planes, const DEmitter *__restrict__ emitters,
-						 DParams P, const float4 *__restrict__ sp, uint32_t n_sp, uint32_t per_wave,
-						 uint32_t slot_b, float4 *__restrict__ contrib,
-						 unsigned long long *__restrict__ ctr)
+__global__ __launch_bounds__(WAVE, OCC) void k_shadow(KShadow ka)
 {
-	extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-	uint32_t *off = (uint32_t *)lds_raw;
-	uint32_t *pstk = off + 80;
-	const uint32_t j0 = blockIdx.x * per_wave;
-	if (j0 >= n_sp)
+	__shared__ KShadow ks;
+	__shared__ uint32_t off[WAVE + 1]; /* first lane slot of each shade point, total */
+	__shared__ uint32_t nls[WAVE];     /* shadow rays of each shade point */
+	__shared__ float Ls[3][WAVE];      /* per shade point light sum, in packet order */
+	const uint32_t j0 = blockIdx.x * ka.per_wave;
+	if (j0 >= ka.n_sp)
 		return;
-	const uint32_t cnt = min(per_wave, n_sp - j0);
+	const uint32_t cnt = min(ka.per_wave, ka.n_sp - j0);
 	const bool own = lane_id() < cnt;
-	const float4 *my = sp + (size_t)(j0 + (own ? lane_id() : 0)) * SPREC;
-	const uint32_t nl_mine = own ? __float_as_uint(my[4].w) : 0u;
+	const uint32_t nl_mine = own ? __float_as_uint(ka.sp[(size_t)(j0 + lane_id()) * SPREC + 4].w) : 0u;
 	/* each point's samples occupy whole lane slots of B lanes (B = power of two), so a point's
 	 * packet partial sums never depend on which other points share its wave: deterministic */
 	uint32_t total;
-	const uint32_t ex = wave_excl_scan((nl_mine + slot_b - 1) / slot_b, &total);
+	const uint32_t ex = wave_excl_scan((nl_mine + ka.slot_b - 1) >> ka.slot_lg, &total);
 	off[lane_id()] = ex;
-	if (lane_id() == 0)
+	nls[lane_id()] = nl_mine;
+	Ls[0][lane_id()] = 0.f;
+	Ls[1][lane_id()] = 0.f;
+	Ls[2][lane_id()] = 0.f;
+	if (lane_id() == 0) {
 		off[WAVE] = total;
+		ks = ka;
+	}
 	lds_sync();
-	f3 L = mk3(0.f, 0.f, 0.f);
 	ShadowCount sc = { 0, 0, 0, 0 };
-	u64 n_rays = 0;
-	const uint32_t slots_per_packet = WAVE / slot_b;
-	for (uint32_t base = 0; base < total; base += slots_per_packet) {
-		const uint32_t slot = base + lane_id() / slot_b;
-		const uint32_t k = slot < total ? owner_of(off, slot) : 0u;
-		const uint32_t idx = (slot - off[k]) * slot_b + lane_id() % slot_b;
-		const bool act = slot < total && idx < __shfl(nl_mine, k, WAVE);
-		n_rays += popc64(ballot(act));
-		const float4 *rec = sp + (size_t)(j0 + k) * SPREC;
+	for (uint32_t base = 0;;) {
+		reread_barrier();
+		const uint32_t tot = uni(off[WAVE]), slot_b = uni(ks.slot_b), slot_lg = uni(ks.slot_lg);
+		if (base >= tot)
+			break;
+		const uint32_t jw = blockIdx.x * uni(ks.per_wave);
+		const uint32_t slot = base + (lane_id() >> slot_lg);
+		const uint32_t k = slot < tot ? owner_of(off, slot) : 0u;
+		const uint32_t idx = ((slot - off[k]) << slot_lg) + (lane_id() & (slot_b - 1));
+		const bool act = slot < tot && idx < nls[k];
+		const float4 *rec = unip(ks.sp) + (size_t)(jw + k) * SPREC;
 		const float4 q0 = rec[0], q4 = rec[4];
 		const f3 p = mk3(q0.x, q0.y, q0.z);
 		const uint32_t obj = __float_as_uint(q4.x);
+		const DEmitter *emitters = unip(ks.emitters);
+		const uint32_t num_emitters = uni(ks.num_emitters);
 		uint32_t j = idx;
 		/* (emitter, light) of this sample: emitters in scene order, the hit object skipped */
 		uint32_t e = 0;
-		for (; e < S.num_emitters; e++) {
+		for (; e < num_emitters; e++) {
 			const uint32_t eo = emitters[e].obj, enl = emitters[e].num_lights;
 			if (eo == obj)
 				continue;
@@ -871,34 +1026,38 @@ __global__ __launch_bounds__(WAVE, OCC) void k_shadow(DScene S, const DNode *__r
 				break;
 			j -= enl;
 		}
-		if (e >= S.num_emitters)
+		if (e >= num_emitters)
 			e = 0;
 		const DEmitter &E = emitters[e];
-		float u1, u2;
-		draw(P, key_of(__float_as_uint(q4.y), __float_as_uint(q4.z)), e, j, u1, u2);
+		float u1 = 0.5f, u2 = 0.5f;
+		if (uni(ks.rng) != RTX_RNG_CONST) /* the key already carries the seed (rtx_key_pixel) */
+			rtx_draw2(key_of(__float_as_uint(q4.y), __float_as_uint(q4.z)), e, j, &u1, &u2);
 		const f3 lp = light_point(E, p, u1, u2);
 		const f3 dv = sub3(lp, p);
 		const float ldist = mag3(dv);
 		const float dsq = magsqr3(dv);
 		const f3 ldir = mul3s(dv, 1.f / ldist);
 		f3 li = ld3(E.li);
-		bool blocked;
-		shadow_packet<COUNT>(nodes, prims, mats, planes, S.num_planes, S.root_ref, pstk, act, p, ldir, ldist,
-				     E.obj, li, blocked, sc);
+		const bool blocked = shadow_packet<COUNT>((const char *)unip(ks.recs), unip(ks.mats), unip(ks.planes),
+							  uni(ks.num_planes), uni(ks.root_ref), act, p, ldir, ldist, E.obj,
+							  li, sc);
+		reread_barrier();
 		f3 contribution = mk3(0.f, 0.f, 0.f);
 		if (act && !blocked) {
-			/* shading terms re-read after the traversal to keep them out of its registers */
-			const float4 q1 = rec[1], q2 = rec[2], q3 = rec[3];
+			/* shading terms (render.c:199-228) read after the traversal */
+			const float4 *r = unip(ks.sp) + (size_t)(blockIdx.x * uni(ks.per_wave) + k) * SPREC;
+			const float4 q1 = r[1], q2 = r[2], q3 = r[3];
 			const f3 n = mk3(q1.x, q1.y, q1.z), dir = mk3(q2.x, q2.y, q2.z);
 			const float a = dot3(ldir, n);
-			if (P.attenuation == RTX_ATT_LIN)
-				li = mul3s(li, 1.f / (P.att_offset + ldist));
-			else if (P.attenuation == RTX_ATT_SQR)
-				li = mul3s(li, 1.f / (P.att_offset + dsq));
-			const DMaterial &m = mats[__float_as_uint(q3.w)];
+			const int32_t att = (int32_t)uni((uint32_t)ks.attenuation);
+			if (att == RTX_ATT_LIN)
+				li = mul3s(li, 1.f / (ks.att_offset + ldist));
+			else if (att == RTX_ATT_SQR)
+				li = mul3s(li, 1.f / (ks.att_offset + dsq));
+			const DMaterial &m = unip(ks.mats)[__float_as_uint(q3.w)];
 			const f3 diff = mul3s(mul3v(mk3(q3.x, q3.y, q3.z), li), fmaxf(0.f, a));
 			float sm;
-			if (P.reflection == RTX_BLINN) {
+			if ((int32_t)uni((uint32_t)ks.reflection) == RTX_BLINN) {
 				sm = -dot3(n, norm3(add3(mul3s(ldir, -1.f), dir)));
 			} else {
 				sm = -dot3(sub3(mul3s(n, 2.f * a), ldir), dir);
@@ -907,7 +1066,8 @@ __global__ __launch_bounds__(WAVE, OCC) void k_shadow(DScene S, const DNode *__r
 			contribution = add3(diff, spec);
 		}
 		/* per-shade-point sums; lanes are ordered by k */
-		const uint32_t last_slot_lane = (min(total - base, slots_per_packet) - 1) * slot_b;
+		const uint32_t t2 = uni(off[WAVE]), sb = uni(ks.slot_b), spp = WAVE / sb;
+		const uint32_t last_slot_lane = (min(t2 - base, spp) - 1) * sb;
 		const uint32_t k0 = readlane(k, 0), k1 = readlane(k, last_slot_lane);
 		for (uint32_t kk = k0; kk <= k1; kk++) {
 			const bool in = act && k == kk;
@@ -916,18 +1076,30 @@ __global__ __launch_bounds__(WAVE, OCC) void k_shadow(DScene S, const DNode *__r
 			const float sx = wave_sum(in ? contribution.x : 0.f);
 			const float sy = wave_sum(in ? contribution.y : 0.f);
 			const float sz = wave_sum(in ? contribution.z : 0.f);
-			if (lane_id() == kk)
-				L = add3(L, mk3(sx, sy, sz));
+			if (lane_id() == 0) {
+				Ls[0][kk] += sx;
+				Ls[1][kk] += sy;
+				Ls[2][kk] += sz;
+			}
 		}
+		lds_sync();
+		base += spp;
 	}
+	reread_barrier();
 	if (own) {
+		const float4 *my = unip(ks.sp) + (size_t)(j0 + lane_id()) * SPREC;
 		const float4 q0 = my[0], q1 = my[1], q2 = my[2], q5 = my[5];
 		const f3 w = mk3(q0.w, q1.w, q2.w);
-		const f3 c = mul3v(w, L);
-		contrib[j0 + lane_id()] = make_float4(c.x, c.y, c.z, q5.x);
+		const f3 c = mul3v(w, mk3(Ls[0][lane_id()], Ls[1][lane_id()], Ls[2][lane_id()]));
+		unip(ks.contrib)[j0 + lane_id()] = make_float4(c.x, c.y, c.z, q5.x);
 	}
+	uint32_t n_rays = own ? nls[lane_id()] : 0u;
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1)
+		n_rays += __shfl_xor(n_rays, o, WAVE);
 	if (lane_id() == 0) {
-		atomicAdd(&ctr[RTX_C_SHADOW], n_rays);
+		unsigned long long *ctr = unip(ks.ctr);
+		atomicAdd(&ctr[RTX_C_SHADOW], (u64)n_rays);
 		if (COUNT) {
 			atomicAdd(&ctr[RTX_C_SNODES], sc.nodes);
 			atomicAdd(&ctr[RTX_C_STRIS], sc.tris);
@@ -1109,7 +1281,8 @@ extern "C" size_t rtx_trace_lds_bytes(uint32_t stack_size)
 
 extern "C" size_t rtx_shadow_lds_bytes(uint32_t stack_size)
 {
-	return 80 * 4 + (((size_t)stack_size + 3) & ~3ull) * 4;
+	(void)stack_size; /* static LDS only; the packet stack lives in a VGPR (depth <= 63, checked at upload) */
+	return 0;
 }
 
 extern "C" hipError_t rtx_trace_occupancy(uint32_t stack_size, int *blocks_per_cu)
@@ -1138,25 +1311,47 @@ extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const
 					uint32_t per_wave, uint32_t slot_b, float4 *contrib, unsigned long long *ctr,
 					int count, hipStream_t stream)
 {
-	const size_t lds = rtx_shadow_lds_bytes(S->stack_size);
 	const uint32_t grid = (n_sp + per_wave - 1) / per_wave;
 	if (!grid)
 		return hipSuccess;
-	/* occupancy variant: RTX_SHADOW_OCC = 0 (compiler's choice), 7 or 8 waves/SIMD (register caps) */
+	if (!slot_b || (slot_b & (slot_b - 1)) || slot_b > WAVE || !per_wave || per_wave > WAVE)
+		return hipErrorInvalidValue;
+	KShadow ka;
+	ka.recs = S->nodes;
+	ka.mats = S->mats;
+	ka.planes = S->planes;
+	ka.emitters = S->emitters;
+	ka.sp = sp;
+	ka.contrib = contrib;
+	ka.ctr = ctr;
+	ka.nnodes = S->num_nodes;
+	ka.root_ref = S->root_ref;
+	ka.num_planes = S->num_planes;
+	ka.num_emitters = S->num_emitters;
+	ka.n_sp = n_sp;
+	ka.per_wave = per_wave;
+	ka.slot_b = slot_b;
+	ka.slot_lg = (uint32_t)__builtin_ctz(slot_b);
+	ka.rng = P->rng;
+	ka.attenuation = P->attenuation;
+	ka.reflection = P->reflection;
+	ka.att_offset = P->att_offset;
+	/* occupancy variant: RTX_SHADOW_OCC = 1 (compiler's choice), 6, 7 or 8 waves/SIMD (register caps) */
 	static int occ = -1;
 	if (occ < 0) {
 		const char *e = getenv("RTX_SHADOW_OCC");
 		occ = e ? atoi(e) : RTX_SHADOW_OCC_DEFAULT;
 	}
 #define RTX_LAUNCH_SHADOW(C, O)                                                                                  \
-	hipLaunchKernelGGL((k_shadow<C, O>), dim3(grid), dim3(WAVE), lds, stream, *S, S->nodes, S->prims, S->mats,     \
-			   S->planes, S->emitters, *P, sp, n_sp, per_wave, slot_b, contrib, ctr)
+	hipLaunchKernelGGL((k_shadow<C, O>), dim3(grid), dim3(WAVE), 0, stream, ka)
 	if (count)
 		RTX_LAUNCH_SHADOW(true, 1);
 	else if (occ == 8)
 		RTX_LAUNCH_SHADOW(false, 8);
 	else if (occ == 7)
 		RTX_LAUNCH_SHADOW(false, 7);
+	else if (occ == 6)
+		RTX_LAUNCH_SHADOW(false, 6);
 	else
 		RTX_LAUNCH_SHADOW(false, 1);
 #undef RTX_LAUNCH_SHADOW

@@ -20,7 +20,7 @@ from .abi import (Frame, Params, SceneDesc, Stats, RTX_OK)  # noqa: F401
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO_ROOT = os.path.dirname(PKG_DIR)
 LIB_DIR = os.path.join(PKG_DIR, "lib")
-LIBRTX = os.path.join(LIB_DIR, "librtx.so")
+LIBRTX = os.environ.get("RTX_LIBRTX") or os.path.join(LIB_DIR, "librtx.so")  # override: build variants
 LIBSCENE = os.path.join(LIB_DIR, "librtxscene.so")
 ENGINE = os.path.join(LIB_DIR, "engine")
 
