@@ -5,6 +5,7 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <float.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
@@ -26,9 +27,13 @@ extern "C" hipError_t rtx_launch_trace(const DScene *S, const DFrame *F, const D
 				       float4 *sp_out, uint32_t sp_cap, uint2 *tile_rec, uint32_t tile_begin,
 				       uint32_t tile_end, unsigned long long *ctr, uint32_t waves, int count,
 				       hipStream_t stream);
-extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const float4 *sp, uint32_t n_sp,
-					uint32_t per_wave, uint32_t slot_b, float4 *contrib, unsigned long long *ctr,
-					int count, hipStream_t stream);
+extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const float4 *sp, const uint32_t *perm,
+					uint32_t n_sp, uint32_t per_wave, uint32_t slot_b, float4 *contrib,
+					unsigned long long *ctr, int count, hipStream_t stream);
+extern "C" hipError_t rtx_spsort_temp_bytes(uint32_t n, size_t *bytes);
+extern "C" hipError_t rtx_launch_spsort(const float4 *sp, uint32_t n, const float lo[3], const float hi[3],
+					uint32_t *keys0, uint32_t *keys1, uint32_t *vals0, uint32_t *vals1, void *temp,
+					size_t temp_bytes, const uint32_t **perm, hipStream_t stream);
 extern "C" hipError_t rtx_launch_accum(const DFrame *F, const DParams *P, const uint2 *tile_rec,
 				       const float4 *contrib, uint32_t tile_begin, uint32_t ntiles, float *rgb,
 				       hipStream_t stream);
@@ -76,6 +81,11 @@ struct rtx_ctx {
 	size_t contrib_bytes = 0;
 	uint2 *d_tile_rec = nullptr;
 	size_t tile_rec_bytes = 0;
+	uint32_t *d_sortbuf = nullptr; /* keys0 | keys1 | vals0 | vals1 (shade-point sort) */
+	size_t sortbuf_bytes = 0;
+	void *d_sorttmp = nullptr;
+	size_t sorttmp_bytes = 0;
+	float bound_lo[3] = { 0, 0, 0 }, bound_hi[3] = { 0, 0, 0 }; /* bounded objects' box */
 	hipEvent_t ev[4] = { nullptr, nullptr, nullptr, nullptr };
 	uint32_t total_lights = 0;
 	unsigned long long *d_ctr = nullptr;
@@ -142,6 +152,8 @@ extern "C" void rtx_close(rtx_ctx *c)
 		(void)hipStreamSynchronize(c->stream);
 	free_scene(c);
 	dfree(c->d_tasks);
+	dfree(c->d_sortbuf);
+	dfree(c->d_sorttmp);
 	dfree(c->d_staging);
 	dfree(c->d_sp);
 	dfree(c->d_contrib);
@@ -291,6 +303,15 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 			hi[3 * (size_t)k + a] = pad_hi(h[a], ext);
 		}
 	}
+	for (int a = 0; a < 3; a++) {
+		c->bound_lo[a] = FLT_MAX;
+		c->bound_hi[a] = -FLT_MAX;
+	}
+	for (uint32_t k = 0; k < nb; k++)
+		for (int a = 0; a < 3; a++) {
+			c->bound_lo[a] = std::min(c->bound_lo[a], lo[3 * (size_t)k + a]);
+			c->bound_hi[a] = std::max(c->bound_hi[a], hi[3 * (size_t)k + a]);
+		}
 	BvhOutput bvh;
 	BvhConfig cfg;
 	bvh_build(BvhInput{ nb, lo.data(), hi.data() }, cfg, bvh);
@@ -503,8 +524,21 @@ static int render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, f
 		}
 		const uint32_t n_sp = (uint32_t)head[RTX_C_SPCOUNT];
 		shade_points += n_sp;
-		HIP_TRY(rtx_launch_shadow(&c->scene, &P, c->d_sp, n_sp, per_wave, slot_b, c->d_contrib, c->d_ctr, p->count_traversal,
-					  stream));
+		/* shade points in Morton order of their position (rtx_sort.hip); RTX_SPSORT=0 keeps
+		 * emission order (same image, bit for bit) */
+		const uint32_t *perm = nullptr;
+		const char *se = getenv("RTX_SPSORT");
+		if (n_sp > 1 && c->scene.root_ref != RTX_EMPTY_REF && !(se && se[0] == '0')) {
+			size_t tmp = 0;
+			HIP_TRY(rtx_spsort_temp_bytes(n_sp, &tmp));
+			HIP_TRY(grow(c->d_sortbuf, c->sortbuf_bytes, (size_t)n_sp * 4 * sizeof(uint32_t)));
+			HIP_TRY(grow(c->d_sorttmp, c->sorttmp_bytes, tmp));
+			uint32_t *b = c->d_sortbuf;
+			HIP_TRY(rtx_launch_spsort(c->d_sp, n_sp, c->bound_lo, c->bound_hi, b, b + n_sp, b + 2 * (size_t)n_sp,
+						  b + 3 * (size_t)n_sp, c->d_sorttmp, c->sorttmp_bytes, &perm, stream));
+		}
+		HIP_TRY(rtx_launch_shadow(&c->scene, &P, c->d_sp, perm, n_sp, per_wave, slot_b, c->d_contrib, c->d_ctr,
+					  p->count_traversal, stream));
 		HIP_TRY(hipEventRecord(c->ev[2], stream));
 		HIP_TRY(rtx_launch_accum(&F, &P, c->d_tile_rec, c->d_contrib, begin, end - begin, d_rgb, stream));
 		HIP_TRY(hipEventRecord(c->ev[3], stream));

@@ -41,7 +41,7 @@
 #define RTX_SH_PF 1  /* touch the children's records before the current step's tests */
 #endif
 #ifndef RTX_SH_OCT
-#define RTX_SH_OCT 0 /* specialise the box test on a packet-uniform direction octant (measured slower) */
+#define RTX_SH_OCT 1 /* specialise the box test on a packet-uniform direction octant */
 #endif
 #ifndef RTX_SH_RCP
 #define RTX_SH_RCP 1 /* any-hit triangle test with v_rcp_f32 instead of IEEE 1/a */
@@ -954,8 +954,10 @@ struct KShadow {
 	const DPlane *planes;
 	const DEmitter *emitters;
 	const float4 *sp;
+	const uint32_t *perm; /* shade points in processing order (Morton-sorted), or null */
 	float4 *contrib;
 	unsigned long long *ctr;
+	uint32_t per_xcd;     /* waves per XCD slice of the grid */
 	uint32_t nnodes, root_ref, num_planes, num_emitters;
 	uint32_t n_sp, per_wave, slot_b, slot_lg;
 	int32_t rng, attenuation, reflection;
@@ -977,19 +979,27 @@ __global__ __launch_bounds__(WAVE, OCC) void k_shadow(KShadow ka)
 	__shared__ KShadow ks;
 	__shared__ uint32_t off[WAVE + 1]; /* first lane slot of each shade point, total */
 	__shared__ uint32_t nls[WAVE];     /* shadow rays of each shade point */
+	__shared__ uint32_t sid[WAVE];     /* each shade point's index in the record array */
 	__shared__ float Ls[3][WAVE];      /* per shade point light sum, in packet order */
-	const uint32_t j0 = blockIdx.x * ka.per_wave;
+	/* blocks are dispatched in order, so the resident waves cover a window of the (spatially
+	 * sorted) shade points: one compact region of the scene at a time on every XCD.
+	 * per_xcd != 0 instead gives each XCD (b % 8) its own contiguous slice (measured: 4x
+	 * slower, the slices' costs differ too much) */
+	const uint32_t w = ka.per_xcd ? (blockIdx.x & 7u) * ka.per_xcd + (blockIdx.x >> 3) : blockIdx.x;
+	const uint32_t j0 = w * ka.per_wave;
 	if (j0 >= ka.n_sp)
 		return;
 	const uint32_t cnt = min(ka.per_wave, ka.n_sp - j0);
 	const bool own = lane_id() < cnt;
-	const uint32_t nl_mine = own ? __float_as_uint(ka.sp[(size_t)(j0 + lane_id()) * SPREC + 4].w) : 0u;
+	const uint32_t my_sid = own ? (ka.perm ? ka.perm[j0 + lane_id()] : j0 + lane_id()) : 0u;
+	const uint32_t nl_mine = own ? __float_as_uint(ka.sp[(size_t)my_sid * SPREC + 4].w) : 0u;
 	/* each point's samples occupy whole lane slots of B lanes (B = power of two), so a point's
 	 * packet partial sums never depend on which other points share its wave: deterministic */
 	uint32_t total;
 	const uint32_t ex = wave_excl_scan((nl_mine + ka.slot_b - 1) >> ka.slot_lg, &total);
 	off[lane_id()] = ex;
 	nls[lane_id()] = nl_mine;
+	sid[lane_id()] = my_sid;
 	Ls[0][lane_id()] = 0.f;
 	Ls[1][lane_id()] = 0.f;
 	Ls[2][lane_id()] = 0.f;
@@ -1004,12 +1014,11 @@ __global__ __launch_bounds__(WAVE, OCC) void k_shadow(KShadow ka)
 		const uint32_t tot = uni(off[WAVE]), slot_b = uni(ks.slot_b), slot_lg = uni(ks.slot_lg);
 		if (base >= tot)
 			break;
-		const uint32_t jw = blockIdx.x * uni(ks.per_wave);
 		const uint32_t slot = base + (lane_id() >> slot_lg);
 		const uint32_t k = slot < tot ? owner_of(off, slot) : 0u;
 		const uint32_t idx = ((slot - off[k]) << slot_lg) + (lane_id() & (slot_b - 1));
 		const bool act = slot < tot && idx < nls[k];
-		const float4 *rec = unip(ks.sp) + (size_t)(jw + k) * SPREC;
+		const float4 *rec = unip(ks.sp) + (size_t)sid[k] * SPREC;
 		const float4 q0 = rec[0], q4 = rec[4];
 		const f3 p = mk3(q0.x, q0.y, q0.z);
 		const uint32_t obj = __float_as_uint(q4.x);
@@ -1045,7 +1054,7 @@ __global__ __launch_bounds__(WAVE, OCC) void k_shadow(KShadow ka)
 		f3 contribution = mk3(0.f, 0.f, 0.f);
 		if (act && !blocked) {
 			/* shading terms (render.c:199-228) read after the traversal */
-			const float4 *r = unip(ks.sp) + (size_t)(blockIdx.x * uni(ks.per_wave) + k) * SPREC;
+			const float4 *r = unip(ks.sp) + (size_t)sid[k] * SPREC;
 			const float4 q1 = r[1], q2 = r[2], q3 = r[3];
 			const f3 n = mk3(q1.x, q1.y, q1.z), dir = mk3(q2.x, q2.y, q2.z);
 			const float a = dot3(ldir, n);
@@ -1087,11 +1096,11 @@ __global__ __launch_bounds__(WAVE, OCC) void k_shadow(KShadow ka)
 	}
 	reread_barrier();
 	if (own) {
-		const float4 *my = unip(ks.sp) + (size_t)(j0 + lane_id()) * SPREC;
+		const float4 *my = unip(ks.sp) + (size_t)my_sid * SPREC;
 		const float4 q0 = my[0], q1 = my[1], q2 = my[2], q5 = my[5];
 		const f3 w = mk3(q0.w, q1.w, q2.w);
 		const f3 c = mul3v(w, mk3(Ls[0][lane_id()], Ls[1][lane_id()], Ls[2][lane_id()]));
-		unip(ks.contrib)[j0 + lane_id()] = make_float4(c.x, c.y, c.z, q5.x);
+		unip(ks.contrib)[my_sid] = make_float4(c.x, c.y, c.z, q5.x);
 	}
 	uint32_t n_rays = own ? nls[lane_id()] : 0u;
 #pragma unroll
@@ -1307,13 +1316,15 @@ extern "C" hipError_t rtx_launch_trace(const DScene *S, const DFrame *F, const D
 	return hipGetLastError();
 }
 
-extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const float4 *sp, uint32_t n_sp,
-					uint32_t per_wave, uint32_t slot_b, float4 *contrib, unsigned long long *ctr,
-					int count, hipStream_t stream)
+extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const float4 *sp, const uint32_t *perm,
+					uint32_t n_sp, uint32_t per_wave, uint32_t slot_b, float4 *contrib,
+					unsigned long long *ctr, int count, hipStream_t stream)
 {
-	const uint32_t grid = (n_sp + per_wave - 1) / per_wave;
-	if (!grid)
+	const uint32_t nw = (n_sp + per_wave - 1) / per_wave;
+	if (!nw)
 		return hipSuccess;
+	const char *xe = getenv("RTX_XCDMAP");
+	const uint32_t per_xcd = (xe && xe[0] == '1') ? (nw + 7) / 8 : 0u, grid = per_xcd ? 8 * per_xcd : nw;
 	if (!slot_b || (slot_b & (slot_b - 1)) || slot_b > WAVE || !per_wave || per_wave > WAVE)
 		return hipErrorInvalidValue;
 	KShadow ka;
@@ -1322,6 +1333,8 @@ extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const
 	ka.planes = S->planes;
 	ka.emitters = S->emitters;
 	ka.sp = sp;
+	ka.perm = perm;
+	ka.per_xcd = per_xcd;
 	ka.contrib = contrib;
 	ka.ctr = ctr;
 	ka.nnodes = S->num_nodes;

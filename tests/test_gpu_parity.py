@@ -187,6 +187,19 @@ def test_gpu_deterministic_and_sharding_exact(renderer):
     assert (tot[0], tot[1]) == (sa.closest_rays, sa.shadow_rays)
 
 
+@pytest.mark.parametrize("name", ["s3_path2", "s5_path2"])
+def test_gpu_shade_point_order_is_invisible(renderer, name, monkeypatch):
+    """k_shadow's Morton ordering of shade points (rtx_sort.hip) changes only which wave
+    computes a point: the image and ray counts are bit-identical to emission order."""
+    scene, frame, params, _ = C.load_config(name)
+    params.rng = abi.RTX_RNG_COUNTER
+    a, za, sa = render(renderer, scene, frame, params)
+    monkeypatch.setenv("RTX_SPSORT", "0")
+    b, zb, sb = render(renderer, scene, frame, params)
+    assert np.array_equal(a, b) and np.array_equal(za, zb)
+    assert (sa.closest_rays, sa.shadow_rays) == (sb.closest_rays, sb.shadow_rays)
+
+
 def test_gpu_shard_leaves_other_tiles_untouched(renderer):
     scene, frame, params, _ = C.load_config("s1_amb")
     params.tile_offset, params.tile_stride = 1, 2

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Sum rocprofv3 counter_collection CSVs per (kernel, counter): pmc_table.py dir [dir...]"""
 import csv, sys, collections
-for d in sys.argv[1:]:
+for d in [a for a in sys.argv[1:] if not a.endswith(".log")]:
     tot = collections.defaultdict(float)
     n = collections.Counter()
     for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
