@@ -730,6 +730,12 @@ typedef const v16u __attribute__((address_space(4))) *crec_t;
 
 __device__ __forceinline__ v16u rec_load(const char *recs, uint32_t off) { return *(crec_t)(recs + off); }
 
+/* the same for other read-only scene tables indexed by wave-uniform values (s_load) */
+template <typename T> __device__ __forceinline__ const __attribute__((address_space(4))) T *cptr(const T *p)
+{
+	return (const __attribute__((address_space(4))) T *)p;
+}
+
 /* prefetch: one dword of a record (s_load_dword), which brings its 64-byte line into the
  * scalar cache and L2 while this step computes.  Issued by inline asm so the compiler neither
  * sinks it nor waits for it; its destination SGPR stays live (hence untouched) until
@@ -817,8 +823,8 @@ __device__ __forceinline__ bool shadow_prim(const v16u &pr, const DMaterial *__r
 	if (!ballot(h))
 		return false;
 	if (meta & RTX_META_TRANSPARENT) {
-		const DMaterial &m = mats[meta & RTX_META_MAT];
-		const f3 kt = mk3(m.kt[0], m.kt[1], m.kt[2]);
+		const auto *m = cptr(mats) + (meta & RTX_META_MAT);
+		const f3 kt = mk3(m->kt[0], m->kt[1], m->kt[2]);
 		if (h)
 			li = mul3v(li, kt);
 		return false;
@@ -826,6 +832,41 @@ __device__ __forceinline__ bool shadow_prim(const v16u &pr, const DMaterial *__r
 	if (h)
 		tl = -1.f;
 	return true;
+}
+
+/* the walk's child decision, branch-free on the scalar unit (the compiler's version of the
+ * same logic spends ~2x the SALU instructions, and the shared scalar unit is what the packet
+ * walk saturates first).  Near child first for the packet's direction octant (order bit
+ * `oct` of the node's order mask; any order is correct).  Returns the near child if its box
+ * is hit by any live ray, else the far child if hit, else RTX_NONE (pop); when both are hit
+ * the far child is pushed: lane sp of the VGPR stack <- far, sp += 1.  A miss writes NONE
+ * into lane sp, above the stack top. */
+__device__ __forceinline__ uint32_t node_step(u64 b0, u64 b1, uint32_t r0, uint32_t r1, uint32_t order, uint32_t oct,
+					      uint32_t &sp, uint32_t &stk)
+{
+	uint32_t next, push, rn, rf, t;
+	u64 bn, bf;
+	asm volatile("s_bitcmp1_b32 %[ord], %[oct]\n\t"
+		     "s_cselect_b32 %[rn], %[r0], %[r1]\n\t"
+		     "s_cselect_b32 %[rf], %[r1], %[r0]\n\t"
+		     "s_cselect_b64 %[bn], %[b0], %[b1]\n\t"
+		     "s_cselect_b64 %[bf], %[b1], %[b0]\n\t"
+		     "s_cmp_lg_u64 %[bf], 0\n\t"
+		     "s_cselect_b32 %[rf], %[rf], -1\n\t"
+		     "s_cmp_lg_u64 %[bn], 0\n\t"
+		     "s_cselect_b32 %[next], %[rn], %[rf]\n\t"
+		     "s_cselect_b32 %[push], %[rf], -1\n\t"
+		     "v_mov_b32 %[t], %[push]\n\t"
+		     "v_cmp_eq_u32 vcc, %[sp], %[lane]\n\t"
+		     "v_cndmask_b32 %[stk], %[stk], %[t], vcc\n\t"
+		     "s_cmp_lg_u32 %[push], -1\n\t"
+		     "s_addc_u32 %[sp], %[sp], 0"
+		     : [next] "=&s"(next), [push] "=&s"(push), [rn] "=&s"(rn), [rf] "=&s"(rf), [bn] "=&s"(bn),
+		       [bf] "=&s"(bf), [t] "=&v"(t), [sp] "+s"(sp), [stk] "+v"(stk)
+		     : [b0] "s"(b0), [b1] "s"(b1), [r0] "s"(r0), [r1] "s"(r1), [ord] "s"(order), [oct] "s"(oct),
+		       [lane] "v"(lane_id())
+		     : "scc", "vcc");
+	return next;
 }
 
 /* is_light_blocked for one packet of shadow rays (accel.c:317-387): the 64 rays walk the BVH
@@ -846,6 +887,7 @@ __device__ __forceinline__ void shadow_walk(const char *__restrict__ recs, const
 		const v16u rec = rec_load(recs, ref & RTX_REF_OFF);
 		if (RTX_SH_PF)
 			consume(pf0, pf1, rec[15]);
+		uint32_t next = RTX_NONE; /* RTX_NONE: pop */
 		if (!(ref & RTX_REF_LEAF)) {
 			if (RTX_SH_PF) {
 				pf0 = touch(recs, rec[12] & RTX_REF_OFF);
@@ -855,22 +897,7 @@ __device__ __forceinline__ void shadow_walk(const char *__restrict__ recs, const
 				sc.nodes += popc64(ballot(tl >= 0.f));
 			const u64 b0 = ballot(box_hit<OCT>(rec, 0, oi, inv, tl));
 			const u64 b1 = ballot(box_hit<OCT>(rec, 6, oi, inv, tl));
-			/* near child first for the packet's direction octant (any order is correct) */
-			const bool lf = (rec[14] >> oct) & 1u;
-			const uint32_t rn = lf ? rec[12] : rec[13], rf = lf ? rec[13] : rec[12];
-			const u64 bn = lf ? b0 : b1, bf = lf ? b1 : b0;
-			if (bn) {
-				if (bf) {
-					stk = lane_id() == sp ? rf : stk;
-					sp++;
-				}
-				ref = rn;
-				continue;
-			}
-			if (bf) {
-				ref = rf;
-				continue;
-			}
+			next = node_step(b0, b1, rec[12], rec[13], rec[14], oct, sp, stk);
 		} else {
 			const uint32_t off = ref & RTX_REF_OFF, cnt = (ref & RTX_REF_CNT) + 1;
 			if (RTX_SH_PF) { /* the leaf's second primitive and the stack top (next pop) */
@@ -882,11 +909,14 @@ __device__ __forceinline__ void shadow_walk(const char *__restrict__ recs, const
 				blk |= shadow_prim<COUNT>(rec_load(recs, off + k * (uint32_t)sizeof(DNode)), mats, o, d, tl, emit_u,
 							 emit_obj, li, sc);
 			if (blk && !ballot(tl >= 0.f))
-				break; /* every ray of the packet is blocked */
+				sp = 0; /* every ray of the packet is blocked: end the walk */
 		}
-		if (sp == 0)
-			break;
-		ref = readlane(stk, --sp);
+		if (next == RTX_NONE) {
+			if (sp == 0)
+				break;
+			next = readlane(stk, --sp);
+		}
+		ref = next;
 	}
 	if (RTX_SH_PF)
 		drain(pf0, pf1);
@@ -901,19 +931,16 @@ __device__ __forceinline__ bool shadow_packet(const char *__restrict__ recs, con
 					      bool act, f3 o, f3 d, float dist, uint32_t emit_obj, f3 &li, ShadowCount &sc)
 {
 	float tl = act ? dist : -1.f;
-	if (act) {
-		for (uint32_t i = 0; i < num_planes; i++) {
-			const DPlane &pl = planes[i];
-			float t;
-			if (hit_plane(ld3(pl.n), pl.d, o, d, pl.eps, t) && t < dist) {
-				const DMaterial &m = mats[pl.mat];
-				if (m.flags & RTX_MF_TRANSPARENT) {
-					li = mul3v(li, ld3(m.kt));
-				} else {
-					tl = -1.f;
-					break;
-				}
-			}
+	for (uint32_t i = 0; i < num_planes; i++) { /* plane records are wave-uniform: s_load */
+		const auto *pl = cptr(planes) + i;
+		const auto *m = cptr(mats) + pl->mat;
+		float t;
+		const bool h = hit_plane(mk3(pl->n[0], pl->n[1], pl->n[2]), pl->d, o, d, pl->eps, t) && t < dist && tl >= 0.f;
+		if (m->flags & RTX_MF_TRANSPARENT) {
+			if (h)
+				li = mul3v(li, mk3(m->kt[0], m->kt[1], m->kt[2]));
+		} else if (h) {
+			tl = -1.f;
 		}
 	}
 	if (COUNT)
