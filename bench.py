@@ -211,17 +211,19 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     rays = 0
-    kms = []
+    kms, sms = [], []
     for i in range(a.steps):
         s, _ = step()
         rays += s.closest_rays + s.shadow_rays
         kms.append(s.kernel_ms)
+        sms.append(s.shadow_ms)
     torch.cuda.synchronize(dev)
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     stats_closest, stats_shadow = s.closest_rays, s.shadow_rays
-    split = {"trace_ms": round(s.trace_ms, 3), "shadow_ms": round(s.shadow_ms, 3), "accum_ms": round(s.accum_ms, 3),
+    split = {"trace_ms": round(s.trace_ms, 3), "sort_ms": round(s.sort_ms, 3), "shadow_ms": round(s.shadow_ms, 3),
+             "accum_ms": round(s.accum_ms, 3),
              "shade_points": int(s.shade_points), "chunks": int(s.chunks)}
 
     if world > 1:
@@ -233,15 +235,19 @@ def main():
         rays = int(rr.item())
 
     kernel_ms = float(np.mean(kms))
+    shadow_ms = float(np.mean(sms))
     roofline = None
     if not a.no_count:
+        # the dominant kernel is k_shadow (~99% of device time): its algorithmic bytes per launch
+        # (SURVEY §8(d) per-ray model, counted per shadow ray by a counting instance of the same
+        # kernel) over its own HIP-event duration in the timed steps
         p2 = rtxpy.default_params(**{f: getattr(params, f) for f, _ in abi.Params._fields_})
         p2.count_traversal = 1
         r.render_device(frame, p2, d_rgb.data_ptr(), d_z.data_ptr(), stream.cuda_stream)
         c = r.stats()
-        algo = (64 * c.node_visits + 48 * c.tri_tests + 32 * c.sphere_tests + 16 * c.plane_tests
-                + 48 * (c.closest_rays + c.shadow_rays))
-        achieved = algo / (kernel_ms * 1e-3) / 1e9
+        algo = (64 * c.shadow_node_visits + 48 * c.shadow_tri_tests + 32 * c.shadow_sphere_tests
+                + 16 * c.shadow_plane_tests + 48 * c.shadow_rays)
+        achieved = algo / (shadow_ms * 1e-3) / 1e9
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
@@ -254,13 +260,16 @@ def main():
             except (OSError, ValueError, KeyError):
                 traffic = None
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "algorithmic_bytes_per_launch": int(algo), "node_visits": int(c.node_visits),
-                    "tri_tests": int(c.tri_tests), "sphere_tests": int(c.sphere_tests),
-                    "plane_tests": int(c.plane_tests), "kernel_ms": round(kernel_ms, 3),
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": "k_shadow",
+                    "algorithmic_bytes_per_launch": int(algo), "shadow_rays": int(c.shadow_rays),
+                    "node_visits": int(c.shadow_node_visits), "tri_tests": int(c.shadow_tri_tests),
+                    "sphere_tests": int(c.shadow_sphere_tests), "plane_tests": int(c.shadow_plane_tests),
+                    "kernel_ms": round(shadow_ms, 3),
                     "note": "B_ray = 64*node_visits + 48*tri_tests + 32*sphere_tests + 16*plane_tests + 48 "
-                            "(SURVEY §8(d)); visits counted per ray (lane) by a counting instance of the "
-                            "same kernel; duration = HIP events around rtx_render_device's launch"}
+                            "per shadow ray (SURVEY §8(d)), visits counted per ray (lane); frac > 1 because a "
+                            "64-ray packet fetches each 64-B record once (s_load_dwordx16) and the BVH is "
+                            "L2/MALL-resident: the kernel is issue-bound, see DESIGN.md §5; traffic = PMC "
+                            "L2->fabric bytes per launch (2*FETCH_SIZE + WRITE_SIZE, profiles/)"}
 
     cpu = port = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -86,7 +86,7 @@ struct rtx_ctx {
 	void *d_sorttmp = nullptr;
 	size_t sorttmp_bytes = 0;
 	float bound_lo[3] = { 0, 0, 0 }, bound_hi[3] = { 0, 0, 0 }; /* bounded objects' box */
-	hipEvent_t ev[4] = { nullptr, nullptr, nullptr, nullptr };
+	hipEvent_t ev[5] = { nullptr, nullptr, nullptr, nullptr, nullptr };
 	uint32_t total_lights = 0;
 	unsigned long long *d_ctr = nullptr;
 	float *d_rgb = nullptr, *d_z = nullptr;
@@ -195,6 +195,7 @@ extern "C" int rtx_open(int device, rtx_ctx **out)
 	    (e = hipEventCreate(&c->ev0)) != hipSuccess || (e = hipEventCreate(&c->ev1)) != hipSuccess ||
 	    (e = hipEventCreate(&c->ev[0])) != hipSuccess || (e = hipEventCreate(&c->ev[1])) != hipSuccess ||
 	    (e = hipEventCreate(&c->ev[2])) != hipSuccess || (e = hipEventCreate(&c->ev[3])) != hipSuccess ||
+	    (e = hipEventCreate(&c->ev[4])) != hipSuccess ||
 	    (e = hipMalloc(&c->d_ctr, sizeof(unsigned long long) * RTX_C_N)) != hipSuccess) {
 		rtx_close(c);
 		return fail(RTX_ERR_HIP, "context setup failed: %s", hipGetErrorString(e));
@@ -369,11 +370,20 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 	if (((uint64_t)nnodes + nb) * sizeof(DNode) > 0xFFFFFFC0ull)
 		return fail(RTX_ERR_SCENE, "scene too large: %u BVH nodes + %u primitives exceed 4 GB of records", nnodes, nb);
 	/* builder refs (node index | RTX_LEAF_BIT leaf) -> device refs (record byte offset | leaf bits) */
-	auto dref = [nnodes](uint32_t r) -> uint32_t {
+	auto dref = [nnodes, &prims](uint32_t r) -> uint32_t {
 		if (r == RTX_EMPTY_REF)
 			return r;
-		if (r & RTX_LEAF_BIT)
-			return (nnodes + ((r >> 4) & 0x7FFFFFFu)) * (uint32_t)sizeof(DNode) | RTX_REF_LEAF | (r & 15u);
+		if (r & RTX_LEAF_BIT) {
+			const uint32_t first = (r >> 4) & 0x7FFFFFFu, cnt = (r & 15u) + 1;
+			uint32_t sph = 0;
+			for (uint32_t k = first; k < first + cnt; k++) {
+				uint32_t meta;
+				memcpy(&meta, &prims[k].c[3], 4);
+				if ((meta >> 24) == RTX_SPHERE)
+					sph = RTX_REF_SPH;
+			}
+			return (nnodes + first) * (uint32_t)sizeof(DNode) | RTX_REF_LEAF | sph | (cnt - 1);
+		}
 		return r * (uint32_t)sizeof(DNode);
 	};
 	std::vector<DNode> recs(nnodes + (size_t)nb);
@@ -483,7 +493,7 @@ static int render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, f
 
 	HIP_TRY(hipMemsetAsync(c->d_ctr, 0, sizeof(unsigned long long) * RTX_C_N, stream));
 	HIP_TRY(hipEventRecord(c->ev0, stream));
-	double t_trace = 0, t_shadow = 0, t_accum = 0;
+	double t_trace = 0, t_sort = 0, t_shadow = 0, t_accum = 0;
 	uint64_t shade_points = 0;
 	uint32_t chunks = 0;
 	/* shadow kernel: lane slots of slot_b = pow2ceil(lights) (<= 64) lanes per point; ~16 packets per wave */
@@ -537,17 +547,20 @@ static int render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, f
 			HIP_TRY(rtx_launch_spsort(c->d_sp, n_sp, c->bound_lo, c->bound_hi, b, b + n_sp, b + 2 * (size_t)n_sp,
 						  b + 3 * (size_t)n_sp, c->d_sorttmp, c->sorttmp_bytes, &perm, stream));
 		}
+		HIP_TRY(hipEventRecord(c->ev[4], stream));
 		HIP_TRY(rtx_launch_shadow(&c->scene, &P, c->d_sp, perm, n_sp, per_wave, slot_b, c->d_contrib, c->d_ctr,
 					  p->count_traversal, stream));
 		HIP_TRY(hipEventRecord(c->ev[2], stream));
 		HIP_TRY(rtx_launch_accum(&F, &P, c->d_tile_rec, c->d_contrib, begin, end - begin, d_rgb, stream));
 		HIP_TRY(hipEventRecord(c->ev[3], stream));
 		HIP_TRY(hipEventSynchronize(c->ev[3]));
-		float a = 0, b = 0, cc = 0;
+		float a = 0, b = 0, cc = 0, so = 0;
 		HIP_TRY(hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
-		HIP_TRY(hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
+		HIP_TRY(hipEventElapsedTime(&so, c->ev[1], c->ev[4]));
+		HIP_TRY(hipEventElapsedTime(&b, c->ev[4], c->ev[2]));
 		HIP_TRY(hipEventElapsedTime(&cc, c->ev[2], c->ev[3]));
 		t_trace += a;
+		t_sort += so;
 		t_shadow += b;
 		t_accum += cc;
 		chunks++;
@@ -571,7 +584,8 @@ static int render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, f
 	st.sphere_tests = ctr[RTX_C_SPHERES] + ctr[RTX_C_SSPHERES];
 	st.plane_tests = ctr[RTX_C_PLANES] + ctr[RTX_C_SPLANES];
 	st.shade_points = shade_points;
-	st.kernel_ms = t_trace + t_shadow + t_accum;
+	st.kernel_ms = t_trace + t_sort + t_shadow + t_accum;
+	st.sort_ms = t_sort;
 	st.trace_ms = t_trace;
 	st.shadow_ms = t_shadow;
 	st.accum_ms = t_accum;

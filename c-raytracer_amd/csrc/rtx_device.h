@@ -4,7 +4,8 @@
  *  DNode  64 B  BVH2 inner node: both children's AABBs + child refs + the
  *               child order per ray-direction octant.  A ref is the byte offset
  *               of the child's 64-byte record from `nodes` (64-aligned), with
- *               RTX_REF_LEAF | (count-1) in its low bits for a leaf of count
+ *               RTX_REF_LEAF | RTX_REF_SPH (has a sphere) | (count-1) in its
+ *               low bits for a leaf of count
  *               <= 16 primitives contiguous in the record array (primitive i
  *               is record num_nodes + i).
  *               Replaces the pointer-linked struct BVH + malloc'd BoundingCuboid
@@ -29,8 +30,9 @@
 #include <stdint.h>
 
 #define RTX_LEAF_BIT 0x80000000u  /* builder-side leaf refs (bvh_build.cpp) */
-#define RTX_REF_LEAF 32u          /* device refs: byte offset | leaf flag | count-1 */
-#define RTX_REF_CNT 31u
+#define RTX_REF_LEAF 32u          /* device refs: byte offset | leaf flag | sphere flag | count-1 */
+#define RTX_REF_SPH 16u           /* leaf holds at least one sphere (else triangles only) */
+#define RTX_REF_CNT 15u
 #define RTX_REF_OFF (~63u)
 #define RTX_PLANE_BIT 0x80000000u
 #define RTX_NONE 0xFFFFFFFFu

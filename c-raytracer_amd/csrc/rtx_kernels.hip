@@ -779,8 +779,12 @@ __device__ __forceinline__ bool box_hit(const v16u &nd, const uint32_t b, f3 oi,
 	return tn <= tf;
 }
 
-/* moller_trumbore (object.c:422-441) as a branch-free any-hit test on (eps, tlim): same
- * accept conditions; 1/a by v_rcp_f32 (1 ulp) since only the hit/miss decision is used */
+/* moller_trumbore (object.c:422-441) as a branch-free any-hit test on (eps, tlim), with the
+ * same accept set for finite inputs:
+ *   reject |a| < eps;  reject u < 0, v < 0, u + v > 1 (u > 1 is implied);  accept eps < t < tlim.
+ * Whenever t is finite, f = 1/a and u, v are finite too, so the three sign conditions fold into
+ * one max3 compare and the t window into one min compare (a NaN or infinite t fails it).
+ * 1/a by v_rcp_f32 (1 ulp): only the hit/miss decision is used. */
 __device__ __forceinline__ bool any_tri(f3 v0, f3 e1, f3 e2, f3 o, f3 d, float eps, float tlim)
 {
 	const f3 h = cross3(d, e2);
@@ -791,7 +795,8 @@ __device__ __forceinline__ bool any_tri(f3 v0, f3 e1, f3 e2, f3 o, f3 d, float e
 	const f3 q = cross3(s, e1);
 	const float v = f * dot3(d, q);
 	const float t = f * dot3(e2, q);
-	return !(a < eps && a > -eps) & !(u < 0.f || u > 1.f) & !(v < 0.f || u + v > 1.f) & (t > eps) & (t < tlim);
+	const float out = fmaxf(fmaxf(-u, -v), (u + v) - 1.f); /* > 0: outside the triangle */
+	return ((int)(fabsf(a) >= eps) & (int)(out <= 0.f) & (int)(fminf(t - eps, tlim - t) > 0.f)) != 0;
 }
 
 /* one primitive of a leaf against the packet (accel.c:362-373): the target emitter skipped,
@@ -869,6 +874,35 @@ __device__ __forceinline__ uint32_t node_step(u64 b0, u64 b1, uint32_t r0, uint3
 	return next;
 }
 
+/* shadow_prim for a leaf of triangles only; tri_emit: some live ray aims at a triangle emitter
+ * (else no triangle here can be the target light and the skip test drops out) */
+template <bool COUNT>
+__device__ __forceinline__ bool shadow_tri(const v16u &pr, const DMaterial *__restrict__ mats, f3 o, f3 d, float &tl,
+					   bool tri_emit, uint32_t emit_obj, f3 &li, ShadowCount &sc)
+{
+	const uint32_t meta = pr[11];
+	if (COUNT)
+		sc.tris += popc64(ballot(tl >= 0.f));
+	bool h = any_tri(mk3(__uint_as_float(pr[0]), __uint_as_float(pr[1]), __uint_as_float(pr[2])),
+			 mk3(__uint_as_float(pr[4]), __uint_as_float(pr[5]), __uint_as_float(pr[6])),
+			 mk3(__uint_as_float(pr[8]), __uint_as_float(pr[9]), __uint_as_float(pr[10])), o, d,
+			 __uint_as_float(pr[3]), tl);
+	if (tri_emit)
+		h = h & (pr[7] != emit_obj);
+	if (!ballot(h))
+		return false;
+	if (meta & RTX_META_TRANSPARENT) {
+		const auto *m = cptr(mats) + (meta & RTX_META_MAT);
+		const f3 kt = mk3(m->kt[0], m->kt[1], m->kt[2]);
+		if (h)
+			li = mul3v(li, kt);
+		return false;
+	}
+	if (h)
+		tl = -1.f;
+	return true;
+}
+
 /* is_light_blocked for one packet of shadow rays (accel.c:317-387): the 64 rays walk the BVH
  * together.  Node and primitive records are wave-uniform (one 64-byte s_load_dwordx16 each),
  * each lane tests its own ray, the ballots pick the children.  A lane's liveness is its
@@ -878,7 +912,7 @@ __device__ __forceinline__ uint32_t node_step(u64 b0, u64 b1, uint32_t r0, uint3
 template <bool COUNT, int OCT>
 __device__ __forceinline__ void shadow_walk(const char *__restrict__ recs, const DMaterial *__restrict__ mats,
 					    uint32_t root_ref, f3 o, f3 d, f3 inv, float &tl, uint32_t emit_u,
-					    uint32_t emit_obj, uint32_t lead_oct, f3 &li, ShadowCount &sc)
+					    uint32_t emit_obj, bool tri_emit, uint32_t lead_oct, f3 &li, ShadowCount &sc)
 {
 	const f3 oi = mul3v(o, inv);
 	const uint32_t oct = OCT < 8 ? (uint32_t)OCT : lead_oct;
@@ -904,10 +938,18 @@ __device__ __forceinline__ void shadow_walk(const char *__restrict__ recs, const
 				pf0 = touch(recs, off + (cnt > 1 ? (uint32_t)sizeof(DNode) : 0u));
 				pf1 = touch(recs, sp ? readlane(stk, sp - 1) & RTX_REF_OFF : off);
 			}
-			bool blk = shadow_prim<COUNT>(rec, mats, o, d, tl, emit_u, emit_obj, li, sc);
-			for (uint32_t k = 1; k < cnt; k++)
-				blk |= shadow_prim<COUNT>(rec_load(recs, off + k * (uint32_t)sizeof(DNode)), mats, o, d, tl, emit_u,
-							 emit_obj, li, sc);
+			bool blk;
+			if (ref & RTX_REF_SPH) {
+				blk = shadow_prim<COUNT>(rec, mats, o, d, tl, emit_u, emit_obj, li, sc);
+				for (uint32_t k = 1; k < cnt; k++)
+					blk |= shadow_prim<COUNT>(rec_load(recs, off + k * (uint32_t)sizeof(DNode)), mats, o, d, tl,
+								 emit_u, emit_obj, li, sc);
+			} else {
+				blk = shadow_tri<COUNT>(rec, mats, o, d, tl, tri_emit, emit_obj, li, sc);
+				for (uint32_t k = 1; k < cnt; k++)
+					blk |= shadow_tri<COUNT>(rec_load(recs, off + k * (uint32_t)sizeof(DNode)), mats, o, d, tl,
+								tri_emit, emit_obj, li, sc);
+			}
 			if (blk && !ballot(tl >= 0.f))
 				sp = 0; /* every ray of the packet is blocked: end the walk */
 		}
@@ -928,7 +970,8 @@ __device__ __forceinline__ void shadow_walk(const char *__restrict__ recs, const
 template <bool COUNT>
 __device__ __forceinline__ bool shadow_packet(const char *__restrict__ recs, const DMaterial *__restrict__ mats,
 					      const DPlane *__restrict__ planes, uint32_t num_planes, uint32_t root_ref,
-					      bool act, f3 o, f3 d, float dist, uint32_t emit_obj, f3 &li, ShadowCount &sc)
+					      bool act, f3 o, f3 d, float dist, uint32_t emit_obj, bool emit_is_tri, f3 &li,
+					      ShadowCount &sc)
 {
 	float tl = act ? dist : -1.f;
 	for (uint32_t i = 0; i < num_planes; i++) { /* plane records are wave-uniform: s_load */
@@ -955,17 +998,18 @@ __device__ __forceinline__ bool shadow_packet(const char *__restrict__ recs, con
 	const uint32_t lead_lane = (uint32_t)__ffsll((long long)live) - 1;
 	const uint32_t lead = readlane(oct, lead_lane), lead_emit = readlane(emit_obj, lead_lane);
 	const uint32_t emit_u = ballot(alive & (emit_obj != lead_emit)) ? RTX_NONE : lead_emit;
+	const bool tri_emit = ballot(alive & emit_is_tri) != 0;
 	const uint32_t sel = (!RTX_SH_OCT || ballot(alive & (oct != lead))) ? 8u : lead;
 	switch (sel) {
 #define RTX_WALK(K)                                                                                                   \
 	case K:                                                                                                           \
-		shadow_walk<COUNT, K>(recs, mats, root_ref, o, d, inv, tl, emit_u, emit_obj, K, li, sc);                     \
+		shadow_walk<COUNT, K>(recs, mats, root_ref, o, d, inv, tl, emit_u, emit_obj, tri_emit, K, li, sc);           \
 		break;
 #if RTX_SH_OCT
 	RTX_WALK(0) RTX_WALK(1) RTX_WALK(2) RTX_WALK(3) RTX_WALK(4) RTX_WALK(5) RTX_WALK(6) RTX_WALK(7)
 #endif
 	default:
-		shadow_walk<COUNT, 8>(recs, mats, root_ref, o, d, inv, tl, emit_u, emit_obj, lead, li, sc);
+		shadow_walk<COUNT, 8>(recs, mats, root_ref, o, d, inv, tl, emit_u, emit_obj, tri_emit, lead, li, sc);
 		break;
 #undef RTX_WALK
 	}
@@ -1076,7 +1120,7 @@ __global__ __launch_bounds__(WAVE, OCC) void k_shadow(KShadow ka)
 		f3 li = ld3(E.li);
 		const bool blocked = shadow_packet<COUNT>((const char *)unip(ks.recs), unip(ks.mats), unip(ks.planes),
 							  uni(ks.num_planes), uni(ks.root_ref), act, p, ldir, ldist, E.obj,
-							  li, sc);
+							  E.type == RTX_TRIANGLE, li, sc);
 		reread_barrier();
 		f3 contribution = mk3(0.f, 0.f, 0.f);
 		if (act && !blocked) {

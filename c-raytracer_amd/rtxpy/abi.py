@@ -62,7 +62,8 @@ class Stats(C.Structure):
                 ("shadow_node_visits", C.c_uint64), ("shadow_tri_tests", C.c_uint64),
                 ("shadow_sphere_tests", C.c_uint64), ("shadow_plane_tests", C.c_uint64),
                 ("shade_points", C.c_uint64), ("kernel_ms", C.c_double), ("trace_ms", C.c_double),
-                ("shadow_ms", C.c_double), ("accum_ms", C.c_double), ("bvh_nodes", C.c_uint32),
+                ("shadow_ms", C.c_double), ("accum_ms", C.c_double), ("sort_ms", C.c_double),
+                ("bvh_nodes", C.c_uint32),
                 ("bvh_depth", C.c_uint32), ("bvh_prims", C.c_uint32), ("waves", C.c_uint32),
                 ("chunks", C.c_uint32), ("pad", C.c_uint32)]
 

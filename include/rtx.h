@@ -188,6 +188,7 @@ typedef struct rtx_stats {
 	double trace_ms;             /* ... closest-hit / shading kernel */
 	double shadow_ms;            /* ... shadow-ray kernel */
 	double accum_ms;             /* ... per-tile accumulation kernel */
+	double sort_ms;              /* ... shade-point ordering (key + radix sort) */
 	uint32_t bvh_nodes;
 	uint32_t bvh_depth;
 	uint32_t bvh_prims;
