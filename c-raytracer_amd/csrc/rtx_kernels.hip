@@ -43,6 +43,9 @@
 #ifndef RTX_SH_OCT
 #define RTX_SH_OCT 1 /* specialise the box test on a packet-uniform direction octant */
 #endif
+#ifndef RTX_SH_PK
+#define RTX_SH_PK 0  /* slab planes by packed FMA (v_pk_fma_f32): fewer VALU, measured 3% slower */
+#endif
 #ifndef RTX_SH_RCP
 #define RTX_SH_RCP 1 /* any-hit triangle test with v_rcp_f32 instead of IEEE 1/a */
 #endif
@@ -761,21 +764,32 @@ __device__ __forceinline__ void drain(uint32_t a, uint32_t b)
  * OCT < 8: every live ray's direction lies in octant OCT (bit a set = inv[a] >= 0), so each
  * axis' entry plane is known at compile time and the per-axis min/max of `slab` drop out;
  * fma is monotone in the plane coordinate, so the answer is the same as slab()'s. */
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+/* both slab planes of one axis by one packed FMA (v_pk_fma_f32): (lo, hi) * inv - o * inv */
+__device__ __forceinline__ f2v slab_pair(uint32_t lo, uint32_t hi, float inv, float oi)
+{
+	const f2v p = { __uint_as_float(lo), __uint_as_float(hi) };
+	const f2v m = { inv, inv }, c = { -oi, -oi };
+	return RTX_SH_PK ? __builtin_elementwise_fma(p, m, c) : f2v{ fmaf(p.x, inv, -oi), fmaf(p.y, inv, -oi) };
+}
+
 template <int OCT>
 __device__ __forceinline__ bool box_hit(const v16u &nd, const uint32_t b, f3 oi, f3 inv, float tlim)
 {
+	const f2v tx = slab_pair(nd[b], nd[b + 1], inv.x, oi.x);
+	const f2v ty = slab_pair(nd[b + 2], nd[b + 3], inv.y, oi.y);
+	const f2v tz = slab_pair(nd[b + 4], nd[b + 5], inv.z, oi.z);
 	if (OCT == 8) {
-		float tn;
-		return slab(__uint_as_float(nd[b]), __uint_as_float(nd[b + 1]), __uint_as_float(nd[b + 2]),
-			    __uint_as_float(nd[b + 3]), __uint_as_float(nd[b + 4]), __uint_as_float(nd[b + 5]), oi, inv, tlim,
-			    tn);
+		const float tn = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fmaxf(fminf(tz.x, tz.y), 0.f));
+		const float tf = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fminf(fmaxf(tz.x, tz.y), tlim));
+		return tn <= tf;
 	}
-	const float nx = __uint_as_float(nd[b + ((OCT & 1) ? 0 : 1)]), fx = __uint_as_float(nd[b + ((OCT & 1) ? 1 : 0)]);
-	const float ny = __uint_as_float(nd[b + ((OCT & 2) ? 2 : 3)]), fy = __uint_as_float(nd[b + ((OCT & 2) ? 3 : 2)]);
-	const float nz = __uint_as_float(nd[b + ((OCT & 4) ? 4 : 5)]), fz = __uint_as_float(nd[b + ((OCT & 4) ? 5 : 4)]);
-	const float tn = fmaxf(fmaxf(fmaf(nx, inv.x, -oi.x), fmaf(ny, inv.y, -oi.y)), fmaxf(fmaf(nz, inv.z, -oi.z), 0.f));
-	const float tf =
-		fminf(fminf(fmaf(fx, inv.x, -oi.x), fmaf(fy, inv.y, -oi.y)), fminf(fmaf(fz, inv.z, -oi.z), tlim));
+	const float nx = (OCT & 1) ? tx.x : tx.y, fx = (OCT & 1) ? tx.y : tx.x;
+	const float ny = (OCT & 2) ? ty.x : ty.y, fy = (OCT & 2) ? ty.y : ty.x;
+	const float nz = (OCT & 4) ? tz.x : tz.y, fz = (OCT & 4) ? tz.y : tz.x;
+	const float tn = fmaxf(fmaxf(nx, ny), fmaxf(nz, 0.f));
+	const float tf = fminf(fminf(fx, fy), fminf(fz, tlim));
 	return tn <= tf;
 }
 
