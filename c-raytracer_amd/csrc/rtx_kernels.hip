@@ -46,6 +46,12 @@
 #ifndef RTX_SH_PK
 #define RTX_SH_PK 0  /* slab planes by packed FMA (v_pk_fma_f32): fewer VALU, measured 3% slower */
 #endif
+#ifndef RTX_DEBUG_NOWALK
+#define RTX_DEBUG_NOWALK 0 /* measurement only: skip the BVH walk (per-packet overhead) */
+#endif
+#ifndef RTX_SH_FMA
+#define RTX_SH_FMA 1 /* fused products in the shadow triangle test */
+#endif
 #ifndef RTX_SH_RCP
 #define RTX_SH_RCP 1 /* any-hit triangle test with v_rcp_f32 instead of IEEE 1/a */
 #endif
@@ -799,16 +805,24 @@ __device__ __forceinline__ bool box_hit(const v16u &nd, const uint32_t b, f3 oi,
  * Whenever t is finite, f = 1/a and u, v are finite too, so the three sign conditions fold into
  * one max3 compare and the t window into one min compare (a NaN or infinite t fails it).
  * 1/a by v_rcp_f32 (1 ulp): only the hit/miss decision is used. */
+__device__ __forceinline__ f3 cross3_fma(f3 a, f3 b)
+{
+	return mk3(fmaf(a.y, b.z, -a.z * b.y), fmaf(a.z, b.x, -a.x * b.z), fmaf(a.x, b.y, -a.y * b.x));
+}
+__device__ __forceinline__ float dot3_fma(f3 a, f3 b) { return fmaf(a.x, b.x, fmaf(a.y, b.y, a.z * b.z)); }
+
 __device__ __forceinline__ bool any_tri(f3 v0, f3 e1, f3 e2, f3 o, f3 d, float eps, float tlim)
 {
-	const f3 h = cross3(d, e2);
-	const float a = dot3(e1, h);
+	/* products fused (RTX_SH_FMA): 40 instead of 57 VALU; only hit decisions at exact
+	 * edges can change, as with the 1-ulp reciprocal */
+	const f3 h = RTX_SH_FMA ? cross3_fma(d, e2) : cross3(d, e2);
+	const float a = RTX_SH_FMA ? dot3_fma(e1, h) : dot3(e1, h);
 	const float f = RTX_SH_RCP ? __builtin_amdgcn_rcpf(a) : 1.f / a;
 	const f3 s = sub3(o, v0);
-	const float u = f * dot3(s, h);
-	const f3 q = cross3(s, e1);
-	const float v = f * dot3(d, q);
-	const float t = f * dot3(e2, q);
+	const float u = f * (RTX_SH_FMA ? dot3_fma(s, h) : dot3(s, h));
+	const f3 q = RTX_SH_FMA ? cross3_fma(s, e1) : cross3(s, e1);
+	const float v = f * (RTX_SH_FMA ? dot3_fma(d, q) : dot3(d, q));
+	const float t = f * (RTX_SH_FMA ? dot3_fma(e2, q) : dot3(e2, q));
 	const float out = fmaxf(fmaxf(-u, -v), (u + v) - 1.f); /* > 0: outside the triangle */
 	return ((int)(fabsf(a) >= eps) & (int)(out <= 0.f) & (int)(fminf(t - eps, tlim - t) > 0.f)) != 0;
 }
@@ -1006,7 +1020,7 @@ __device__ __forceinline__ bool shadow_packet(const char *__restrict__ recs, con
 	const u64 live = ballot(alive);
 	if (!live || root_ref == RTX_EMPTY_REF)
 		return act && !alive;
-	const f3 inv = safe_inv(d);
+	const f3 inv = safe_inv_fast(d); /* boxes are padded 2e-6 relative: a 1-ulp 1/d keeps the test conservative */
 	const uint32_t oct = ((~__float_as_uint(inv.x)) >> 31) | (((~__float_as_uint(inv.y)) >> 31) << 1) |
 			     (((~__float_as_uint(inv.z)) >> 31) << 2);
 	const uint32_t lead_lane = (uint32_t)__ffsll((long long)live) - 1;
@@ -1133,7 +1147,7 @@ __global__ __launch_bounds__(WAVE, OCC) void k_shadow(KShadow ka)
 		const f3 ldir = mul3s(dv, 1.f / ldist);
 		f3 li = ld3(E.li);
 		const bool blocked = shadow_packet<COUNT>((const char *)unip(ks.recs), unip(ks.mats), unip(ks.planes),
-							  uni(ks.num_planes), uni(ks.root_ref), act, p, ldir, ldist, E.obj,
+							  uni(ks.num_planes), RTX_DEBUG_NOWALK ? RTX_EMPTY_REF : uni(ks.root_ref), act, p, ldir, ldist, E.obj,
 							  E.type == RTX_TRIANGLE, li, sc);
 		reread_barrier();
 		f3 contribution = mk3(0.f, 0.f, 0.f);

@@ -148,6 +148,14 @@ __device__ __forceinline__ f3 safe_inv(f3 d)
 		   fabsf(d.z) > 1e-30f ? 1.f / d.z : copysignf(1e30f, d.z));
 }
 
+/* the same with v_rcp_f32 (1 ulp) for the shadow walk's culling-only box tests */
+__device__ __forceinline__ f3 safe_inv_fast(f3 d)
+{
+	return mk3(fabsf(d.x) > 1e-30f ? __builtin_amdgcn_rcpf(d.x) : copysignf(1e30f, d.x),
+		   fabsf(d.y) > 1e-30f ? __builtin_amdgcn_rcpf(d.y) : copysignf(1e30f, d.y),
+		   fabsf(d.z) > 1e-30f ? __builtin_amdgcn_rcpf(d.z) : copysignf(1e30f, d.z));
+}
+
 /* slab test on the traversal path: hit iff [max(tnear,0), min(tfar,tlim)] non-empty */
 __device__ __forceinline__ bool slab(float lox, float hix, float loy, float hiy, float loz, float hiz, f3 oi, f3 inv,
 				     float tlim, float &tnear)
