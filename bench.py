@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--scene", default="scene5", choices=["scene5", "scene5_l8", "scene6", "scene3", "scene1"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the traversal-counting pass (roofline)")
+    ap.add_argument("--no-post", action="store_true", help="skip the postprocess (DoF + mist) side leg")
     ap.add_argument("--cpu-target-s", type=float, default=12.0)
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
@@ -151,6 +152,61 @@ def cpu_reference(scene_file, flags, width, height, target_s, log):
                               f"'Commencing raytracing' -> 'Saving image' log stamps; rays from the instrumented "
                               f"build on the same config", "seconds": round(tr, 2), "rays": rays}
     return None
+
+
+POST_FLAGS = ["--dof", "3", "-13", "--mist", "6", "4", "lin", "0.5", "0.5", "0.6"]
+
+
+def post_leg(r, d_rgb, d_z, w, h, dev, log, reps=5):
+    """§8(f) #1: the postprocess path (rtx_postprocess_device) on the benchmark's own rendered
+    frame, next to the reference postprocessor (oracle/_ref/postprocess, single-threaded as it
+    ships) on the same raw frame; the 8-bit outputs are compared byte for byte."""
+    import subprocess
+    import tempfile
+    import numpy as np
+    import torch
+    import rtxpy
+    from rtxpy.tiffread import read_tiff
+    post = rtxpy.post_from_args(POST_FLAGS)
+    src = d_rgb.clone()
+    out = torch.empty_like(d_rgb)
+    stream = torch.cuda.current_stream(dev)
+    times = []
+    for i in range(reps + 1):
+        out.copy_(src)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        r.postprocess_device(post, w, h, out.data_ptr(), d_z.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        if i:
+            times.append(time.perf_counter() - t0)
+    res = {"flags": " ".join(POST_FLAGS), "gpu_ms": round(1e3 * float(np.median(times)), 3),
+           "workload": f"{w}x{h} frame rendered by this bench", "timing": "wall, median of %d, synchronised" % reps}
+    ref = os.path.join(ROOT, "oracle", "_ref", "postprocess")
+    if not os.path.exists(ref):
+        return res
+    with tempfile.TemporaryDirectory() as wd:
+        raw, o8, g8 = (os.path.join(wd, n) for n in ("in.tif", "ref.tif", "gpu.tif"))
+        rgb_h = src.cpu().numpy().reshape(h, w, 3)
+        rtxpy.write_tiff(raw, rgb_h, d_z.cpu().numpy().reshape(h, w), raw=True)
+        try:
+            p = subprocess.run([ref, raw, o8] + POST_FLAGS, capture_output=True, text=True, timeout=300)
+        except (subprocess.TimeoutExpired, OSError) as e:
+            log(f"reference postprocess unusable: {e}")
+            return res
+        if p.returncode != 0:
+            log(f"reference postprocess rc={p.returncode}")
+            return res
+        stamps = [float(l[1:l.index("]")]) for l in p.stdout.splitlines()
+                  if "Commencing Postprocessing" in l or "Saving image." in l]
+        if len(stamps) == 2:
+            res["cpu_ref_ms"] = round(1e3 * (stamps[1] - stamps[0]), 1)
+            res["cpu_ref_cores"] = 1
+        rtxpy.write_tiff(g8, out.cpu().numpy().reshape(h, w, 3))
+        res["u8_identical_to_reference"] = bool(np.array_equal(read_tiff(g8)["rgb"], read_tiff(o8)["rgb"]))
+    log(f"postprocess: gpu {res['gpu_ms']} ms, reference {res.get('cpu_ref_ms')} ms, "
+        f"identical {res.get('u8_identical_to_reference')}")
+    return res
 
 
 def main():
@@ -271,6 +327,13 @@ def main():
                             "L2/MALL-resident: the kernel is issue-bound, see DESIGN.md §5; traffic = PMC "
                             "L2->fabric bytes per launch (2*FETCH_SIZE + WRITE_SIZE, profiles/)"}
 
+    post = None
+    if rank == 0 and world == 1 and not a.no_post:
+        try:
+            post = post_leg(r, d_rgb, d_z, a.width, a.height, dev, log)
+        except Exception as e:  # never let the side leg kill the measurement
+            log(f"postprocess leg failed: {e}")
+
     cpu = port = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
@@ -300,6 +363,8 @@ def main():
             out["config"]["gpu_over_cpu"] = round(value / cpu["value"], 1)
         if port:
             out["cpu_port"] = port
+        if post:
+            out["postprocess"] = post
         print(json.dumps(out), flush=True)
     r.close()
     if world > 1:

@@ -30,6 +30,8 @@ extern "C" hipError_t rtx_launch_trace(const DScene *S, const DFrame *F, const D
 extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const float4 *sp, const uint32_t *perm,
 					uint32_t n_sp, uint32_t per_wave, uint32_t slot_b, float4 *contrib,
 					unsigned long long *ctr, int count, hipStream_t stream);
+extern "C" hipError_t rtx_launch_post(uint32_t w, uint32_t h, const rtx_post *pp, float *rgb, const float *z,
+				      int *rad, float4 *pv, unsigned *scratch, hipStream_t stream);
 extern "C" hipError_t rtx_spsort_temp_bytes(uint32_t n, size_t *bytes);
 extern "C" hipError_t rtx_launch_spsort(const float4 *sp, uint32_t n, const float lo[3], const float hi[3],
 					uint32_t *keys0, uint32_t *keys1, uint32_t *vals0, uint32_t *vals1, void *temp,
@@ -85,6 +87,10 @@ struct rtx_ctx {
 	size_t sortbuf_bytes = 0;
 	void *d_sorttmp = nullptr;
 	size_t sorttmp_bytes = 0;
+	int *d_post_rad = nullptr; /* postprocess: per-pixel DoF radius, pv, scratch */
+	float4 *d_post_pv = nullptr;
+	size_t post_pixels = 0;
+	unsigned *d_post_scratch = nullptr;
 	float bound_lo[3] = { 0, 0, 0 }, bound_hi[3] = { 0, 0, 0 }; /* bounded objects' box */
 	hipEvent_t ev[5] = { nullptr, nullptr, nullptr, nullptr, nullptr };
 	uint32_t total_lights = 0;
@@ -154,6 +160,9 @@ extern "C" void rtx_close(rtx_ctx *c)
 	dfree(c->d_tasks);
 	dfree(c->d_sortbuf);
 	dfree(c->d_sorttmp);
+	dfree(c->d_post_rad);
+	dfree(c->d_post_pv);
+	dfree(c->d_post_scratch);
 	dfree(c->d_staging);
 	dfree(c->d_sp);
 	dfree(c->d_contrib);
@@ -631,6 +640,66 @@ extern "C" int rtx_render(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, 
 		HIP_TRY(hipMemcpy(rgb, c->d_rgb, px * 12, hipMemcpyDeviceToHost));
 	if (z)
 		HIP_TRY(hipMemcpy(z, c->d_z, px * 4, hipMemcpyDeviceToHost));
+	return RTX_OK;
+}
+
+static int post_common(rtx_ctx *c, uint32_t w, uint32_t h, const rtx_post *pp, float *d_rgb, const float *d_z,
+		       hipStream_t stream)
+{
+	if (!w || !h || (uint64_t)w * h > 0xFFFFFFFFull)
+		return fail(RTX_ERR_ARG, "bad postprocess size %ux%u", w, h);
+	if (pp->mist && (pp->mist_falloff < RTX_FALLOFF_QUAD || pp->mist_falloff > RTX_FALLOFF_INV_QUAD))
+		return fail(RTX_ERR_ARG, "bad mist falloff %d", pp->mist_falloff);
+	if (pp->dof < RTX_DOF_NONE || pp->dof > RTX_DOF_CAMERA)
+		return fail(RTX_ERR_ARG, "bad dof mode %d", pp->dof);
+	const size_t n = (size_t)w * h;
+	if (n > c->post_pixels) {
+		dfree(c->d_post_rad);
+		dfree(c->d_post_pv);
+		c->post_pixels = 0;
+		HIP_TRY(hipMalloc(&c->d_post_rad, n * sizeof(int)));
+		HIP_TRY(hipMalloc(&c->d_post_pv, n * sizeof(float4)));
+		c->post_pixels = n;
+	}
+	if (!c->d_post_scratch)
+		HIP_TRY(hipMalloc(&c->d_post_scratch, 4 * sizeof(unsigned)));
+	HIP_TRY(rtx_launch_post(w, h, pp, d_rgb, d_z, c->d_post_rad, c->d_post_pv, c->d_post_scratch, stream));
+	HIP_TRY(hipStreamSynchronize(stream));
+	return RTX_OK;
+}
+
+extern "C" int rtx_postprocess_device(rtx_ctx *c, uint32_t w, uint32_t h, const rtx_post *pp, void *d_rgb,
+				      const void *d_z, void *stream)
+{
+	if (!c || !pp || !d_rgb || !d_z)
+		return fail(RTX_ERR_ARG, "null argument");
+	HIP_TRY(hipSetDevice(c->device));
+	return post_common(c, w, h, pp, (float *)d_rgb, (const float *)d_z,
+			   stream ? (hipStream_t)stream : c->stream);
+}
+
+extern "C" int rtx_postprocess(rtx_ctx *c, uint32_t w, uint32_t h, const rtx_post *pp, float *rgb, const float *z)
+{
+	if (!c || !pp || !rgb || !z)
+		return fail(RTX_ERR_ARG, "null argument");
+	if (!w || !h)
+		return fail(RTX_ERR_ARG, "bad postprocess size %ux%u", w, h);
+	HIP_TRY(hipSetDevice(c->device));
+	const size_t px = (size_t)w * h;
+	if (px > c->fb_pixels) {
+		dfree(c->d_rgb);
+		dfree(c->d_z);
+		c->fb_pixels = 0;
+		HIP_TRY(hipMalloc(&c->d_rgb, px * 3 * sizeof(float)));
+		HIP_TRY(hipMalloc(&c->d_z, px * sizeof(float)));
+		c->fb_pixels = px;
+	}
+	HIP_TRY(hipMemcpyAsync(c->d_rgb, rgb, px * 12, hipMemcpyHostToDevice, c->stream));
+	HIP_TRY(hipMemcpyAsync(c->d_z, z, px * 4, hipMemcpyHostToDevice, c->stream));
+	int rc = post_common(c, w, h, pp, c->d_rgb, c->d_z, c->stream);
+	if (rc)
+		return rc;
+	HIP_TRY(hipMemcpy(rgb, c->d_rgb, px * 12, hipMemcpyDeviceToHost));
 	return RTX_OK;
 }
 

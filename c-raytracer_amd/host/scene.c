@@ -767,3 +767,59 @@ int rtx_stl_write(const char *path, uint32_t n, const float *tris)
 	fclose(f);
 	return RTX_OK;
 }
+
+/* ---- postprocessor flags: src/postprocess/postproc.c:36-91 with argv.c:36-55 semantics ---- */
+static int post_arg(int argc, char **argv, const char *flag, int nargs)
+{
+	const uint32_t hsh = rtx_hash_djb(flag);
+	int idx = 0;
+	for (int i = 1; i < argc; i++) /* argv_check: first argument (after argv[0]) with this hash */
+		if (argv[i] && rtx_hash_djb(argv[i]) == hsh) {
+			idx = i;
+			break;
+		}
+	return idx + nargs < argc ? idx : 0; /* argv_check_with_args */
+}
+
+int rtx_post_from_argv(int argc, char **argv, rtx_post *post)
+{
+	if (!post || (argc > 0 && !argv))
+		return set_err(RTX_ERR_ARG, "null argument");
+	memset(post, 0, sizeof(*post));
+	int idx = post_arg(argc, argv, "-b", 1);
+	if (idx) {
+		post->brighten = 1;
+		post->brighten_factor = (float)atof(argv[idx + 1]);
+	}
+	if ((idx = post_arg(argc, argv, "--dof", 2))) {
+		post->dof = RTX_DOF_SCALE_BIAS;
+		post->dof_scale = (float)atof(argv[idx + 1]);
+		post->dof_bias = (float)atof(argv[idx + 2]);
+	} else if ((idx = post_arg(argc, argv, "--dof-camera", 3))) {
+		post->dof = RTX_DOF_CAMERA;
+		post->aperture = (float)atof(argv[idx + 1]);
+		post->focal_length = (float)atof(argv[idx + 2]);
+		post->plane_in_focus = (float)atof(argv[idx + 3]);
+	}
+	if ((idx = post_arg(argc, argv, "--mist", 6))) {
+		post->mist = 1;
+		post->mist_start = (float)atof(argv[idx + 1]);
+		post->mist_depth = (float)atof(argv[idx + 2]);
+		switch (rtx_hash_djb(argv[idx + 3])) {
+		case 2088106052u: /* quad */
+			post->mist_falloff = RTX_FALLOFF_QUAD;
+			break;
+		case 193412846u: /* lin */
+			post->mist_falloff = RTX_FALLOFF_LIN;
+			break;
+		case 624812280u: /* inv-quad */
+			post->mist_falloff = RTX_FALLOFF_INV_QUAD;
+			break;
+		default:
+			return set_err(RTX_ERR_ARG, "Unrecognized falloff type [%s].", argv[idx + 3]);
+		}
+		for (int a = 0; a < 3; a++)
+			post->mist_color[a] = (float)atof(argv[idx + 4 + a]);
+	}
+	return RTX_OK;
+}

@@ -146,3 +146,149 @@ int rtx_tiff_write(const char *path, uint32_t w, uint32_t h, const float *rgb, c
 	fclose(f);
 	return bad ? RTX_ERR_IO : RTX_OK;
 }
+
+/* ---- raw TIFF reader: what src/postprocess/image.c:29-75 (image_load) accepts ---- */
+typedef struct {
+	const unsigned char *p;
+	size_t n;
+	int be; /* big-endian file ("MM") */
+} tbuf;
+
+static uint32_t rd16(const tbuf *t, size_t o)
+{
+	if (o + 2 > t->n)
+		return 0;
+	const unsigned char *q = t->p + o;
+	return t->be ? (uint32_t)(q[0] << 8 | q[1]) : (uint32_t)(q[1] << 8 | q[0]);
+}
+static uint32_t rd32(const tbuf *t, size_t o)
+{
+	if (o + 4 > t->n)
+		return 0;
+	const unsigned char *q = t->p + o;
+	return t->be ? ((uint32_t)q[0] << 24 | (uint32_t)q[1] << 16 | (uint32_t)q[2] << 8 | q[3])
+		     : ((uint32_t)q[3] << 24 | (uint32_t)q[2] << 16 | (uint32_t)q[1] << 8 | q[0]);
+}
+
+typedef struct {
+	uint32_t type, count, value; /* value = inline value or offset */
+	size_t at;                   /* file offset of the 4-byte value field */
+	int present;
+} tfield;
+
+static uint32_t tsize(uint32_t type) { return type == T_SHORT ? 2u : (type == 1 || type == 2 || type == 6 || type == 7) ? 1u : (type == 12 ? 8u : 4u); }
+
+/* element i of a field (SHORT or LONG), inline or at its offset */
+static uint32_t tget(const tbuf *t, const tfield *f, uint32_t i)
+{
+	const uint32_t sz = tsize(f->type);
+	const size_t base = (uint64_t)f->count * sz <= 4 ? f->at : f->value;
+	return f->type == T_SHORT ? rd16(t, base + 2 * (size_t)i) : rd32(t, base + 4 * (size_t)i);
+}
+
+int rtx_tiff_read_raw(const char *path, uint32_t *width, uint32_t *height, float **rgb, float **z)
+{
+	if (!path || !width || !height || !rgb || !z)
+		return RTX_ERR_ARG;
+	*rgb = NULL;
+	*z = NULL;
+	FILE *f = fopen(path, "rb");
+	if (!f)
+		return RTX_ERR_IO; /* image.c:37 "Failed to open input file" */
+	fseek(f, 0, SEEK_END);
+	long len = ftell(f);
+	fseek(f, 0, SEEK_SET);
+	unsigned char *buf = len > 8 ? malloc((size_t)len) : NULL;
+	if (!buf || fread(buf, 1, (size_t)len, f) != (size_t)len) {
+		free(buf);
+		fclose(f);
+		return RTX_ERR_IO;
+	}
+	fclose(f);
+	tbuf t = { buf, (size_t)len, buf[0] == 'M' };
+	int rc = RTX_ERR_IO;
+	if (!((buf[0] == 'I' && buf[1] == 'I') || (buf[0] == 'M' && buf[1] == 'M')) || rd16(&t, 2) != 42)
+		goto out;
+	const uint32_t ifd = rd32(&t, 4);
+	const uint32_t n = rd16(&t, ifd);
+	tfield fw = { 0 }, fh = { 0 }, fbps = { 0 }, fcomp = { 0 }, fso = { 0 }, fspp = { 0 }, fsbc = { 0 }, fpc = { 0 },
+	       fz = { 0 };
+	for (uint32_t i = 0; i < n; i++) {
+		const size_t e = ifd + 2 + 12 * (size_t)i;
+		tfield x = { rd16(&t, e + 2), rd32(&t, e + 4), rd32(&t, e + 8), e + 8, 1 };
+		if (x.type == T_SHORT && x.count == 1)
+			x.value = rd16(&t, e + 8);
+		switch (rd16(&t, e)) {
+		case 256: fw = x; break;
+		case 257: fh = x; break;
+		case 258: fbps = x; break;
+		case 259: fcomp = x; break;
+		case 273: fso = x; break;
+		case 277: fspp = x; break;
+		case 279: fsbc = x; break;
+		case 284: fpc = x; break;
+		case 65000: fz = x; break;
+		default: break;
+		}
+	}
+	if (!fw.present || !fh.present || !fso.present)
+		goto out;
+	const uint32_t w = fw.type == T_SHORT ? fw.value & 0xFFFF : fw.value;
+	const uint32_t h = fh.type == T_SHORT ? fh.value & 0xFFFF : fh.value;
+	/* image.c:47-49: 3 samples, 32 bits, contiguous */
+	if ((fspp.present ? fspp.value : 1) != 3 || !fbps.present || tget(&t, &fbps, 0) != 32 ||
+	    (fpc.present && fpc.value != 1) || (fcomp.present && fcomp.value != 1) || !w || !h) {
+		rc = RTX_ERR_ARG;
+		goto out;
+	}
+	const size_t px = (size_t)w * h;
+	/* image.c:70-73: "Corrupted Z-Buffer." unless the tag holds exactly W*H floats */
+	if (!fz.present || fz.count != px || fz.type != T_FLOAT) {
+		rc = RTX_ERR_ARG;
+		goto out;
+	}
+	float *c = malloc(px * 12), *d = malloc(px * 4);
+	if (!c || !d) {
+		free(c);
+		free(d);
+		rc = RTX_ERR_NOMEM;
+		goto out;
+	}
+	/* strips in order, rows contiguous */
+	size_t at = 0;
+	const size_t total = px * 12;
+	for (uint32_t s = 0; s < fso.count && at < total; s++) {
+		const uint32_t so = tget(&t, &fso, s);
+		uint32_t sc = fsbc.present ? tget(&t, &fsbc, s) : (uint32_t)(total - at);
+		if (sc > total - at)
+			sc = (uint32_t)(total - at);
+		if ((size_t)so + sc > t.n)
+			break;
+		memcpy((unsigned char *)c + at, buf + so, sc);
+		at += sc;
+	}
+	const size_t zo = px == 1 ? fz.at : fz.value;
+	if (at != total || zo + px * 4 > t.n) {
+		free(c);
+		free(d);
+		goto out;
+	}
+	memcpy(d, buf + zo, px * 4);
+	if (t.be) { /* byte-swap samples of a big-endian file */
+		uint32_t *u = (uint32_t *)c, *v = (uint32_t *)d;
+		for (size_t i = 0; i < px * 3; i++)
+			u[i] = __builtin_bswap32(u[i]);
+		for (size_t i = 0; i < px; i++)
+			v[i] = __builtin_bswap32(v[i]);
+	}
+	*width = w;
+	*height = h;
+	*rgb = c;
+	*z = d;
+	rc = RTX_OK;
+out:
+	free(buf);
+	return rc;
+}
+
+void rtx_buffer_free(void *p) { free(p); }

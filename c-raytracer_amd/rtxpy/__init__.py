@@ -169,6 +169,35 @@ def write_tiff(path, rgb, z=None, raw=False):
         raise RtxError(rc, f"tiff write failed: {path}")
 
 
+def read_tiff_raw(path):
+    """rtx_tiff_read_raw (librtxscene): (rgb (H,W,3), z (H,W)) float32 of a raw TIFF."""
+    w, h = C.c_uint32(), C.c_uint32()
+    prgb, pz = C.c_void_p(), C.c_void_p()
+    rc = scene_lib().rtx_tiff_read_raw(os.fsencode(path), C.byref(w), C.byref(h), C.byref(prgb), C.byref(pz))
+    if rc != RTX_OK:
+        raise RtxError(rc, f"raw tiff read failed: {path}")
+    try:
+        n = w.value * h.value
+        rgb = np.ctypeslib.as_array((C.c_float * (3 * n)).from_address(prgb.value)).reshape(h.value, w.value, 3).copy()
+        z = np.ctypeslib.as_array((C.c_float * n).from_address(pz.value)).reshape(h.value, w.value).copy()
+    finally:
+        scene_lib().rtx_buffer_free(prgb)
+        scene_lib().rtx_buffer_free(pz)
+    return rgb, z
+
+
+def post_from_args(args):
+    """rtx_post_from_argv over ["postprocess", "<in>", "<out>"] + args (the reference's argv layout)."""
+    from .abi import Post
+    argv = [b"postprocess", b"in.tif", b"out.tif"] + [a.encode() for a in args]
+    arr = (C.c_char_p * len(argv))(*argv)
+    p = Post()
+    rc = scene_lib().rtx_post_from_argv(len(argv), arr, C.byref(p))
+    if rc != RTX_OK:
+        raise RtxError(rc, scene_lib().rtx_scene_last_error().decode())
+    return p
+
+
 def write_stl(path, tris):
     tris = np.ascontiguousarray(tris, dtype=np.float32).reshape(-1, 9)
     _check_scene(scene_lib().rtx_stl_write(os.fsencode(path), tris.shape[0], tris.ctypes.data))
@@ -201,6 +230,18 @@ class Renderer:
         """d_rgb / d_z: device pointers (ints), stream: hipStream_t as int or None."""
         _check(self.lib.rtx_render_device(self._ctx, C.byref(frame), C.byref(params), C.c_void_p(d_rgb),
                                           C.c_void_p(d_z), C.c_void_p(stream) if stream else None))
+
+    def postprocess(self, post, rgb, z):
+        """rtx_postprocess on host arrays: returns the postprocessed (H,W,3) float32 copy."""
+        out = np.ascontiguousarray(rgb, dtype=np.float32).copy()
+        zz = np.ascontiguousarray(z, dtype=np.float32)
+        h, w = out.shape[:2]
+        _check(self.lib.rtx_postprocess(self._ctx, w, h, C.byref(post), out.ctypes.data, zz.ctypes.data))
+        return out
+
+    def postprocess_device(self, post, width, height, d_rgb, d_z, stream=None):
+        _check(self.lib.rtx_postprocess_device(self._ctx, width, height, C.byref(post), C.c_void_p(d_rgb),
+                                               C.c_void_p(d_z), C.c_void_p(stream) if stream else None))
 
     def stats(self):
         s = Stats()

@@ -68,6 +68,18 @@ class Stats(C.Structure):
                 ("chunks", C.c_uint32), ("pad", C.c_uint32)]
 
 
+RTX_DOF_NONE, RTX_DOF_SCALE_BIAS, RTX_DOF_CAMERA = 0, 1, 2
+RTX_FALLOFF_QUAD, RTX_FALLOFF_LIN, RTX_FALLOFF_INV_QUAD = 0, 1, 2
+
+
+class Post(C.Structure):
+    _fields_ = [("brighten", C.c_int32), ("brighten_factor", C.c_float), ("dof", C.c_int32),
+                ("dof_scale", C.c_float), ("dof_bias", C.c_float), ("aperture", C.c_float),
+                ("focal_length", C.c_float), ("plane_in_focus", C.c_float), ("mist", C.c_int32),
+                ("mist_start", C.c_float), ("mist_depth", C.c_float), ("mist_falloff", C.c_int32),
+                ("mist_color", F3)]
+
+
 # include/rtx_kat.h
 KAT_MOLLER, KAT_SPHERE, KAT_PLANE, KAT_SLAB, KAT_NOISE, KAT_TEXTURE, KAT_SPH_LIGHT, KAT_TRI_LIGHT, \
     KAT_MORTON, KAT_U32, KAT_GI_DIR, KAT_REFRACT = range(12)
@@ -78,10 +90,12 @@ KAT_NAMES = ["moller", "sphere", "plane", "slab", "noise", "texture", "sph_light
 
 # symbols include/rtx.h declares (checked by tests/test_abi.py)
 RTX_SYMBOLS = ["rtx_params_default", "rtx_device_count", "rtx_open", "rtx_upload_scene", "rtx_render",
-               "rtx_render_device", "rtx_get_stats", "rtx_close", "rtx_last_error", "rtx_kat"]
+               "rtx_render_device", "rtx_get_stats", "rtx_close", "rtx_last_error", "rtx_kat", "rtx_postprocess",
+               "rtx_postprocess_device"]
 RTX_SCENE_SYMBOLS = ["rtx_scene_load", "rtx_scene_parse", "rtx_scene_desc_of", "rtx_scene_num_json_objects",
                      "rtx_scene_free", "rtx_scene_last_error", "rtx_frame_setup", "rtx_tiff_write", "rtx_hash_djb",
-                     "rtx_params_from_argv", "rtx_stl_write"]
+                     "rtx_params_from_argv", "rtx_stl_write", "rtx_tiff_read_raw", "rtx_buffer_free",
+                     "rtx_post_from_argv"]
 
 
 def declare_scene(lib):
@@ -108,6 +122,13 @@ def declare_scene(lib):
     lib.rtx_params_from_argv.restype = None
     lib.rtx_stl_write.argtypes = [C.c_char_p, C.c_uint32, C.c_void_p]
     lib.rtx_stl_write.restype = C.c_int
+    lib.rtx_tiff_read_raw.argtypes = [C.c_char_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                                      C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
+    lib.rtx_tiff_read_raw.restype = C.c_int
+    lib.rtx_buffer_free.argtypes = [C.c_void_p]
+    lib.rtx_buffer_free.restype = None
+    lib.rtx_post_from_argv.argtypes = [C.c_int, C.POINTER(C.c_char_p), C.POINTER(Post)]
+    lib.rtx_post_from_argv.restype = C.c_int
 
 
 def declare_rtx(lib):
@@ -132,6 +153,11 @@ def declare_rtx(lib):
     lib.rtx_last_error.restype = C.c_char_p
     lib.rtx_kat.argtypes = [C.c_int, C.c_uint32, C.c_void_p, C.c_void_p, C.POINTER(Params)]
     lib.rtx_kat.restype = C.c_int
+    lib.rtx_postprocess.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(Post), C.c_void_p, C.c_void_p]
+    lib.rtx_postprocess.restype = C.c_int
+    lib.rtx_postprocess_device.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(Post), C.c_void_p,
+                                           C.c_void_p, C.c_void_p]
+    lib.rtx_postprocess_device.restype = C.c_int
 
 
 def declare_oracle(lib):

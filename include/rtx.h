@@ -217,6 +217,36 @@ void rtx_close(rtx_ctx *ctx);
 const char *rtx_last_error(void);
 
 /*
+ * Postprocess: the reference's separate `postprocess` binary
+ * (src/postprocess/postproc.c:36-188) applied on the device to an rgb+z frame:
+ * brighten (-b), depth of field (--dof scale bias | --dof-camera aperture focal plane),
+ * mist (--mist start depth falloff r g b), in that order, with the reference's float
+ * arithmetic; the DoF scatter is restated as an ordered gather so every output pixel
+ * sums its contributions in the reference's order (bit-identical results).
+ */
+enum { RTX_DOF_NONE = 0, RTX_DOF_SCALE_BIAS = 1, RTX_DOF_CAMERA = 2 };
+enum { RTX_FALLOFF_QUAD = 0, RTX_FALLOFF_LIN = 1, RTX_FALLOFF_INV_QUAD = 2 };
+
+typedef struct rtx_post {
+	int32_t brighten;           /* -b given (postproc.c:43-47) */
+	float brighten_factor;
+	int32_t dof;                /* RTX_DOF_* (postproc.c:49-68) */
+	float dof_scale, dof_bias;  /* --dof */
+	float aperture, focal_length, plane_in_focus; /* --dof-camera */
+	int32_t mist;               /* --mist given (postproc.c:70-90) */
+	float mist_start, mist_depth;
+	int32_t mist_falloff;       /* RTX_FALLOFF_* */
+	float mist_color[3];
+} rtx_post;
+
+/* rgb[W*H*3] in/out and z[W*H] in, HOST buffers (replaces postprocess() between
+ * image_load() and save_image(), src/postprocess/main.c:66-68). */
+int rtx_postprocess(rtx_ctx *ctx, uint32_t width, uint32_t height, const rtx_post *post, float *rgb, const float *z);
+/* Same on DEVICE buffers, enqueued on `stream` (NULL = the context's stream); synchronises it. */
+int rtx_postprocess_device(rtx_ctx *ctx, uint32_t width, uint32_t height, const rtx_post *post, void *d_rgb,
+			   const void *d_z, void *stream);
+
+/*
  * Known-answer entry: evaluates one device function over n inputs on the GPU
  * (used by the -m gpu parity tests against the oracle's KAT fixtures).
  * kind / record layouts are listed in rtx_kat.h.

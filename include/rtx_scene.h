@@ -53,6 +53,17 @@ void rtx_params_from_argv(int argc, char **argv, rtx_params *p);
  * stand-in mesh generators; tris = n * 9 floats. */
 int rtx_stl_write(const char *path, uint32_t n, const float *tris);
 
+/* Read a raw TIFF as written by the reference's save_tiff_raw (-f) or by rtx_tiff_write(raw):
+ * 3 x 32-bit float samples per pixel, contiguous, plus the z-buffer in private tag 65000
+ * (what src/postprocess/image.c:29-75 image_load accepts, with its error checks).  *rgb and
+ * *z are malloc'd; release them with rtx_buffer_free. */
+int rtx_tiff_read_raw(const char *path, uint32_t *width, uint32_t *height, float **rgb, float **z);
+void rtx_buffer_free(void *p);
+
+/* The postprocessor's flags (src/postprocess/postproc.c:36-91, argv.c hashing semantics) into
+ * *post; RTX_ERR_ARG with rtx_scene_last_error() for an unknown falloff name. */
+int rtx_post_from_argv(int argc, char **argv, rtx_post *post);
+
 #ifdef __cplusplus
 }
 #endif

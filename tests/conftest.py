@@ -93,3 +93,19 @@ def box_filter(img, k=8):
     h2, w2 = h // k * k, w // k * k
     x = img[:h2, :w2]
     return x.reshape(h2 // k, k, w2 // k, k, -1).mean(axis=(1, 3))
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _torch_hip_first():
+    """torch ships its own HIP runtime: initialise it before librtx.so's (the order bench.py
+    uses), so GPU tests that hand torch device buffers to the C-ABI can run in one process."""
+    if os.environ.get("RTX_TESTS_NO_TORCH"):
+        yield
+        return
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except Exception:
+        pass
+    yield

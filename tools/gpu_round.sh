@@ -27,12 +27,12 @@ for s in $STEPS; do
     testsall) run testsall 1500 python3 -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) run bench 900 python3 bench.py --verbose ;;
     benchq) run benchq 600 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --verbose ;;
-    occsweep) for o in ${OCCS:-1 6 7 8}; do RTX_SHADOW_OCC=$o run occ$o 600 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-count; done ;;
-    variants) for v in ${VARS:-$(ls c-raytracer_amd/lib/var)}; do RTX_LIBRTX=$PWD/c-raytracer_amd/lib/var/$v/librtx.so run var_$v 600 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-count; done ;;
-    prof) run prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-count ;;
-    pmcf) run pmcf 900 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count ;;
-    pmcw) run pmcw 900 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count ;;
-    pmcv) run pmcv 900 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES -d "$OUT/pmc_valu" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count ;;
+    occsweep) for o in ${OCCS:-1 6 7 8}; do RTX_SHADOW_OCC=$o run occ$o 600 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-count --no-post; done ;;
+    variants) for v in ${VARS:-$(ls c-raytracer_amd/lib/var)}; do RTX_LIBRTX=$PWD/c-raytracer_amd/lib/var/$v/librtx.so run var_$v 600 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-count --no-post; done ;;
+    prof) run prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-count --no-post ;;
+    pmcf) run pmcf 900 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post ;;
+    pmcw) run pmcw 900 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post ;;
+    pmcv) run pmcv 900 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES -d "$OUT/pmc_valu" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post ;;
   esac
 done
 echo done

@@ -15,7 +15,7 @@ for v in "$@"; do
     name=${s%%:*}; ctrs=${s#*:}
     echo "=== $v $name ($(date +%T))"
     RTX_LIBRTX=$lib timeout -k 10 600 rocprofv3 --pmc $ctrs -d "$OUT/${v}_$name" -o run --output-format csv -- \
-      python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count > "$OUT/${v}_$name.log" 2>&1
+      python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post > "$OUT/${v}_$name.log" 2>&1
     rc=$?; echo "=== rc=$rc"; tail -2 "$OUT/${v}_$name.log"
     if [ $rc -ge 124 ]; then exit $rc; fi
   done
