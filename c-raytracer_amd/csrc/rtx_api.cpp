@@ -324,6 +324,13 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 		}
 	BvhOutput bvh;
 	BvhConfig cfg;
+	/* builder knobs for measurement (defaults are the tuned values) */
+	if (const char *e = getenv("RTX_BVH_LEAF"))
+		cfg.max_leaf = (uint32_t)std::min(16, std::max(1, atoi(e)));
+	if (const char *e = getenv("RTX_BVH_CT"))
+		cfg.c_trav = (float)atof(e);
+	if (const char *e = getenv("RTX_BVH_CI"))
+		cfg.c_isect = (float)atof(e);
 	bvh_build(BvhInput{ nb, lo.data(), hi.data() }, cfg, bvh);
 
 	std::vector<DPrim> prims(nb);
