@@ -327,6 +327,28 @@ def main():
                             "L2/MALL-resident: the kernel is issue-bound, see DESIGN.md §5; traffic = PMC "
                             "L2->fabric bytes per launch (2*FETCH_SIZE + WRITE_SIZE, profiles/)"}
 
+    build = None
+    if rank == 0 and world == 1 and not a.no_post:
+        # §8(f) #2: both BVH builders on the benchmark scene (build time, then one frame each)
+        try:
+            build = {"sah_host_ms": round(st.build_ms, 1)}
+            r.set_builder(abi.RTX_BUILD_LBVH_GPU)
+            r.upload(scene)
+            sl = r.stats()
+            build.update({"lbvh_gpu_ms": round(sl.build_ms, 1), "lbvh_nodes": int(sl.bvh_nodes),
+                          "lbvh_depth": int(sl.bvh_depth), "sah_nodes": int(st.bvh_nodes),
+                          "sah_depth": int(st.bvh_depth)})
+            r.render_device(frame, params, d_rgb.data_ptr(), d_z.data_ptr(), stream.cuda_stream)
+            build["lbvh_shadow_ms"] = round(r.stats().shadow_ms, 1)
+            build["sah_shadow_ms"] = round(float(np.mean(sms)), 1)
+            r.set_builder(abi.RTX_BUILD_SAH_HOST)
+            r.upload(scene)
+            r.render_device(frame, params, d_rgb.data_ptr(), d_z.data_ptr(), stream.cuda_stream)
+            log(f"builders: {build}")
+        except Exception as e:
+            log(f"builder leg failed: {e}")
+            build = None
+
     post = None
     if rank == 0 and world == 1 and not a.no_post:
         try:
@@ -365,6 +387,8 @@ def main():
             out["cpu_port"] = port
         if post:
             out["postprocess"] = post
+        if build:
+            out["bvh_build"] = build
         print(json.dumps(out), flush=True)
     r.close()
     if world > 1:

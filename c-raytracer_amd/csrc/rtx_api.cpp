@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <vector>
 
@@ -33,6 +34,9 @@ extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const
 extern "C" hipError_t rtx_launch_post(uint32_t w, uint32_t h, const rtx_post *pp, float *rgb, const float *z,
 				      int *rad, float4 *pv, unsigned *scratch, hipStream_t stream);
 extern "C" hipError_t rtx_spsort_temp_bytes(uint32_t n, size_t *bytes);
+extern "C" hipError_t rtx_lbvh_build(uint32_t n, const float *d_lo, const float *d_hi, const DPrim *d_prims_in,
+				     const float blo[3], const float bhi[3], uint32_t max_leaf, DNode **recs_out,
+				     uint32_t *nnodes_out, uint32_t *root_out, uint32_t *depth_out, hipStream_t st);
 extern "C" hipError_t rtx_launch_spsort(const float4 *sp, uint32_t n, const float lo[3], const float hi[3],
 					uint32_t *keys0, uint32_t *keys1, uint32_t *vals0, uint32_t *vals1, void *temp,
 					size_t temp_bytes, const uint32_t **perm, hipStream_t stream);
@@ -62,6 +66,7 @@ static int fail(int code, const char *fmt, ...)
 
 struct rtx_ctx {
 	int device = 0;
+	int builder = RTX_BUILD_SAH_HOST;
 	hipStream_t stream = nullptr;
 	hipEvent_t ev0 = nullptr, ev1 = nullptr;
 	int cus = 0;
@@ -322,7 +327,6 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 			c->bound_lo[a] = std::min(c->bound_lo[a], lo[3 * (size_t)k + a]);
 			c->bound_hi[a] = std::max(c->bound_hi[a], hi[3 * (size_t)k + a]);
 		}
-	BvhOutput bvh;
 	BvhConfig cfg;
 	/* builder knobs for measurement (defaults are the tuned values) */
 	if (const char *e = getenv("RTX_BVH_LEAF"))
@@ -331,14 +335,11 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 		cfg.c_trav = (float)atof(e);
 	if (const char *e = getenv("RTX_BVH_CI"))
 		cfg.c_isect = (float)atof(e);
-	bvh_build(BvhInput{ nb, lo.data(), hi.data() }, cfg, bvh);
 
-	std::vector<DPrim> prims(nb);
-	std::vector<uint32_t> prim_of(sc->num_objects, RTX_NONE);
-	for (uint32_t k = 0; k < nb; k++) {
-		const uint32_t oi = bounded[bvh.order[k]];
+	/* one 64-byte primitive record (rtx_device.h DPrim) of bounded object oi */
+	auto make_prim = [&](uint32_t oi) {
 		const rtx_object &o = sc->objects[oi];
-		DPrim &p = prims[k];
+		DPrim p;
 		memset(&p, 0, sizeof(p));
 		uint32_t meta = ((uint32_t)o.type << 24) | (uint32_t)o.material;
 		if (mats[o.material].flags & RTX_MF_TRANSPARENT)
@@ -354,8 +355,13 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 		}
 		memcpy(&p.b[3], &oi, 4);
 		memcpy(&p.c[3], &meta, 4);
-		prim_of[oi] = k;
-	}
+		return p;
+	};
+	auto is_sphere = [](const DPrim &p) {
+		uint32_t meta;
+		memcpy(&meta, &p.c[3], 4);
+		return (meta >> 24) == RTX_SPHERE;
+	};
 
 	std::vector<DEmitter> emit(sc->num_emitters);
 	for (uint32_t i = 0; i < sc->num_emitters; i++) {
@@ -380,39 +386,81 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 		e.radius = o.radius;
 	}
 
-	/* nodes and primitives in one array of 64-byte records: the shadow walk addresses both
-	 * through one base pointer (record num_nodes + i = primitive i) */
-	const uint32_t nnodes = (uint32_t)bvh.nodes.size();
-	if (((uint64_t)nnodes + nb) * sizeof(DNode) > 0xFFFFFFC0ull)
-		return fail(RTX_ERR_SCENE, "scene too large: %u BVH nodes + %u primitives exceed 4 GB of records", nnodes, nb);
-	/* builder refs (node index | RTX_LEAF_BIT leaf) -> device refs (record byte offset | leaf bits) */
-	auto dref = [nnodes, &prims](uint32_t r) -> uint32_t {
-		if (r == RTX_EMPTY_REF)
-			return r;
-		if (r & RTX_LEAF_BIT) {
-			const uint32_t first = (r >> 4) & 0x7FFFFFFu, cnt = (r & 15u) + 1;
-			uint32_t sph = 0;
-			for (uint32_t k = first; k < first + cnt; k++) {
-				uint32_t meta;
-				memcpy(&meta, &prims[k].c[3], 4);
-				if ((meta >> 24) == RTX_SPHERE)
-					sph = RTX_REF_SPH;
-			}
-			return (nnodes + first) * (uint32_t)sizeof(DNode) | RTX_REF_LEAF | sph | (cnt - 1);
-		}
-		return r * (uint32_t)sizeof(DNode);
-	};
-	std::vector<DNode> recs(nnodes + (size_t)nb);
-	for (uint32_t i = 0; i < nnodes; i++) {
-		recs[i] = bvh.nodes[i];
-		recs[i].ref0 = dref(recs[i].ref0);
-		recs[i].ref1 = dref(recs[i].ref1);
-	}
-	if (nb)
-		memcpy(recs.data() + nnodes, prims.data(), nb * sizeof(DPrim));
+	const auto tb0 = std::chrono::steady_clock::now();
+	uint32_t nnodes = 0, root_ref = RTX_EMPTY_REF, depth = 0;
 	int rc;
-	if ((rc = upload(c->d_nodes, recs)) ||
-	    (rc = upload(c->d_planes, planes)) || (rc = upload(c->d_mats, mats)) || (rc = upload(c->d_emitters, emit)))
+	if (c->builder == RTX_BUILD_LBVH_GPU && nb) {
+		/* GPU linear BVH (rtx_build.hip): primitives uploaded in input order, records emitted on the device */
+		std::vector<DPrim> prims_in(nb);
+		uint32_t sph = 0;
+		for (uint32_t k = 0; k < nb; k++) {
+			prims_in[k] = make_prim(bounded[k]);
+			if (is_sphere(prims_in[k]))
+				sph = RTX_REF_SPH;
+		}
+		float *d_lo = nullptr, *d_hi = nullptr;
+		DPrim *d_in = nullptr;
+		DNode *recs = nullptr;
+		if ((rc = upload(d_lo, lo)) || (rc = upload(d_hi, hi)) || (rc = upload(d_in, prims_in))) {
+			dfree(d_lo);
+			dfree(d_hi);
+			dfree(d_in);
+			return rc;
+		}
+		hipError_t e = rtx_lbvh_build(nb, d_lo, d_hi, d_in, c->bound_lo, c->bound_hi, cfg.max_leaf, &recs, &nnodes,
+					      &root_ref, &depth, c->stream);
+		dfree(d_lo);
+		dfree(d_hi);
+		dfree(d_in);
+		if (e != hipSuccess)
+			return fail(RTX_ERR_HIP, "GPU BVH build failed: %s", hipGetErrorString(e));
+		c->d_nodes = recs;
+		if (root_ref == RTX_EMPTY_REF) /* nb <= max_leaf: a single leaf */
+			root_ref = RTX_REF_LEAF | sph | (nb - 1);
+		if (((uint64_t)nnodes + nb) * sizeof(DNode) > 0xFFFFFFC0ull)
+			return fail(RTX_ERR_SCENE, "scene too large: %u BVH nodes + %u primitives exceed 4 GB of records", nnodes,
+				    nb);
+	} else {
+		BvhOutput bvh;
+		bvh_build(BvhInput{ nb, lo.data(), hi.data() }, cfg, bvh);
+		std::vector<DPrim> prims(nb);
+		for (uint32_t k = 0; k < nb; k++)
+			prims[k] = make_prim(bounded[bvh.order[k]]);
+		/* nodes and primitives in one array of 64-byte records: the shadow walk addresses both
+		 * through one base pointer (record num_nodes + i = primitive i) */
+		nnodes = (uint32_t)bvh.nodes.size();
+		if (((uint64_t)nnodes + nb) * sizeof(DNode) > 0xFFFFFFC0ull)
+			return fail(RTX_ERR_SCENE, "scene too large: %u BVH nodes + %u primitives exceed 4 GB of records", nnodes,
+				    nb);
+		/* builder refs (node index | RTX_LEAF_BIT leaf) -> device refs (record byte offset | leaf bits) */
+		auto dref = [nnodes, &prims, &is_sphere](uint32_t r) -> uint32_t {
+			if (r == RTX_EMPTY_REF)
+				return r;
+			if (r & RTX_LEAF_BIT) {
+				const uint32_t first = (r >> 4) & 0x7FFFFFFu, cnt = (r & 15u) + 1;
+				uint32_t sph = 0;
+				for (uint32_t k = first; k < first + cnt; k++)
+					if (is_sphere(prims[k]))
+						sph = RTX_REF_SPH;
+				return (nnodes + first) * (uint32_t)sizeof(DNode) | RTX_REF_LEAF | sph | (cnt - 1);
+			}
+			return r * (uint32_t)sizeof(DNode);
+		};
+		std::vector<DNode> recs(nnodes + (size_t)nb);
+		for (uint32_t i = 0; i < nnodes; i++) {
+			recs[i] = bvh.nodes[i];
+			recs[i].ref0 = dref(recs[i].ref0);
+			recs[i].ref1 = dref(recs[i].ref1);
+		}
+		if (nb)
+			memcpy(recs.data() + nnodes, prims.data(), nb * sizeof(DPrim));
+		if ((rc = upload(c->d_nodes, recs)))
+			return rc;
+		root_ref = dref(bvh.root_ref);
+		depth = bvh.depth;
+	}
+	c->stats.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count();
+	if ((rc = upload(c->d_planes, planes)) || (rc = upload(c->d_mats, mats)) || (rc = upload(c->d_emitters, emit)))
 		return rc;
 
 	DScene &S = c->scene;
@@ -423,20 +471,21 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 	S.planes = c->d_planes;
 	S.mats = c->d_mats;
 	S.emitters = c->d_emitters;
-	S.root_ref = nb ? dref(bvh.root_ref) : RTX_EMPTY_REF;
+	S.root_ref = nb ? root_ref : RTX_EMPTY_REF;
 	S.num_prims = nb;
 	S.num_planes = (uint32_t)planes.size();
 	S.num_emitters = sc->num_emitters;
-	S.stack_size = std::max<uint32_t>(bvh.depth + 1, 4);
-	if (bvh.depth > 63) /* k_shadow keeps its packet stack in the 64 lanes of one VGPR */
-		return fail(RTX_ERR_SCENE, "BVH depth %u exceeds 63", bvh.depth);
+	S.stack_size = std::max<uint32_t>(depth + 1, 4);
+	if (depth > 63) /* k_shadow keeps its packet stack in the 64 lanes of one VGPR */
+		return fail(RTX_ERR_SCENE, "BVH depth %u exceeds 63", depth);
 	c->total_lights = 0;
 	for (const DEmitter &e : emit)
 		c->total_lights += e.num_lights;
 	memcpy(S.ambient, sc->ambient, 12);
 	c->have_scene = true;
-	c->stats.bvh_nodes = (uint32_t)bvh.nodes.size();
-	c->stats.bvh_depth = bvh.depth;
+	c->stats.bvh_nodes = nnodes;
+	c->stats.bvh_depth = depth;
+	c->stats.builder = (uint32_t)c->builder;
 	c->stats.bvh_prims = nb;
 	return RTX_OK;
 }
@@ -707,6 +756,16 @@ extern "C" int rtx_postprocess(rtx_ctx *c, uint32_t w, uint32_t h, const rtx_pos
 	if (rc)
 		return rc;
 	HIP_TRY(hipMemcpy(rgb, c->d_rgb, px * 12, hipMemcpyDeviceToHost));
+	return RTX_OK;
+}
+
+extern "C" int rtx_set_builder(rtx_ctx *c, int builder)
+{
+	if (!c)
+		return fail(RTX_ERR_ARG, "null argument");
+	if (builder != RTX_BUILD_SAH_HOST && builder != RTX_BUILD_LBVH_GPU)
+		return fail(RTX_ERR_ARG, "unknown BVH builder %d", builder);
+	c->builder = builder;
 	return RTX_OK;
 }
 

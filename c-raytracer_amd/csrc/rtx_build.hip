@@ -1,0 +1,361 @@
+/*
+ * GPU BVH build (replacing accel_init accel.c:266-315 on the device):
+ * a linear BVH in the reference's own spirit (Morton codes of leaf-box centroids, sorted,
+ * Karras-split hierarchy: accel.c:83-88, 183-264), built in parallel and emitted straight
+ * into the device record layout the kernels traverse (rtx_device.h):
+ *
+ *   k_lb_morton   63-bit Morton code (21 bits/axis) of each padded leaf box's centroid,
+ *                 normalised by the scene extents; value = primitive index
+ *   radix sort    rocPRIM via hipCUB (64-bit keys)
+ *   k_lb_karras   Karras 2012 "Maximizing parallelism in the construction of BVHs":
+ *                 one thread per internal node finds its key range and split from the
+ *                 longest-common-prefix function (ties broken by index, as the
+ *                 reference's equal-code median split does)
+ *   k_lb_refit    bottom-up boxes: each leaf climbs, the second child to arrive at a node
+ *                 unions both boxes and continues (atomic arrival counters)
+ *   k_lb_keep     internal nodes kept as device nodes: the root and every node covering
+ *                 more than max_leaf primitives; smaller subtrees become one leaf of their
+ *                 contiguous primitive range; prefix sum -> record index
+ *   k_lb_depth    kept-node depth of every leaf (the shadow walk's VGPR stack bound)
+ *   k_lb_emit     DNode records (child boxes, byte-offset refs, per-octant child order)
+ *                 and the primitives gathered into leaf order after them
+ * The host binned-SAH builder (bvh_build.cpp) stays the default: it gives the tracer fewer
+ * node visits; this builder trades some of that for build time.
+ */
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <float.h>
+#include <stdint.h>
+
+#include "rtx.h"
+#include "rtx_device.h"
+
+#define LB_LEAF 0x80000000u /* child encoding during the build: LB_LEAF | sorted primitive index */
+
+__device__ __forceinline__ uint64_t spread21(uint64_t v)
+{
+	v &= 0x1FFFFFull;
+	v = (v | (v << 32)) & 0x1F00000000FFFFull;
+	v = (v | (v << 16)) & 0x1F0000FF0000FFull;
+	v = (v | (v << 8)) & 0x100F00F00F00F00Full;
+	v = (v | (v << 4)) & 0x10C30C30C30C30C3ull;
+	v = (v | (v << 2)) & 0x1249249249249249ull;
+	return v;
+}
+
+__global__ __launch_bounds__(256) void k_lb_morton(uint32_t n, const float *__restrict__ lo, const float *__restrict__ hi,
+						    float bx, float by, float bz, float sx, float sy, float sz,
+						    uint64_t *__restrict__ keys, uint32_t *__restrict__ vals)
+{
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= n)
+		return;
+	const float c[3] = { 0.5f * (lo[3 * i] + hi[3 * i]), 0.5f * (lo[3 * i + 1] + hi[3 * i + 1]),
+			     0.5f * (lo[3 * i + 2] + hi[3 * i + 2]) };
+	const float b[3] = { bx, by, bz }, s[3] = { sx, sy, sz };
+	uint64_t q[3];
+	for (int a = 0; a < 3; a++)
+		q[a] = (uint64_t)fminf(fmaxf((c[a] - b[a]) * s[a], 0.f), 2097151.f);
+	keys[i] = spread21(q[0]) << 2 | spread21(q[1]) << 1 | spread21(q[2]);
+	vals[i] = i;
+}
+
+/* longest common prefix of sorted keys i and j (-1 outside [0, n)) */
+__device__ __forceinline__ int lcp(const uint64_t *k, int n, int i, int j)
+{
+	if (j < 0 || j >= n)
+		return -1;
+	const uint64_t x = k[i] ^ k[j];
+	return x ? __clzll((long long)x) : 64 + __clz(i ^ j);
+}
+
+/* internal node i: children (LB_LEAF | prim or internal index), range, parents */
+__global__ __launch_bounds__(256) void k_lb_karras(int n, const uint64_t *__restrict__ k, uint32_t *__restrict__ child,
+						    uint2 *__restrict__ range, uint32_t *__restrict__ parent_int,
+						    uint32_t *__restrict__ parent_leaf)
+{
+	const int i = (int)(blockIdx.x * 256u + threadIdx.x);
+	if (i >= n - 1)
+		return;
+	const int d = (lcp(k, n, i, i + 1) - lcp(k, n, i, i - 1)) >= 0 ? 1 : -1;
+	const int dmin = lcp(k, n, i, i - d);
+	int lmax = 2;
+	while (lcp(k, n, i, i + lmax * d) > dmin)
+		lmax <<= 1;
+	int l = 0;
+	for (int t = lmax >> 1; t >= 1; t >>= 1)
+		if (lcp(k, n, i, i + (l + t) * d) > dmin)
+			l += t;
+	const int j = i + l * d;
+	const int dnode = lcp(k, n, i, j);
+	int s = 0;
+	for (int t = (l + 1) >> 1;; t = (t + 1) >> 1) {
+		if (lcp(k, n, i, i + (s + t) * d) > dnode)
+			s += t;
+		if (t == 1)
+			break;
+	}
+	const int g = i + s * d + min(d, 0);
+	const int first = min(i, j), last = max(i, j);
+	const uint32_t left = (first == g) ? (LB_LEAF | (uint32_t)g) : (uint32_t)g;
+	const uint32_t right = (last == g + 1) ? (LB_LEAF | (uint32_t)(g + 1)) : (uint32_t)(g + 1);
+	child[2 * i] = left;
+	child[2 * i + 1] = right;
+	range[i] = make_uint2((uint32_t)first, (uint32_t)last);
+	if (left & LB_LEAF)
+		parent_leaf[left & ~LB_LEAF] = (uint32_t)i;
+	else
+		parent_int[left] = (uint32_t)i;
+	if (right & LB_LEAF)
+		parent_leaf[right & ~LB_LEAF] = (uint32_t)i;
+	else
+		parent_int[right] = (uint32_t)i;
+}
+
+__global__ __launch_bounds__(256) void k_lb_refit(int n, const uint32_t *__restrict__ perm, const float *__restrict__ lo,
+						   const float *__restrict__ hi, const uint32_t *__restrict__ child,
+						   const uint32_t *__restrict__ parent_int, const uint32_t *__restrict__ parent_leaf,
+						   unsigned *__restrict__ arrive, float *__restrict__ nbox)
+{
+	const int k = (int)(blockIdx.x * 256u + threadIdx.x);
+	if (k >= n)
+		return;
+	uint32_t node = parent_leaf[k];
+	for (;;) {
+		__threadfence();
+		if (atomicAdd(&arrive[node], 1u) == 0)
+			return; /* the sibling's thread finishes this node */
+		__threadfence();
+		float b[6] = { FLT_MAX, FLT_MAX, FLT_MAX, -FLT_MAX, -FLT_MAX, -FLT_MAX };
+		for (int c = 0; c < 2; c++) {
+			const uint32_t ch = child[2 * node + c];
+			float cb[6];
+			if (ch & LB_LEAF) {
+				const uint32_t p = perm[ch & ~LB_LEAF];
+				for (int a = 0; a < 3; a++) {
+					cb[a] = lo[3 * p + a];
+					cb[3 + a] = hi[3 * p + a];
+				}
+			} else {
+				for (int a = 0; a < 6; a++) /* written by another thread: bypass stale L1 */
+					cb[a] = __hip_atomic_load(&nbox[6 * ch + a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			}
+			for (int a = 0; a < 3; a++) {
+				b[a] = fminf(b[a], cb[a]);
+				b[3 + a] = fmaxf(b[3 + a], cb[3 + a]);
+			}
+		}
+		for (int a = 0; a < 6; a++)
+			__hip_atomic_store(&nbox[6 * node + a], b[a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		if (node == 0)
+			return;
+		node = parent_int[node];
+	}
+}
+
+__global__ __launch_bounds__(256) void k_lb_keep(int n, uint32_t max_leaf, const uint2 *__restrict__ range,
+						  uint32_t *__restrict__ keep)
+{
+	const int i = (int)(blockIdx.x * 256u + threadIdx.x);
+	if (i >= n - 1)
+		return;
+	keep[i] = (i == 0 || range[i].y - range[i].x + 1 > max_leaf) ? 1u : 0u;
+}
+
+/* kept internal nodes on the path from each primitive to the root */
+__global__ __launch_bounds__(256) void k_lb_depth(int n, const uint32_t *__restrict__ keep,
+						   const uint32_t *__restrict__ parent_int,
+						   const uint32_t *__restrict__ parent_leaf, unsigned *__restrict__ depth)
+{
+	const int k = (int)(blockIdx.x * 256u + threadIdx.x);
+	if (k >= n)
+		return;
+	uint32_t node = parent_leaf[k];
+	unsigned dd = 0;
+	for (int guard = 0; guard < 4096; guard++) {
+		dd += keep[node];
+		if (node == 0)
+			break;
+		node = parent_int[node];
+	}
+	atomicMax(depth, dd);
+}
+
+__device__ __forceinline__ uint32_t leaf_ref(uint32_t nnodes, uint32_t first, uint32_t cnt,
+					     const uint32_t *__restrict__ perm, const DPrim *__restrict__ prims_in)
+{
+	uint32_t sph = 0;
+	for (uint32_t q = first; q < first + cnt; q++)
+		if ((__float_as_uint(prims_in[perm[q]].c[3]) >> 24) == RTX_SPHERE)
+			sph = RTX_REF_SPH;
+	return (nnodes + first) * (uint32_t)sizeof(DNode) | RTX_REF_LEAF | sph | (cnt - 1);
+}
+
+__global__ __launch_bounds__(256) void k_lb_emit(int n_int, int n, uint32_t nnodes, const uint32_t *__restrict__ keep,
+						  const uint32_t *__restrict__ idx, const uint32_t *__restrict__ child,
+						  const uint2 *__restrict__ range, const float *__restrict__ nbox,
+						  const uint32_t *__restrict__ perm, const float *__restrict__ lo,
+						  const float *__restrict__ hi, const DPrim *__restrict__ prims_in,
+						  DNode *__restrict__ recs)
+{
+	const int i = (int)(blockIdx.x * 256u + threadIdx.x);
+	if (i < n_int && keep[i]) {
+		float box[2][6];
+		uint32_t ref[2];
+		for (int c = 0; c < 2; c++) {
+			const uint32_t ch = child[2 * i + c];
+			if (ch & LB_LEAF) {
+				const uint32_t q = ch & ~LB_LEAF, p = perm[q];
+				for (int a = 0; a < 3; a++) {
+					box[c][a] = lo[3 * p + a];
+					box[c][3 + a] = hi[3 * p + a];
+				}
+				ref[c] = leaf_ref(nnodes, q, 1, perm, prims_in);
+			} else {
+				for (int a = 0; a < 6; a++)
+					box[c][a] = nbox[6 * ch + a];
+				ref[c] = keep[ch] ? idx[ch] * (uint32_t)sizeof(DNode)
+						  : leaf_ref(nnodes, range[ch].x, range[ch].y - range[ch].x + 1, perm, prims_in);
+			}
+		}
+		DNode d;
+		float *f = &d.lo0x;
+		for (int c = 0; c < 2; c++)
+			for (int a = 0; a < 3; a++) {
+				f[6 * c + 2 * a] = box[c][a];
+				f[6 * c + 2 * a + 1] = box[c][3 + a];
+			}
+		d.ref0 = ref[0];
+		d.ref1 = ref[1];
+		/* child order per octant: split axis = largest centroid separation (bvh_build.cpp) */
+		int ax = 0;
+		float best = -1.f;
+		for (int a = 0; a < 3; a++) {
+			const float sep = fabsf((box[0][a] + box[0][3 + a]) - (box[1][a] + box[1][3 + a]));
+			if (sep > best) {
+				best = sep;
+				ax = a;
+			}
+		}
+		const bool lcg = (box[0][ax] + box[0][3 + ax]) > (box[1][ax] + box[1][3 + ax]);
+		d.order = 0;
+		for (uint32_t o = 0; o < 8; o++)
+			d.order |= ((((o >> ax) & 1u) != 0) != lcg) ? 1u << o : 0u;
+		d.pad = 0;
+		recs[idx[i]] = d;
+	}
+	if (i < n) /* primitives in leaf order after the nodes */
+		recs[nnodes + i] = *(const DNode *)&prims_in[perm[i]];
+}
+
+extern "C" hipError_t rtx_lbvh_build(uint32_t n, const float *d_lo, const float *d_hi, const DPrim *d_prims_in,
+				     const float blo[3], const float bhi[3], uint32_t max_leaf, DNode **recs_out,
+				     uint32_t *nnodes_out, uint32_t *root_out, uint32_t *depth_out, hipStream_t st)
+{
+	hipError_t e = hipSuccess;
+	*recs_out = nullptr;
+	*nnodes_out = 0;
+	*depth_out = 0;
+	void *temp = nullptr;
+	uint64_t *keys = nullptr;
+	uint32_t *vals = nullptr, *child = nullptr, *pint = nullptr, *pleaf = nullptr, *keep = nullptr, *idx = nullptr;
+	uint2 *range = nullptr;
+	unsigned *arrive = nullptr, *scal = nullptr;
+	float *nbox = nullptr;
+	const int ni = (int)n - 1 > 0 ? (int)n - 1 : 1;
+#define TRY(x)                                  \
+	do {                                    \
+		if ((e = (x)) != hipSuccess)    \
+			goto done;              \
+	} while (0)
+	TRY(hipMalloc(&keys, 2 * (size_t)n * sizeof(uint64_t)));
+	TRY(hipMalloc(&vals, 2 * (size_t)n * sizeof(uint32_t)));
+	TRY(hipMalloc(&child, 2 * (size_t)ni * sizeof(uint32_t)));
+	TRY(hipMalloc(&range, (size_t)ni * sizeof(uint2)));
+	TRY(hipMalloc(&pint, (size_t)ni * sizeof(uint32_t)));
+	TRY(hipMalloc(&pleaf, (size_t)n * sizeof(uint32_t)));
+	TRY(hipMalloc(&arrive, (size_t)ni * sizeof(unsigned)));
+	TRY(hipMalloc(&nbox, 6 * (size_t)ni * sizeof(float)));
+	TRY(hipMalloc(&keep, (size_t)ni * sizeof(uint32_t)));
+	TRY(hipMalloc(&idx, ((size_t)ni + 1) * sizeof(uint32_t)));
+	TRY(hipMalloc(&scal, 4 * sizeof(unsigned)));
+	{
+		float s[3];
+		for (int a = 0; a < 3; a++) {
+			const float ext = bhi[a] - blo[a];
+			s[a] = ext > 0.f ? 2097151.f / ext : 0.f;
+		}
+		const dim3 gn((n + 255) / 256), gi((ni + 255) / 256);
+		hipLaunchKernelGGL(k_lb_morton, gn, dim3(256), 0, st, n, d_lo, d_hi, blo[0], blo[1], blo[2], s[0], s[1], s[2],
+				   keys, vals);
+		TRY(hipGetLastError());
+		hipcub::DoubleBuffer<uint64_t> kb(keys, keys + n);
+		hipcub::DoubleBuffer<uint32_t> vb(vals, vals + n);
+		size_t tb = 0;
+		TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kb, vb, (int)n, 0, 63, st));
+		TRY(hipMalloc(&temp, tb));
+		TRY(hipcub::DeviceRadixSort::SortPairs(temp, tb, kb, vb, (int)n, 0, 63, st));
+		const uint64_t *sk = kb.Current();
+		const uint32_t *perm = vb.Current();
+		uint32_t nnodes = 0, root = 0, depth = 0;
+		if (n > max_leaf) {
+			hipLaunchKernelGGL(k_lb_karras, gi, dim3(256), 0, st, (int)n, sk, child, range, pint, pleaf);
+			TRY(hipGetLastError());
+			TRY(hipMemsetAsync(arrive, 0, (size_t)ni * sizeof(unsigned), st));
+			hipLaunchKernelGGL(k_lb_refit, gn, dim3(256), 0, st, (int)n, perm, d_lo, d_hi, child, pint, pleaf, arrive,
+					   nbox);
+			hipLaunchKernelGGL(k_lb_keep, gi, dim3(256), 0, st, (int)n, max_leaf, range, keep);
+			TRY(hipGetLastError());
+			size_t tb2 = 0;
+			TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, keep, idx, ni, st));
+			void *temp2 = nullptr;
+			TRY(hipMalloc(&temp2, tb2));
+			e = hipcub::DeviceScan::ExclusiveSum(temp2, tb2, keep, idx, ni, st);
+			(void)hipFreeAsync(temp2, st);
+			TRY(e);
+			TRY(hipMemsetAsync(scal, 0, 4 * sizeof(unsigned), st));
+			hipLaunchKernelGGL(k_lb_depth, gn, dim3(256), 0, st, (int)n, keep, pint, pleaf, scal);
+			TRY(hipGetLastError());
+			uint32_t last[2];
+			TRY(hipMemcpyAsync(&last[0], idx + (ni - 1), 4, hipMemcpyDeviceToHost, st));
+			TRY(hipMemcpyAsync(&last[1], keep + (ni - 1), 4, hipMemcpyDeviceToHost, st));
+			TRY(hipMemcpyAsync(&depth, scal, 4, hipMemcpyDeviceToHost, st));
+			TRY(hipStreamSynchronize(st));
+			nnodes = last[0] + last[1];
+			root = 0;
+		} else {
+			root = RTX_EMPTY_REF;
+		}
+		DNode *recs = nullptr;
+		TRY(hipMalloc(&recs, ((size_t)nnodes + n) * sizeof(DNode)));
+		/* n <= max_leaf: no internal nodes, the caller makes the root one leaf of all primitives */
+		hipLaunchKernelGGL(k_lb_emit, gn, dim3(256), 0, st, n > max_leaf ? (int)n - 1 : 0, (int)n, nnodes, keep, idx,
+				   child, range, nbox, perm, d_lo, d_hi, d_prims_in, recs);
+		e = hipGetLastError();
+		if (e == hipSuccess)
+			e = hipStreamSynchronize(st);
+		if (e != hipSuccess) {
+			(void)hipFree(recs);
+			goto done;
+		}
+		*recs_out = recs;
+		*nnodes_out = nnodes;
+		*root_out = root;
+		*depth_out = depth;
+	}
+done:
+#undef TRY
+	(void)hipFree(temp);
+	(void)hipFree(keys);
+	(void)hipFree(vals);
+	(void)hipFree(child);
+	(void)hipFree(range);
+	(void)hipFree(pint);
+	(void)hipFree(pleaf);
+	(void)hipFree(arrive);
+	(void)hipFree(nbox);
+	(void)hipFree(keep);
+	(void)hipFree(idx);
+	(void)hipFree(scal);
+	return e;
+}

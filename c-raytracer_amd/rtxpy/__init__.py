@@ -212,6 +212,10 @@ class Renderer:
         _check(self.lib.rtx_open(device, C.byref(self._ctx)))
         self.device = device
 
+    def set_builder(self, builder):
+        """rtx_set_builder: abi.RTX_BUILD_SAH_HOST (default) or abi.RTX_BUILD_LBVH_GPU."""
+        _check(self.lib.rtx_set_builder(self._ctx, builder))
+
     def upload(self, scene):
         _check(self.lib.rtx_upload_scene(self._ctx, C.byref(scene.desc)))
 

@@ -62,12 +62,13 @@ class Stats(C.Structure):
                 ("shadow_node_visits", C.c_uint64), ("shadow_tri_tests", C.c_uint64),
                 ("shadow_sphere_tests", C.c_uint64), ("shadow_plane_tests", C.c_uint64),
                 ("shade_points", C.c_uint64), ("kernel_ms", C.c_double), ("trace_ms", C.c_double),
-                ("shadow_ms", C.c_double), ("accum_ms", C.c_double), ("sort_ms", C.c_double),
+                ("shadow_ms", C.c_double), ("accum_ms", C.c_double), ("sort_ms", C.c_double), ("build_ms", C.c_double),
                 ("bvh_nodes", C.c_uint32),
                 ("bvh_depth", C.c_uint32), ("bvh_prims", C.c_uint32), ("waves", C.c_uint32),
-                ("chunks", C.c_uint32), ("pad", C.c_uint32)]
+                ("chunks", C.c_uint32), ("builder", C.c_uint32)]
 
 
+RTX_BUILD_SAH_HOST, RTX_BUILD_LBVH_GPU = 0, 1
 RTX_DOF_NONE, RTX_DOF_SCALE_BIAS, RTX_DOF_CAMERA = 0, 1, 2
 RTX_FALLOFF_QUAD, RTX_FALLOFF_LIN, RTX_FALLOFF_INV_QUAD = 0, 1, 2
 
@@ -91,7 +92,7 @@ KAT_NAMES = ["moller", "sphere", "plane", "slab", "noise", "texture", "sph_light
 # symbols include/rtx.h declares (checked by tests/test_abi.py)
 RTX_SYMBOLS = ["rtx_params_default", "rtx_device_count", "rtx_open", "rtx_upload_scene", "rtx_render",
                "rtx_render_device", "rtx_get_stats", "rtx_close", "rtx_last_error", "rtx_kat", "rtx_postprocess",
-               "rtx_postprocess_device"]
+               "rtx_postprocess_device", "rtx_set_builder"]
 RTX_SCENE_SYMBOLS = ["rtx_scene_load", "rtx_scene_parse", "rtx_scene_desc_of", "rtx_scene_num_json_objects",
                      "rtx_scene_free", "rtx_scene_last_error", "rtx_frame_setup", "rtx_tiff_write", "rtx_hash_djb",
                      "rtx_params_from_argv", "rtx_stl_write", "rtx_tiff_read_raw", "rtx_buffer_free",
@@ -153,6 +154,8 @@ def declare_rtx(lib):
     lib.rtx_last_error.restype = C.c_char_p
     lib.rtx_kat.argtypes = [C.c_int, C.c_uint32, C.c_void_p, C.c_void_p, C.POINTER(Params)]
     lib.rtx_kat.restype = C.c_int
+    lib.rtx_set_builder.argtypes = [C.c_void_p, C.c_int]
+    lib.rtx_set_builder.restype = C.c_int
     lib.rtx_postprocess.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(Post), C.c_void_p, C.c_void_p]
     lib.rtx_postprocess.restype = C.c_int
     lib.rtx_postprocess_device.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(Post), C.c_void_p,

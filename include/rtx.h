@@ -189,15 +189,22 @@ typedef struct rtx_stats {
 	double shadow_ms;            /* ... shadow-ray kernel */
 	double accum_ms;             /* ... per-tile accumulation kernel */
 	double sort_ms;              /* ... shade-point ordering (key + radix sort) */
+	double build_ms;             /* host wall time of the last rtx_upload_scene's BVH build (incl. its uploads) */
 	uint32_t bvh_nodes;
 	uint32_t bvh_depth;
 	uint32_t bvh_prims;
 	uint32_t waves;              /* persistent waves of the closest-hit kernel */
 	uint32_t chunks;             /* tile chunks the frame was split into */
-	uint32_t pad;
+	uint32_t builder;            /* RTX_BUILD_* used by the last upload */
 } rtx_stats;
 
 typedef struct rtx_ctx rtx_ctx;
+
+/* BVH builders for rtx_upload_scene (replacing accel_init, accel.c:266-315) */
+enum {
+	RTX_BUILD_SAH_HOST = 0, /* binned SAH on the host (default: fewest node visits) */
+	RTX_BUILD_LBVH_GPU = 1  /* Morton-code linear BVH built on the device (rtx_build.hip) */
+};
 
 int rtx_device_count(int *count);
 /* Open a context on HIP device `device` (must be gfx950). */
@@ -213,6 +220,8 @@ int rtx_render(rtx_ctx *ctx, const rtx_frame *frame, const rtx_params *params, f
 int rtx_render_device(rtx_ctx *ctx, const rtx_frame *frame, const rtx_params *params, void *d_rgb, void *d_z,
 		      void *stream);
 int rtx_get_stats(const rtx_ctx *ctx, rtx_stats *out);
+/* Builder used by subsequent rtx_upload_scene calls on this context (RTX_BUILD_*). */
+int rtx_set_builder(rtx_ctx *ctx, int builder);
 void rtx_close(rtx_ctx *ctx);
 const char *rtx_last_error(void);
 
