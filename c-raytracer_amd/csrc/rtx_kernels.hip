@@ -1072,6 +1072,71 @@ template <typename T> __device__ __forceinline__ T *unip(T *p)
 	return (T *)(((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v));
 }
 
+/* one light sample per lane of the shade point `rec` (render.c:170-229): the light point of
+ * sample idx (emitters in scene order, the hit object skipped), its shadow ray through the
+ * packet walk, attenuation and Phong / Blinn.  Argument-block fields are read from LDS behind
+ * reread barriers so none stays in registers across the walk. */
+template <bool COUNT>
+__device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec, uint32_t idx, bool act,
+					   ShadowCount &sc)
+{
+	reread_barrier();
+	const float4 q0 = rec[0], q4 = rec[4];
+	const f3 p = mk3(q0.x, q0.y, q0.z);
+	const uint32_t obj = __float_as_uint(q4.x);
+	const DEmitter *emitters = unip(ks.emitters);
+	const uint32_t num_emitters = uni(ks.num_emitters);
+	uint32_t j = idx;
+	uint32_t e = 0;
+	for (; e < num_emitters; e++) {
+		const uint32_t eo = emitters[e].obj, enl = emitters[e].num_lights;
+		if (eo == obj)
+			continue;
+		if (j < enl)
+			break;
+		j -= enl;
+	}
+	if (e >= num_emitters)
+		e = 0;
+	const DEmitter &E = emitters[e];
+	float u1 = 0.5f, u2 = 0.5f;
+	if (uni(ks.rng) != RTX_RNG_CONST) /* the key already carries the seed (rtx_key_pixel) */
+		rtx_draw2(key_of(__float_as_uint(q4.y), __float_as_uint(q4.z)), e, j, &u1, &u2);
+	const f3 lp = light_point(E, p, u1, u2);
+	const f3 dv = sub3(lp, p);
+	const float ldist = mag3(dv);
+	const float dsq = magsqr3(dv);
+	const f3 ldir = mul3s(dv, 1.f / ldist);
+	f3 li = ld3(E.li);
+	const bool blocked = shadow_packet<COUNT>((const char *)unip(ks.recs), unip(ks.mats), unip(ks.planes),
+						  uni(ks.num_planes), RTX_DEBUG_NOWALK ? RTX_EMPTY_REF : uni(ks.root_ref),
+						  act, p, ldir, ldist, E.obj, E.type == RTX_TRIANGLE, li, sc);
+	reread_barrier();
+	f3 contribution = mk3(0.f, 0.f, 0.f);
+	if (act && !blocked) {
+		/* shading terms (render.c:199-228) read after the traversal */
+		const float4 q1 = rec[1], q2 = rec[2], q3 = rec[3];
+		const f3 n = mk3(q1.x, q1.y, q1.z), dir = mk3(q2.x, q2.y, q2.z);
+		const float a = dot3(ldir, n);
+		const int32_t att = (int32_t)uni((uint32_t)ks.attenuation);
+		if (att == RTX_ATT_LIN)
+			li = mul3s(li, 1.f / (ks.att_offset + ldist));
+		else if (att == RTX_ATT_SQR)
+			li = mul3s(li, 1.f / (ks.att_offset + dsq));
+		const DMaterial &m = unip(ks.mats)[__float_as_uint(q3.w)];
+		const f3 diff = mul3s(mul3v(mk3(q3.x, q3.y, q3.z), li), fmaxf(0.f, a));
+		float sm;
+		if ((int32_t)uni((uint32_t)ks.reflection) == RTX_BLINN) {
+			sm = -dot3(n, norm3(add3(mul3s(ldir, -1.f), dir)));
+		} else {
+			sm = -dot3(sub3(mul3s(n, 2.f * a), ldir), dir);
+		}
+		const f3 spec = mul3s(mul3v(ld3(m.ks), li), fmaxf(0.f, powf(sm, m.shininess)));
+		contribution = add3(diff, spec);
+	}
+	return contribution;
+}
+
 template <bool COUNT, int OCC>
 __global__ __launch_bounds__(WAVE, OCC) void k_shadow(KShadow ka)
 {
@@ -1108,90 +1173,60 @@ __global__ __launch_bounds__(WAVE, OCC) void k_shadow(KShadow ka)
 	}
 	lds_sync();
 	ShadowCount sc = { 0, 0, 0, 0 };
-	for (uint32_t base = 0;;) {
-		reread_barrier();
-		const uint32_t tot = uni(off[WAVE]), slot_b = uni(ks.slot_b), slot_lg = uni(ks.slot_lg);
-		if (base >= tot)
-			break;
-		const uint32_t slot = base + (lane_id() >> slot_lg);
-		const uint32_t k = slot < tot ? owner_of(off, slot) : 0u;
-		const uint32_t idx = ((slot - off[k]) << slot_lg) + (lane_id() & (slot_b - 1));
-		const bool act = slot < tot && idx < nls[k];
-		const float4 *rec = unip(ks.sp) + (size_t)sid[k] * SPREC;
-		const float4 q0 = rec[0], q4 = rec[4];
-		const f3 p = mk3(q0.x, q0.y, q0.z);
-		const uint32_t obj = __float_as_uint(q4.x);
-		const DEmitter *emitters = unip(ks.emitters);
-		const uint32_t num_emitters = uni(ks.num_emitters);
-		uint32_t j = idx;
-		/* (emitter, light) of this sample: emitters in scene order, the hit object skipped */
-		uint32_t e = 0;
-		for (; e < num_emitters; e++) {
-			const uint32_t eo = emitters[e].obj, enl = emitters[e].num_lights;
-			if (eo == obj)
-				continue;
-			if (j < enl)
-				break;
-			j -= enl;
-		}
-		if (e >= num_emitters)
-			e = 0;
-		const DEmitter &E = emitters[e];
-		float u1 = 0.5f, u2 = 0.5f;
-		if (uni(ks.rng) != RTX_RNG_CONST) /* the key already carries the seed (rtx_key_pixel) */
-			rtx_draw2(key_of(__float_as_uint(q4.y), __float_as_uint(q4.z)), e, j, &u1, &u2);
-		const f3 lp = light_point(E, p, u1, u2);
-		const f3 dv = sub3(lp, p);
-		const float ldist = mag3(dv);
-		const float dsq = magsqr3(dv);
-		const f3 ldir = mul3s(dv, 1.f / ldist);
-		f3 li = ld3(E.li);
-		const bool blocked = shadow_packet<COUNT>((const char *)unip(ks.recs), unip(ks.mats), unip(ks.planes),
-							  uni(ks.num_planes), RTX_DEBUG_NOWALK ? RTX_EMPTY_REF : uni(ks.root_ref), act, p, ldir, ldist, E.obj,
-							  E.type == RTX_TRIANGLE, li, sc);
-		reread_barrier();
-		f3 contribution = mk3(0.f, 0.f, 0.f);
-		if (act && !blocked) {
-			/* shading terms (render.c:199-228) read after the traversal */
-			const float4 *r = unip(ks.sp) + (size_t)sid[k] * SPREC;
-			const float4 q1 = r[1], q2 = r[2], q3 = r[3];
-			const f3 n = mk3(q1.x, q1.y, q1.z), dir = mk3(q2.x, q2.y, q2.z);
-			const float a = dot3(ldir, n);
-			const int32_t att = (int32_t)uni((uint32_t)ks.attenuation);
-			if (att == RTX_ATT_LIN)
-				li = mul3s(li, 1.f / (ks.att_offset + ldist));
-			else if (att == RTX_ATT_SQR)
-				li = mul3s(li, 1.f / (ks.att_offset + dsq));
-			const DMaterial &m = unip(ks.mats)[__float_as_uint(q3.w)];
-			const f3 diff = mul3s(mul3v(mk3(q3.x, q3.y, q3.z), li), fmaxf(0.f, a));
-			float sm;
-			if ((int32_t)uni((uint32_t)ks.reflection) == RTX_BLINN) {
-				sm = -dot3(n, norm3(add3(mul3s(ldir, -1.f), dir)));
-			} else {
-				sm = -dot3(sub3(mul3s(n, 2.f * a), ldir), dir);
+	if (ka.slot_b == WAVE) {
+		/* >= 64 lights: every packet is 64 samples of ONE shade point.  The point is wave-uniform
+		 * (its record is read once per packet through one address, no owner search), each lane
+		 * sums its samples over the point's packets, and one butterfly per point reduces them. */
+		for (uint32_t k = 0; k < cnt; k++) {
+			reread_barrier();
+			const uint32_t nl = uni(nls[k]);
+			const float4 *rec = unip(ks.sp) + (size_t)uni(sid[k]) * SPREC;
+			f3 acc = mk3(0.f, 0.f, 0.f);
+			for (uint32_t base = 0; base < nl; base += WAVE) {
+				const uint32_t idx = base + lane_id();
+				acc = add3(acc, light_sample<COUNT>(ks, rec, idx, idx < nl, sc));
 			}
-			const f3 spec = mul3s(mul3v(ld3(m.ks), li), fmaxf(0.f, powf(sm, m.shininess)));
-			contribution = add3(diff, spec);
-		}
-		/* per-shade-point sums; lanes are ordered by k */
-		const uint32_t t2 = uni(off[WAVE]), sb = uni(ks.slot_b), spp = WAVE / sb;
-		const uint32_t last_slot_lane = (min(t2 - base, spp) - 1) * sb;
-		const uint32_t k0 = readlane(k, 0), k1 = readlane(k, last_slot_lane);
-		for (uint32_t kk = k0; kk <= k1; kk++) {
-			const bool in = act && k == kk;
-			if (!ballot(in))
-				continue;
-			const float sx = wave_sum(in ? contribution.x : 0.f);
-			const float sy = wave_sum(in ? contribution.y : 0.f);
-			const float sz = wave_sum(in ? contribution.z : 0.f);
+			const float sx = wave_sum(acc.x), sy = wave_sum(acc.y), sz = wave_sum(acc.z);
 			if (lane_id() == 0) {
-				Ls[0][kk] += sx;
-				Ls[1][kk] += sy;
-				Ls[2][kk] += sz;
+				Ls[0][k] = sx;
+				Ls[1][k] = sy;
+				Ls[2][k] = sz;
 			}
 		}
 		lds_sync();
-		base += spp;
+	} else {
+		/* fewer lights: several points share a packet, each in its own power-of-two lane slot */
+		for (uint32_t base = 0;;) {
+			reread_barrier();
+			const uint32_t tot = uni(off[WAVE]), slot_b = uni(ks.slot_b), slot_lg = uni(ks.slot_lg);
+			if (base >= tot)
+				break;
+			const uint32_t slot = base + (lane_id() >> slot_lg);
+			const uint32_t k = slot < tot ? owner_of(off, slot) : 0u;
+			const uint32_t idx = ((slot - off[k]) << slot_lg) + (lane_id() & (slot_b - 1));
+			const bool act = slot < tot && idx < nls[k];
+			const float4 *rec = unip(ks.sp) + (size_t)sid[k] * SPREC;
+			const f3 contribution = light_sample<COUNT>(ks, rec, idx, act, sc);
+			/* per-shade-point sums; lanes are ordered by k */
+			const uint32_t t2 = uni(off[WAVE]), sb = uni(ks.slot_b), spp = WAVE / sb;
+			const uint32_t last_slot_lane = (min(t2 - base, spp) - 1) * sb;
+			const uint32_t k0 = readlane(k, 0), k1 = readlane(k, last_slot_lane);
+			for (uint32_t kk = k0; kk <= k1; kk++) {
+				const bool in = act && k == kk;
+				if (!ballot(in))
+					continue;
+				const float sx = wave_sum(in ? contribution.x : 0.f);
+				const float sy = wave_sum(in ? contribution.y : 0.f);
+				const float sz = wave_sum(in ? contribution.z : 0.f);
+				if (lane_id() == 0) {
+					Ls[0][kk] += sx;
+					Ls[1][kk] += sy;
+					Ls[2][kk] += sz;
+				}
+			}
+			lds_sync();
+			base += spp;
+		}
 	}
 	reread_barrier();
 	if (own) {
