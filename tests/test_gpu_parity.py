@@ -187,7 +187,7 @@ def test_gpu_deterministic_and_sharding_exact(renderer):
     assert (tot[0], tot[1]) == (sa.closest_rays, sa.shadow_rays)
 
 
-@pytest.mark.parametrize("name", ["s3_path2", "s5_path2"])
+@pytest.mark.parametrize("name", ["s3_path2", "s5_path2", "st_amb"])
 def test_gpu_shade_point_order_is_invisible(renderer, name, monkeypatch):
     """k_shadow's Morton ordering of shade points (rtx_sort.hip) changes only which wave
     computes a point: the image and ray counts are bit-identical to emission order."""
