@@ -52,6 +52,9 @@
 #ifndef RTX_SH_FMA
 #define RTX_SH_FMA 1 /* fused products in the shadow triangle test */
 #endif
+#ifndef RTX_SH_RAWMIN
+#define RTX_SH_RAWMIN 1 /* segment-end min of the octant box test in asm (no canonicalise) */
+#endif
 #ifndef RTX_SH_RCP
 #define RTX_SH_RCP 1 /* any-hit triangle test with v_rcp_f32 instead of IEEE 1/a */
 #endif
@@ -795,7 +798,14 @@ __device__ __forceinline__ bool box_hit(const v16u &nd, const uint32_t b, f3 oi,
 	const float ny = (OCT & 2) ? ty.x : ty.y, fy = (OCT & 2) ? ty.y : ty.x;
 	const float nz = (OCT & 4) ? tz.x : tz.y, fz = (OCT & 4) ? tz.y : tz.x;
 	const float tn = fmaxf(fmaxf(nx, ny), fmaxf(nz, 0.f));
+#if RTX_SH_RAWMIN
+	/* min with the segment end in asm: tlim is a loop-carried value the compiler would
+	 * canonicalise before every fminf (one extra VALU per node step); no NaN reaches here */
+	float tf = fminf(fminf(fx, fy), fz);
+	asm("v_min_f32 %0, %0, %1" : "+v"(tf) : "v"(tlim));
+#else
 	const float tf = fminf(fminf(fx, fy), fminf(fz, tlim));
+#endif
 	return tn <= tf;
 }
 
@@ -874,31 +884,38 @@ __device__ __forceinline__ bool shadow_prim(const v16u &pr, const DMaterial *__r
  * is hit by any live ray, else the far child if hit, else RTX_NONE (pop); when both are hit
  * the far child is pushed: lane sp of the VGPR stack <- far, sp += 1.  A miss writes NONE
  * into lane sp, above the stack top. */
+#define RTX_NODE_STEP_ASM(OCTC)                                                                               \
+	asm volatile("s_bitcmp1_b32 %[ord], %[oct]\n\t"                                                        \
+		     "s_cselect_b32 %[rn], %[r0], %[r1]\n\t"                                                   \
+		     "s_cselect_b32 %[rf], %[r1], %[r0]\n\t"                                                   \
+		     "s_cselect_b64 %[bn], %[b0], %[b1]\n\t"                                                   \
+		     "s_cselect_b64 %[bf], %[b1], %[b0]\n\t"                                                   \
+		     "s_cmp_lg_u64 %[bf], 0\n\t"                                                               \
+		     "s_cselect_b32 %[rf], %[rf], -1\n\t"                                                      \
+		     "s_cmp_lg_u64 %[bn], 0\n\t"                                                               \
+		     "s_cselect_b32 %[next], %[rn], %[rf]\n\t"                                                 \
+		     "s_cselect_b32 %[push], %[rf], -1\n\t"                                                    \
+		     "v_mov_b32 %[t], %[push]\n\t"                                                             \
+		     "v_cmp_eq_u32 vcc, %[sp], %[lane]\n\t"                                                    \
+		     "v_cndmask_b32 %[stk], %[stk], %[t], vcc\n\t"                                             \
+		     "s_cmp_lg_u32 %[push], -1\n\t"                                                            \
+		     "s_addc_u32 %[sp], %[sp], 0"                                                              \
+		     : [next] "=&s"(next), [push] "=&s"(push), [rn] "=&s"(rn), [rf] "=&s"(rf), [bn] "=&s"(bn), \
+		       [bf] "=&s"(bf), [t] "=&v"(t), [sp] "+s"(sp), [stk] "+v"(stk)                            \
+		     : [b0] "s"(b0), [b1] "s"(b1), [r0] "s"(r0), [r1] "s"(r1), [ord] "s"(order), OCTC,         \
+		       [lane] "v"(lane_id())                                                                   \
+		     : "scc", "vcc")
+
+template <int OCT>
 __device__ __forceinline__ uint32_t node_step(u64 b0, u64 b1, uint32_t r0, uint32_t r1, uint32_t order, uint32_t oct,
 					      uint32_t &sp, uint32_t &stk)
 {
 	uint32_t next, push, rn, rf, t;
 	u64 bn, bf;
-	asm volatile("s_bitcmp1_b32 %[ord], %[oct]\n\t"
-		     "s_cselect_b32 %[rn], %[r0], %[r1]\n\t"
-		     "s_cselect_b32 %[rf], %[r1], %[r0]\n\t"
-		     "s_cselect_b64 %[bn], %[b0], %[b1]\n\t"
-		     "s_cselect_b64 %[bf], %[b1], %[b0]\n\t"
-		     "s_cmp_lg_u64 %[bf], 0\n\t"
-		     "s_cselect_b32 %[rf], %[rf], -1\n\t"
-		     "s_cmp_lg_u64 %[bn], 0\n\t"
-		     "s_cselect_b32 %[next], %[rn], %[rf]\n\t"
-		     "s_cselect_b32 %[push], %[rf], -1\n\t"
-		     "v_mov_b32 %[t], %[push]\n\t"
-		     "v_cmp_eq_u32 vcc, %[sp], %[lane]\n\t"
-		     "v_cndmask_b32 %[stk], %[stk], %[t], vcc\n\t"
-		     "s_cmp_lg_u32 %[push], -1\n\t"
-		     "s_addc_u32 %[sp], %[sp], 0"
-		     : [next] "=&s"(next), [push] "=&s"(push), [rn] "=&s"(rn), [rf] "=&s"(rf), [bn] "=&s"(bn),
-		       [bf] "=&s"(bf), [t] "=&v"(t), [sp] "+s"(sp), [stk] "+v"(stk)
-		     : [b0] "s"(b0), [b1] "s"(b1), [r0] "s"(r0), [r1] "s"(r1), [ord] "s"(order), [oct] "s"(oct),
-		       [lane] "v"(lane_id())
-		     : "scc", "vcc");
+	if constexpr (OCT < 8) /* octant as an inline constant of s_bitcmp1_b32 */
+		RTX_NODE_STEP_ASM([oct] "n"(OCT));
+	else
+		RTX_NODE_STEP_ASM([oct] "s"(oct));
 	return next;
 }
 
@@ -959,7 +976,7 @@ __device__ __forceinline__ void shadow_walk(const char *__restrict__ recs, const
 				sc.nodes += popc64(ballot(tl >= 0.f));
 			const u64 b0 = ballot(box_hit<OCT>(rec, 0, oi, inv, tl));
 			const u64 b1 = ballot(box_hit<OCT>(rec, 6, oi, inv, tl));
-			next = node_step(b0, b1, rec[12], rec[13], rec[14], oct, sp, stk);
+			next = node_step<OCT>(b0, b1, rec[12], rec[13], rec[14], oct, sp, stk);
 		} else {
 			const uint32_t off = ref & RTX_REF_OFF, cnt = (ref & RTX_REF_CNT) + 1;
 			if (RTX_SH_PF) { /* the leaf's second primitive and the stack top (next pop) */
