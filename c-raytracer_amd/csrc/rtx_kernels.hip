@@ -55,6 +55,9 @@
 #ifndef RTX_SH_RAWMIN
 #define RTX_SH_RAWMIN 1 /* segment-end min of the octant box test in asm (no canonicalise) */
 #endif
+#ifndef RTX_SH_MASK
+#define RTX_SH_MASK 1 /* triangle any-hit decided on wave masks (no VGPR round trip) */
+#endif
 #ifndef RTX_SH_RCP
 #define RTX_SH_RCP 1 /* any-hit triangle test with v_rcp_f32 instead of IEEE 1/a */
 #endif
@@ -837,6 +840,30 @@ __device__ __forceinline__ bool any_tri(f3 v0, f3 e1, f3 e2, f3 o, f3 d, float e
 	return ((int)(fabsf(a) >= eps) & (int)(out <= 0.f) & (int)(fminf(t - eps, tlim - t) > 0.f)) != 0;
 }
 
+/* any_tri as a wave mask: each compare's ballot is its v_cmp result, ANDed on the scalar
+ * unit (a per-lane bool would be materialised in a VGPR and compared back before the branch) */
+__device__ __forceinline__ u64 any_tri_mask(f3 v0, f3 e1, f3 e2, f3 o, f3 d, float eps, float tlim)
+{
+	const f3 h = cross3_fma(d, e2);
+	const float a = dot3_fma(e1, h);
+	const float f = RTX_SH_RCP ? __builtin_amdgcn_rcpf(a) : 1.f / a;
+	const f3 s = sub3(o, v0);
+	const float u = f * dot3_fma(s, h);
+	const f3 q = cross3_fma(s, e1);
+	const float v = f * dot3_fma(d, q);
+	const float t = f * dot3_fma(e2, q);
+	const float out = fmaxf(fmaxf(-u, -v), (u + v) - 1.f);
+	return ballot(fabsf(a) >= eps) & ballot(out <= 0.f) & ballot(fminf(t - eps, tlim - t) > 0.f);
+}
+
+/* per-lane select by a wave mask held in SGPRs: m's bit set -> b, else a */
+__device__ __forceinline__ float msel(u64 m, float a, float b)
+{
+	float r;
+	asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+	return r;
+}
+
 /* one primitive of a leaf against the packet (accel.c:362-373): the target emitter skipped,
  * opaque hit -> the lane is blocked (tl = -1: no later test can hit it), transparent hit ->
  * li *= kt.  Returns true when a lane was blocked. */
@@ -928,6 +955,23 @@ __device__ __forceinline__ bool shadow_tri(const v16u &pr, const DMaterial *__re
 	const uint32_t meta = pr[11];
 	if (COUNT)
 		sc.tris += popc64(ballot(tl >= 0.f));
+#if RTX_SH_MASK
+	u64 hm = any_tri_mask(mk3(__uint_as_float(pr[0]), __uint_as_float(pr[1]), __uint_as_float(pr[2])),
+			      mk3(__uint_as_float(pr[4]), __uint_as_float(pr[5]), __uint_as_float(pr[6])),
+			      mk3(__uint_as_float(pr[8]), __uint_as_float(pr[9]), __uint_as_float(pr[10])), o, d,
+			      __uint_as_float(pr[3]), tl);
+	if (tri_emit)
+		hm &= ballot(pr[7] != emit_obj);
+	if (!hm)
+		return false;
+	if (meta & RTX_META_TRANSPARENT) {
+		const auto *m = cptr(mats) + (meta & RTX_META_MAT);
+		li = mk3(msel(hm, li.x, li.x * m->kt[0]), msel(hm, li.y, li.y * m->kt[1]), msel(hm, li.z, li.z * m->kt[2]));
+		return false;
+	}
+	tl = msel(hm, tl, -1.f);
+	return true;
+#else
 	bool h = any_tri(mk3(__uint_as_float(pr[0]), __uint_as_float(pr[1]), __uint_as_float(pr[2])),
 			 mk3(__uint_as_float(pr[4]), __uint_as_float(pr[5]), __uint_as_float(pr[6])),
 			 mk3(__uint_as_float(pr[8]), __uint_as_float(pr[9]), __uint_as_float(pr[10])), o, d,
@@ -946,6 +990,7 @@ __device__ __forceinline__ bool shadow_tri(const v16u &pr, const DMaterial *__re
 	if (h)
 		tl = -1.f;
 	return true;
+#endif
 }
 
 /* is_light_blocked for one packet of shadow rays (accel.c:317-387): the 64 rays walk the BVH
@@ -1119,6 +1164,18 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	float u1 = 0.5f, u2 = 0.5f;
 	if (uni(ks.rng) != RTX_RNG_CONST) /* the key already carries the seed (rtx_key_pixel) */
 		rtx_draw2(key_of(__float_as_uint(q4.y), __float_as_uint(q4.z)), e, j, &u1, &u2);
+#ifdef RTX_SH_STRAT /* measurement only: Morton-stratified light samples (packet coherence bound) */
+	{
+		const uint32_t m = j * 1024u / emitters[e].num_lights;
+		uint32_t x = 0, y = 0;
+		for (int b = 0; b < 5; b++) {
+			x |= ((m >> (2 * b)) & 1u) << b;
+			y |= ((m >> (2 * b + 1)) & 1u) << b;
+		}
+		u1 = (x + u1) * (1.f / 32.f);
+		u2 = (y + u2) * (1.f / 32.f);
+	}
+#endif
 	const f3 lp = light_point(E, p, u1, u2);
 	const f3 dv = sub3(lp, p);
 	const float ldist = mag3(dv);
