@@ -320,6 +320,9 @@ def main():
                     "algorithmic_bytes_per_launch": int(algo), "shadow_rays": int(c.shadow_rays),
                     "node_visits": int(c.shadow_node_visits), "tri_tests": int(c.shadow_tri_tests),
                     "sphere_tests": int(c.shadow_sphere_tests), "plane_tests": int(c.shadow_plane_tests),
+                    "packet_node_records": int(c.shadow_packet_nodes),
+                    "packet_prim_records": int(c.shadow_packet_prims),
+                    "ray_need_nodes": int(c.shadow_ray_nodes), "ray_need_prims": int(c.shadow_ray_prims),
                     "kernel_ms": round(shadow_ms, 3),
                     "note": "B_ray = 64*node_visits + 48*tri_tests + 32*sphere_tests + 16*plane_tests + 48 "
                             "per shadow ray (SURVEY §8(d)), visits counted per ray (lane); frac > 1 because a "

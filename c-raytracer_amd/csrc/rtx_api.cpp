@@ -29,8 +29,8 @@ extern "C" hipError_t rtx_launch_trace(const DScene *S, const DFrame *F, const D
 				       uint32_t tile_end, unsigned long long *ctr, uint32_t waves, int count,
 				       hipStream_t stream);
 extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const float4 *sp, const uint32_t *perm,
-					uint32_t n_sp, uint32_t per_wave, uint32_t slot_b, float4 *contrib,
-					unsigned long long *ctr, int count, hipStream_t stream);
+					uint32_t n_sp, uint32_t per_wave, uint32_t slot_b, uint32_t rays_per_lane,
+					float4 *contrib, unsigned long long *ctr, int count, hipStream_t stream);
 extern "C" hipError_t rtx_launch_post(uint32_t w, uint32_t h, const rtx_post *pp, float *rgb, const float *z,
 				      int *rad, float4 *pv, unsigned *scratch, hipStream_t stream);
 extern "C" hipError_t rtx_spsort_temp_bytes(uint32_t n, size_t *bytes);
@@ -75,6 +75,7 @@ struct rtx_ctx {
 	DPlane *d_planes = nullptr;
 	DMaterial *d_mats = nullptr;
 	DEmitter *d_emitters = nullptr;
+	DThread *d_threads = nullptr;
 	DScene scene{};
 	bool have_scene = false;
 	/* work buffers (grow-only) */
@@ -151,6 +152,7 @@ static void free_scene(rtx_ctx *c)
 	dfree(c->d_planes);
 	dfree(c->d_mats);
 	dfree(c->d_emitters);
+	dfree(c->d_threads);
 	c->have_scene = false;
 }
 
@@ -226,6 +228,52 @@ template <class T> static int upload(T *&dst, const std::vector<T> &v)
 	if (!v.empty())
 		HIP_TRY(hipMemcpy(dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
 	return RTX_OK;
+}
+
+/* DThread preorder of the subtree at device ref `ref` (rtx_device.h): the node itself with the
+ * box it has in its parent, then its left and right subtrees.  A left subtree continues at its
+ * right sibling, a right subtree at its parent's continuation, so the skip link of every node
+ * is known when it is written (subtree sizes from `size`, filled by thread_sizes). */
+static uint32_t thread_sizes(const std::vector<DNode> &recs, uint32_t ref, std::vector<uint32_t> &size)
+{
+	if (ref & RTX_REF_LEAF)
+		return 1;
+	const uint32_t i = (ref & RTX_REF_OFF) / (uint32_t)sizeof(DNode);
+	const DNode &n = recs[i];
+	size[i] = 1 + thread_sizes(recs, n.ref0, size) + thread_sizes(recs, n.ref1, size);
+	return size[i];
+}
+
+static void thread_emit(const std::vector<DNode> &recs, const std::vector<uint32_t> &size, uint32_t ref,
+			const float lo[3], const float hi[3], uint32_t skip, std::vector<DThread> &out)
+{
+	DThread t;
+	memcpy(t.lo, lo, 12);
+	memcpy(t.hi, hi, 12);
+	t.skip = skip;
+	t.ref = (ref & RTX_REF_LEAF) ? ref : 0u;
+	const uint32_t me = (uint32_t)out.size();
+	out.push_back(t);
+	if (ref & RTX_REF_LEAF)
+		return;
+	const DNode &n = recs[(ref & RTX_REF_OFF) / (uint32_t)sizeof(DNode)];
+	const float l0[3] = { n.lo0x, n.lo0y, n.lo0z }, h0[3] = { n.hi0x, n.hi0y, n.hi0z };
+	const float l1[3] = { n.lo1x, n.lo1y, n.lo1z }, h1[3] = { n.hi1x, n.hi1y, n.hi1z };
+	const uint32_t left_size = (n.ref0 & RTX_REF_LEAF) ? 1u : size[(n.ref0 & RTX_REF_OFF) / (uint32_t)sizeof(DNode)];
+	thread_emit(recs, size, n.ref0, l0, h0, me + 1 + left_size, out);
+	thread_emit(recs, size, n.ref1, l1, h1, skip, out);
+}
+
+static void thread_bvh(const std::vector<DNode> &inner, uint32_t root_ref, const float lo[3], const float hi[3],
+		       std::vector<DThread> &out)
+{
+	out.clear();
+	if (root_ref == RTX_EMPTY_REF)
+		return;
+	std::vector<uint32_t> size(inner.size(), 0);
+	const uint32_t total = thread_sizes(inner, root_ref, size);
+	out.reserve(total);
+	thread_emit(inner, size, root_ref, lo, hi, RTX_NONE, out);
 }
 
 static inline float pad_lo(float x, float ext) { return x - (std::fabs(x) + ext) * 2e-6f - 1e-30f; }
@@ -388,6 +436,7 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 
 	const auto tb0 = std::chrono::steady_clock::now();
 	uint32_t nnodes = 0, root_ref = RTX_EMPTY_REF, depth = 0;
+	std::vector<DNode> inner; /* host copy of the inner-node records, for the threaded BVH */
 	int rc;
 	if (c->builder == RTX_BUILD_LBVH_GPU && nb) {
 		/* GPU linear BVH (rtx_build.hip): primitives uploaded in input order, records emitted on the device */
@@ -420,6 +469,9 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 		if (((uint64_t)nnodes + nb) * sizeof(DNode) > 0xFFFFFFC0ull)
 			return fail(RTX_ERR_SCENE, "scene too large: %u BVH nodes + %u primitives exceed 4 GB of records", nnodes,
 				    nb);
+		inner.resize(nnodes);
+		if (nnodes)
+			HIP_TRY(hipMemcpy(inner.data(), recs, nnodes * sizeof(DNode), hipMemcpyDeviceToHost));
 	} else {
 		BvhOutput bvh;
 		bvh_build(BvhInput{ nb, lo.data(), hi.data() }, cfg, bvh);
@@ -458,7 +510,13 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 			return rc;
 		root_ref = dref(bvh.root_ref);
 		depth = bvh.depth;
+		inner.assign(recs.begin(), recs.begin() + nnodes);
 	}
+	std::vector<DThread> threads;
+	if (nb)
+		thread_bvh(inner, root_ref, c->bound_lo, c->bound_hi, threads);
+	if ((rc = upload(c->d_threads, threads)))
+		return rc;
 	c->stats.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count();
 	if ((rc = upload(c->d_planes, planes)) || (rc = upload(c->d_mats, mats)) || (rc = upload(c->d_emitters, emit)))
 		return rc;
@@ -471,6 +529,8 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 	S.planes = c->d_planes;
 	S.mats = c->d_mats;
 	S.emitters = c->d_emitters;
+	S.threads = threads.empty() ? nullptr : c->d_threads;
+	S.num_threads = (uint32_t)threads.size();
 	S.root_ref = nb ? root_ref : RTX_EMPTY_REF;
 	S.num_prims = nb;
 	S.num_planes = (uint32_t)planes.size();
@@ -567,6 +627,13 @@ static int render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, f
 		slot_b <<= 1;
 	const uint32_t slots_per_point = (std::max<uint32_t>(c->total_lights, 1) + slot_b - 1) / slot_b;
 	const uint32_t per_wave = std::max<uint32_t>(1, std::min<uint32_t>(64, 1024 / (slot_b * slots_per_point)));
+	/* >= 64 lights: RTX_SH_R = R shadow rays per lane (one shared-origin walk per 64*R samples
+	 * of a point), R <= 5.  Off by default: on the bench frame R = 5 walks 2.4x fewer records
+	 * but drags each ray through 2x the nodes (k_shadow 2236 vs 1699 ms, gpurun_out r01z) */
+	uint32_t rays_per_lane = 1;
+	if (const char *e = getenv("RTX_SH_R"))
+		if (slot_b == 64)
+			rays_per_lane = std::max(1, std::min(5, atoi(e)));
 	for (uint32_t begin = 0; begin < P.ntiles;) {
 		const uint32_t end = std::min<uint32_t>(P.ntiles, begin + chunk_tiles);
 		const uint64_t sp_cap64 = std::min<uint64_t>((uint64_t)(end - begin) * avg_tile + staging_cap, 0xFFFFFFF0ull);
@@ -613,7 +680,7 @@ static int render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, f
 						  b + 3 * (size_t)n_sp, c->d_sorttmp, c->sorttmp_bytes, &perm, stream));
 		}
 		HIP_TRY(hipEventRecord(c->ev[4], stream));
-		HIP_TRY(rtx_launch_shadow(&c->scene, &P, c->d_sp, perm, n_sp, per_wave, slot_b, c->d_contrib, c->d_ctr,
+		HIP_TRY(rtx_launch_shadow(&c->scene, &P, c->d_sp, perm, n_sp, per_wave, slot_b, rays_per_lane, c->d_contrib, c->d_ctr,
 					  p->count_traversal, stream));
 		HIP_TRY(hipEventRecord(c->ev[2], stream));
 		HIP_TRY(rtx_launch_accum(&F, &P, c->d_tile_rec, c->d_contrib, begin, end - begin, d_rgb, stream));
@@ -644,6 +711,10 @@ static int render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, f
 	st.shadow_tri_tests = ctr[RTX_C_STRIS];
 	st.shadow_sphere_tests = ctr[RTX_C_SSPHERES];
 	st.shadow_plane_tests = ctr[RTX_C_SPLANES];
+	st.shadow_packet_nodes = ctr[RTX_C_SSTEPS];
+	st.shadow_packet_prims = ctr[RTX_C_SPSTEPS];
+	st.shadow_ray_nodes = ctr[RTX_C_SRNODES];
+	st.shadow_ray_prims = ctr[RTX_C_SRTRIS];
 	st.node_visits = ctr[RTX_C_NODES] + ctr[RTX_C_SNODES];
 	st.tri_tests = ctr[RTX_C_TRIS] + ctr[RTX_C_STRIS];
 	st.sphere_tests = ctr[RTX_C_SPHERES] + ctr[RTX_C_SSPHERES];

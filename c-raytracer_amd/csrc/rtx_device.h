@@ -66,6 +66,18 @@ typedef struct __attribute__((aligned(64))) DPrim {
 	float d[4];
 } DPrim;
 
+/* threaded (skip-link) copy of the BVH for the ray-by-ray shadow walk, in preorder: a node's
+ * own box (its parent's child slot; the scene bound for the root), the index to continue at
+ * when the box is missed or the subtree is done (RTX_NONE: end), and for a leaf its device
+ * ref (record byte offset | RTX_REF_LEAF | RTX_REF_SPH | count-1; 0 for an inner node, whose
+ * first child is the next node).  Any-hit needs no visit order, so no stack. */
+typedef struct __attribute__((aligned(32))) DThread {
+	float lo[3];
+	uint32_t skip;
+	float hi[3];
+	uint32_t ref;
+} DThread;
+
 typedef struct DPlane {
 	float n[3];
 	float d;
@@ -102,6 +114,8 @@ typedef struct DScene {
 	const DPlane *planes;
 	const DMaterial *mats;
 	const DEmitter *emitters;
+	const DThread *threads; /* threaded BVH (num_threads nodes), null when the BVH is empty */
+	uint32_t num_threads;
 	uint32_t root_ref;
 	uint32_t num_nodes;    /* prims == (const DPrim *)(nodes + num_nodes) */
 	uint32_t num_prims;
@@ -158,6 +172,10 @@ enum {
 	RTX_C_STRIS,
 	RTX_C_SSPHERES,
 	RTX_C_SPLANES,
+	RTX_C_SSTEPS,     /* shadow walk: node records stepped through, per packet (count mode) */
+	RTX_C_SPSTEPS,    /* shadow walk: primitive records tested, per packet (count mode) */
+	RTX_C_SRNODES,    /* shadow walk: inner nodes whose box the ray itself hits (count mode) */
+	RTX_C_SRTRIS,     /* shadow walk: leaf primitives under boxes the ray itself hits (count mode) */
 	RTX_C_N
 };
 #define RTX_C_CHUNK_N 4 /* counters reset per chunk */

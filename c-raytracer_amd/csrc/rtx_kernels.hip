@@ -49,6 +49,9 @@
 #ifndef RTX_DEBUG_NOWALK
 #define RTX_DEBUG_NOWALK 0 /* measurement only: skip the BVH walk (per-packet overhead) */
 #endif
+#ifndef RTX_DEBUG_NOLEAF
+#define RTX_DEBUG_NOLEAF 0 /* register-pressure experiments only */
+#endif
 #ifndef RTX_SH_FMA
 #define RTX_SH_FMA 1 /* fused products in the shadow triangle test */
 #endif
@@ -60,6 +63,9 @@
 #endif
 #ifndef RTX_SH_RCP
 #define RTX_SH_RCP 1 /* any-hit triangle test with v_rcp_f32 instead of IEEE 1/a */
+#endif
+#ifndef RTX_SHADOW_OCC_R
+#define RTX_SHADOW_OCC_R 6 /* waves/SIMD cap of the R-rays-per-lane walk (1: compiler's choice) */
 #endif
 #ifndef RTX_SHADOW_OCC_DEFAULT
 #define RTX_SHADOW_OCC_DEFAULT 8
@@ -735,8 +741,18 @@ __global__ __launch_bounds__(WAVE) void k_trace(DScene S, DFrame F, DParams P, f
 /* loads), each lane tests its own ray, __ballot picks the children.        */
 /* ------------------------------------------------------------------------ */
 struct ShadowCount {
-	u64 nodes, tris, sph, pln;
+	u64 nodes, tris, sph, pln, steps, psteps;
+	u64 rnodes, rprims; /* per-ray need: inner nodes / leaf primitives under boxes the ray hits */
 };
+
+/* count mode: the rays of ballot b that hit the child `ref` would visit it in a ray-by-ray walk */
+__device__ __forceinline__ void count_need(ShadowCount &sc, u64 b, uint32_t ref)
+{
+	if (ref & RTX_REF_LEAF)
+		sc.rprims += (u64)popc64(b) * ((ref & RTX_REF_CNT) + 1);
+	else
+		sc.rnodes += popc64(b);
+}
 
 /* 64-byte BVH records are read through the constant address space: with a wave-uniform
  * address that is one s_load_dwordx16 into SGPRs, whatever the compiler can prove about
@@ -879,11 +895,15 @@ __device__ __forceinline__ bool shadow_prim(const v16u &pr, const DMaterial *__r
 	if ((meta >> 24) == RTX_SPHERE) {
 		if (COUNT)
 			sc.sph += popc64(ballot(tl >= 0.f));
+		if (COUNT)
+			sc.psteps++;
 		float t = 0.f;
 		h = hit_sphere(a, __uint_as_float(pr[4]), o, d, __uint_as_float(pr[3]), t) & (t < tl);
 	} else {
 		if (COUNT)
 			sc.tris += popc64(ballot(tl >= 0.f));
+		if (COUNT)
+			sc.psteps++;
 		h = any_tri(a, mk3(__uint_as_float(pr[4]), __uint_as_float(pr[5]), __uint_as_float(pr[6])),
 			    mk3(__uint_as_float(pr[8]), __uint_as_float(pr[9]), __uint_as_float(pr[10])), o, d,
 			    __uint_as_float(pr[3]), tl);
@@ -955,6 +975,8 @@ __device__ __forceinline__ bool shadow_tri(const v16u &pr, const DMaterial *__re
 	const uint32_t meta = pr[11];
 	if (COUNT)
 		sc.tris += popc64(ballot(tl >= 0.f));
+	if (COUNT)
+		sc.psteps++;
 #if RTX_SH_MASK
 	u64 hm = any_tri_mask(mk3(__uint_as_float(pr[0]), __uint_as_float(pr[1]), __uint_as_float(pr[2])),
 			      mk3(__uint_as_float(pr[4]), __uint_as_float(pr[5]), __uint_as_float(pr[6])),
@@ -1007,6 +1029,8 @@ __device__ __forceinline__ void shadow_walk(const char *__restrict__ recs, const
 	const f3 oi = mul3v(o, inv);
 	const uint32_t oct = OCT < 8 ? (uint32_t)OCT : lead_oct;
 	uint32_t ref = root_ref, sp = 0, stk = 0, pf0 = 0, pf1 = 0;
+	if (COUNT)
+		count_need(sc, ballot(tl >= 0.f), root_ref);
 	for (;;) {
 		const v16u rec = rec_load(recs, ref & RTX_REF_OFF);
 		if (RTX_SH_PF)
@@ -1017,10 +1041,16 @@ __device__ __forceinline__ void shadow_walk(const char *__restrict__ recs, const
 				pf0 = touch(recs, rec[12] & RTX_REF_OFF);
 				pf1 = touch(recs, rec[13] & RTX_REF_OFF);
 			}
-			if (COUNT)
+			if (COUNT) {
 				sc.nodes += popc64(ballot(tl >= 0.f));
+				sc.steps++;
+			}
 			const u64 b0 = ballot(box_hit<OCT>(rec, 0, oi, inv, tl));
 			const u64 b1 = ballot(box_hit<OCT>(rec, 6, oi, inv, tl));
+			if (COUNT) {
+				count_need(sc, b0, rec[12]);
+				count_need(sc, b1, rec[13]);
+			}
 			next = node_step<OCT>(b0, b1, rec[12], rec[13], rec[14], oct, sp, stk);
 		} else {
 			const uint32_t off = ref & RTX_REF_OFF, cnt = (ref & RTX_REF_CNT) + 1;
@@ -1054,12 +1084,124 @@ __device__ __forceinline__ void shadow_walk(const char *__restrict__ recs, const
 		drain(pf0, pf1);
 }
 
+/* ------------------------------------------------------------------------ */
+/* ray-by-ray any-hit walk over the threaded BVH (DThread, skip links)      */
+/* ------------------------------------------------------------------------ */
+/* Measured on the benchmark frame (count mode): a 64-ray packet fetched 58 node records and
+ * tested 27.6 primitives per ray, while each ray's own boxes cover only 7.6 inner nodes and
+ * 2.2 primitives - deep in the tree the rays of one shade point part ways, and the packet
+ * drags every ray through the union of their paths.  Here each lane walks alone: its node
+ * index is its whole state (any-hit needs no order, so skip links replace the stack), a node
+ * is two 16-byte vector loads (own box + skip, box + leaf ref), and lanes at different nodes
+ * cost only their own steps.  The wave's cost is its longest ray, not the union of its rays. */
+template <int OCT>
+__device__ __forceinline__ bool box_hit_lh(float4 a, float4 b, f3 oi, f3 inv, float tlim)
+{
+	const float tx0 = fmaf(a.x, inv.x, -oi.x), tx1 = fmaf(b.x, inv.x, -oi.x);
+	const float ty0 = fmaf(a.y, inv.y, -oi.y), ty1 = fmaf(b.y, inv.y, -oi.y);
+	const float tz0 = fmaf(a.z, inv.z, -oi.z), tz1 = fmaf(b.z, inv.z, -oi.z);
+	if (OCT == 8) {
+		const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.f));
+		const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlim));
+		return tn <= tf;
+	}
+	const float nx = (OCT & 1) ? tx0 : tx1, fx = (OCT & 1) ? tx1 : tx0;
+	const float ny = (OCT & 2) ? ty0 : ty1, fy = (OCT & 2) ? ty1 : ty0;
+	const float nz = (OCT & 4) ? tz0 : tz1, fz = (OCT & 4) ? tz1 : tz0;
+	const float tn = fmaxf(fmaxf(nx, ny), fmaxf(nz, 0.f));
+	float tf = fminf(fminf(fx, fy), fz);
+	asm("v_min_f32 %0, %0, %1" : "+v"(tf) : "v"(tlim));
+	return tn <= tf;
+}
+
+/* one primitive record of a leaf against this lane's shadow ray (accel.c:362-373): the target
+ * emitter skipped; transparent hit -> li *= kt; opaque hit -> true (blocked) */
+template <bool COUNT>
+__device__ __forceinline__ bool shadow_prim_ray(const float4 *pr, const DMaterial *__restrict__ mats, f3 o, f3 d,
+						 float tl, uint32_t emit_obj, f3 &li, uint32_t &ntri, uint32_t &nsph)
+{
+	const float4 a = pr[0], b = pr[1], c = pr[2];
+	const uint32_t meta = __float_as_uint(c.w), obj = __float_as_uint(b.w);
+	if (obj == emit_obj)
+		return false;
+	bool h;
+	if ((meta >> 24) == RTX_SPHERE) {
+		if (COUNT)
+			nsph++;
+		float t = 0.f;
+		h = hit_sphere(mk3(a.x, a.y, a.z), b.x, o, d, a.w, t) && t < tl;
+	} else {
+		if (COUNT)
+			ntri++;
+		h = any_tri(mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z), mk3(c.x, c.y, c.z), o, d, a.w, tl);
+	}
+	if (!h)
+		return false;
+	if (meta & RTX_META_TRANSPARENT) {
+		const DMaterial &m = mats[meta & RTX_META_MAT];
+		li = mul3v(li, mk3(m.kt[0], m.kt[1], m.kt[2]));
+		return false;
+	}
+	return true;
+}
+
+template <bool COUNT, int OCT>
+__device__ __forceinline__ void shadow_walk_ray(const DThread *__restrict__ T, const char *__restrict__ recs,
+						const DMaterial *__restrict__ mats, f3 o, f3 d, f3 inv, float &tl,
+						uint32_t emit_obj, f3 &li, ShadowCount &sc)
+{
+	const f3 oi = mul3v(o, inv);
+	uint32_t i = tl >= 0.f ? 0u : RTX_NONE;
+	uint32_t nnode = 0, ntri = 0, nsph = 0;
+	while (i != RTX_NONE) {
+		const float4 *t = (const float4 *)(T + i);
+		const float4 a = t[0], b = t[1];
+		if (COUNT)
+			nnode++;
+		const uint32_t skip = __float_as_uint(a.w), ref = __float_as_uint(b.w);
+		const bool hit = box_hit_lh<OCT>(a, b, oi, inv, tl);
+		uint32_t next = hit ? i + 1 : skip;
+		if (hit && (ref & RTX_REF_LEAF)) {
+			next = skip;
+			const char *p = recs + (ref & RTX_REF_OFF);
+			const uint32_t cnt = (ref & RTX_REF_CNT) + 1;
+			for (uint32_t k = 0; k < cnt; k++) {
+				if (shadow_prim_ray<COUNT>((const float4 *)(p + k * (uint32_t)sizeof(DNode)), mats, o, d, tl,
+							   emit_obj, li, ntri, nsph)) {
+					tl = -1.f;
+					next = RTX_NONE;
+					break;
+				}
+			}
+		}
+		i = next;
+	}
+	if (COUNT) {
+		uint32_t a = nnode, b = ntri, c = nsph;
+#pragma unroll
+		for (int s = 32; s > 0; s >>= 1) {
+			a += __shfl_xor(a, s, WAVE);
+			b += __shfl_xor(b, s, WAVE);
+			c += __shfl_xor(c, s, WAVE);
+		}
+		sc.nodes += uni(a);
+		sc.tris += uni(b);
+		sc.sph += uni(c);
+		sc.steps++;
+	}
+}
+
+#ifndef RTX_SH_RAY
+#define RTX_SH_RAY 1 /* ray-by-ray threaded walk (0: the 64-ray packet walk) */
+#endif
+
 /* planes first (unbound_objects_is_light_blocked, object.c:183-197), then the BVH walk,
  * specialised on the packet's direction octant when all live rays share it.  Returns the
  * lane's blocked flag; li carries the transmittance product. */
 template <bool COUNT>
-__device__ __forceinline__ bool shadow_packet(const char *__restrict__ recs, const DMaterial *__restrict__ mats,
-					      const DPlane *__restrict__ planes, uint32_t num_planes, uint32_t root_ref,
+__device__ __forceinline__ bool shadow_packet(const DThread *__restrict__ threads, const char *__restrict__ recs,
+					      const DMaterial *__restrict__ mats, const DPlane *__restrict__ planes,
+					      uint32_t num_planes, uint32_t root_ref,
 					      bool act, f3 o, f3 d, float dist, uint32_t emit_obj, bool emit_is_tri, f3 &li,
 					      ShadowCount &sc)
 {
@@ -1091,6 +1233,20 @@ __device__ __forceinline__ bool shadow_packet(const char *__restrict__ recs, con
 	const bool tri_emit = ballot(alive & emit_is_tri) != 0;
 	const uint32_t sel = (!RTX_SH_OCT || ballot(alive & (oct != lead))) ? 8u : lead;
 	switch (sel) {
+#if RTX_SH_RAY
+		(void)emit_u;
+		(void)tri_emit;
+#define RTX_WALK(K)                                                                                                 \
+	case K:                                                                                                           \
+		shadow_walk_ray<COUNT, K>(threads, recs, mats, o, d, inv, tl, emit_obj, li, sc);                              \
+		break;
+#if RTX_SH_OCT
+	RTX_WALK(0) RTX_WALK(1) RTX_WALK(2) RTX_WALK(3) RTX_WALK(4) RTX_WALK(5) RTX_WALK(6) RTX_WALK(7)
+#endif
+	default:
+		shadow_walk_ray<COUNT, 8>(threads, recs, mats, o, d, inv, tl, emit_obj, li, sc);
+		break;
+#else
 #define RTX_WALK(K)                                                                                                   \
 	case K:                                                                                                           \
 		shadow_walk<COUNT, K>(recs, mats, root_ref, o, d, inv, tl, emit_u, emit_obj, tri_emit, K, li, sc);           \
@@ -1101,6 +1257,7 @@ __device__ __forceinline__ bool shadow_packet(const char *__restrict__ recs, con
 	default:
 		shadow_walk<COUNT, 8>(recs, mats, root_ref, o, d, inv, tl, emit_u, emit_obj, tri_emit, lead, li, sc);
 		break;
+#endif
 #undef RTX_WALK
 	}
 	return act && tl < 0.f;
@@ -1111,6 +1268,7 @@ __device__ __forceinline__ bool shadow_packet(const char *__restrict__ recs, con
  * the traversal, which needs every SGPR it can get at 8 waves/SIMD. */
 struct KShadow {
 	const DNode *recs; /* BVH nodes, then primitives from record nnodes */
+	const DThread *threads; /* threaded BVH (ray-by-ray walk) */
 	const DMaterial *mats;
 	const DPlane *planes;
 	const DEmitter *emitters;
@@ -1132,6 +1290,29 @@ template <typename T> __device__ __forceinline__ T *unip(T *p)
 {
 	const uint64_t v = (uint64_t)p;
 	return (T *)(((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v));
+}
+
+/* direct-lighting terms of one unblocked light sample (render.c:199-228), read after the walk */
+__device__ __forceinline__ f3 shade_light(const KShadow &ks, const float4 *rec, f3 ldir, f3 li, float ldist, float dsq)
+{
+	const float4 q1 = rec[1], q2 = rec[2], q3 = rec[3];
+	const f3 n = mk3(q1.x, q1.y, q1.z), dir = mk3(q2.x, q2.y, q2.z);
+	const float a = dot3(ldir, n);
+	const int32_t att = (int32_t)uni((uint32_t)ks.attenuation);
+	if (att == RTX_ATT_LIN)
+		li = mul3s(li, 1.f / (ks.att_offset + ldist));
+	else if (att == RTX_ATT_SQR)
+		li = mul3s(li, 1.f / (ks.att_offset + dsq));
+	const DMaterial &m = unip(ks.mats)[__float_as_uint(q3.w)];
+	const f3 diff = mul3s(mul3v(mk3(q3.x, q3.y, q3.z), li), fmaxf(0.f, a));
+	float sm;
+	if ((int32_t)uni((uint32_t)ks.reflection) == RTX_BLINN) {
+		sm = -dot3(n, norm3(add3(mul3s(ldir, -1.f), dir)));
+	} else {
+		sm = -dot3(sub3(mul3s(n, 2.f * a), ldir), dir);
+	}
+	const f3 spec = mul3s(mul3v(ld3(m.ks), li), fmaxf(0.f, powf(sm, m.shininess)));
+	return add3(diff, spec);
 }
 
 /* one light sample per lane of the shade point `rec` (render.c:170-229): the light point of
@@ -1182,39 +1363,389 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	const float dsq = magsqr3(dv);
 	const f3 ldir = mul3s(dv, 1.f / ldist);
 	f3 li = ld3(E.li);
-	const bool blocked = shadow_packet<COUNT>((const char *)unip(ks.recs), unip(ks.mats), unip(ks.planes),
+	const bool blocked = shadow_packet<COUNT>(unip(ks.threads), (const char *)unip(ks.recs), unip(ks.mats), unip(ks.planes),
 						  uni(ks.num_planes), RTX_DEBUG_NOWALK ? RTX_EMPTY_REF : uni(ks.root_ref),
 						  act, p, ldir, ldist, E.obj, E.type == RTX_TRIANGLE, li, sc);
 	reread_barrier();
 	f3 contribution = mk3(0.f, 0.f, 0.f);
-	if (act && !blocked) {
-		/* shading terms (render.c:199-228) read after the traversal */
-		const float4 q1 = rec[1], q2 = rec[2], q3 = rec[3];
-		const f3 n = mk3(q1.x, q1.y, q1.z), dir = mk3(q2.x, q2.y, q2.z);
-		const float a = dot3(ldir, n);
-		const int32_t att = (int32_t)uni((uint32_t)ks.attenuation);
-		if (att == RTX_ATT_LIN)
-			li = mul3s(li, 1.f / (ks.att_offset + ldist));
-		else if (att == RTX_ATT_SQR)
-			li = mul3s(li, 1.f / (ks.att_offset + dsq));
-		const DMaterial &m = unip(ks.mats)[__float_as_uint(q3.w)];
-		const f3 diff = mul3s(mul3v(mk3(q3.x, q3.y, q3.z), li), fmaxf(0.f, a));
-		float sm;
-		if ((int32_t)uni((uint32_t)ks.reflection) == RTX_BLINN) {
-			sm = -dot3(n, norm3(add3(mul3s(ldir, -1.f), dir)));
-		} else {
-			sm = -dot3(sub3(mul3s(n, 2.f * a), ldir), dir);
-		}
-		const f3 spec = mul3s(mul3v(ld3(m.ks), li), fmaxf(0.f, powf(sm, m.shininess)));
-		contribution = add3(diff, spec);
-	}
+	if (act && !blocked)
+		contribution = shade_light(ks, rec, ldir, li, ldist, dsq);
 	return contribution;
 }
 
-template <bool COUNT, int OCC>
+/* ------------------------------------------------------------------------ */
+/* single-origin packets: R shadow rays per lane                            */
+/* ------------------------------------------------------------------------ */
+/* In single-point mode (>= 64 lights) every ray of a packet starts at the same shade point P.
+ * Everything a node or a triangle contributes to a test that depends on P alone is then
+ * wave-uniform: the box planes relative to P, and for Moller-Trumbore s = P - v0, q = s x e1,
+ * e2 . q and e2 x s.  Each lane carries R rays (64*R per walk), so one record load, one set of
+ * P-relative terms and one scalar child decision serve R times as many rays as the one-ray
+ * walk; the per-ray work left is a few products and compares. */
+
+/* box test from P-relative planes: dn / df = near / far plane minus P per axis for octant OCT
+ * (OCT == 8: lo / hi minus P, order decided per lane).  (plane - P) is exact to half an ulp
+ * and the boxes are padded 2e-6 relative, so the test stays conservative like box_hit's. */
+template <int OCT>
+__device__ __forceinline__ bool box_hit_so(f3 dn, f3 df, f3 inv, float tlim)
+{
+	const float ax = dn.x * inv.x, bx = df.x * inv.x;
+	const float ay = dn.y * inv.y, by = df.y * inv.y;
+	const float az = dn.z * inv.z, bz = df.z * inv.z;
+	if (OCT == 8) {
+		const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.f));
+		const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tlim));
+		return tn <= tf;
+	}
+	const float tn = fmaxf(fmaxf(ax, ay), fmaxf(az, 0.f));
+	float tf = fminf(fminf(bx, by), bz);
+	asm("v_min_f32 %0, %0, %1" : "+v"(tf) : "v"(tlim));
+	return tn <= tf;
+}
+
+/* the P-relative planes of the child box at rec[b..b+5] = lo.x, hi.x, lo.y, hi.y, lo.z, hi.z */
+template <int OCT>
+__device__ __forceinline__ void box_planes_so(const v16u &nd, const uint32_t b, f3 o, f3 &dn, f3 &df)
+{
+	const float lx = __uint_as_float(nd[b]) - o.x, hx = __uint_as_float(nd[b + 1]) - o.x;
+	const float ly = __uint_as_float(nd[b + 2]) - o.y, hy = __uint_as_float(nd[b + 3]) - o.y;
+	const float lz = __uint_as_float(nd[b + 4]) - o.z, hz = __uint_as_float(nd[b + 5]) - o.z;
+	if (OCT == 8) {
+		dn = mk3(lx, ly, lz);
+		df = mk3(hx, hy, hz);
+		return;
+	}
+	dn = mk3((OCT & 1) ? lx : hx, (OCT & 2) ? ly : hy, (OCT & 4) ? lz : hz);
+	df = mk3((OCT & 1) ? hx : lx, (OCT & 2) ? hy : ly, (OCT & 4) ? hz : lz);
+}
+
+/* moller_trumbore (object.c:422-441) with a shared origin, by the triple-product identities
+ *   a = e1.(d x e2) = d.(e2 x e1),  u a = s.(d x e2) = d.(e2 x s),  v a = d.q,  t a = e2.q
+ * (s = P - v0, q = s x e1): the per-ray part is three dot products.  Same accept set as
+ * any_tri (|a| >= eps, u, v >= 0, u + v <= 1, eps < t < tlim). */
+struct TriSO {
+	f3 ca, cu, q;
+	float tq;
+};
+__device__ __forceinline__ TriSO tri_so(f3 v0, f3 e1, f3 e2, f3 o)
+{
+	const f3 s = sub3(o, v0);
+	TriSO T;
+	T.ca = cross3_fma(e2, e1);
+	T.cu = cross3_fma(e2, s);
+	T.q = cross3_fma(s, e1);
+	T.tq = dot3_fma(e2, T.q);
+	return T;
+}
+__device__ __forceinline__ u64 any_tri_so_mask(const TriSO &T, f3 d, float eps, float tlim)
+{
+	const float a = dot3_fma(d, T.ca);
+	const float f = __builtin_amdgcn_rcpf(a);
+	const float u = f * dot3_fma(d, T.cu);
+	const float v = f * dot3_fma(d, T.q);
+	const float t = f * T.tq;
+	const float out = fmaxf(fmaxf(-u, -v), (u + v) - 1.f);
+	return ballot(fabsf(a) >= eps) & ballot(out <= 0.f) & ballot(fminf(t - eps, tlim - t) > 0.f);
+}
+
+/* keeps the per-ray tests of one record in sequence: the scheduler would otherwise interleave
+ * all R rays' temporaries and run out of registers (other waves supply the parallelism) */
+#ifndef RTX_SO_SCHED
+#define RTX_SO_SCHED 1
+#endif
+#define RTX_SO_SERIAL()                                                                                             \
+	do {                                                                                                            \
+		if (RTX_SO_SCHED)                                                                                           \
+			__builtin_amdgcn_sched_barrier(0);                                                                      \
+	} while (0)
+
+/* the packet of R rays per lane walking the BVH (shadow_walk with shared-origin tests).
+ * Per-ray state in registers is only what every test reads: direction, its reciprocal and the
+ * segment end.  The transmittance product li lives in LDS ([component][ray][lane]) and is
+ * touched only on a transparent hit; emit_lds[ray][lane] is the index of the emitter the ray
+ * aims at, read only when the packet's rays aim at different emitters (emit_u == RTX_NONE)
+ * or at a triangle emitter (tri_emit). */
+template <bool COUNT, int OCT, int R>
+__device__ __forceinline__ void shadow_walk_so(const char *__restrict__ recs, const DMaterial *__restrict__ mats,
+					       const DEmitter *__restrict__ emitters, uint32_t root_ref, f3 o,
+					       const f3 (&d)[R], const f3 (&inv)[R], float (&tl)[R], float *li_lds,
+					       uint32_t emit_u, const uint8_t *emit_lds, bool tri_emit, uint32_t lead_oct,
+					       ShadowCount &sc)
+{
+	const uint32_t oct = OCT < 8 ? (uint32_t)OCT : lead_oct;
+	uint32_t ref = root_ref, sp = 0, stk = 0, pf0 = 0, pf1 = 0;
+	for (;;) {
+		const v16u rec = rec_load(recs, ref & RTX_REF_OFF);
+		if (RTX_SH_PF)
+			consume(pf0, pf1, rec[15]);
+		uint32_t next = RTX_NONE; /* RTX_NONE: pop */
+		if (!(ref & RTX_REF_LEAF)) {
+			if (RTX_SH_PF) {
+				pf0 = touch(recs, rec[12] & RTX_REF_OFF);
+				pf1 = touch(recs, rec[13] & RTX_REF_OFF);
+			}
+			if (COUNT) {
+#pragma unroll
+				for (int r = 0; r < R; r++)
+					sc.nodes += popc64(ballot(tl[r] >= 0.f));
+				sc.steps++;
+			}
+			u64 b0 = 0, b1 = 0;
+			{
+				f3 dn, df;
+				box_planes_so<OCT>(rec, 0, o, dn, df);
+#pragma unroll
+				for (int r = 0; r < R; r++) {
+					b0 |= ballot(box_hit_so<OCT>(dn, df, inv[r], tl[r]));
+					RTX_SO_SERIAL();
+				}
+			}
+			{
+				f3 dn, df;
+				box_planes_so<OCT>(rec, 6, o, dn, df);
+#pragma unroll
+				for (int r = 0; r < R; r++) {
+					b1 |= ballot(box_hit_so<OCT>(dn, df, inv[r], tl[r]));
+					RTX_SO_SERIAL();
+				}
+			}
+			next = node_step<OCT>(b0, b1, rec[12], rec[13], rec[14], oct, sp, stk);
+		} else {
+			const uint32_t off = ref & RTX_REF_OFF, cnt = (ref & RTX_REF_CNT) + 1;
+			if (RTX_SH_PF) { /* the leaf's second primitive and the stack top (next pop) */
+				pf0 = touch(recs, off + (cnt > 1 ? (uint32_t)sizeof(DNode) : 0u));
+				pf1 = touch(recs, sp ? readlane(stk, sp - 1) & RTX_REF_OFF : off);
+			}
+			bool blk = false;
+			for (uint32_t k = 0; k < (RTX_DEBUG_NOLEAF ? 0u : cnt); k++) {
+				const v16u pr = k ? rec_load(recs, off + k * (uint32_t)sizeof(DNode)) : rec;
+				const uint32_t meta = pr[11], obj = pr[7];
+				if (obj == emit_u)
+					continue;
+				const f3 a = mk3(__uint_as_float(pr[0]), __uint_as_float(pr[1]), __uint_as_float(pr[2]));
+				const float eps = __uint_as_float(pr[3]);
+				const bool sphere = (meta >> 24) == RTX_SPHERE;
+				u64 hm[R], any = 0;
+				if (COUNT)
+					sc.psteps++;
+				if (sphere) {
+#pragma unroll
+					for (int r = 0; r < R; r++) {
+						if (COUNT)
+							sc.sph += popc64(ballot(tl[r] >= 0.f));
+						float t = 0.f;
+						hm[r] = ballot(hit_sphere(a, __uint_as_float(pr[4]), o, d[r], eps, t) & (t < tl[r]));
+						RTX_SO_SERIAL();
+					}
+				} else {
+					const TriSO T = tri_so(a, mk3(__uint_as_float(pr[4]), __uint_as_float(pr[5]), __uint_as_float(pr[6])),
+							       mk3(__uint_as_float(pr[8]), __uint_as_float(pr[9]), __uint_as_float(pr[10])), o);
+#pragma unroll
+					for (int r = 0; r < R; r++) {
+						if (COUNT)
+							sc.tris += popc64(ballot(tl[r] >= 0.f));
+						hm[r] = any_tri_so_mask(T, d[r], eps, tl[r]);
+						RTX_SO_SERIAL();
+					}
+				}
+				if (sphere ? emit_u == RTX_NONE : tri_emit) {
+#pragma unroll
+					for (int r = 0; r < R; r++)
+						hm[r] &= ballot(emitters[emit_lds[r * WAVE + lane_id()]].obj != obj);
+				}
+#pragma unroll
+				for (int r = 0; r < R; r++)
+					any |= hm[r];
+				if (!any)
+					continue;
+				if (meta & RTX_META_TRANSPARENT) {
+					const auto *m = cptr(mats) + (meta & RTX_META_MAT);
+					const float k0 = m->kt[0], k1 = m->kt[1], k2 = m->kt[2];
+#pragma unroll
+					for (int r = 0; r < R; r++) {
+						if (!hm[r])
+							continue;
+						float *l = li_lds + r * WAVE + lane_id();
+						const float x = l[0], y = l[R * WAVE], z = l[2 * R * WAVE];
+						l[0] = msel(hm[r], x, x * k0);
+						l[R * WAVE] = msel(hm[r], y, y * k1);
+						l[2 * R * WAVE] = msel(hm[r], z, z * k2);
+					}
+				} else {
+#pragma unroll
+					for (int r = 0; r < R; r++)
+						tl[r] = msel(hm[r], tl[r], -1.f);
+					blk = true;
+				}
+			}
+			if (blk) {
+				u64 alive = 0;
+#pragma unroll
+				for (int r = 0; r < R; r++)
+					alive |= ballot(tl[r] >= 0.f);
+				if (!alive)
+					sp = 0; /* every ray of the packet is blocked: end the walk */
+			}
+		}
+		if (next == RTX_NONE) {
+			if (sp == 0)
+				break;
+			next = readlane(stk, --sp);
+		}
+		ref = next;
+	}
+	if (RTX_SH_PF)
+		drain(pf0, pf1);
+}
+
+/* R light samples per lane of the shade point `rec`, indices base + r * 64 + lane (render.c:
+ * 170-229), through one shared-origin walk.  Each lane adds its samples' contributions to acc
+ * in index order, the same sequence of float additions as the one-ray packets. */
+template <bool COUNT, int R>
+__device__ __forceinline__ void light_chunk(const KShadow &ks, const float4 *rec, uint32_t base, uint32_t nl,
+					    float *li_lds, uint8_t *emit_lds, f3 &acc, ShadowCount &sc)
+{
+	reread_barrier();
+	const float4 q0 = rec[0], q4 = rec[4];
+	const f3 p = mk3(q0.x, q0.y, q0.z);
+	const uint32_t obj = __float_as_uint(q4.x);
+	const DEmitter *emitters = unip(ks.emitters);
+	const uint32_t num_emitters = uni(ks.num_emitters);
+	const bool rng_const = uni(ks.rng) == RTX_RNG_CONST;
+	f3 d[R], inv[R];
+	float tl[R], ldist[R], dsq[R];
+	u64 live = 0, tri_any = 0;
+#pragma unroll
+	for (int r = 0; r < R; r++) {
+		const uint32_t idx = base + (uint32_t)r * WAVE + lane_id();
+		const bool act = idx < nl;
+		uint32_t j = idx, e = 0;
+		for (; e < num_emitters; e++) {
+			const uint32_t eo = emitters[e].obj, enl = emitters[e].num_lights;
+			if (eo == obj)
+				continue;
+			if (j < enl)
+				break;
+			j -= enl;
+		}
+		if (e >= num_emitters)
+			e = 0;
+		const DEmitter &E = emitters[e];
+		float u1 = 0.5f, u2 = 0.5f;
+		if (!rng_const)
+			rtx_draw2(key_of(__float_as_uint(q4.y), __float_as_uint(q4.z)), e, j, &u1, &u2);
+		const f3 lp = light_point(E, p, u1, u2);
+		const f3 dv = sub3(lp, p);
+		ldist[r] = mag3(dv);
+		dsq[r] = magsqr3(dv);
+		d[r] = mul3s(dv, 1.f / ldist[r]);
+		float *l = li_lds + r * WAVE + lane_id();
+		l[0] = E.li[0];
+		l[R * WAVE] = E.li[1];
+		l[2 * R * WAVE] = E.li[2];
+		tl[r] = act ? ldist[r] : -1.f;
+		emit_lds[r * WAVE + lane_id()] = (uint8_t)e;
+		tri_any |= ballot(act & (E.type == RTX_TRIANGLE));
+	}
+	/* planes first (unbound_objects_is_light_blocked, object.c:183-197) */
+	const DPlane *planes = unip(ks.planes);
+	const uint32_t num_planes = uni(ks.num_planes);
+	for (uint32_t i = 0; i < num_planes; i++) {
+		const auto *pl = cptr(planes) + i;
+		const auto *m = cptr(unip(ks.mats)) + pl->mat;
+		const f3 pn = mk3(pl->n[0], pl->n[1], pl->n[2]);
+		const bool transparent = (m->flags & RTX_MF_TRANSPARENT) != 0;
+#pragma unroll
+		for (int r = 0; r < R; r++) {
+			float t;
+			const bool h = hit_plane(pn, pl->d, p, d[r], pl->eps, t) && t < ldist[r] && tl[r] >= 0.f;
+			if (transparent) {
+				if (h) {
+					float *l = li_lds + r * WAVE + lane_id();
+					l[0] = l[0] * m->kt[0];
+					l[R * WAVE] = l[R * WAVE] * m->kt[1];
+					l[2 * R * WAVE] = l[2 * R * WAVE] * m->kt[2];
+				}
+			} else if (h) {
+				tl[r] = -1.f;
+			}
+		}
+	}
+	if (COUNT)
+#pragma unroll
+		for (int r = 0; r < R; r++)
+			sc.pln += (u64)popc64(ballot(base + (uint32_t)r * WAVE + lane_id() < nl)) * num_planes;
+	uint32_t oct[R];
+	uint32_t lead_r = R, lead_lane = 0;
+#pragma unroll
+	for (int r = R - 1; r >= 0; r--) {
+		inv[r] = safe_inv_fast(d[r]);
+		oct[r] = ((~__float_as_uint(inv[r].x)) >> 31) | (((~__float_as_uint(inv[r].y)) >> 31) << 1) |
+			 (((~__float_as_uint(inv[r].z)) >> 31) << 2);
+		const u64 lv = ballot(tl[r] >= 0.f);
+		live |= lv;
+		if (lv) {
+			lead_r = (uint32_t)r;
+			lead_lane = (uint32_t)__ffsll((long long)lv) - 1;
+		}
+	}
+	const uint32_t root_ref = uni(ks.root_ref);
+	if (live && root_ref != RTX_EMPTY_REF && !RTX_DEBUG_NOWALK) {
+		uint32_t lead = 0, lead_emit = 0;
+#pragma unroll
+		for (int r = 0; r < R; r++)
+			if ((uint32_t)r == lead_r) {
+				lead = readlane(oct[r], lead_lane);
+				lead_emit = readlane(emit_lds[r * WAVE + lane_id()], lead_lane);
+			}
+		u64 mixed_oct = 0, mixed_emit = 0;
+#pragma unroll
+		for (int r = 0; r < R; r++) {
+			const bool alive = tl[r] >= 0.f;
+			mixed_oct |= ballot(alive & (oct[r] != lead));
+			mixed_emit |= ballot(alive & ((uint32_t)emit_lds[r * WAVE + lane_id()] != lead_emit));
+		}
+		const uint32_t emit_u = mixed_emit ? RTX_NONE : uni(emitters[uni(lead_emit)].obj);
+		const bool tri_emit = tri_any != 0;
+		const uint32_t sel = (!RTX_SH_OCT || mixed_oct) ? 8u : lead;
+		const char *recs = (const char *)unip(ks.recs);
+		const DMaterial *mats = unip(ks.mats);
+		switch (sel) {
+#define RTX_WALK_SO(K)                                                                                              \
+	case K:                                                                                                         \
+		shadow_walk_so<COUNT, K, R>(recs, mats, emitters, root_ref, p, d, inv, tl, li_lds, emit_u, emit_lds,        \
+					    tri_emit, K, sc);                                                               \
+		break;
+#if RTX_SH_OCT
+			RTX_WALK_SO(0) RTX_WALK_SO(1) RTX_WALK_SO(2) RTX_WALK_SO(3) RTX_WALK_SO(4) RTX_WALK_SO(5) RTX_WALK_SO(6)
+			RTX_WALK_SO(7)
+#endif
+		default:
+			shadow_walk_so<COUNT, 8, R>(recs, mats, emitters, root_ref, p, d, inv, tl, li_lds, emit_u, emit_lds,
+						    tri_emit, lead, sc);
+			break;
+#undef RTX_WALK_SO
+		}
+	}
+	reread_barrier();
+#pragma unroll
+	for (int r = 0; r < R; r++) {
+		const uint32_t idx = base + (uint32_t)r * WAVE + lane_id();
+		f3 contribution = mk3(0.f, 0.f, 0.f);
+		if (idx < nl && tl[r] >= 0.f) {
+			const float *l = li_lds + r * WAVE + lane_id();
+			contribution = shade_light(ks, rec, d[r], mk3(l[0], l[R * WAVE], l[2 * R * WAVE]), ldist[r], dsq[r]);
+		}
+		acc = add3(acc, contribution);
+	}
+}
+
+template <bool COUNT, int OCC, int R>
 __global__ __launch_bounds__(WAVE, OCC) void k_shadow(KShadow ka)
 {
 	__shared__ KShadow ks;
+	__shared__ float li_lds[3 * R * WAVE];  /* R > 1: each ray's light intensity x transmittance */
+	__shared__ uint8_t emit_lds[R * WAVE];  /* R > 1: the emitter each ray aims at */
 	__shared__ uint32_t off[WAVE + 1]; /* first lane slot of each shade point, total */
 	__shared__ uint32_t nls[WAVE];     /* shadow rays of each shade point */
 	__shared__ uint32_t sid[WAVE];     /* each shade point's index in the record array */
@@ -1246,7 +1777,7 @@ __global__ __launch_bounds__(WAVE, OCC) void k_shadow(KShadow ka)
 		ks = ka;
 	}
 	lds_sync();
-	ShadowCount sc = { 0, 0, 0, 0 };
+	ShadowCount sc = { 0, 0, 0, 0, 0, 0, 0, 0 };
 	if (ka.slot_b == WAVE) {
 		/* >= 64 lights: every packet is 64 samples of ONE shade point.  The point is wave-uniform
 		 * (its record is read once per packet through one address, no owner search), each lane
@@ -1256,9 +1787,14 @@ __global__ __launch_bounds__(WAVE, OCC) void k_shadow(KShadow ka)
 			const uint32_t nl = uni(nls[k]);
 			const float4 *rec = unip(ks.sp) + (size_t)uni(sid[k]) * SPREC;
 			f3 acc = mk3(0.f, 0.f, 0.f);
-			for (uint32_t base = 0; base < nl; base += WAVE) {
-				const uint32_t idx = base + lane_id();
-				acc = add3(acc, light_sample<COUNT>(ks, rec, idx, idx < nl, sc));
+			if (R > 1) {
+				for (uint32_t base = 0; base < nl; base += R * WAVE)
+					light_chunk<COUNT, R>(ks, rec, base, nl, li_lds, emit_lds, acc, sc);
+			} else {
+				for (uint32_t base = 0; base < nl; base += WAVE) {
+					const uint32_t idx = base + lane_id();
+					acc = add3(acc, light_sample<COUNT>(ks, rec, idx, idx < nl, sc));
+				}
 			}
 			const float sx = wave_sum(acc.x), sy = wave_sum(acc.y), sz = wave_sum(acc.z);
 			if (lane_id() == 0) {
@@ -1268,7 +1804,7 @@ __global__ __launch_bounds__(WAVE, OCC) void k_shadow(KShadow ka)
 			}
 		}
 		lds_sync();
-	} else {
+	} else if constexpr (R == 1) {
 		/* fewer lights: several points share a packet, each in its own power-of-two lane slot */
 		for (uint32_t base = 0;;) {
 			reread_barrier();
@@ -1322,6 +1858,10 @@ __global__ __launch_bounds__(WAVE, OCC) void k_shadow(KShadow ka)
 			atomicAdd(&ctr[RTX_C_STRIS], sc.tris);
 			atomicAdd(&ctr[RTX_C_SSPHERES], sc.sph);
 			atomicAdd(&ctr[RTX_C_SPLANES], sc.pln);
+			atomicAdd(&ctr[RTX_C_SSTEPS], sc.steps);
+			atomicAdd(&ctr[RTX_C_SPSTEPS], sc.psteps);
+			atomicAdd(&ctr[RTX_C_SRNODES], sc.rnodes);
+			atomicAdd(&ctr[RTX_C_SRTRIS], sc.rprims);
 		}
 	}
 }
@@ -1525,18 +2065,20 @@ extern "C" hipError_t rtx_launch_trace(const DScene *S, const DFrame *F, const D
 }
 
 extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const float4 *sp, const uint32_t *perm,
-					uint32_t n_sp, uint32_t per_wave, uint32_t slot_b, float4 *contrib,
-					unsigned long long *ctr, int count, hipStream_t stream)
+					uint32_t n_sp, uint32_t per_wave, uint32_t slot_b, uint32_t rays_per_lane,
+					float4 *contrib, unsigned long long *ctr, int count, hipStream_t stream)
 {
 	const uint32_t nw = (n_sp + per_wave - 1) / per_wave;
 	if (!nw)
 		return hipSuccess;
 	const char *xe = getenv("RTX_XCDMAP");
 	const uint32_t per_xcd = (xe && xe[0] == '1') ? (nw + 7) / 8 : 0u, grid = per_xcd ? 8 * per_xcd : nw;
-	if (!slot_b || (slot_b & (slot_b - 1)) || slot_b > WAVE || !per_wave || per_wave > WAVE)
+	if (!slot_b || (slot_b & (slot_b - 1)) || slot_b > WAVE || !per_wave || per_wave > WAVE || !rays_per_lane ||
+	    rays_per_lane > 5 || (rays_per_lane > 1 && slot_b != WAVE))
 		return hipErrorInvalidValue;
 	KShadow ka;
 	ka.recs = S->nodes;
+	ka.threads = S->threads;
 	ka.mats = S->mats;
 	ka.planes = S->planes;
 	ka.emitters = S->emitters;
@@ -1563,18 +2105,30 @@ extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const
 		const char *e = getenv("RTX_SHADOW_OCC");
 		occ = e ? atoi(e) : RTX_SHADOW_OCC_DEFAULT;
 	}
-#define RTX_LAUNCH_SHADOW(C, O)                                                                                  \
-	hipLaunchKernelGGL((k_shadow<C, O>), dim3(grid), dim3(WAVE), 0, stream, ka)
-	if (count)
-		RTX_LAUNCH_SHADOW(true, 1);
-	else if (occ == 8)
-		RTX_LAUNCH_SHADOW(false, 8);
-	else if (occ == 7)
-		RTX_LAUNCH_SHADOW(false, 7);
-	else if (occ == 6)
-		RTX_LAUNCH_SHADOW(false, 6);
-	else
-		RTX_LAUNCH_SHADOW(false, 1);
+#define RTX_LAUNCH_SHADOW(C, O, R)                                                                               \
+	hipLaunchKernelGGL((k_shadow<C, O, R>), dim3(grid), dim3(WAVE), 0, stream, ka)
+#define RTX_LAUNCH_SHADOW_R(C, O)                                                                                \
+	switch (rays_per_lane) {                                                                                     \
+	case 2: RTX_LAUNCH_SHADOW(C, O, 2); break;                                                                   \
+	case 3: RTX_LAUNCH_SHADOW(C, O, 3); break;                                                                   \
+	case 4: RTX_LAUNCH_SHADOW(C, O, 4); break;                                                                   \
+	case 5: RTX_LAUNCH_SHADOW(C, O, 5); break;                                                                   \
+	default: RTX_LAUNCH_SHADOW(C, O, 1); break;                                                                  \
+	}
+	if (count) {
+		RTX_LAUNCH_SHADOW_R(true, 1);
+	} else if (rays_per_lane > 1) {
+		RTX_LAUNCH_SHADOW_R(false, RTX_SHADOW_OCC_R);
+	} else if (occ == 8) {
+		RTX_LAUNCH_SHADOW(false, 8, 1);
+	} else if (occ == 7) {
+		RTX_LAUNCH_SHADOW(false, 7, 1);
+	} else if (occ == 6) {
+		RTX_LAUNCH_SHADOW(false, 6, 1);
+	} else {
+		RTX_LAUNCH_SHADOW(false, 1, 1);
+	}
+#undef RTX_LAUNCH_SHADOW_R
 #undef RTX_LAUNCH_SHADOW
 	return hipGetLastError();
 }

@@ -65,7 +65,9 @@ class Stats(C.Structure):
                 ("shadow_ms", C.c_double), ("accum_ms", C.c_double), ("sort_ms", C.c_double), ("build_ms", C.c_double),
                 ("bvh_nodes", C.c_uint32),
                 ("bvh_depth", C.c_uint32), ("bvh_prims", C.c_uint32), ("waves", C.c_uint32),
-                ("chunks", C.c_uint32), ("builder", C.c_uint32)]
+                ("chunks", C.c_uint32), ("builder", C.c_uint32),
+                ("shadow_packet_nodes", C.c_uint64), ("shadow_packet_prims", C.c_uint64),
+                ("shadow_ray_nodes", C.c_uint64), ("shadow_ray_prims", C.c_uint64)]
 
 
 RTX_BUILD_SAH_HOST, RTX_BUILD_LBVH_GPU = 0, 1

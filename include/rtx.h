@@ -196,6 +196,15 @@ typedef struct rtx_stats {
 	uint32_t waves;              /* persistent waves of the closest-hit kernel */
 	uint32_t chunks;             /* tile chunks the frame was split into */
 	uint32_t builder;            /* RTX_BUILD_* used by the last upload */
+	/* only with count_traversal: records a shadow packet walk fetched, summed over packets
+	 * (a packet = the 64 or 64*R shadow rays walking the BVH together) */
+	uint64_t shadow_packet_nodes;
+	uint64_t shadow_packet_prims;
+	/* only with count_traversal: what a ray-by-ray walk would fetch, summed over shadow rays:
+	 * inner nodes (root + children whose box the ray hits) and primitives in leaves whose
+	 * box the ray hits.  shadow_node_visits / shadow_ray_nodes = the packets' overhead */
+	uint64_t shadow_ray_nodes;
+	uint64_t shadow_ray_prims;
 } rtx_stats;
 
 typedef struct rtx_ctx rtx_ctx;

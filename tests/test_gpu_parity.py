@@ -200,6 +200,24 @@ def test_gpu_shade_point_order_is_invisible(renderer, name, monkeypatch):
     assert (sa.closest_rays, sa.shadow_rays) == (sb.closest_rays, sb.shadow_rays)
 
 
+@pytest.mark.parametrize("r", ["2", "5"])
+@pytest.mark.parametrize("name", ["s5_path2", "s3_path2"])
+def test_gpu_shared_origin_walk_matches(renderer, name, r, monkeypatch):
+    """The opt-in R-rays-per-lane shadow walk (RTX_SH_R, points with >= 64 lights) sums each
+    lane's samples in the same order as the one-ray packets and differs only in the rounding
+    of its shared-origin triangle test: same z and ray counts, colour within the parity
+    tolerance."""
+    scene, frame, params, _ = C.load_config(name)
+    params.rng = abi.RTX_RNG_COUNTER
+    a, za, sa = render(renderer, scene, frame, params)
+    monkeypatch.setenv("RTX_SH_R", r)
+    b, zb, sb = render(renderer, scene, frame, params)
+    assert np.array_equal(za, zb)
+    ok, info = C.compare_const(b, zb, a, za)
+    assert ok, info
+    assert (sa.closest_rays, sa.shadow_rays) == (sb.closest_rays, sb.shadow_rays)
+
+
 def test_gpu_shard_leaves_other_tiles_untouched(renderer):
     scene, frame, params, _ = C.load_config("s1_amb")
     params.tile_offset, params.tile_stride = 1, 2

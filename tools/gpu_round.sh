@@ -28,6 +28,8 @@ for s in $STEPS; do
     bench) run bench 900 python3 bench.py --verbose ;;
     benchq) run benchq 600 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --verbose ;;
     occsweep) for o in ${OCCS:-1 6 7 8}; do RTX_SHADOW_OCC=$o run occ$o 600 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-count --no-post; done ;;
+    benchr1) RTX_SH_R=1 run benchr1 600 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-post --verbose ;;
+    variantsc) for v in ${VARS:-$(ls c-raytracer_amd/lib/var)}; do RTX_LIBRTX=$PWD/c-raytracer_amd/lib/var/$v/librtx.so run varc_$v 600 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-post --verbose; done ;;
     variants) for v in ${VARS:-$(ls c-raytracer_amd/lib/var)}; do RTX_LIBRTX=$PWD/c-raytracer_amd/lib/var/$v/librtx.so run var_$v 600 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-count --no-post; done ;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-count --no-post ;;
     pmcf) run pmcf 900 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post ;;
