@@ -75,7 +75,7 @@ struct rtx_ctx {
 	DPlane *d_planes = nullptr;
 	DMaterial *d_mats = nullptr;
 	DEmitter *d_emitters = nullptr;
-	DThread *d_threads = nullptr;
+	DQNode *d_qnodes = nullptr;
 	DScene scene{};
 	bool have_scene = false;
 	/* work buffers (grow-only) */
@@ -152,7 +152,7 @@ static void free_scene(rtx_ctx *c)
 	dfree(c->d_planes);
 	dfree(c->d_mats);
 	dfree(c->d_emitters);
-	dfree(c->d_threads);
+	dfree(c->d_qnodes);
 	c->have_scene = false;
 }
 
@@ -230,10 +230,10 @@ template <class T> static int upload(T *&dst, const std::vector<T> &v)
 	return RTX_OK;
 }
 
-/* DThread preorder of the subtree at device ref `ref` (rtx_device.h): the node itself with the
- * box it has in its parent, then its left and right subtrees.  A left subtree continues at its
- * right sibling, a right subtree at its parent's continuation, so the skip link of every node
- * is known when it is written (subtree sizes from `size`, filled by thread_sizes). */
+/* DQNode preorder of the subtree at device ref `ref` (rtx_device.h): the node itself with the
+ * box it has in its parent, then its left and right subtrees.  An inner node's link is the
+ * index after its subtree (subtree sizes from `size`, filled by thread_sizes); a leaf keeps
+ * its device ref. */
 static uint32_t thread_sizes(const std::vector<DNode> &recs, uint32_t ref, std::vector<uint32_t> &size)
 {
 	if (ref & RTX_REF_LEAF)
@@ -244,36 +244,60 @@ static uint32_t thread_sizes(const std::vector<DNode> &recs, uint32_t ref, std::
 	return size[i];
 }
 
-static void thread_emit(const std::vector<DNode> &recs, const std::vector<uint32_t> &size, uint32_t ref,
-			const float lo[3], const float hi[3], uint32_t skip, std::vector<DThread> &out)
+struct QFrame {
+	float qo[3], qs[3];
+};
+
+/* one plane pair quantised conservatively: lo down, hi up, one extra step each way */
+static uint32_t quantise(float lo, float hi, float qo, float qs)
 {
-	DThread t;
-	memcpy(t.lo, lo, 12);
-	memcpy(t.hi, hi, 12);
-	t.skip = skip;
-	t.ref = (ref & RTX_REF_LEAF) ? ref : 0u;
-	const uint32_t me = (uint32_t)out.size();
-	out.push_back(t);
-	if (ref & RTX_REF_LEAF)
-		return;
-	const DNode &n = recs[(ref & RTX_REF_OFF) / (uint32_t)sizeof(DNode)];
-	const float l0[3] = { n.lo0x, n.lo0y, n.lo0z }, h0[3] = { n.hi0x, n.hi0y, n.hi0z };
-	const float l1[3] = { n.lo1x, n.lo1y, n.lo1z }, h1[3] = { n.hi1x, n.hi1y, n.hi1z };
-	const uint32_t left_size = (n.ref0 & RTX_REF_LEAF) ? 1u : size[(n.ref0 & RTX_REF_OFF) / (uint32_t)sizeof(DNode)];
-	thread_emit(recs, size, n.ref0, l0, h0, me + 1 + left_size, out);
-	thread_emit(recs, size, n.ref1, l1, h1, skip, out);
+	const double a = std::floor(((double)lo - qo) * (double)qs) - 1.0, b = std::ceil(((double)hi - qo) * (double)qs) + 1.0;
+	const uint32_t ql = (uint32_t)std::min(65535.0, std::max(0.0, a)), qh = (uint32_t)std::min(65535.0, std::max(0.0, b));
+	return ql | (qh << 16);
 }
 
+static void thread_emit(const std::vector<DNode> &recs, const std::vector<uint32_t> &size, const QFrame &F,
+			uint32_t ref, const float lo[3], const float hi[3], std::vector<DQNode> &out)
+{
+	DQNode t;
+	t.x = quantise(lo[0], hi[0], F.qo[0], F.qs[0]);
+	t.y = quantise(lo[1], hi[1], F.qo[1], F.qs[1]);
+	t.z = quantise(lo[2], hi[2], F.qo[2], F.qs[2]);
+	const uint32_t me = (uint32_t)out.size();
+	if (ref & RTX_REF_LEAF) {
+		t.link = ref;
+		out.push_back(t);
+		return;
+	}
+	const uint32_t i = (ref & RTX_REF_OFF) / (uint32_t)sizeof(DNode);
+	t.link = (me + size[i]) << 6;
+	out.push_back(t);
+	const DNode &n = recs[i];
+	const float l0[3] = { n.lo0x, n.lo0y, n.lo0z }, h0[3] = { n.hi0x, n.hi0y, n.hi0z };
+	const float l1[3] = { n.lo1x, n.lo1y, n.lo1z }, h1[3] = { n.hi1x, n.hi1y, n.hi1z };
+	thread_emit(recs, size, F, n.ref0, l0, h0, out);
+	thread_emit(recs, size, F, n.ref1, l1, h1, out);
+}
+
+/* the quantised threaded BVH and its frame: the bounded objects' box, 65533 steps per axis */
 static void thread_bvh(const std::vector<DNode> &inner, uint32_t root_ref, const float lo[3], const float hi[3],
-		       std::vector<DThread> &out)
+		       std::vector<DQNode> &out, QFrame &F)
 {
 	out.clear();
+	float ext_max = 0.f;
+	for (int a = 0; a < 3; a++)
+		ext_max = std::max(ext_max, hi[a] - lo[a]);
+	for (int a = 0; a < 3; a++) {
+		F.qo[a] = lo[a];
+		const float ext = std::max(hi[a] - lo[a], std::max(ext_max, 1.f) * 1e-6f);
+		F.qs[a] = 65533.f / ext;
+	}
 	if (root_ref == RTX_EMPTY_REF)
 		return;
 	std::vector<uint32_t> size(inner.size(), 0);
 	const uint32_t total = thread_sizes(inner, root_ref, size);
 	out.reserve(total);
-	thread_emit(inner, size, root_ref, lo, hi, RTX_NONE, out);
+	thread_emit(inner, size, F, root_ref, lo, hi, out);
 }
 
 static inline float pad_lo(float x, float ext) { return x - (std::fabs(x) + ext) * 2e-6f - 1e-30f; }
@@ -512,10 +536,12 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 		depth = bvh.depth;
 		inner.assign(recs.begin(), recs.begin() + nnodes);
 	}
-	std::vector<DThread> threads;
-	if (nb)
-		thread_bvh(inner, root_ref, c->bound_lo, c->bound_hi, threads);
-	if ((rc = upload(c->d_threads, threads)))
+	std::vector<DQNode> qnodes;
+	QFrame qf;
+	thread_bvh(inner, nb ? root_ref : RTX_EMPTY_REF, c->bound_lo, c->bound_hi, qnodes, qf);
+	if (qnodes.size() >= (1u << 26))
+		return fail(RTX_ERR_SCENE, "scene too large: %zu threaded BVH nodes (max 2^26)", qnodes.size());
+	if ((rc = upload(c->d_qnodes, qnodes)))
 		return rc;
 	c->stats.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count();
 	if ((rc = upload(c->d_planes, planes)) || (rc = upload(c->d_mats, mats)) || (rc = upload(c->d_emitters, emit)))
@@ -529,8 +555,10 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 	S.planes = c->d_planes;
 	S.mats = c->d_mats;
 	S.emitters = c->d_emitters;
-	S.threads = threads.empty() ? nullptr : c->d_threads;
-	S.num_threads = (uint32_t)threads.size();
+	S.qnodes = qnodes.empty() ? nullptr : c->d_qnodes;
+	S.num_qnodes = (uint32_t)qnodes.size();
+	memcpy(S.qo, qf.qo, 12);
+	memcpy(S.qs, qf.qs, 12);
 	S.root_ref = nb ? root_ref : RTX_EMPTY_REF;
 	S.num_prims = nb;
 	S.num_planes = (uint32_t)planes.size();

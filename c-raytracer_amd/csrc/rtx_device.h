@@ -66,17 +66,21 @@ typedef struct __attribute__((aligned(64))) DPrim {
 	float d[4];
 } DPrim;
 
-/* threaded (skip-link) copy of the BVH for the ray-by-ray shadow walk, in preorder: a node's
- * own box (its parent's child slot; the scene bound for the root), the index to continue at
- * when the box is missed or the subtree is done (RTX_NONE: end), and for a leaf its device
- * ref (record byte offset | RTX_REF_LEAF | RTX_REF_SPH | count-1; 0 for an inner node, whose
- * first child is the next node).  Any-hit needs no visit order, so no stack. */
-typedef struct __attribute__((aligned(32))) DThread {
-	float lo[3];
-	uint32_t skip;
-	float hi[3];
-	uint32_t ref;
-} DThread;
+/* threaded (skip-link) copy of the BVH for the ray-by-ray shadow walk: one 16-byte record per
+ * BVH node in preorder, so a node is ONE 16-byte vector load.
+ *   x, y, z: the node's box (its parent's child slot; the scene bound for the root) quantised
+ *            to 16 bits per plane in the frame of the bounded objects' box,
+ *            q = (coordinate - qo) * qs, lo rounded down and hi up, then widened by one step
+ *            (conservative; lo in the low half, hi in the high half)
+ *   link:    inner node: index of the node after its subtree << 6 (where a missed box
+ *            continues; a hit continues at the first child, the next record);
+ *            leaf: its device ref (record byte offset | RTX_REF_LEAF | RTX_REF_SPH | count-1),
+ *            and the walk continues at the next record whether the box is hit or not.
+ * Any-hit needs no visit order, so no stack: the walk ends at index num_qnodes. */
+typedef struct __attribute__((aligned(16))) DQNode {
+	uint32_t x, y, z;
+	uint32_t link;
+} DQNode;
 
 typedef struct DPlane {
 	float n[3];
@@ -114,8 +118,9 @@ typedef struct DScene {
 	const DPlane *planes;
 	const DMaterial *mats;
 	const DEmitter *emitters;
-	const DThread *threads; /* threaded BVH (num_threads nodes), null when the BVH is empty */
-	uint32_t num_threads;
+	const DQNode *qnodes;   /* threaded quantised BVH (num_qnodes records), null when the BVH is empty */
+	uint32_t num_qnodes;
+	float qo[3], qs[3];     /* its quantisation frame: q = (x - qo) * qs */
 	uint32_t root_ref;
 	uint32_t num_nodes;    /* prims == (const DPrim *)(nodes + num_nodes) */
 	uint32_t num_prims;

@@ -1085,21 +1085,41 @@ __device__ __forceinline__ void shadow_walk(const char *__restrict__ recs, const
 }
 
 /* ------------------------------------------------------------------------ */
-/* ray-by-ray any-hit walk over the threaded BVH (DThread, skip links)      */
+/* ray-by-ray any-hit walk over the threaded quantised BVH (DQNode)         */
 /* ------------------------------------------------------------------------ */
 /* Measured on the benchmark frame (count mode): a 64-ray packet fetched 58 node records and
  * tested 27.6 primitives per ray, while each ray's own boxes cover only 7.6 inner nodes and
  * 2.2 primitives - deep in the tree the rays of one shade point part ways, and the packet
  * drags every ray through the union of their paths.  Here each lane walks alone: its node
  * index is its whole state (any-hit needs no order, so skip links replace the stack), a node
- * is two 16-byte vector loads (own box + skip, box + leaf ref), and lanes at different nodes
- * cost only their own steps.  The wave's cost is its longest ray, not the union of its rays. */
-template <int OCT>
-__device__ __forceinline__ bool box_hit_lh(float4 a, float4 b, f3 oi, f3 inv, float tlim)
+ * is one 16-byte vector load (quantised box + link), and lanes at different nodes cost only
+ * their own steps.  The wave's cost is its longest ray, not the union of its rays.  With
+ * per-lane loads the vector L1's tag rate is the scarce resource, hence one load per node. */
+/* per-lane loads through the global address space (global_load, not flat_load: the pointers
+ * come from LDS and the compiler cannot prove where they point) */
+template <typename T> __device__ __forceinline__ const __attribute__((address_space(1))) T *gptr(const T *p)
 {
-	const float tx0 = fmaf(a.x, inv.x, -oi.x), tx1 = fmaf(b.x, inv.x, -oi.x);
-	const float ty0 = fmaf(a.y, inv.y, -oi.y), ty1 = fmaf(b.y, inv.y, -oi.y);
-	const float tz0 = fmaf(a.z, inv.z, -oi.z), tz1 = fmaf(b.z, inv.z, -oi.z);
+	return (const __attribute__((address_space(1))) T *)p;
+}
+typedef float f4v __attribute__((ext_vector_type(4)));
+/* 16-byte global load at byte offset off of p */
+__device__ __forceinline__ float4 ldg4(const void *p, uint32_t off)
+{
+	const f4v v = *(const __attribute__((address_space(1))) f4v *)((const char *)p + off);
+	return make_float4(v.x, v.y, v.z, v.w);
+}
+
+/* the slab test against a DQNode box, in the quantisation frame: the ray is transformed once
+ * per walk (o' = (o - qo) * qs, inv' = inv / qs, oi = o' * inv'), so t = q * inv' - oi is the
+ * world ray parameter and the test is box_hit's, with 16-bit integers for the planes (each
+ * converted by one SDWA v_cvt_f32_u32 of its half-word).  The boxes are widened by a full
+ * step on both sides, far more than the rounding of the transform. */
+template <int OCT>
+__device__ __forceinline__ bool box_hit_q(uint4 n, f3 oi, f3 inv, float tlim)
+{
+	const float tx0 = fmaf((float)(n.x & 0xFFFFu), inv.x, -oi.x), tx1 = fmaf((float)(n.x >> 16), inv.x, -oi.x);
+	const float ty0 = fmaf((float)(n.y & 0xFFFFu), inv.y, -oi.y), ty1 = fmaf((float)(n.y >> 16), inv.y, -oi.y);
+	const float tz0 = fmaf((float)(n.z & 0xFFFFu), inv.z, -oi.z), tz1 = fmaf((float)(n.z >> 16), inv.z, -oi.z);
 	if (OCT == 8) {
 		const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.f));
 		const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlim));
@@ -1114,13 +1134,20 @@ __device__ __forceinline__ bool box_hit_lh(float4 a, float4 b, f3 oi, f3 inv, fl
 	return tn <= tf;
 }
 
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ldg4u(const void *p)
+{
+	const u4v v = *(const __attribute__((address_space(1))) u4v *)p;
+	return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 /* one primitive record of a leaf against this lane's shadow ray (accel.c:362-373): the target
  * emitter skipped; transparent hit -> li *= kt; opaque hit -> true (blocked) */
 template <bool COUNT>
-__device__ __forceinline__ bool shadow_prim_ray(const float4 *pr, const DMaterial *__restrict__ mats, f3 o, f3 d,
+__device__ __forceinline__ bool shadow_prim_ray(const float4 *pr_, const DMaterial *__restrict__ mats, f3 o, f3 d,
 						 float tl, uint32_t emit_obj, f3 &li, uint32_t &ntri, uint32_t &nsph)
 {
-	const float4 a = pr[0], b = pr[1], c = pr[2];
+	const float4 a = ldg4(pr_, 0), b = ldg4(pr_, 16), c = ldg4(pr_, 32);
 	const uint32_t meta = __float_as_uint(c.w), obj = __float_as_uint(b.w);
 	if (obj == emit_obj)
 		return false;
@@ -1138,56 +1165,69 @@ __device__ __forceinline__ bool shadow_prim_ray(const float4 *pr, const DMateria
 	if (!h)
 		return false;
 	if (meta & RTX_META_TRANSPARENT) {
-		const DMaterial &m = mats[meta & RTX_META_MAT];
-		li = mul3v(li, mk3(m.kt[0], m.kt[1], m.kt[2]));
+		const auto *m = gptr(mats) + (meta & RTX_META_MAT);
+		li = mul3v(li, mk3(m->kt[0], m->kt[1], m->kt[2]));
 		return false;
 	}
 	return true;
 }
 
+/* the quantised threaded BVH and its frame (rtx_device.h DQNode) */
+struct QBvh {
+	const DQNode *q;
+	uint32_t n;
+	f3 qo, qs;
+};
+
 template <bool COUNT, int OCT>
-__device__ __forceinline__ void shadow_walk_ray(const DThread *__restrict__ T, const char *__restrict__ recs,
+__device__ __forceinline__ void shadow_walk_ray(const QBvh &Q, const char *__restrict__ recs,
 						const DMaterial *__restrict__ mats, f3 o, f3 d, f3 inv, float &tl,
 						uint32_t emit_obj, f3 &li, ShadowCount &sc)
 {
-	const f3 oi = mul3v(o, inv);
-	uint32_t i = tl >= 0.f ? 0u : RTX_NONE;
+	const f3 invq = mk3(inv.x / Q.qs.x, inv.y / Q.qs.y, inv.z / Q.qs.z);
+	const f3 oq = mk3((o.x - Q.qo.x) * Q.qs.x, (o.y - Q.qo.y) * Q.qs.y, (o.z - Q.qo.z) * Q.qs.z);
+	const f3 oi = mul3v(oq, invq);
+	const uint32_t n = Q.n;
+	uint32_t i = tl >= 0.f ? 0u : n;
 	uint32_t nnode = 0, ntri = 0, nsph = 0;
-	while (i != RTX_NONE) {
-		const float4 *t = (const float4 *)(T + i);
-		const float4 a = t[0], b = t[1];
+	while (i < n) {
+		const uint4 nd = ldg4u(Q.q + i);
 		if (COUNT)
 			nnode++;
-		const uint32_t skip = __float_as_uint(a.w), ref = __float_as_uint(b.w);
-		const bool hit = box_hit_lh<OCT>(a, b, oi, inv, tl);
-		uint32_t next = hit ? i + 1 : skip;
-		if (hit && (ref & RTX_REF_LEAF)) {
-			next = skip;
-			const char *p = recs + (ref & RTX_REF_OFF);
-			const uint32_t cnt = (ref & RTX_REF_CNT) + 1;
-			for (uint32_t k = 0; k < cnt; k++) {
-				if (shadow_prim_ray<COUNT>((const float4 *)(p + k * (uint32_t)sizeof(DNode)), mats, o, d, tl,
-							   emit_obj, li, ntri, nsph)) {
-					tl = -1.f;
-					next = RTX_NONE;
-					break;
+		const bool hit = box_hit_q<OCT>(nd, oi, invq, tl);
+		uint32_t next = i + 1;
+		if (nd.w & RTX_REF_LEAF) {
+			if (hit) {
+				const char *p = recs + (nd.w & RTX_REF_OFF);
+				const uint32_t cnt = (nd.w & RTX_REF_CNT) + 1;
+				for (uint32_t k = 0; k < cnt; k++) {
+					if (shadow_prim_ray<COUNT>((const float4 *)(p + k * (uint32_t)sizeof(DNode)), mats, o, d, tl,
+								   emit_obj, li, ntri, nsph)) {
+						tl = -1.f;
+						next = n;
+						break;
+					}
 				}
 			}
+		} else if (!hit) {
+			next = nd.w >> 6;
 		}
 		i = next;
 	}
 	if (COUNT) {
-		uint32_t a = nnode, b = ntri, c = nsph;
+		uint32_t a = nnode, b = ntri, c = nsph, m = nnode;
 #pragma unroll
 		for (int s = 32; s > 0; s >>= 1) {
 			a += __shfl_xor(a, s, WAVE);
 			b += __shfl_xor(b, s, WAVE);
 			c += __shfl_xor(c, s, WAVE);
+			m = max(m, (uint32_t)__shfl_xor(m, s, WAVE));
 		}
 		sc.nodes += uni(a);
 		sc.tris += uni(b);
 		sc.sph += uni(c);
-		sc.steps++;
+		sc.steps += uni(m); /* the wave's node steps: its longest ray */
+		sc.psteps++;        /* walks */
 	}
 }
 
@@ -1199,7 +1239,7 @@ __device__ __forceinline__ void shadow_walk_ray(const DThread *__restrict__ T, c
  * specialised on the packet's direction octant when all live rays share it.  Returns the
  * lane's blocked flag; li carries the transmittance product. */
 template <bool COUNT>
-__device__ __forceinline__ bool shadow_packet(const DThread *__restrict__ threads, const char *__restrict__ recs,
+__device__ __forceinline__ bool shadow_packet(const QBvh &Q, const char *__restrict__ recs,
 					      const DMaterial *__restrict__ mats, const DPlane *__restrict__ planes,
 					      uint32_t num_planes, uint32_t root_ref,
 					      bool act, f3 o, f3 d, float dist, uint32_t emit_obj, bool emit_is_tri, f3 &li,
@@ -1238,13 +1278,13 @@ __device__ __forceinline__ bool shadow_packet(const DThread *__restrict__ thread
 		(void)tri_emit;
 #define RTX_WALK(K)                                                                                                 \
 	case K:                                                                                                           \
-		shadow_walk_ray<COUNT, K>(threads, recs, mats, o, d, inv, tl, emit_obj, li, sc);                              \
+		shadow_walk_ray<COUNT, K>(Q, recs, mats, o, d, inv, tl, emit_obj, li, sc);                              \
 		break;
 #if RTX_SH_OCT
 	RTX_WALK(0) RTX_WALK(1) RTX_WALK(2) RTX_WALK(3) RTX_WALK(4) RTX_WALK(5) RTX_WALK(6) RTX_WALK(7)
 #endif
 	default:
-		shadow_walk_ray<COUNT, 8>(threads, recs, mats, o, d, inv, tl, emit_obj, li, sc);
+		shadow_walk_ray<COUNT, 8>(Q, recs, mats, o, d, inv, tl, emit_obj, li, sc);
 		break;
 #else
 #define RTX_WALK(K)                                                                                                   \
@@ -1268,7 +1308,8 @@ __device__ __forceinline__ bool shadow_packet(const DThread *__restrict__ thread
  * the traversal, which needs every SGPR it can get at 8 waves/SIMD. */
 struct KShadow {
 	const DNode *recs; /* BVH nodes, then primitives from record nnodes */
-	const DThread *threads; /* threaded BVH (ray-by-ray walk) */
+	const DQNode *qnodes; /* threaded quantised BVH (ray-by-ray walk) */
+	float qo[3], qs[3];
 	const DMaterial *mats;
 	const DPlane *planes;
 	const DEmitter *emitters;
@@ -1277,7 +1318,7 @@ struct KShadow {
 	float4 *contrib;
 	unsigned long long *ctr;
 	uint32_t per_xcd;     /* waves per XCD slice of the grid */
-	uint32_t nnodes, root_ref, num_planes, num_emitters;
+	uint32_t nnodes, root_ref, num_planes, num_emitters, nq;
 	uint32_t n_sp, per_wave, slot_b, slot_lg;
 	int32_t rng, attenuation, reflection;
 	float att_offset;
@@ -1363,7 +1404,12 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	const float dsq = magsqr3(dv);
 	const f3 ldir = mul3s(dv, 1.f / ldist);
 	f3 li = ld3(E.li);
-	const bool blocked = shadow_packet<COUNT>(unip(ks.threads), (const char *)unip(ks.recs), unip(ks.mats), unip(ks.planes),
+	QBvh Q;
+	Q.q = unip(ks.qnodes);
+	Q.n = uni(ks.nq);
+	Q.qo = mk3(ks.qo[0], ks.qo[1], ks.qo[2]);
+	Q.qs = mk3(ks.qs[0], ks.qs[1], ks.qs[2]);
+	const bool blocked = shadow_packet<COUNT>(Q, (const char *)unip(ks.recs), unip(ks.mats), unip(ks.planes),
 						  uni(ks.num_planes), RTX_DEBUG_NOWALK ? RTX_EMPTY_REF : uni(ks.root_ref),
 						  act, p, ldir, ldist, E.obj, E.type == RTX_TRIANGLE, li, sc);
 	reread_barrier();
@@ -2078,7 +2124,12 @@ extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const
 		return hipErrorInvalidValue;
 	KShadow ka;
 	ka.recs = S->nodes;
-	ka.threads = S->threads;
+	ka.qnodes = S->qnodes;
+	for (int a = 0; a < 3; a++) {
+		ka.qo[a] = S->qo[a];
+		ka.qs[a] = S->qs[a];
+	}
+	ka.nq = S->num_qnodes;
 	ka.mats = S->mats;
 	ka.planes = S->planes;
 	ka.emitters = S->emitters;
