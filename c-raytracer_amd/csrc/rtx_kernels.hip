@@ -1141,13 +1141,13 @@ __device__ __forceinline__ uint4 ldg4u(const void *p)
 	return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-/* one primitive record of a leaf against this lane's shadow ray (accel.c:362-373): the target
- * emitter skipped; transparent hit -> li *= kt; opaque hit -> true (blocked) */
+/* one primitive record (a, b, c = its first 48 bytes) against this lane's shadow ray
+ * (accel.c:362-373): the target emitter skipped; transparent hit -> li *= kt; opaque hit ->
+ * true (blocked) */
 template <bool COUNT>
-__device__ __forceinline__ bool shadow_prim_ray(const float4 *pr_, const DMaterial *__restrict__ mats, f3 o, f3 d,
-						 float tl, uint32_t emit_obj, f3 &li, uint32_t &ntri, uint32_t &nsph)
+__device__ __forceinline__ bool shadow_prim_ray(float4 a, float4 b, float4 c, const DMaterial *__restrict__ mats, f3 o,
+						 f3 d, float tl, uint32_t emit_obj, f3 &li, uint32_t &ntri, uint32_t &nsph)
 {
-	const float4 a = ldg4(pr_, 0), b = ldg4(pr_, 16), c = ldg4(pr_, 32);
 	const uint32_t meta = __float_as_uint(c.w), obj = __float_as_uint(b.w);
 	if (obj == emit_obj)
 		return false;
@@ -1179,6 +1179,11 @@ struct QBvh {
 	f3 qo, qs;
 };
 
+/* The walk is software-pipelined: a leaf whose box the ray hits only records its primitives
+ * (pend, pcnt), and they are tested in the next iterations, their loads issued together with
+ * the next node's.  A wave step in which some lane reached a leaf then costs one memory round
+ * trip, not a node trip followed by a primitive trip.  Leaves of several primitives hold the
+ * node walk until their last primitive is in flight. */
 template <bool COUNT, int OCT>
 __device__ __forceinline__ void shadow_walk_ray(const QBvh &Q, const char *__restrict__ recs,
 						const DMaterial *__restrict__ mats, f3 o, f3 d, f3 inv, float &tl,
@@ -1189,30 +1194,45 @@ __device__ __forceinline__ void shadow_walk_ray(const QBvh &Q, const char *__res
 	const f3 oi = mul3v(oq, invq);
 	const uint32_t n = Q.n;
 	uint32_t i = tl >= 0.f ? 0u : n;
+	uint32_t pend = 0, pcnt = 0; /* pending primitives: next record's byte offset, count */
 	uint32_t nnode = 0, ntri = 0, nsph = 0;
-	while (i < n) {
-		const uint4 nd = ldg4u(Q.q + i);
-		if (COUNT)
-			nnode++;
-		const bool hit = box_hit_q<OCT>(nd, oi, invq, tl);
-		uint32_t next = i + 1;
-		if (nd.w & RTX_REF_LEAF) {
-			if (hit) {
-				const char *p = recs + (nd.w & RTX_REF_OFF);
-				const uint32_t cnt = (nd.w & RTX_REF_CNT) + 1;
-				for (uint32_t k = 0; k < cnt; k++) {
-					if (shadow_prim_ray<COUNT>((const float4 *)(p + k * (uint32_t)sizeof(DNode)), mats, o, d, tl,
-								   emit_obj, li, ntri, nsph)) {
-						tl = -1.f;
-						next = n;
-						break;
-					}
-				}
-			}
-		} else if (!hit) {
-			next = nd.w >> 6;
+	while (i < n || pcnt) {
+		const bool step = i < n && pcnt <= 1;
+		uint4 nd;
+		float4 a, b, c;
+		if (step)
+			nd = ldg4u(Q.q + i);
+		if (pcnt) {
+			a = ldg4(recs + pend, 0);
+			b = ldg4(recs + pend, 16);
+			c = ldg4(recs + pend, 32);
 		}
-		i = next;
+		bool blocked = false;
+		if (pcnt) {
+			blocked = shadow_prim_ray<COUNT>(a, b, c, mats, o, d, tl, emit_obj, li, ntri, nsph);
+			pend += (uint32_t)sizeof(DNode);
+			pcnt--;
+			if (blocked) {
+				tl = -1.f;
+				i = n;
+				pcnt = 0;
+			}
+		}
+		if (step && !blocked) {
+			if (COUNT)
+				nnode++;
+			const bool hit = box_hit_q<OCT>(nd, oi, invq, tl);
+			uint32_t next = i + 1;
+			if (nd.w & RTX_REF_LEAF) {
+				if (hit) {
+					pend = nd.w & RTX_REF_OFF;
+					pcnt = (nd.w & RTX_REF_CNT) + 1;
+				}
+			} else if (!hit) {
+				next = nd.w >> 6;
+			}
+			i = next;
+		}
 	}
 	if (COUNT) {
 		uint32_t a = nnode, b = ntri, c = nsph, m = nnode;
