@@ -76,6 +76,7 @@ struct rtx_ctx {
 	DMaterial *d_mats = nullptr;
 	DEmitter *d_emitters = nullptr;
 	DQNode *d_qnodes = nullptr;
+	uint32_t *d_top = nullptr;
 	DScene scene{};
 	bool have_scene = false;
 	/* work buffers (grow-only) */
@@ -153,6 +154,7 @@ static void free_scene(rtx_ctx *c)
 	dfree(c->d_mats);
 	dfree(c->d_emitters);
 	dfree(c->d_qnodes);
+	dfree(c->d_top);
 	c->have_scene = false;
 }
 
@@ -257,7 +259,8 @@ static uint32_t quantise(float lo, float hi, float qo, float qs)
 }
 
 static void thread_emit(const std::vector<DNode> &recs, const std::vector<uint32_t> &size, const QFrame &F,
-			uint32_t ref, const float lo[3], const float hi[3], std::vector<DQNode> &out)
+			uint32_t ref, const float lo[3], const float hi[3], std::vector<DQNode> &out, uint32_t dep,
+			std::vector<uint32_t> &depth)
 {
 	DQNode t;
 	t.x = quantise(lo[0], hi[0], F.qo[0], F.qs[0]);
@@ -267,23 +270,26 @@ static void thread_emit(const std::vector<DNode> &recs, const std::vector<uint32
 	if (ref & RTX_REF_LEAF) {
 		t.link = ref;
 		out.push_back(t);
+		depth.push_back(dep);
 		return;
 	}
 	const uint32_t i = (ref & RTX_REF_OFF) / (uint32_t)sizeof(DNode);
 	t.link = (me + size[i]) << 6;
 	out.push_back(t);
+	depth.push_back(dep);
 	const DNode &n = recs[i];
 	const float l0[3] = { n.lo0x, n.lo0y, n.lo0z }, h0[3] = { n.hi0x, n.hi0y, n.hi0z };
 	const float l1[3] = { n.lo1x, n.lo1y, n.lo1z }, h1[3] = { n.hi1x, n.hi1y, n.hi1z };
-	thread_emit(recs, size, F, n.ref0, l0, h0, out);
-	thread_emit(recs, size, F, n.ref1, l1, h1, out);
+	thread_emit(recs, size, F, n.ref0, l0, h0, out, dep + 1, depth);
+	thread_emit(recs, size, F, n.ref1, l1, h1, out, dep + 1, depth);
 }
 
 /* the quantised threaded BVH and its frame: the bounded objects' box, 65533 steps per axis */
 static void thread_bvh(const std::vector<DNode> &inner, uint32_t root_ref, const float lo[3], const float hi[3],
-		       std::vector<DQNode> &out, QFrame &F)
+		       std::vector<DQNode> &out, QFrame &F, std::vector<uint32_t> &depth)
 {
 	out.clear();
+	depth.clear();
 	float ext_max = 0.f;
 	for (int a = 0; a < 3; a++)
 		ext_max = std::max(ext_max, hi[a] - lo[a]);
@@ -297,7 +303,51 @@ static void thread_bvh(const std::vector<DNode> &inner, uint32_t root_ref, const
 	std::vector<uint32_t> size(inner.size(), 0);
 	const uint32_t total = thread_sizes(inner, root_ref, size);
 	out.reserve(total);
-	thread_emit(inner, size, F, root_ref, lo, hi, out);
+	thread_emit(inner, size, F, root_ref, lo, hi, out, 0, depth);
+}
+
+/* the LDS copy of the threaded BVH's top levels (rtx_device.h RTX_QTOP_CUT): every node
+ * shallower than the deepest cut that keeps at most RTX_TOP_MAX records */
+static uint32_t thread_top(const std::vector<DQNode> &q, const std::vector<uint32_t> &depth, std::vector<uint32_t> &top)
+{
+	top.clear();
+	if (q.empty())
+		return 0;
+	std::vector<size_t> hist(66, 0);
+	for (uint32_t dj : depth)
+		hist[std::min<uint32_t>(dj, 65)]++;
+	uint32_t D = 1; /* the top = nodes of depth < D */
+	size_t cnt = hist[0];
+	while (D < 65 && hist[D] && cnt + hist[D] <= RTX_TOP_MAX) {
+		cnt += hist[D];
+		D++;
+	}
+	std::vector<uint32_t> id(q.size(), RTX_NONE);
+	uint32_t nt = 0;
+	for (size_t j = 0; j < q.size(); j++)
+		if (depth[j] < D)
+			id[j] = nt++;
+	top.assign(5 * (size_t)nt, 0);
+	for (size_t j = 0; j < q.size(); j++) {
+		if (id[j] == RTX_NONE)
+			continue;
+		uint32_t *T = &top[4 * (size_t)id[j]];
+		T[0] = q[j].x;
+		T[1] = q[j].y;
+		T[2] = q[j].z;
+		const uint32_t link = q[j].link;
+		if (link & RTX_REF_LEAF) {
+			T[3] = link;
+		} else if (depth[j] == D - 1) {
+			T[3] = (((uint32_t)j + 1) << 6) | RTX_QTOP_CUT;
+			top[4 * (size_t)nt + id[j]] = link >> 6;
+		} else {
+			/* the node after an above-cut subtree is a sibling's or an ancestor's: in the top */
+			const uint32_t e = link >> 6;
+			T[3] = (e < q.size() ? id[e] : nt) << 6;
+		}
+	}
+	return nt;
 }
 
 static inline float pad_lo(float x, float ext) { return x - (std::fabs(x) + ext) * 2e-6f - 1e-30f; }
@@ -537,11 +587,16 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 		inner.assign(recs.begin(), recs.begin() + nnodes);
 	}
 	std::vector<DQNode> qnodes;
+	std::vector<uint32_t> qdepth;
 	QFrame qf;
-	thread_bvh(inner, nb ? root_ref : RTX_EMPTY_REF, c->bound_lo, c->bound_hi, qnodes, qf);
+	thread_bvh(inner, nb ? root_ref : RTX_EMPTY_REF, c->bound_lo, c->bound_hi, qnodes, qf, qdepth);
 	if (qnodes.size() >= (1u << 26))
 		return fail(RTX_ERR_SCENE, "scene too large: %zu threaded BVH nodes (max 2^26)", qnodes.size());
 	if ((rc = upload(c->d_qnodes, qnodes)))
+		return rc;
+	std::vector<uint32_t> qtop;
+	const uint32_t ntop = thread_top(qnodes, qdepth, qtop);
+	if ((rc = upload(c->d_top, qtop)))
 		return rc;
 	c->stats.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count();
 	if ((rc = upload(c->d_planes, planes)) || (rc = upload(c->d_mats, mats)) || (rc = upload(c->d_emitters, emit)))
@@ -559,6 +614,8 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 	S.num_qnodes = (uint32_t)qnodes.size();
 	memcpy(S.qo, qf.qo, 12);
 	memcpy(S.qs, qf.qs, 12);
+	S.top = ntop ? c->d_top : nullptr;
+	S.num_top = ntop;
 	S.root_ref = nb ? root_ref : RTX_EMPTY_REF;
 	S.num_prims = nb;
 	S.num_planes = (uint32_t)planes.size();
@@ -735,7 +792,8 @@ static int render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, f
 	rtx_stats &st = c->stats;
 	st.closest_rays = ctr[RTX_C_CLOSEST];
 	st.shadow_rays = ctr[RTX_C_SHADOW];
-	st.shadow_node_visits = ctr[RTX_C_SNODES];
+	/* the threaded walk counts box tests; a node visit is a BVH2 inner node (two box tests) */
+	st.shadow_node_visits = RTX_SH_RAY ? ctr[RTX_C_SNODES] / 2 : ctr[RTX_C_SNODES];
 	st.shadow_tri_tests = ctr[RTX_C_STRIS];
 	st.shadow_sphere_tests = ctr[RTX_C_SSPHERES];
 	st.shadow_plane_tests = ctr[RTX_C_SPLANES];
@@ -743,7 +801,7 @@ static int render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, f
 	st.shadow_packet_prims = ctr[RTX_C_SPSTEPS];
 	st.shadow_ray_nodes = ctr[RTX_C_SRNODES];
 	st.shadow_ray_prims = ctr[RTX_C_SRTRIS];
-	st.node_visits = ctr[RTX_C_NODES] + ctr[RTX_C_SNODES];
+	st.node_visits = ctr[RTX_C_NODES] + st.shadow_node_visits;
 	st.tri_tests = ctr[RTX_C_TRIS] + ctr[RTX_C_STRIS];
 	st.sphere_tests = ctr[RTX_C_SPHERES] + ctr[RTX_C_SSPHERES];
 	st.plane_tests = ctr[RTX_C_PLANES] + ctr[RTX_C_SPLANES];

@@ -82,6 +82,24 @@ typedef struct __attribute__((aligned(16))) DQNode {
 	uint32_t link;
 } DQNode;
 
+/* The threaded BVH's top levels, copied to LDS once per k_shadow workgroup (DScene.top):
+ * num_top 16-byte records (x, y, z as in DQNode, for every node shallower than the cut depth,
+ * in preorder), then num_top 32-bit words.  Record link: a leaf's ref (the walk continues at
+ * the next top record); an inner node above the cut: the top index after its top subtree << 6;
+ * a cut node (an inner node whose children lie below the cut): its first child's DQNode index
+ * << 6 | RTX_QTOP_CUT, and its word = the DQNode index after its subtree.  A hit on a cut
+ * node walks that DQNode range, then continues at the next top record. */
+#define RTX_QTOP_CUT 1u
+#ifndef RTX_TOP_MAX
+#define RTX_TOP_MAX 2048 /* top records per workgroup (20 B each in LDS) */
+#endif
+#ifndef RTX_SH_NW
+#define RTX_SH_NW 16 /* waves per k_shadow workgroup (they share the top copy) */
+#endif
+#ifndef RTX_SH_RAY
+#define RTX_SH_RAY 1 /* k_shadow walks rays one by one over DQNode (0: 64-ray packets, measurement) */
+#endif
+
 typedef struct DPlane {
 	float n[3];
 	float d;
@@ -121,6 +139,8 @@ typedef struct DScene {
 	const DQNode *qnodes;   /* threaded quantised BVH (num_qnodes records), null when the BVH is empty */
 	uint32_t num_qnodes;
 	float qo[3], qs[3];     /* its quantisation frame: q = (x - qo) * qs */
+	const uint32_t *top;    /* its top levels (num_top records + num_top words, see RTX_QTOP_CUT) */
+	uint32_t num_top;
 	uint32_t root_ref;
 	uint32_t num_nodes;    /* prims == (const DPrim *)(nodes + num_nodes) */
 	uint32_t num_prims;
@@ -167,6 +187,7 @@ enum {
 	RTX_C_SPCOUNT,    /* shade points emitted (per chunk) */
 	RTX_C_OVERFLOW,   /* task-stack / staging overflow (per chunk) */
 	RTX_C_SPOVERFLOW, /* chunk shade-point array overflow (per chunk) */
+	RTX_C_SPQUEUE,    /* k_shadow work queue head (per chunk) */
 	RTX_C_CLOSEST,
 	RTX_C_SHADOW,
 	RTX_C_NODES,      /* closest-hit traversal counts (count mode) */
@@ -183,6 +204,6 @@ enum {
 	RTX_C_SRTRIS,     /* shadow walk: leaf primitives under boxes the ray itself hits (count mode) */
 	RTX_C_N
 };
-#define RTX_C_CHUNK_N 4 /* counters reset per chunk */
+#define RTX_C_CHUNK_N 5 /* counters reset per chunk */
 
 #endif

@@ -1177,13 +1177,28 @@ struct QBvh {
 	const DQNode *q;
 	uint32_t n;
 	f3 qo, qs;
+	const uint4 *top;     /* the workgroup's LDS copy of the top records */
+	const uint32_t *tend; /* ... and of the cut records' range ends */
+	uint32_t nt;
 };
 
-/* The walk is software-pipelined: a leaf whose box the ray hits only records its primitives
- * (pend, pcnt), and they are tested in the next iterations, their loads issued together with
- * the next node's.  A wave step in which some lane reached a leaf then costs one memory round
- * trip, not a node trip followed by a primitive trip.  Leaves of several primitives hold the
- * node walk until their last primitive is in flight. */
+/* LDS reads through generic pointers that point into LDS */
+__device__ __forceinline__ uint4 lds4u(const void *p)
+{
+	const u4v v = *(const __attribute__((address_space(3))) u4v *)p;
+	return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint32_t lds1u(const uint32_t *p)
+{
+	return *(const __attribute__((address_space(3))) uint32_t *)p;
+}
+
+/* The walk starts in the workgroup's LDS copy of the tree's top levels (DScene.top): a cut
+ * record whose box is hit hands the lane to the DQNode array for the index range of its
+ * children's subtrees, and the lane returns to the top copy at the next top record when the
+ * range ends.  The nodes visited, and their order, are the plain threaded walk's.  Every
+ * global node load costs a vector-L1 lookup per lane, the resource the walk saturates; the
+ * top levels, which nearly every ray tests, come from LDS instead. */
 template <bool COUNT, int OCT>
 __device__ __forceinline__ void shadow_walk_ray(const QBvh &Q, const char *__restrict__ recs,
 						const DMaterial *__restrict__ mats, f3 o, f3 d, f3 inv, float &tl,
@@ -1192,52 +1207,58 @@ __device__ __forceinline__ void shadow_walk_ray(const QBvh &Q, const char *__res
 	const f3 invq = mk3(inv.x / Q.qs.x, inv.y / Q.qs.y, inv.z / Q.qs.z);
 	const f3 oq = mk3((o.x - Q.qo.x) * Q.qs.x, (o.y - Q.qo.y) * Q.qs.y, (o.z - Q.qo.z) * Q.qs.z);
 	const f3 oi = mul3v(oq, invq);
-	const uint32_t n = Q.n;
-	uint32_t i = tl >= 0.f ? 0u : n;
-	uint32_t pend = 0, pcnt = 0; /* pending primitives: next record's byte offset, count */
-	uint32_t nnode = 0, ntri = 0, nsph = 0;
-	while (i < n || pcnt) {
-		const bool step = i < n && pcnt <= 1;
+	const uint32_t nt = Q.nt;
+	uint32_t t = tl >= 0.f ? 0u : nt, g = 0, ge = 0;
+	uint32_t nnode = 0, nglob = 0, ntri = 0, nsph = 0;
+	while (t < nt || g < ge) {
+		const bool ing = g < ge;
 		uint4 nd;
-		float4 a, b, c;
-		if (step)
-			nd = ldg4u(Q.q + i);
-		if (pcnt) {
-			a = ldg4(recs + pend, 0);
-			b = ldg4(recs + pend, 16);
-			c = ldg4(recs + pend, 32);
+		if (ing)
+			nd = ldg4u(Q.q + g);
+		else
+			nd = lds4u(Q.top + t);
+		if (COUNT) {
+			nnode++;
+			nglob += ing ? 1u : 0u;
 		}
-		bool blocked = false;
-		if (pcnt) {
-			blocked = shadow_prim_ray<COUNT>(a, b, c, mats, o, d, tl, emit_obj, li, ntri, nsph);
-			pend += (uint32_t)sizeof(DNode);
-			pcnt--;
-			if (blocked) {
-				tl = -1.f;
-				i = n;
-				pcnt = 0;
-			}
-		}
-		if (step && !blocked) {
-			if (COUNT)
-				nnode++;
-			const bool hit = box_hit_q<OCT>(nd, oi, invq, tl);
-			uint32_t next = i + 1;
-			if (nd.w & RTX_REF_LEAF) {
-				if (hit) {
-					pend = nd.w & RTX_REF_OFF;
-					pcnt = (nd.w & RTX_REF_CNT) + 1;
+		const bool hit = box_hit_q<OCT>(nd, oi, invq, tl);
+		const uint32_t L = nd.w;
+		if (L & RTX_REF_LEAF) {
+			if (ing)
+				g++;
+			else
+				t++;
+			if (hit) {
+				const char *p = recs + (L & RTX_REF_OFF);
+				const uint32_t cnt = (L & RTX_REF_CNT) + 1;
+				for (uint32_t k = 0; k < cnt; k++) {
+					const char *pr = p + k * (uint32_t)sizeof(DNode);
+					if (shadow_prim_ray<COUNT>(ldg4(pr, 0), ldg4(pr, 16), ldg4(pr, 32), mats, o, d, tl, emit_obj,
+								   li, ntri, nsph)) {
+						tl = -1.f;
+						t = nt;
+						ge = 0;
+						break;
+					}
 				}
-			} else if (!hit) {
-				next = nd.w >> 6;
 			}
-			i = next;
+		} else if (ing) {
+			g = hit ? g + 1 : L >> 6;
+		} else if (L & RTX_QTOP_CUT) {
+			if (hit) {
+				g = L >> 6;
+				ge = lds1u(Q.tend + t);
+			}
+			t++;
+		} else {
+			t = hit ? t + 1 : L >> 6;
 		}
 	}
 	if (COUNT) {
-		uint32_t a = nnode, b = ntri, c = nsph, m = nnode;
+		uint32_t a = nnode, b = ntri, c = nsph, m = nnode, gq = nglob;
 #pragma unroll
 		for (int s = 32; s > 0; s >>= 1) {
+			gq += __shfl_xor(gq, s, WAVE);
 			a += __shfl_xor(a, s, WAVE);
 			b += __shfl_xor(b, s, WAVE);
 			c += __shfl_xor(c, s, WAVE);
@@ -1246,14 +1267,12 @@ __device__ __forceinline__ void shadow_walk_ray(const QBvh &Q, const char *__res
 		sc.nodes += uni(a);
 		sc.tris += uni(b);
 		sc.sph += uni(c);
+		sc.rnodes += uni(gq); /* box tests whose node came from the DQNode array, not the LDS top */
 		sc.steps += uni(m); /* the wave's node steps: its longest ray */
 		sc.psteps++;        /* walks */
 	}
 }
 
-#ifndef RTX_SH_RAY
-#define RTX_SH_RAY 1 /* ray-by-ray threaded walk (0: the 64-ray packet walk) */
-#endif
 
 /* planes first (unbound_objects_is_light_blocked, object.c:183-197), then the BVH walk,
  * specialised on the packet's direction octant when all live rays share it.  Returns the
@@ -1330,6 +1349,8 @@ struct KShadow {
 	const DNode *recs; /* BVH nodes, then primitives from record nnodes */
 	const DQNode *qnodes; /* threaded quantised BVH (ray-by-ray walk) */
 	float qo[3], qs[3];
+	const uint32_t *top;  /* its top levels (rtx_device.h RTX_QTOP_CUT), copied to LDS per workgroup */
+	uint32_t ntop;
 	const DMaterial *mats;
 	const DPlane *planes;
 	const DEmitter *emitters;
@@ -1337,7 +1358,6 @@ struct KShadow {
 	const uint32_t *perm; /* shade points in processing order (Morton-sorted), or null */
 	float4 *contrib;
 	unsigned long long *ctr;
-	uint32_t per_xcd;     /* waves per XCD slice of the grid */
 	uint32_t nnodes, root_ref, num_planes, num_emitters, nq;
 	uint32_t n_sp, per_wave, slot_b, slot_lg;
 	int32_t rng, attenuation, reflection;
@@ -1382,7 +1402,7 @@ __device__ __forceinline__ f3 shade_light(const KShadow &ks, const float4 *rec, 
  * reread barriers so none stays in registers across the walk. */
 template <bool COUNT>
 __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec, uint32_t idx, bool act,
-					   ShadowCount &sc)
+					   ShadowCount &sc, const uint4 *top_q, const uint32_t *top_e)
 {
 	reread_barrier();
 	const float4 q0 = rec[0], q4 = rec[4];
@@ -1429,6 +1449,9 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	Q.n = uni(ks.nq);
 	Q.qo = mk3(ks.qo[0], ks.qo[1], ks.qo[2]);
 	Q.qs = mk3(ks.qs[0], ks.qs[1], ks.qs[2]);
+	Q.top = top_q;
+	Q.tend = top_e;
+	Q.nt = uni(ks.ntop);
 	const bool blocked = shadow_packet<COUNT>(Q, (const char *)unip(ks.recs), unip(ks.mats), unip(ks.planes),
 						  uni(ks.num_planes), RTX_DEBUG_NOWALK ? RTX_EMPTY_REF : uni(ks.root_ref),
 						  act, p, ldir, ldist, E.obj, E.type == RTX_TRIANGLE, li, sc);
@@ -1806,119 +1829,144 @@ __device__ __forceinline__ void light_chunk(const KShadow &ks, const float4 *rec
 	}
 }
 
+/* Persistent workgroups of RTX_SH_NW waves.  A workgroup copies the threaded BVH's top levels
+ * (DScene.top) to LDS once; then each wave takes per_wave shade points at a time from a global
+ * queue (RTX_C_SPQUEUE), in processing (Morton) order, until the points run out.  The resident
+ * waves so work on one compact region of the scene at a time, and no workgroup waits on a tail.
+ * A point's result depends only on the point (its sums run inside one wave, in lane order), not
+ * on which wave takes it. */
 template <bool COUNT, int OCC, int R>
-__global__ __launch_bounds__(WAVE, OCC) void k_shadow(KShadow ka)
+__global__ __launch_bounds__(WAVE * RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 {
-	__shared__ KShadow ks;
-	__shared__ float li_lds[3 * R * WAVE];  /* R > 1: each ray's light intensity x transmittance */
-	__shared__ uint8_t emit_lds[R * WAVE];  /* R > 1: the emitter each ray aims at */
-	__shared__ uint32_t off[WAVE + 1]; /* first lane slot of each shade point, total */
-	__shared__ uint32_t nls[WAVE];     /* shadow rays of each shade point */
-	__shared__ uint32_t sid[WAVE];     /* each shade point's index in the record array */
-	__shared__ float Ls[3][WAVE];      /* per shade point light sum, in packet order */
-	/* blocks are dispatched in order, so the resident waves cover a window of the (spatially
-	 * sorted) shade points: one compact region of the scene at a time on every XCD.
-	 * per_xcd != 0 instead gives each XCD (b % 8) its own contiguous slice (measured: 4x
-	 * slower, the slices' costs differ too much) */
-	const uint32_t w = ka.per_xcd ? (blockIdx.x & 7u) * ka.per_xcd + (blockIdx.x >> 3) : blockIdx.x;
-	const uint32_t j0 = w * ka.per_wave;
-	if (j0 >= ka.n_sp)
-		return;
-	const uint32_t cnt = min(ka.per_wave, ka.n_sp - j0);
-	const bool own = lane_id() < cnt;
-	const uint32_t my_sid = own ? (ka.perm ? ka.perm[j0 + lane_id()] : j0 + lane_id()) : 0u;
-	const uint32_t nl_mine = own ? __float_as_uint(ka.sp[(size_t)my_sid * SPREC + 4].w) : 0u;
-	/* each point's samples occupy whole lane slots of B lanes (B = power of two), so a point's
-	 * packet partial sums never depend on which other points share its wave: deterministic */
-	uint32_t total;
-	const uint32_t ex = wave_excl_scan((nl_mine + ka.slot_b - 1) >> ka.slot_lg, &total);
-	off[lane_id()] = ex;
-	nls[lane_id()] = nl_mine;
-	sid[lane_id()] = my_sid;
-	Ls[0][lane_id()] = 0.f;
-	Ls[1][lane_id()] = 0.f;
-	Ls[2][lane_id()] = 0.f;
-	if (lane_id() == 0) {
-		off[WAVE] = total;
-		ks = ka;
+	__shared__ uint4 top_q[RTX_TOP_MAX];             /* the top records (rtx_device.h RTX_QTOP_CUT) */
+	__shared__ uint32_t top_e[RTX_TOP_MAX];          /* cut records: the DQNode index after the subtree */
+	__shared__ KShadow ks_w[RTX_SH_NW];
+	__shared__ float li_w[RTX_SH_NW][R > 1 ? 3 * R * WAVE : 1]; /* R > 1: each ray's light intensity x transmittance */
+	__shared__ uint8_t emit_w[RTX_SH_NW][R > 1 ? R * WAVE : 1]; /* R > 1: the emitter each ray aims at */
+	__shared__ uint32_t off_w[RTX_SH_NW][WAVE + 1]; /* first lane slot of each shade point, total */
+	__shared__ uint32_t nls_w[RTX_SH_NW][WAVE];     /* shadow rays of each shade point */
+	__shared__ uint32_t sid_w[RTX_SH_NW][WAVE];     /* each shade point's index in the record array */
+	__shared__ float Ls_w[RTX_SH_NW][3][WAVE];      /* per shade point light sum, in packet order */
+	const uint32_t ntop = ka.ntop;
+	for (uint32_t i = threadIdx.x; i < ntop; i += WAVE * RTX_SH_NW) {
+		top_q[i] = ldg4u(ka.top + 4 * i);
+		top_e[i] = gptr(ka.top)[4 * ntop + i];
 	}
-	lds_sync();
+	const uint32_t wv = uni(threadIdx.x / WAVE);
+	if (lane_id() == 0)
+		ks_w[wv] = ka;
+	__syncthreads();
+	KShadow &ks = ks_w[wv];
+	float *li_lds = li_w[wv];
+	uint8_t *emit_lds = emit_w[wv];
+	uint32_t *off = off_w[wv], *nls = nls_w[wv], *sid = sid_w[wv];
+	float(*Ls)[WAVE] = Ls_w[wv];
 	ShadowCount sc = { 0, 0, 0, 0, 0, 0, 0, 0 };
-	if (ka.slot_b == WAVE) {
-		/* >= 64 lights: every packet is 64 samples of ONE shade point.  The point is wave-uniform
-		 * (its record is read once per packet through one address, no owner search), each lane
-		 * sums its samples over the point's packets, and one butterfly per point reduces them. */
-		for (uint32_t k = 0; k < cnt; k++) {
-			reread_barrier();
-			const uint32_t nl = uni(nls[k]);
-			const float4 *rec = unip(ks.sp) + (size_t)uni(sid[k]) * SPREC;
-			f3 acc = mk3(0.f, 0.f, 0.f);
-			if (R > 1) {
-				for (uint32_t base = 0; base < nl; base += R * WAVE)
-					light_chunk<COUNT, R>(ks, rec, base, nl, li_lds, emit_lds, acc, sc);
-			} else {
-				for (uint32_t base = 0; base < nl; base += WAVE) {
-					const uint32_t idx = base + lane_id();
-					acc = add3(acc, light_sample<COUNT>(ks, rec, idx, idx < nl, sc));
-				}
-			}
-			const float sx = wave_sum(acc.x), sy = wave_sum(acc.y), sz = wave_sum(acc.z);
-			if (lane_id() == 0) {
-				Ls[0][k] = sx;
-				Ls[1][k] = sy;
-				Ls[2][k] = sz;
-			}
-		}
+	u64 rays_total = 0;
+	for (;;) {
+		reread_barrier();
+		uint32_t j0 = 0;
+		if (lane_id() == 0)
+			j0 = (uint32_t)atomicAdd(unip(ks.ctr) + RTX_C_SPQUEUE, (unsigned long long)uni(ks.per_wave));
+		j0 = readlane(j0, 0);
+		const uint32_t n_sp = uni(ks.n_sp);
+		if (j0 >= n_sp)
+			break;
+		const uint32_t cnt = min(uni(ks.per_wave), n_sp - j0);
+		const bool own = lane_id() < cnt;
+		const uint32_t *perm = unip(ks.perm);
+		const uint32_t my_sid = own ? (perm ? perm[j0 + lane_id()] : j0 + lane_id()) : 0u;
+		const uint32_t nl_mine = own ? __float_as_uint(unip(ks.sp)[(size_t)my_sid * SPREC + 4].w) : 0u;
+		/* each point's samples occupy whole lane slots of B lanes (B = power of two), so a point's
+		 * packet partial sums never depend on which other points share its wave: deterministic */
+		uint32_t total;
+		const uint32_t ex = wave_excl_scan((nl_mine + uni(ks.slot_b) - 1) >> uni(ks.slot_lg), &total);
+		off[lane_id()] = ex;
+		nls[lane_id()] = nl_mine;
+		sid[lane_id()] = my_sid;
+		Ls[0][lane_id()] = 0.f;
+		Ls[1][lane_id()] = 0.f;
+		Ls[2][lane_id()] = 0.f;
+		if (lane_id() == 0)
+			off[WAVE] = total;
 		lds_sync();
-	} else if constexpr (R == 1) {
-		/* fewer lights: several points share a packet, each in its own power-of-two lane slot */
-		for (uint32_t base = 0;;) {
-			reread_barrier();
-			const uint32_t tot = uni(off[WAVE]), slot_b = uni(ks.slot_b), slot_lg = uni(ks.slot_lg);
-			if (base >= tot)
-				break;
-			const uint32_t slot = base + (lane_id() >> slot_lg);
-			const uint32_t k = slot < tot ? owner_of(off, slot) : 0u;
-			const uint32_t idx = ((slot - off[k]) << slot_lg) + (lane_id() & (slot_b - 1));
-			const bool act = slot < tot && idx < nls[k];
-			const float4 *rec = unip(ks.sp) + (size_t)sid[k] * SPREC;
-			const f3 contribution = light_sample<COUNT>(ks, rec, idx, act, sc);
-			/* per-shade-point sums; lanes are ordered by k */
-			const uint32_t t2 = uni(off[WAVE]), sb = uni(ks.slot_b), spp = WAVE / sb;
-			const uint32_t last_slot_lane = (min(t2 - base, spp) - 1) * sb;
-			const uint32_t k0 = readlane(k, 0), k1 = readlane(k, last_slot_lane);
-			for (uint32_t kk = k0; kk <= k1; kk++) {
-				const bool in = act && k == kk;
-				if (!ballot(in))
-					continue;
-				const float sx = wave_sum(in ? contribution.x : 0.f);
-				const float sy = wave_sum(in ? contribution.y : 0.f);
-				const float sz = wave_sum(in ? contribution.z : 0.f);
+		if (uni(ks.slot_b) == WAVE) {
+			/* >= 64 lights: every packet is 64 samples of ONE shade point.  The point is wave-uniform
+			 * (its record is read once per packet through one address, no owner search), each lane
+			 * sums its samples over the point's packets, and one butterfly per point reduces them. */
+			for (uint32_t k = 0; k < cnt; k++) {
+				reread_barrier();
+				const uint32_t nl = uni(nls[k]);
+				const float4 *rec = unip(ks.sp) + (size_t)uni(sid[k]) * SPREC;
+				f3 acc = mk3(0.f, 0.f, 0.f);
+				if (R > 1) {
+					for (uint32_t base = 0; base < nl; base += R * WAVE)
+						light_chunk<COUNT, R>(ks, rec, base, nl, li_lds, emit_lds, acc, sc);
+				} else {
+					for (uint32_t base = 0; base < nl; base += WAVE) {
+						const uint32_t idx = base + lane_id();
+						acc = add3(acc, light_sample<COUNT>(ks, rec, idx, idx < nl, sc, top_q, top_e));
+					}
+				}
+				const float sx = wave_sum(acc.x), sy = wave_sum(acc.y), sz = wave_sum(acc.z);
 				if (lane_id() == 0) {
-					Ls[0][kk] += sx;
-					Ls[1][kk] += sy;
-					Ls[2][kk] += sz;
+					Ls[0][k] = sx;
+					Ls[1][k] = sy;
+					Ls[2][k] = sz;
 				}
 			}
 			lds_sync();
-			base += spp;
+		} else if constexpr (R == 1) {
+			/* fewer lights: several points share a packet, each in its own power-of-two lane slot */
+			for (uint32_t base = 0;;) {
+				reread_barrier();
+				const uint32_t tot = uni(off[WAVE]), slot_b = uni(ks.slot_b), slot_lg = uni(ks.slot_lg);
+				if (base >= tot)
+					break;
+				const uint32_t slot = base + (lane_id() >> slot_lg);
+				const uint32_t k = slot < tot ? owner_of(off, slot) : 0u;
+				const uint32_t idx = ((slot - off[k]) << slot_lg) + (lane_id() & (slot_b - 1));
+				const bool act = slot < tot && idx < nls[k];
+				const float4 *rec = unip(ks.sp) + (size_t)sid[k] * SPREC;
+				const f3 contribution = light_sample<COUNT>(ks, rec, idx, act, sc, top_q, top_e);
+				/* per-shade-point sums; lanes are ordered by k */
+				const uint32_t t2 = uni(off[WAVE]), sb = uni(ks.slot_b), spp = WAVE / sb;
+				const uint32_t last_slot_lane = (min(t2 - base, spp) - 1) * sb;
+				const uint32_t k0 = readlane(k, 0), k1 = readlane(k, last_slot_lane);
+				for (uint32_t kk = k0; kk <= k1; kk++) {
+					const bool in = act && k == kk;
+					if (!ballot(in))
+						continue;
+					const float sx = wave_sum(in ? contribution.x : 0.f);
+					const float sy = wave_sum(in ? contribution.y : 0.f);
+					const float sz = wave_sum(in ? contribution.z : 0.f);
+					if (lane_id() == 0) {
+						Ls[0][kk] += sx;
+						Ls[1][kk] += sy;
+						Ls[2][kk] += sz;
+					}
+				}
+				lds_sync();
+				base += spp;
+			}
 		}
-	}
-	reread_barrier();
-	if (own) {
-		const float4 *my = unip(ks.sp) + (size_t)my_sid * SPREC;
-		const float4 q0 = my[0], q1 = my[1], q2 = my[2], q5 = my[5];
-		const f3 w = mk3(q0.w, q1.w, q2.w);
-		const f3 c = mul3v(w, mk3(Ls[0][lane_id()], Ls[1][lane_id()], Ls[2][lane_id()]));
-		unip(ks.contrib)[my_sid] = make_float4(c.x, c.y, c.z, q5.x);
-	}
-	uint32_t n_rays = own ? nls[lane_id()] : 0u;
+		reread_barrier();
+		if (own) {
+			const float4 *my = unip(ks.sp) + (size_t)my_sid * SPREC;
+			const float4 q0 = my[0], q1 = my[1], q2 = my[2], q5 = my[5];
+			const f3 w = mk3(q0.w, q1.w, q2.w);
+			const f3 c = mul3v(w, mk3(Ls[0][lane_id()], Ls[1][lane_id()], Ls[2][lane_id()]));
+			unip(ks.contrib)[my_sid] = make_float4(c.x, c.y, c.z, q5.x);
+		}
+		uint32_t n_rays = own ? nls[lane_id()] : 0u;
 #pragma unroll
-	for (int o = 32; o > 0; o >>= 1)
-		n_rays += __shfl_xor(n_rays, o, WAVE);
+		for (int o = 32; o > 0; o >>= 1)
+			n_rays += __shfl_xor(n_rays, o, WAVE);
+		rays_total += uni(n_rays);
+	}
 	if (lane_id() == 0) {
 		unsigned long long *ctr = unip(ks.ctr);
-		atomicAdd(&ctr[RTX_C_SHADOW], (u64)n_rays);
+		atomicAdd(&ctr[RTX_C_SHADOW], rays_total);
 		if (COUNT) {
 			atomicAdd(&ctr[RTX_C_SNODES], sc.nodes);
 			atomicAdd(&ctr[RTX_C_STRIS], sc.tris);
@@ -2130,6 +2178,24 @@ extern "C" hipError_t rtx_launch_trace(const DScene *S, const DFrame *F, const D
 	return hipGetLastError();
 }
 
+/* the persistent k_shadow grid: as many workgroups as are resident on the device at once (no
+ * more than the work needs); the waves then share the shade points through RTX_C_SPQUEUE */
+template <bool C, int O, int R> static void launch_shadow(const KShadow &ka, uint32_t nw, hipStream_t stream)
+{
+	static uint32_t slots = 0;
+	if (!slots) {
+		int dev = 0, cus = 0, per_cu = 0;
+		if (hipGetDevice(&dev) != hipSuccess ||
+		    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+		    hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(&k_shadow<C, O, R>),
+								 WAVE * RTX_SH_NW, 0) != hipSuccess)
+			per_cu = 0;
+		slots = per_cu > 0 && cus > 0 ? (uint32_t)(per_cu * cus) : 1024u;
+	}
+	const uint32_t need = (nw + RTX_SH_NW - 1) / RTX_SH_NW;
+	hipLaunchKernelGGL((k_shadow<C, O, R>), dim3(need < slots ? need : slots), dim3(WAVE * RTX_SH_NW), 0, stream, ka);
+}
+
 extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const float4 *sp, const uint32_t *perm,
 					uint32_t n_sp, uint32_t per_wave, uint32_t slot_b, uint32_t rays_per_lane,
 					float4 *contrib, unsigned long long *ctr, int count, hipStream_t stream)
@@ -2137,14 +2203,16 @@ extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const
 	const uint32_t nw = (n_sp + per_wave - 1) / per_wave;
 	if (!nw)
 		return hipSuccess;
-	const char *xe = getenv("RTX_XCDMAP");
-	const uint32_t per_xcd = (xe && xe[0] == '1') ? (nw + 7) / 8 : 0u, grid = per_xcd ? 8 * per_xcd : nw;
 	if (!slot_b || (slot_b & (slot_b - 1)) || slot_b > WAVE || !per_wave || per_wave > WAVE || !rays_per_lane ||
 	    rays_per_lane > 5 || (rays_per_lane > 1 && slot_b != WAVE))
+		return hipErrorInvalidValue;
+	if (S->num_top > RTX_TOP_MAX)
 		return hipErrorInvalidValue;
 	KShadow ka;
 	ka.recs = S->nodes;
 	ka.qnodes = S->qnodes;
+	ka.top = S->top;
+	ka.ntop = S->num_top;
 	for (int a = 0; a < 3; a++) {
 		ka.qo[a] = S->qo[a];
 		ka.qs[a] = S->qs[a];
@@ -2155,7 +2223,6 @@ extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const
 	ka.emitters = S->emitters;
 	ka.sp = sp;
 	ka.perm = perm;
-	ka.per_xcd = per_xcd;
 	ka.contrib = contrib;
 	ka.ctr = ctr;
 	ka.nnodes = S->num_nodes;
@@ -2176,8 +2243,7 @@ extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const
 		const char *e = getenv("RTX_SHADOW_OCC");
 		occ = e ? atoi(e) : RTX_SHADOW_OCC_DEFAULT;
 	}
-#define RTX_LAUNCH_SHADOW(C, O, R)                                                                               \
-	hipLaunchKernelGGL((k_shadow<C, O, R>), dim3(grid), dim3(WAVE), 0, stream, ka)
+#define RTX_LAUNCH_SHADOW(C, O, R) launch_shadow<C, O, R>(ka, nw, stream)
 #define RTX_LAUNCH_SHADOW_R(C, O)                                                                                \
 	switch (rays_per_lane) {                                                                                     \
 	case 2: RTX_LAUNCH_SHADOW(C, O, 2); break;                                                                   \
