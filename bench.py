@@ -325,10 +325,11 @@ def main():
                     "ray_need_nodes": int(c.shadow_ray_nodes), "ray_need_prims": int(c.shadow_ray_prims),
                     "kernel_ms": round(shadow_ms, 3),
                     "note": "B_ray = 64*node_visits + 48*tri_tests + 32*sphere_tests + 16*plane_tests + 48 "
-                            "per shadow ray (SURVEY §8(d)), visits counted per ray (lane); frac > 1 because a "
-                            "64-ray packet fetches each 64-B record once (s_load_dwordx16) and the BVH is "
-                            "L2/MALL-resident: the kernel is issue-bound, see DESIGN.md §5; traffic = PMC "
-                            "L2->fabric bytes per launch (2*FETCH_SIZE + WRITE_SIZE, profiles/)"}
+                            "per shadow ray (SURVEY §8(d), the reference's 64-B node model), visits counted "
+                            "per ray in BVH2 units; frac > 1 because the walk reads 16-B quantised threaded "
+                            "nodes (the top 2048 from LDS) and the 33 MB BVH is L2/MALL-resident, so HBM is "
+                            "not the bound: the kernel is issue/latency-bound, see DESIGN.md §5; traffic = "
+                            "PMC L2->fabric bytes per launch (2*FETCH_SIZE + WRITE_SIZE, profiles/)"}
 
     build = None
     if rank == 0 and world == 1 and not a.no_post:
