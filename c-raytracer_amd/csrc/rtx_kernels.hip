@@ -1462,6 +1462,168 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	return contribution;
 }
 
+/* All nl light samples of one shade point (single-point mode, >= 64 lights) with lane refill.
+ * A 64-ray packet runs until its longest ray ends, so most lanes idle through the tail of
+ * every packet.  Here a lane whose ray has ended takes the point's next unassigned sample
+ * (render.c:170-229 per sample, as light_sample) once at least RTX_SH_REFILL lanes are idle
+ * or none is walking, so the wave keeps walking until the point's samples run out.  Which
+ * lane takes which sample depends only on the walk lengths, i.e. on the point: the per-lane
+ * sums, and the point's result, stay deterministic and independent of scheduling. */
+#ifndef RTX_SH_REFILL
+#define RTX_SH_REFILL 0
+#endif
+template <bool COUNT>
+__device__ __forceinline__ f3 point_refill(const KShadow &ks, const float4 *rec, uint32_t nl, ShadowCount &sc,
+					   const uint4 *top_q, const uint32_t *top_e)
+{
+	reread_barrier();
+	const float4 q0 = rec[0], q4 = rec[4];
+	const f3 p = mk3(q0.x, q0.y, q0.z);
+	const uint32_t obj = __float_as_uint(q4.x);
+	const uint32_t key_a = __float_as_uint(q4.y), key_b = __float_as_uint(q4.z);
+	const uint32_t nt = uni(ks.ntop);
+	const bool have_tree = uni(ks.root_ref) != RTX_EMPTY_REF && !RTX_DEBUG_NOWALK;
+	f3 acc = mk3(0.f, 0.f, 0.f);
+	f3 d = mk3(0.f, 0.f, 0.f), invq = d, oi = d, li = d;
+	float tl = -1.f, ldist = 1.f, dsq = 1.f;
+	uint32_t emit_obj = RTX_NONE, t = nt, g = 0, ge = 0;
+	bool has = false; /* the lane holds a sample whose terms are not yet in acc */
+	uint32_t next = 0; /* wave-uniform: the point's next unassigned sample */
+	uint32_t nnode = 0, ntri = 0, nsph = 0, nsteps = 0;
+	for (;;) {
+		const bool walking = t < nt || g < ge;
+		const u64 wl = ballot(walking);
+		const uint32_t idle = (uint32_t)popc64(~wl);
+		if (!wl || (idle >= RTX_SH_REFILL && next < nl)) {
+			reread_barrier();
+			/* finish this lane's ended sample, then take a new one */
+			if (has && !walking) {
+				if (tl >= 0.f)
+					acc = add3(acc, shade_light(ks, rec, d, li, ldist, dsq));
+				has = false;
+			}
+			const u64 want = ballot(!walking);
+			const uint32_t idx = next + (uint32_t)__builtin_amdgcn_mbcnt_hi(
+							   (uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
+			next = min(nl, next + (uint32_t)popc64(want));
+			if (COUNT)
+				sc.pln += (u64)popc64(ballot(!walking && idx < nl)) * uni(ks.num_planes);
+			if (!walking && idx < nl) {
+				const DEmitter *emitters = unip(ks.emitters);
+				const uint32_t num_emitters = uni(ks.num_emitters);
+				uint32_t j = idx, e = 0;
+				for (; e < num_emitters; e++) {
+					const uint32_t eo = emitters[e].obj, enl = emitters[e].num_lights;
+					if (eo == obj)
+						continue;
+					if (j < enl)
+						break;
+					j -= enl;
+				}
+				if (e >= num_emitters)
+					e = 0;
+				const DEmitter &E = emitters[e];
+				float u1 = 0.5f, u2 = 0.5f;
+				if (uni(ks.rng) != RTX_RNG_CONST)
+					rtx_draw2(key_of(key_a, key_b), e, j, &u1, &u2);
+				const f3 lp = light_point(E, p, u1, u2);
+				const f3 dv = sub3(lp, p);
+				ldist = mag3(dv);
+				dsq = magsqr3(dv);
+				d = mul3s(dv, 1.f / ldist);
+				li = ld3(E.li);
+				emit_obj = E.obj;
+				tl = ldist;
+				/* planes first (unbound_objects_is_light_blocked, object.c:183-197) */
+				const DPlane *planes = unip(ks.planes);
+				const uint32_t num_planes = uni(ks.num_planes);
+				for (uint32_t i = 0; i < num_planes; i++) {
+					const auto *pl = cptr(planes) + i;
+					const auto *m = cptr(unip(ks.mats)) + pl->mat;
+					float tp;
+					const bool h = hit_plane(mk3(pl->n[0], pl->n[1], pl->n[2]), pl->d, p, d, pl->eps, tp) &&
+						       tp < ldist && tl >= 0.f;
+					if (m->flags & RTX_MF_TRANSPARENT) {
+						if (h)
+							li = mul3v(li, mk3(m->kt[0], m->kt[1], m->kt[2]));
+					} else if (h) {
+						tl = -1.f;
+					}
+				}
+				const f3 inv = safe_inv_fast(d);
+				invq = mk3(inv.x / ks.qs[0], inv.y / ks.qs[1], inv.z / ks.qs[2]);
+				const f3 oq = mk3((p.x - ks.qo[0]) * ks.qs[0], (p.y - ks.qo[1]) * ks.qs[1], (p.z - ks.qo[2]) * ks.qs[2]);
+				oi = mul3v(oq, invq);
+				t = (tl >= 0.f && have_tree) ? 0u : nt;
+				g = 0;
+				ge = 0;
+				has = true;
+			}
+			if (!ballot(has))
+				break;
+			continue;
+		}
+		if (COUNT)
+			nsteps++;
+		if (walking) {
+			const bool ing = g < ge;
+			uint4 nd;
+			if (ing)
+				nd = ldg4u(unip(ks.qnodes) + g);
+			else
+				nd = lds4u(top_q + t);
+			if (COUNT)
+				nnode++;
+			const bool hit = box_hit_q<8>(nd, oi, invq, tl);
+			const uint32_t L = nd.w;
+			if (L & RTX_REF_LEAF) {
+				if (ing)
+					g++;
+				else
+					t++;
+				if (hit) {
+					const char *pr = (const char *)unip(ks.recs) + (L & RTX_REF_OFF);
+					const uint32_t cnt = (L & RTX_REF_CNT) + 1;
+					for (uint32_t k = 0; k < cnt; k++, pr += sizeof(DNode)) {
+						if (shadow_prim_ray<COUNT>(ldg4(pr, 0), ldg4(pr, 16), ldg4(pr, 32), unip(ks.mats), p, d, tl,
+									   emit_obj, li, ntri, nsph)) {
+							tl = -1.f;
+							t = nt;
+							ge = 0;
+							break;
+						}
+					}
+				}
+			} else if (ing) {
+				g = hit ? g + 1 : L >> 6;
+			} else if (L & RTX_QTOP_CUT) {
+				if (hit) {
+					g = L >> 6;
+					ge = lds1u(top_e + t);
+				}
+				t++;
+			} else {
+				t = hit ? t + 1 : L >> 6;
+			}
+		}
+	}
+	if (COUNT) {
+		uint32_t a = nnode, b = ntri, c = nsph;
+#pragma unroll
+		for (int s = 32; s > 0; s >>= 1) {
+			a += __shfl_xor(a, s, WAVE);
+			b += __shfl_xor(b, s, WAVE);
+			c += __shfl_xor(c, s, WAVE);
+		}
+		sc.nodes += uni(a);
+		sc.tris += uni(b);
+		sc.sph += uni(c);
+		sc.steps += uni(nsteps);
+		sc.psteps++;
+	}
+	return acc;
+}
+
 /* ------------------------------------------------------------------------ */
 /* single-origin packets: R shadow rays per lane                            */
 /* ------------------------------------------------------------------------ */
@@ -1902,6 +2064,8 @@ __global__ __launch_bounds__(WAVE * RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 				if (R > 1) {
 					for (uint32_t base = 0; base < nl; base += R * WAVE)
 						light_chunk<COUNT, R>(ks, rec, base, nl, li_lds, emit_lds, acc, sc);
+				} else if (RTX_SH_REFILL > 0) {
+					acc = point_refill<COUNT>(ks, rec, nl, sc, top_q, top_e);
 				} else {
 					for (uint32_t base = 0; base < nl; base += WAVE) {
 						const uint32_t idx = base + lane_id();
