@@ -1373,6 +1373,37 @@ template <typename T> __device__ __forceinline__ T *unip(T *p)
 	return (T *)(((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v));
 }
 
+/* light_point (object.c:293-304) for the shadow kernel: on a sphere emitter the inclination and
+ * azimuth are u * 2pi, so their sines and cosines come straight from the hardware's
+ * revolution-scaled v_sin_f32 / v_cos_f32 instead of OCML's range-reduced sinf / cosf
+ * (|error| ~1e-6 of the radius, far inside the frame tolerance; the KAT suite keeps checking the
+ * exact light_point).  RTX_SH_FASTTRIG=0 restores the exact version here too. */
+#ifndef RTX_SH_FASTTRIG
+#define RTX_SH_FASTTRIG 1
+#endif
+/* 1/x in the shadow kernel's light sampling and attenuation: v_rcp_f32 (1 ulp) instead of the
+ * IEEE division sequence when RTX_SH_FASTDIV (the shadow ray direction and the attenuated
+ * intensity move by <= 1 ulp; the closest-hit path keeps IEEE division). */
+#ifndef RTX_SH_FASTDIV
+#define RTX_SH_FASTDIV 1
+#endif
+__device__ __forceinline__ float sh_rcp(float x) { return RTX_SH_FASTDIV ? __builtin_amdgcn_rcpf(x) : 1.f / x; }
+
+__device__ __forceinline__ f3 light_point_sh(const DEmitter &e, f3 p, float u1, float u2)
+{
+	if (RTX_SH_FASTTRIG && e.type == RTX_SPHERE) {
+		const f3 c = ld3(e.p0);
+		const f3 nrm = sub3(c, p);
+		const float si = __builtin_amdgcn_sinf(u1), ci = __builtin_amdgcn_cosf(u1);
+		const float sa = __builtin_amdgcn_sinf(u2), ca = __builtin_amdgcn_cosf(u2);
+		f3 ld = mk3(e.radius * ca * si, e.radius * sa * si, e.radius * ci);
+		if (dot3(nrm, ld) != 0.f)
+			ld = mul3s(ld, -1.f);
+		return add3(c, ld);
+	}
+	return light_point(e, p, u1, u2);
+}
+
 /* direct-lighting terms of one unblocked light sample (render.c:199-228), read after the walk */
 __device__ __forceinline__ f3 shade_light(const KShadow &ks, const float4 *rec, f3 ldir, f3 li, float ldist, float dsq)
 {
@@ -1381,9 +1412,9 @@ __device__ __forceinline__ f3 shade_light(const KShadow &ks, const float4 *rec, 
 	const float a = dot3(ldir, n);
 	const int32_t att = (int32_t)uni((uint32_t)ks.attenuation);
 	if (att == RTX_ATT_LIN)
-		li = mul3s(li, 1.f / (ks.att_offset + ldist));
+		li = mul3s(li, sh_rcp(ks.att_offset + ldist));
 	else if (att == RTX_ATT_SQR)
-		li = mul3s(li, 1.f / (ks.att_offset + dsq));
+		li = mul3s(li, sh_rcp(ks.att_offset + dsq));
 	const DMaterial &m = unip(ks.mats)[__float_as_uint(q3.w)];
 	const f3 diff = mul3s(mul3v(mk3(q3.x, q3.y, q3.z), li), fmaxf(0.f, a));
 	float sm;
@@ -1438,11 +1469,11 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 		u2 = (y + u2) * (1.f / 32.f);
 	}
 #endif
-	const f3 lp = light_point(E, p, u1, u2);
+	const f3 lp = light_point_sh(E, p, u1, u2);
 	const f3 dv = sub3(lp, p);
 	const float ldist = mag3(dv);
 	const float dsq = magsqr3(dv);
-	const f3 ldir = mul3s(dv, 1.f / ldist);
+	const f3 ldir = mul3s(dv, sh_rcp(ldist));
 	f3 li = ld3(E.li);
 	QBvh Q;
 	Q.q = unip(ks.qnodes);
@@ -1526,11 +1557,11 @@ __device__ __forceinline__ f3 point_refill(const KShadow &ks, const float4 *rec,
 				float u1 = 0.5f, u2 = 0.5f;
 				if (uni(ks.rng) != RTX_RNG_CONST)
 					rtx_draw2(key_of(key_a, key_b), e, j, &u1, &u2);
-				const f3 lp = light_point(E, p, u1, u2);
+				const f3 lp = light_point_sh(E, p, u1, u2);
 				const f3 dv = sub3(lp, p);
 				ldist = mag3(dv);
 				dsq = magsqr3(dv);
-				d = mul3s(dv, 1.f / ldist);
+				d = mul3s(dv, sh_rcp(ldist));
 				li = ld3(E.li);
 				emit_obj = E.obj;
 				tl = ldist;
@@ -1885,11 +1916,11 @@ __device__ __forceinline__ void light_chunk(const KShadow &ks, const float4 *rec
 		float u1 = 0.5f, u2 = 0.5f;
 		if (!rng_const)
 			rtx_draw2(key_of(__float_as_uint(q4.y), __float_as_uint(q4.z)), e, j, &u1, &u2);
-		const f3 lp = light_point(E, p, u1, u2);
+		const f3 lp = light_point_sh(E, p, u1, u2);
 		const f3 dv = sub3(lp, p);
 		ldist[r] = mag3(dv);
 		dsq[r] = magsqr3(dv);
-		d[r] = mul3s(dv, 1.f / ldist[r]);
+		d[r] = mul3s(dv, sh_rcp(ldist[r]));
 		float *l = li_lds + r * WAVE + lane_id();
 		l[0] = E.li[0];
 		l[R * WAVE] = E.li[1];
