@@ -1274,6 +1274,26 @@ __device__ __forceinline__ void shadow_walk_ray(const QBvh &Q, const char *__res
 }
 
 
+/* |v| of the light vector: v_sqrt_f32 (1 ulp) instead of the correctly rounded sqrt sequence
+ * when RTX_SH_FASTSQRT; shadow-ray plane tests then also take t from v_rcp_f32. */
+#ifndef RTX_SH_FASTSQRT
+#define RTX_SH_FASTSQRT 0
+#endif
+__device__ __forceinline__ float sh_mag(f3 v)
+{
+	return RTX_SH_FASTSQRT ? __builtin_amdgcn_sqrtf(magsqr3(v)) : mag3(v);
+}
+__device__ __forceinline__ bool sh_hit_plane(f3 n, float dd, f3 o, f3 d, float eps, float &t)
+{
+	if (!RTX_SH_FASTSQRT)
+		return hit_plane(n, dd, o, d, eps, t);
+	const float a = dot3(n, d);
+	if (fabsf(a) < eps)
+		return false;
+	t = (dd - dot3(n, o)) * __builtin_amdgcn_rcpf(a);
+	return t > eps;
+}
+
 /* planes first (unbound_objects_is_light_blocked, object.c:183-197), then the BVH walk,
  * specialised on the packet's direction octant when all live rays share it.  Returns the
  * lane's blocked flag; li carries the transmittance product. */
@@ -1289,7 +1309,7 @@ __device__ __forceinline__ bool shadow_packet(const QBvh &Q, const char *__restr
 		const auto *pl = cptr(planes) + i;
 		const auto *m = cptr(mats) + pl->mat;
 		float t;
-		const bool h = hit_plane(mk3(pl->n[0], pl->n[1], pl->n[2]), pl->d, o, d, pl->eps, t) && t < dist && tl >= 0.f;
+		const bool h = sh_hit_plane(mk3(pl->n[0], pl->n[1], pl->n[2]), pl->d, o, d, pl->eps, t) && t < dist && tl >= 0.f;
 		if (m->flags & RTX_MF_TRANSPARENT) {
 			if (h)
 				li = mul3v(li, mk3(m->kt[0], m->kt[1], m->kt[2]));
@@ -1471,7 +1491,7 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 #endif
 	const f3 lp = light_point_sh(E, p, u1, u2);
 	const f3 dv = sub3(lp, p);
-	const float ldist = mag3(dv);
+	const float ldist = sh_mag(dv);
 	const float dsq = magsqr3(dv);
 	const f3 ldir = mul3s(dv, sh_rcp(ldist));
 	f3 li = ld3(E.li);
@@ -1559,7 +1579,7 @@ __device__ __forceinline__ f3 point_refill(const KShadow &ks, const float4 *rec,
 					rtx_draw2(key_of(key_a, key_b), e, j, &u1, &u2);
 				const f3 lp = light_point_sh(E, p, u1, u2);
 				const f3 dv = sub3(lp, p);
-				ldist = mag3(dv);
+				ldist = sh_mag(dv);
 				dsq = magsqr3(dv);
 				d = mul3s(dv, sh_rcp(ldist));
 				li = ld3(E.li);
@@ -1572,7 +1592,7 @@ __device__ __forceinline__ f3 point_refill(const KShadow &ks, const float4 *rec,
 					const auto *pl = cptr(planes) + i;
 					const auto *m = cptr(unip(ks.mats)) + pl->mat;
 					float tp;
-					const bool h = hit_plane(mk3(pl->n[0], pl->n[1], pl->n[2]), pl->d, p, d, pl->eps, tp) &&
+					const bool h = sh_hit_plane(mk3(pl->n[0], pl->n[1], pl->n[2]), pl->d, p, d, pl->eps, tp) &&
 						       tp < ldist && tl >= 0.f;
 					if (m->flags & RTX_MF_TRANSPARENT) {
 						if (h)
@@ -1918,7 +1938,7 @@ __device__ __forceinline__ void light_chunk(const KShadow &ks, const float4 *rec
 			rtx_draw2(key_of(__float_as_uint(q4.y), __float_as_uint(q4.z)), e, j, &u1, &u2);
 		const f3 lp = light_point_sh(E, p, u1, u2);
 		const f3 dv = sub3(lp, p);
-		ldist[r] = mag3(dv);
+		ldist[r] = sh_mag(dv);
 		dsq[r] = magsqr3(dv);
 		d[r] = mul3s(dv, sh_rcp(ldist[r]));
 		float *l = li_lds + r * WAVE + lane_id();
@@ -1940,7 +1960,7 @@ __device__ __forceinline__ void light_chunk(const KShadow &ks, const float4 *rec
 #pragma unroll
 		for (int r = 0; r < R; r++) {
 			float t;
-			const bool h = hit_plane(pn, pl->d, p, d[r], pl->eps, t) && t < ldist[r] && tl[r] >= 0.f;
+			const bool h = sh_hit_plane(pn, pl->d, p, d[r], pl->eps, t) && t < ldist[r] && tl[r] >= 0.f;
 			if (transparent) {
 				if (h) {
 					float *l = li_lds + r * WAVE + lane_id();
