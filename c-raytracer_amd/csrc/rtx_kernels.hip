@@ -1520,6 +1520,9 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
  * or none is walking, so the wave keeps walking until the point's samples run out.  Which
  * lane takes which sample depends only on the walk lengths, i.e. on the point: the per-lane
  * sums, and the point's result, stay deterministic and independent of scheduling. */
+#ifndef RTX_SH_STREAM
+#define RTX_SH_STREAM 0 /* > 0: stream single-point samples across points, batches of this many points */
+#endif
 #ifndef RTX_SH_REFILL
 #define RTX_SH_REFILL 0
 #endif
@@ -2103,7 +2106,54 @@ __global__ __launch_bounds__(WAVE * RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 		if (lane_id() == 0)
 			off[WAVE] = total;
 		lds_sync();
-		if (uni(ks.slot_b) == WAVE) {
+		uint32_t nmin = own ? nl_mine : 0xFFFFFFFFu;
+		#pragma unroll
+		for (int o = 32; o > 0; o >>= 1)
+			nmin = min(nmin, (uint32_t)__shfl_xor(nmin, o, WAVE));
+		if (RTX_SH_STREAM && R == 1 && uni(ks.slot_b) == WAVE && uni(nmin) >= WAVE) {
+			/* Streamed samples: the batch's points' samples, concatenated, fill packets of 64 lanes,
+			 * so a point's last part-filled packet is shared with the next point (each has >= 64
+			 * samples, so a packet spans at most two).  Lane s keeps the running sum of the samples
+			 * i == s (mod 64) of the current point (acc) and of the next (accn), pulled from whichever
+			 * lane computed them: the same additions in the same order as the unstreamed loop, so
+			 * every point's sum is bit-identical to it. */
+			uint32_t tot_s;
+			const uint32_t so = wave_excl_scan(own ? nl_mine : 0u, &tot_s);
+			uint32_t k = 0;
+			f3 acc = mk3(0.f, 0.f, 0.f), accn = acc;
+			for (uint32_t base = 0; base < tot_s; base += WAVE) {
+				reread_barrier();
+				const uint32_t g = base + lane_id();
+				const bool act = g < tot_s;
+				const bool has2 = k + 1 < cnt;
+				const uint32_t s0 = readlane(so, k), s1 = has2 ? readlane(so, k + 1) : tot_s;
+				const bool second = has2 && g >= s1;
+				const uint32_t kl = second ? k + 1 : k;
+				const float4 *rec = unip(ks.sp) + (size_t)sid[kl] * SPREC;
+				const f3 c = light_sample<COUNT>(ks, rec, g - (second ? s1 : s0), act, sc, top_q, top_e);
+				const bool in0 = act && !second, in1 = act && second;
+				const int la = (int)((lane_id() + s0 - base) & (WAVE - 1));
+				const int lb = (int)((lane_id() + s1 - base) & (WAVE - 1));
+				acc.x += __shfl(in0 ? c.x : 0.f, la, WAVE);
+				acc.y += __shfl(in0 ? c.y : 0.f, la, WAVE);
+				acc.z += __shfl(in0 ? c.z : 0.f, la, WAVE);
+				accn.x += __shfl(in1 ? c.x : 0.f, lb, WAVE);
+				accn.y += __shfl(in1 ? c.y : 0.f, lb, WAVE);
+				accn.z += __shfl(in1 ? c.z : 0.f, lb, WAVE);
+				if (base + WAVE >= s1) { /* point k ends in this packet */
+					const float sx = wave_sum(acc.x), sy = wave_sum(acc.y), sz = wave_sum(acc.z);
+					if (lane_id() == 0) {
+						Ls[0][k] = sx;
+						Ls[1][k] = sy;
+						Ls[2][k] = sz;
+					}
+					acc = accn;
+					accn = mk3(0.f, 0.f, 0.f);
+					k++;
+				}
+			}
+			lds_sync();
+		} else if (uni(ks.slot_b) == WAVE) {
 			/* >= 64 lights: every packet is 64 samples of ONE shade point.  The point is wave-uniform
 			 * (its record is read once per packet through one address, no owner search), each lane
 			 * sums its samples over the point's packets, and one butterfly per point reduces them. */
@@ -2415,6 +2465,8 @@ extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const
 					uint32_t n_sp, uint32_t per_wave, uint32_t slot_b, uint32_t rays_per_lane,
 					float4 *contrib, unsigned long long *ctr, int count, hipStream_t stream)
 {
+	if (RTX_SH_STREAM && slot_b == WAVE && rays_per_lane == 1 && per_wave < RTX_SH_STREAM)
+		per_wave = RTX_SH_STREAM; /* streamed samples: more points per batch, fewer part-filled packets */
 	const uint32_t nw = (n_sp + per_wave - 1) / per_wave;
 	if (!nw)
 		return hipSuccess;
