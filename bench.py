@@ -12,8 +12,11 @@ RCCL all-gather of the packed tiles (16 B/px), so the image is complete on
 every rank.  Rays = cast_ray calls + is_light_blocked calls, exactly as the
 reference defines its work; counted by the kernel.
 
-Launch: python bench.py [--gpus 1] [--steps K] [--warmup W]
+Launch: python bench.py [--gpus N] [--steps K] [--warmup W]
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+`--gpus N` always means N ranks: without a torchrun environment, bench.py starts
+torch.distributed.run itself (one child process per GPU, before anything touches a GPU)
+and exits with its code; under torchrun, WORLD_SIZE must equal N or it exits non-zero.
 """
 import argparse
 import json
@@ -27,6 +30,26 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 METRIC = "Mrays/s (primary+secondary) at 1920×1080×64spp; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# MI355X_MICROARCH.md: 256 CUs x 4 SIMDs, 2.4 GHz max clock, one wave64 VALU instruction per SIMD
+# every 2 cycles -> peak VALU issue in wave-instructions per second
+VALU_PEAK_GINST = 256 * 4 * 2.4e9 / 2 / 1e9
+# useful VALU per operation of k_shadow (the minimal instruction count of the arithmetic the
+# reference's algorithm needs, per lane): box_hit_q octant form 17 (6 cvt, 6 fma,
+# max/max3/min3/min, cmp), any_tri 39, a plane test 12, and per light sample 100 (counter RNG,
+# light point, direction, attenuation, Phong/Blinn incl. powf)
+USEFUL_VALU = {"box": 17, "tri": 39, "sphere": 25, "plane": 12, "sample": 100}
+SHADOW_SRCS = ["c-raytracer_amd/csrc/rtx_shadow.hip", "c-raytracer_amd/csrc/rtx_wave.h",
+               "c-raytracer_amd/csrc/rtx_math.h", "c-raytracer_amd/csrc/rtx_device.h", "include/rtx_rng.h"]
+
+
+def shadow_src_sha():
+    """sha1 over k_shadow's sources: ties a committed PMC summary to the kernel it measured"""
+    import hashlib
+    h = hashlib.sha1()
+    for f in SHADOW_SRCS:
+        with open(os.path.join(ROOT, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def parse():
@@ -43,7 +66,55 @@ def parse():
     ap.add_argument("--no-post", action="store_true", help="skip the postprocess (DoF + mist) side leg")
     ap.add_argument("--cpu-target-s", type=float, default=12.0)
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="rank bring-up only (gloo, no GPU): print the ranks' world and exit (tests)")
     return ap.parse_args()
+
+
+def launch_ranks(a):
+    """`--gpus N` without a torchrun environment: start N ranks through torch.distributed.run as a
+    child process (nothing here has touched a GPU, so this is not an exec of a GPU process) and
+    return its exit code.  Under torchrun, WORLD_SIZE must equal --gpus.  Returns None when this
+    process is itself the (only) rank to run."""
+    import socket
+    import subprocess
+    world = os.environ.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != a.gpus:
+            print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}: refusing to report a different "
+                  f"GPU count than asked", file=sys.stderr)
+            return 2
+        return None
+    if a.gpus < 1:
+        print(f"bench.py: --gpus {a.gpus}: need at least one", file=sys.stderr)
+        return 2
+    if a.gpus == 1:
+        return None
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def dry_run(a):
+    """Rank bring-up without a GPU: every rank joins a gloo group; rank 0 prints the world size
+    the JSON line would carry."""
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        torch.distributed.init_process_group("gloo")
+        t = torch.ones(1)
+        torch.distributed.all_reduce(t)
+        ranks = int(t.item())
+        torch.distributed.destroy_process_group()
+    else:
+        ranks = 1
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_joined": ranks, "gpus_flag": a.gpus}), flush=True)
 
 
 def scene_path(which):
@@ -95,7 +166,9 @@ def cpu_reference(scene_file, flags, width, height, target_s, log):
     """The reference itself (oracle/_ref/engine_seed_*: /root/reference's sources built with its own
     Makefile.rt flags + the determinism shim), timed on the host cores at a reduced resolution of the
     same scene and flags (Mrays/s is intensive: scale the resolution, not the spp).
-    Rays are counted by the instrumented build (engine_count_*) on the same config."""
+    Both thread modes SURVEY §8(d) asks for are timed, `-m 1` and `-m max` (all host threads), each
+    on a frame sized for ~target_s/2 of rendering; the faster is the baseline.  Rays are counted by
+    the instrumented build (engine_count_*) on the same config."""
     import subprocess
     import tempfile
     refdir = os.path.join(ROOT, "oracle", "_ref")
@@ -105,10 +178,11 @@ def cpu_reference(scene_file, flags, width, height, target_s, log):
         os.symlink(os.path.join(golden, "meshes"), os.path.join(wd, "meshes"))
         os.symlink(os.path.dirname(scene_file), os.path.join(wd, "scenes"))
         rel = os.path.join("scenes", os.path.basename(scene_file))
-        env = dict(os.environ, RTX_REF_SEED="1", OMP_NUM_THREADS=str(threads))
 
-        def run(binary, w, h):
-            cmd = [binary, rel, os.path.join(wd, "o.tif"), str(w), str(h), "-m", "max"] + flags
+        def run(binary, w, h, nthreads):
+            env = dict(os.environ, RTX_REF_SEED="1", OMP_NUM_THREADS=str(nthreads))
+            cmd = [binary, rel, os.path.join(wd, "o.tif"), str(w), str(h), "-m",
+                   "1" if nthreads == 1 else "max"] + flags
             t0 = time.perf_counter()
             p = subprocess.run(cmd, cwd=wd, env=env, capture_output=True, text=True, timeout=600)
             dt = time.perf_counter() - t0
@@ -132,26 +206,97 @@ def cpu_reference(scene_file, flags, width, height, target_s, log):
             cnt = os.path.join(refdir, f"engine_count_{arch}")
             if not (os.path.exists(eng) and os.path.exists(cnt)):
                 continue
+            modes = {}
             try:
-                # calibrate on a tiny frame, then size the frame for ~target_s of rendering
-                w, h = 16, 9
-                _, tr, _ = run(eng, w, h)
-                _, _, rays = run(cnt, w, h)
-                rate = rays / max(tr, 0.05)
-                scale = min(64.0, max(1.0, rate * target_s / rays) ** 0.5)
-                w, h = max(16, int(w * scale)), max(9, int(h * scale))
-                _, tr, _ = run(eng, w, h)
-                _, _, rays = run(cnt, w, h)
+                for nthreads in (1, threads):
+                    # calibrate on a tiny frame, then size the frame for ~target_s/2 of rendering
+                    w, h = 16, 9
+                    _, tr, _ = run(eng, w, h, nthreads)
+                    _, _, rays = run(cnt, w, h, nthreads)
+                    rate = rays / max(tr, 0.05)
+                    scale = min(64.0, max(1.0, rate * target_s / 2 / rays) ** 0.5)
+                    w, h = max(16, int(w * scale)), max(9, int(h * scale))
+                    _, tr, _ = run(eng, w, h, nthreads)
+                    _, _, rays = run(cnt, w, h, nthreads)
+                    log(f"cpu reference ({arch}, -m {'1' if nthreads == 1 else 'max'}): {w}x{h} "
+                        f"{' '.join(flags)}: {rays} rays in {tr:.2f}s on {nthreads} threads")
+                    modes[nthreads] = {"value": round(rays / tr / 1e6, 4), "cores": nthreads,
+                                       "seconds": round(tr, 2), "rays": rays, "frame": f"{w}x{h}"}
             except (RuntimeError, subprocess.TimeoutExpired, OSError) as e:
                 log(f"reference {arch} unusable here: {e}")
                 continue
-            log(f"cpu reference ({arch}): {w}x{h} {' '.join(flags)}: {rays} rays in {tr:.2f}s on {threads} threads")
-            return {"value": round(rays / tr / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "reference",
+            best = max(modes.values(), key=lambda m: m["value"])
+            return {"value": best["value"], "unit": "Mrays/s", "cores": best["cores"], "kind": "reference",
                     "sample": f"reference engine (Makefile.rt flags, -march={'native' if arch == 'native' else 'x86-64-v3'}"
-                              f", -m max) on the same scene and flags at {w}x{h}; render window = its own "
+                              f") on the same scene and flags at a reduced resolution, timed at -m 1 and -m max "
+                              f"({threads} host threads); the faster is the value; render window = its own "
                               f"'Commencing raytracing' -> 'Saving image' log stamps; rays from the instrumented "
-                              f"build on the same config", "seconds": round(tr, 2), "rays": rays}
+                              f"build on the same config",
+                    "seconds": best["seconds"], "rays": best["rays"],
+                    "m1": modes.get(1), "mmax": modes.get(threads)}
     return None
+
+
+def shadow_roofline(r, frame, params, d_rgb, d_z, stream, shadow_ms, a, world):
+    """Roofline of the dominant kernel, k_shadow (~97 % of device time).  Its counts come from a
+    counting instance of the same kernel over the same frame; its duration is the HIP-event time
+    of k_shadow in the timed steps (rocprofv3 agrees: profiles/).
+      bound:  VALU issue (the walk is divergent branchy scalar work; its BVH is L2/MALL-resident,
+              so HBM is far from saturated).  achieved = useful VALU wave-instructions (USEFUL_VALU
+              per box test / triangle / plane / light sample, / 64 lanes) per second; peak = the
+              chip's VALU issue rate.  issued = PMC SQ_INSTS_VALU of the same kernel build.
+      hbm:    algorithmic bytes = the records k_shadow reads from memory: 16 B per box test whose
+              record comes from the DQNode array (LDS top records excluded, reported apart), 48 B
+              per primitive test, 96 B per shade-point record + 4 B of its Morton index + 16 B
+              written per point; traffic = PMC 2*FETCH_SIZE + WRITE_SIZE (gfx950 correction)."""
+    from rtxpy import abi
+    import rtxpy
+    p2 = rtxpy.default_params(**{f: getattr(params, f) for f, _ in abi.Params._fields_})
+    p2.count_traversal = 1
+    r.render_device(frame, p2, d_rgb.data_ptr(), d_z.data_ptr(), stream.cuda_stream)
+    c = r.stats()
+    dur = shadow_ms * 1e-3
+    n_pts = int(c.shade_points)
+    prim_tests = int(c.shadow_tri_tests + c.shadow_sphere_tests)
+    glob = int(c.shadow_global_box_tests)
+    lds_box = int(c.shadow_box_tests) - glob
+    algo_bytes = 16 * glob + 48 * prim_tests + (96 + 4 + 16) * n_pts
+    useful = (USEFUL_VALU["box"] * c.shadow_box_tests + USEFUL_VALU["tri"] * c.shadow_tri_tests
+              + USEFUL_VALU["sphere"] * c.shadow_sphere_tests + USEFUL_VALU["plane"] * c.shadow_plane_tests
+              + USEFUL_VALU["sample"] * c.shadow_rays) / 64.0
+    achieved = useful / dur / 1e9
+    out = {"bound": "valu", "achieved": round(achieved, 1), "peak": VALU_PEAK_GINST, "unit": "Ginst/s",
+           "frac": round(achieved / VALU_PEAK_GINST, 4), "traffic": None, "kernel": "k_shadow",
+           "kernel_ms": round(shadow_ms, 3), "useful_valu_per_launch": int(useful),
+           "useful_valu_model": USEFUL_VALU, "shadow_rays": int(c.shadow_rays), "shade_points": n_pts,
+           "box_tests": int(c.shadow_box_tests), "box_tests_global": glob, "box_tests_lds": lds_box,
+           "tri_tests": int(c.shadow_tri_tests), "sphere_tests": int(c.shadow_sphere_tests),
+           "plane_tests": int(c.shadow_plane_tests), "wave_steps": int(c.shadow_wave_steps),
+           "wave_walks": int(c.shadow_wave_walks),
+           "hbm": {"algorithmic_bytes_per_launch": int(algo_bytes), "lds_bytes_per_launch": 16 * lds_box,
+                   "achieved": round(algo_bytes / dur / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                   "frac": round(algo_bytes / dur / 1e9 / HBM_PEAK_GBS, 4)}}
+    assert out["frac"] <= 1.0 and out["hbm"]["frac"] <= 1.0, out
+    pmc = os.path.join(ROOT, "profiles", "pmc_k_shadow.json")
+    key = f"{a.scene}_{a.width}x{a.height}_n{a.spp}_g{world}"
+    try:
+        with open(pmc) as fh:
+            rec = json.load(fh).get(key)
+    except (OSError, ValueError):
+        rec = None
+    if rec:
+        out["pmc"] = {"source": rec.get("source"), "kernel_src_sha": rec.get("kernel_src_sha"),
+                      "matches_this_kernel": rec.get("kernel_src_sha") == shadow_src_sha()}
+        if "hbm_bytes_per_launch" in rec:
+            out["traffic"] = int(rec["hbm_bytes_per_launch"])
+            out["hbm"]["traffic_GBs"] = round(rec["hbm_bytes_per_launch"] / dur / 1e9, 1)
+            out["hbm"]["traffic_frac"] = round(rec["hbm_bytes_per_launch"] / dur / 1e9 / HBM_PEAK_GBS, 4)
+        if "sq_insts_valu" in rec:
+            issued = rec["sq_insts_valu"] / dur / 1e9
+            out["issued"] = round(issued, 1)
+            out["issued_frac"] = round(issued / VALU_PEAK_GINST, 4)
+            out["useful_over_issued"] = round(useful / rec["sq_insts_valu"], 4)
+    return out
 
 
 POST_FLAGS = ["--dof", "3", "-13", "--mist", "6", "4", "lin", "0.5", "0.5", "0.6"]
@@ -211,6 +356,12 @@ def post_leg(r, d_rgb, d_z, w, h, dev, log, reps=5):
 
 def main():
     a = parse()
+    rc = launch_ranks(a)
+    if rc is not None:
+        sys.exit(rc)
+    if a.dry_run:
+        dry_run(a)
+        return
     import numpy as np
     import torch
     import rtxpy
@@ -294,42 +445,7 @@ def main():
     shadow_ms = float(np.mean(sms))
     roofline = None
     if not a.no_count:
-        # the dominant kernel is k_shadow (~99% of device time): its algorithmic bytes per launch
-        # (SURVEY §8(d) per-ray model, counted per shadow ray by a counting instance of the same
-        # kernel) over its own HIP-event duration in the timed steps
-        p2 = rtxpy.default_params(**{f: getattr(params, f) for f, _ in abi.Params._fields_})
-        p2.count_traversal = 1
-        r.render_device(frame, p2, d_rgb.data_ptr(), d_z.data_ptr(), stream.cuda_stream)
-        c = r.stats()
-        algo = (64 * c.shadow_node_visits + 48 * c.shadow_tri_tests + 32 * c.shadow_sphere_tests
-                + 16 * c.shadow_plane_tests + 48 * c.shadow_rays)
-        achieved = algo / (shadow_ms * 1e-3) / 1e9
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
-            try:
-                with open(pmc) as fh:
-                    tr = json.load(fh)
-                key = f"{a.scene}_{a.width}x{a.height}_n{a.spp}_g{world}"
-                if key in tr:
-                    traffic = tr[key]["hbm_bytes_per_launch"]
-            except (OSError, ValueError, KeyError):
-                traffic = None
-        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": "k_shadow",
-                    "algorithmic_bytes_per_launch": int(algo), "shadow_rays": int(c.shadow_rays),
-                    "node_visits": int(c.shadow_node_visits), "tri_tests": int(c.shadow_tri_tests),
-                    "sphere_tests": int(c.shadow_sphere_tests), "plane_tests": int(c.shadow_plane_tests),
-                    "packet_node_records": int(c.shadow_packet_nodes),
-                    "packet_prim_records": int(c.shadow_packet_prims),
-                    "ray_need_nodes": int(c.shadow_ray_nodes), "ray_need_prims": int(c.shadow_ray_prims),
-                    "kernel_ms": round(shadow_ms, 3),
-                    "note": "B_ray = 64*node_visits + 48*tri_tests + 32*sphere_tests + 16*plane_tests + 48 "
-                            "per shadow ray (SURVEY §8(d), the reference's 64-B node model), visits counted "
-                            "per ray in BVH2 units; frac > 1 because the walk reads 16-B quantised threaded "
-                            "nodes (the top 2048 from LDS) and the 33 MB BVH is L2/MALL-resident, so HBM is "
-                            "not the bound: the kernel is issue/latency-bound, see DESIGN.md §5; traffic = "
-                            "PMC L2->fabric bytes per launch (2*FETCH_SIZE + WRITE_SIZE, profiles/)"}
+        roofline = shadow_roofline(r, frame, params, d_rgb, d_z, stream, shadow_ms, a, world)
 
     build = None
     if rank == 0 and world == 1 and not a.no_post:

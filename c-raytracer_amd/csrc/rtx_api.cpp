@@ -19,6 +19,7 @@
 #include "rtx.h"
 #include "rtx_device.h"
 #include "rtx_kat.h"
+#include "rtx_quant.h"
 
 extern "C" size_t rtx_trace_lds_bytes(uint32_t stack_size);
 extern "C" size_t rtx_shadow_lds_bytes(uint32_t stack_size);
@@ -29,8 +30,8 @@ extern "C" hipError_t rtx_launch_trace(const DScene *S, const DFrame *F, const D
 				       uint32_t tile_end, unsigned long long *ctr, uint32_t waves, int count,
 				       hipStream_t stream);
 extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const float4 *sp, const uint32_t *perm,
-					uint32_t n_sp, uint32_t per_wave, uint32_t slot_b, uint32_t rays_per_lane,
-					float4 *contrib, unsigned long long *ctr, int count, hipStream_t stream);
+					uint32_t n_sp, uint32_t per_wave, uint32_t slot_b, float4 *contrib,
+					unsigned long long *ctr, int count, uint32_t cus, hipStream_t stream);
 extern "C" hipError_t rtx_launch_post(uint32_t w, uint32_t h, const rtx_post *pp, float *rgb, const float *z,
 				      int *rad, float4 *pv, unsigned *scratch, hipStream_t stream);
 extern "C" hipError_t rtx_spsort_temp_bytes(uint32_t n, size_t *bytes);
@@ -45,6 +46,7 @@ extern "C" hipError_t rtx_launch_accum(const DFrame *F, const DParams *P, const 
 				       hipStream_t stream);
 extern "C" hipError_t rtx_launch_kat(int kind, uint32_t n, const float *in, float *out, int u32mode,
 				     hipStream_t stream);
+extern "C" hipError_t rtx_launch_kat_shadow(int kind, uint32_t n, const float *in, float *out, hipStream_t stream);
 
 static thread_local char g_err[512] = "";
 
@@ -250,13 +252,8 @@ struct QFrame {
 	float qo[3], qs[3];
 };
 
-/* one plane pair quantised conservatively: lo down, hi up, one extra step each way */
-static uint32_t quantise(float lo, float hi, float qo, float qs)
-{
-	const double a = std::floor(((double)lo - qo) * (double)qs) - 1.0, b = std::ceil(((double)hi - qo) * (double)qs) + 1.0;
-	const uint32_t ql = (uint32_t)std::min(65535.0, std::max(0.0, a)), qh = (uint32_t)std::min(65535.0, std::max(0.0, b));
-	return ql | (qh << 16);
-}
+/* one plane pair quantised conservatively (rtx_quant.h) */
+static uint32_t quantise(float lo, float hi, float qo, float qs) { return rtx_quantise(lo, hi, qo, qs); }
 
 static void thread_emit(const std::vector<DNode> &recs, const std::vector<uint32_t> &size, const QFrame &F,
 			uint32_t ref, const float lo[3], const float hi[3], std::vector<DQNode> &out, uint32_t dep,
@@ -621,8 +618,6 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 	S.num_planes = (uint32_t)planes.size();
 	S.num_emitters = sc->num_emitters;
 	S.stack_size = std::max<uint32_t>(depth + 1, 4);
-	if (depth > 63) /* k_shadow keeps its packet stack in the 64 lanes of one VGPR */
-		return fail(RTX_ERR_SCENE, "BVH depth %u exceeds 63", depth);
 	c->total_lights = 0;
 	for (const DEmitter &e : emit)
 		c->total_lights += e.num_lights;
@@ -686,7 +681,8 @@ static int render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, f
 	const uint64_t avg_tile = 64ull * (1 + gi_n) * 5 / 4 + 64;
 	size_t free_b = 0, total_b = 0;
 	HIP_TRY(hipMemGetInfo(&free_b, &total_b));
-	const uint64_t budget = std::min<uint64_t>(24ull << 30, free_b / 3);
+	/* shade points of a chunk: up to a third of free HBM (96 GB cap; 288 GB per MI355X) */
+	const uint64_t budget = std::min<uint64_t>(96ull << 30, free_b / 3);
 	uint32_t chunk_tiles = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(P.ntiles, budget / (avg_tile * 112)));
 
 	auto grow = [](auto *&ptr, size_t &have, size_t need) -> hipError_t {
@@ -701,24 +697,19 @@ static int render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, f
 	};
 	HIP_TRY(grow(c->d_tasks, c->task_bytes, (size_t)waves * task_cap * sizeof(DTask)));
 
-	HIP_TRY(hipMemsetAsync(c->d_ctr, 0, sizeof(unsigned long long) * RTX_C_N, stream));
 	HIP_TRY(hipEventRecord(c->ev0, stream));
 	double t_trace = 0, t_sort = 0, t_shadow = 0, t_accum = 0;
 	uint64_t shade_points = 0;
 	uint32_t chunks = 0;
+	unsigned long long tot[RTX_C_N] = {}; /* counters of the chunks that completed */
 	/* shadow kernel: lane slots of slot_b = pow2ceil(lights) (<= 64) lanes per point; ~16 packets per wave */
 	uint32_t slot_b = 1;
 	while (slot_b < 64 && slot_b < c->total_lights)
 		slot_b <<= 1;
 	const uint32_t slots_per_point = (std::max<uint32_t>(c->total_lights, 1) + slot_b - 1) / slot_b;
 	const uint32_t per_wave = std::max<uint32_t>(1, std::min<uint32_t>(64, 1024 / (slot_b * slots_per_point)));
-	/* >= 64 lights: RTX_SH_R = R shadow rays per lane (one shared-origin walk per 64*R samples
-	 * of a point), R <= 5.  Off by default: on the bench frame R = 5 walks 2.4x fewer records
-	 * but drags each ray through 2x the nodes (k_shadow 2236 vs 1699 ms, gpurun_out r01z) */
-	uint32_t rays_per_lane = 1;
-	if (const char *e = getenv("RTX_SH_R"))
-		if (slot_b == 64)
-			rays_per_lane = std::max(1, std::min(5, atoi(e)));
+	const char *se = getenv("RTX_SPSORT");
+	const bool spsort = !(se && se[0] == '0');
 	for (uint32_t begin = 0; begin < P.ntiles;) {
 		const uint32_t end = std::min<uint32_t>(P.ntiles, begin + chunk_tiles);
 		const uint64_t sp_cap64 = std::min<uint64_t>((uint64_t)(end - begin) * avg_tile + staging_cap, 0xFFFFFFF0ull);
@@ -727,20 +718,22 @@ static int render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, f
 		HIP_TRY(grow(c->d_sp, c->sp_bytes, (size_t)sp_cap * 6 * sizeof(float4)));
 		HIP_TRY(grow(c->d_contrib, c->contrib_bytes, (size_t)sp_cap * sizeof(float4)));
 		HIP_TRY(grow(c->d_tile_rec, c->tile_rec_bytes, (size_t)(end - begin) * sizeof(uint2)));
-		HIP_TRY(hipMemsetAsync(c->d_ctr, 0, sizeof(unsigned long long) * RTX_C_CHUNK_N, stream));
+		HIP_TRY(hipMemsetAsync(c->d_ctr, 0, sizeof(unsigned long long) * RTX_C_N, stream));
 		HIP_TRY(hipEventRecord(c->ev[0], stream));
 		HIP_TRY(rtx_launch_trace(&c->scene, &F, &P, d_rgb, d_z, c->d_tasks, task_cap, c->d_staging,
 					 (uint32_t)staging_cap, c->d_sp, sp_cap, c->d_tile_rec, begin, end, c->d_ctr,
 					 std::min<uint32_t>(waves, end - begin), p->count_traversal, stream));
 		HIP_TRY(hipEventRecord(c->ev[1], stream));
-		unsigned long long head[RTX_C_CHUNK_N];
+		unsigned long long head[RTX_C_N];
 		HIP_TRY(hipMemcpyAsync(head, c->d_ctr, sizeof(head), hipMemcpyDeviceToHost, stream));
 		HIP_TRY(hipStreamSynchronize(stream));
+		if (head[RTX_C_TASKOVERFLOW])
+			return fail(RTX_ERR_STATE, "reflection/refraction task stack overflow (%u entries per wave)", task_cap);
 		if (head[RTX_C_OVERFLOW]) {
 			if (staging_cap >= (1ull << 26))
-				return fail(RTX_ERR_STATE, "secondary-ray storage overflow (task stack or %llu shade points per tile)",
+				return fail(RTX_ERR_STATE, "shade-point staging overflow (%llu shade points per tile)",
 					    (unsigned long long)staging_cap);
-			staging_cap *= 2; /* retry the chunk with room for larger ray trees */
+			staging_cap *= 2; /* retry the chunk (counters reset) with room for larger ray trees */
 			continue;
 		}
 		if (head[RTX_C_SPOVERFLOW]) {
@@ -754,8 +747,7 @@ static int render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, f
 		/* shade points in Morton order of their position (rtx_sort.hip); RTX_SPSORT=0 keeps
 		 * emission order (same image, bit for bit) */
 		const uint32_t *perm = nullptr;
-		const char *se = getenv("RTX_SPSORT");
-		if (n_sp > 1 && c->scene.root_ref != RTX_EMPTY_REF && !(se && se[0] == '0')) {
+		if (n_sp > 1 && c->scene.root_ref != RTX_EMPTY_REF && spsort) {
 			size_t tmp = 0;
 			HIP_TRY(rtx_spsort_temp_bytes(n_sp, &tmp));
 			HIP_TRY(grow(c->d_sortbuf, c->sortbuf_bytes, (size_t)n_sp * 4 * sizeof(uint32_t)));
@@ -765,12 +757,16 @@ static int render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, f
 						  b + 3 * (size_t)n_sp, c->d_sorttmp, c->sorttmp_bytes, &perm, stream));
 		}
 		HIP_TRY(hipEventRecord(c->ev[4], stream));
-		HIP_TRY(rtx_launch_shadow(&c->scene, &P, c->d_sp, perm, n_sp, per_wave, slot_b, rays_per_lane, c->d_contrib, c->d_ctr,
-					  p->count_traversal, stream));
+		HIP_TRY(rtx_launch_shadow(&c->scene, &P, c->d_sp, perm, n_sp, per_wave, slot_b, c->d_contrib, c->d_ctr,
+					  p->count_traversal, (uint32_t)c->cus, stream));
 		HIP_TRY(hipEventRecord(c->ev[2], stream));
 		HIP_TRY(rtx_launch_accum(&F, &P, c->d_tile_rec, c->d_contrib, begin, end - begin, d_rgb, stream));
 		HIP_TRY(hipEventRecord(c->ev[3], stream));
-		HIP_TRY(hipEventSynchronize(c->ev[3]));
+		unsigned long long ctr[RTX_C_N];
+		HIP_TRY(hipMemcpyAsync(ctr, c->d_ctr, sizeof(ctr), hipMemcpyDeviceToHost, stream));
+		HIP_TRY(hipStreamSynchronize(stream));
+		for (int k = RTX_C_CLOSEST; k < RTX_C_N; k++)
+			tot[k] += ctr[k];
 		float a = 0, b = 0, cc = 0, so = 0;
 		HIP_TRY(hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
 		HIP_TRY(hipEventElapsedTime(&so, c->ev[1], c->ev[4]));
@@ -784,23 +780,20 @@ static int render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, f
 		begin = end;
 	}
 	HIP_TRY(hipEventRecord(c->ev1, stream));
-	unsigned long long ctr[RTX_C_N];
-	HIP_TRY(hipMemcpyAsync(ctr, c->d_ctr, sizeof(ctr), hipMemcpyDeviceToHost, stream));
 	HIP_TRY(hipStreamSynchronize(stream));
-	float ms = 0.f;
-	HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+	const unsigned long long *ctr = tot;
 	rtx_stats &st = c->stats;
 	st.closest_rays = ctr[RTX_C_CLOSEST];
 	st.shadow_rays = ctr[RTX_C_SHADOW];
 	/* the threaded walk counts box tests; a node visit is a BVH2 inner node (two box tests) */
-	st.shadow_node_visits = RTX_SH_RAY ? ctr[RTX_C_SNODES] / 2 : ctr[RTX_C_SNODES];
+	st.shadow_node_visits = ctr[RTX_C_SBOXES] / 2;
 	st.shadow_tri_tests = ctr[RTX_C_STRIS];
 	st.shadow_sphere_tests = ctr[RTX_C_SSPHERES];
 	st.shadow_plane_tests = ctr[RTX_C_SPLANES];
-	st.shadow_packet_nodes = ctr[RTX_C_SSTEPS];
-	st.shadow_packet_prims = ctr[RTX_C_SPSTEPS];
-	st.shadow_ray_nodes = ctr[RTX_C_SRNODES];
-	st.shadow_ray_prims = ctr[RTX_C_SRTRIS];
+	st.shadow_box_tests = ctr[RTX_C_SBOXES];
+	st.shadow_global_box_tests = ctr[RTX_C_SGBOXES];
+	st.shadow_wave_steps = ctr[RTX_C_SSTEPS];
+	st.shadow_wave_walks = ctr[RTX_C_SWALKS];
 	st.node_visits = ctr[RTX_C_NODES] + st.shadow_node_visits;
 	st.tri_tests = ctr[RTX_C_TRIS] + ctr[RTX_C_STRIS];
 	st.sphere_tests = ctr[RTX_C_SPHERES] + ctr[RTX_C_SSPHERES];
@@ -813,7 +806,6 @@ static int render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, f
 	st.accum_ms = t_accum;
 	st.waves = waves;
 	st.chunks = chunks;
-	(void)ms;
 	return RTX_OK;
 }
 
@@ -955,7 +947,8 @@ extern "C" int rtx_kat(int kind, uint32_t n, const float *in, float *out, const 
 	int rc = RTX_OK;
 	hipError_t e = hipMemcpy(din, in, bi, hipMemcpyHostToDevice);
 	if (e == hipSuccess)
-		e = rtx_launch_kat(kind, n, din, dout, params ? params->u32conv : RTX_U32_SAT, nullptr);
+		e = kind >= RTX_KAT_FIRST_SHADOW ? rtx_launch_kat_shadow(kind, n, din, dout, nullptr)
+						 : rtx_launch_kat(kind, n, din, dout, params ? params->u32conv : RTX_U32_SAT, nullptr);
 	if (e == hipSuccess)
 		e = hipMemcpy(out, dout, bo, hipMemcpyDeviceToHost);
 	if (e != hipSuccess)

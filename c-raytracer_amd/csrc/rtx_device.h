@@ -96,9 +96,6 @@ typedef struct __attribute__((aligned(16))) DQNode {
 #ifndef RTX_SH_NW
 #define RTX_SH_NW 16 /* waves per k_shadow workgroup (they share the top copy) */
 #endif
-#ifndef RTX_SH_RAY
-#define RTX_SH_RAY 1 /* k_shadow walks rays one by one over DQNode (0: 64-ray packets, measurement) */
-#endif
 
 typedef struct DPlane {
 	float n[3];
@@ -181,29 +178,29 @@ typedef struct DTask {
 	uint32_t slot;
 } DTask;
 
-/* global counters written by the kernels */
+/* counters written by the kernels; all of them are reset at the start of every chunk and read
+ * back after it, so a chunk that is retried (staging overflow) never counts twice */
 enum {
-	RTX_C_TILE = 0,   /* k_trace work queue head (per chunk) */
-	RTX_C_SPCOUNT,    /* shade points emitted (per chunk) */
-	RTX_C_OVERFLOW,   /* task-stack / staging overflow (per chunk) */
-	RTX_C_SPOVERFLOW, /* chunk shade-point array overflow (per chunk) */
-	RTX_C_SPQUEUE,    /* k_shadow work queue head (per chunk) */
-	RTX_C_CLOSEST,
-	RTX_C_SHADOW,
-	RTX_C_NODES,      /* closest-hit traversal counts (count mode) */
+	RTX_C_TILE = 0,     /* k_trace work queue head */
+	RTX_C_SPCOUNT,      /* shade points emitted */
+	RTX_C_OVERFLOW,     /* per-tile shade-point staging overflow (host retries with more staging) */
+	RTX_C_TASKOVERFLOW, /* reflection/refraction task-stack overflow (host fails: bounded by design) */
+	RTX_C_SPOVERFLOW,   /* chunk shade-point array overflow (host retries with fewer tiles) */
+	RTX_C_SPQUEUE,      /* k_shadow work queue head */
+	RTX_C_CLOSEST,      /* cast_ray() calls */
+	RTX_C_SHADOW,       /* is_light_blocked() calls */
+	RTX_C_NODES,        /* closest-hit traversal counts (count mode) */
 	RTX_C_TRIS,
 	RTX_C_SPHERES,
 	RTX_C_PLANES,
-	RTX_C_SNODES,     /* shadow traversal counts (count mode) */
-	RTX_C_STRIS,
+	RTX_C_SBOXES,       /* shadow walk (count mode): box tests summed over rays */
+	RTX_C_SGBOXES,      /* ... of which read from the DQNode array (the rest from the LDS top) */
+	RTX_C_STRIS,        /* ... primitive tests */
 	RTX_C_SSPHERES,
 	RTX_C_SPLANES,
-	RTX_C_SSTEPS,     /* shadow walk: node records stepped through, per packet (count mode) */
-	RTX_C_SPSTEPS,    /* shadow walk: primitive records tested, per packet (count mode) */
-	RTX_C_SRNODES,    /* shadow walk: inner nodes whose box the ray itself hits (count mode) */
-	RTX_C_SRTRIS,     /* shadow walk: leaf primitives under boxes the ray itself hits (count mode) */
+	RTX_C_SSTEPS,       /* ... walk-loop iterations of the waves */
+	RTX_C_SWALKS,       /* ... wave walks (64 shadow rays each) */
 	RTX_C_N
 };
-#define RTX_C_CHUNK_N 5 /* counters reset per chunk */
 
 #endif

@@ -1,0 +1,716 @@
+/*
+ * k_shadow: direct lighting of every shade point (render.c:170-229) on gfx950.
+ *
+ * Shadow rays are 95.9-99.6 % of the reference's rays (is_light_blocked,
+ * render.c:126-134 -> object.c:183-197 + accel.c:360-387).  Each (shade point,
+ * light sample) pair is one lane: the lane samples its light point, tests the
+ * unbound planes, walks the BVH for any opaque blocker (multiplying the
+ * transmittance of transparent ones), then evaluates Phong / Blinn.
+ *
+ * The walk: every lane walks its own shadow ray over the threaded, quantised
+ * BVH (rtx_device.h DQNode), one 16-byte record per step and no stack (any-hit
+ * needs no visit order: a hit box continues at the next record, a missed one
+ * jumps to its skip link).  The top levels of the tree sit in LDS, copied once
+ * per persistent 16-wave workgroup (DScene.top).
+ *
+ * Scheduling: persistent workgroups; each wave takes `per_wave` shade points at
+ * a time from a global queue in Morton order of their position (rtx_sort.hip),
+ * so the resident waves share one compact region of the tree in L2.  A point's
+ * samples fill whole power-of-two lane slots and its sum runs inside one wave
+ * in lane order, so its result does not depend on which wave takes it.
+ */
+#include <hip/hip_runtime.h>
+#include <float.h>
+#include <stdlib.h>
+
+#include "rtx_kat.h"
+#include "rtx_quant.h"
+#include "rtx_wave.h"
+
+#ifndef RTX_DEBUG_NOWALK
+#define RTX_DEBUG_NOWALK 0 /* measurement only: skip the BVH walk (everything else in k_shadow stays) */
+#endif
+#ifndef RTX_SHADOW_OCC_DEFAULT
+#define RTX_SHADOW_OCC_DEFAULT 8 /* waves per SIMD the walk is register-capped for */
+#endif
+/* light_point (object.c:293-304) in k_shadow: a sphere light's inclination and azimuth are
+ * u * 2pi, so their sines and cosines come from the revolution-scaled v_sin_f32 / v_cos_f32
+ * instead of OCML's range-reduced sinf / cosf.  KAT: RTX_KAT_SPH_LIGHT_SH, <= 4e-6 of the
+ * radius.  RTX_SH_FASTTRIG=0 restores the exact light_point. */
+#ifndef RTX_SH_FASTTRIG
+#define RTX_SH_FASTTRIG 1
+#endif
+/* 1/x in light sampling and attenuation: v_rcp_f32 (1 ulp) instead of the IEEE division
+ * sequence (the closest-hit path keeps IEEE division).  RTX_SH_FASTDIV=0 restores it. */
+#ifndef RTX_SH_FASTDIV
+#define RTX_SH_FASTDIV 1
+#endif
+
+/* ------------------------------------------------------------------------ */
+/* loads                                                                    */
+/* ------------------------------------------------------------------------ */
+/* per-lane loads through the global address space (global_load, not flat_load: the pointers
+ * come from LDS and the compiler cannot prove where they point) */
+template <typename T> __device__ __forceinline__ const __attribute__((address_space(1))) T *gptr(const T *p)
+{
+	return (const __attribute__((address_space(1))) T *)p;
+}
+/* wave-uniform reads of read-only scene tables (s_load) */
+template <typename T> __device__ __forceinline__ const __attribute__((address_space(4))) T *cptr(const T *p)
+{
+	return (const __attribute__((address_space(4))) T *)p;
+}
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ldg4(const void *p, uint32_t off)
+{
+	const f4v v = *(const __attribute__((address_space(1))) f4v *)((const char *)p + off);
+	return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint4 ldg4u(const void *p)
+{
+	const u4v v = *(const __attribute__((address_space(1))) u4v *)p;
+	return make_uint4(v.x, v.y, v.z, v.w);
+}
+/* LDS reads through generic pointers that point into LDS */
+__device__ __forceinline__ uint4 lds4u(const void *p)
+{
+	const u4v v = *(const __attribute__((address_space(3))) u4v *)p;
+	return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint32_t lds1u(const uint32_t *p)
+{
+	return *(const __attribute__((address_space(3))) uint32_t *)p;
+}
+
+/* ------------------------------------------------------------------------ */
+/* intersection tests of the any-hit walk                                   */
+/* ------------------------------------------------------------------------ */
+/* The slab test (accel.c:112-158) against a DQNode box, in the quantisation frame: the ray is
+ * transformed once per walk (o' = (o - qo) * qs, inv' = inv / qs, oi = o' * inv'), so
+ * t = q * inv' - oi is the world ray parameter, with the 16-bit plane coordinates converted by
+ * one SDWA v_cvt_f32_u32 each.  OCT < 8: every live lane's direction lies in octant OCT (bit a
+ * set: inv[a] >= 0), so each axis' entry plane is known at compile time.  The boxes are
+ * widened by one quantisation step on both sides, far more than the transform's rounding, so
+ * the test is conservative (KAT: RTX_KAT_BOX_Q). */
+template <int OCT> __device__ __forceinline__ bool box_hit_q(uint4 n, f3 oi, f3 inv, float tlim)
+{
+	const float tx0 = fmaf((float)(n.x & 0xFFFFu), inv.x, -oi.x), tx1 = fmaf((float)(n.x >> 16), inv.x, -oi.x);
+	const float ty0 = fmaf((float)(n.y & 0xFFFFu), inv.y, -oi.y), ty1 = fmaf((float)(n.y >> 16), inv.y, -oi.y);
+	const float tz0 = fmaf((float)(n.z & 0xFFFFu), inv.z, -oi.z), tz1 = fmaf((float)(n.z >> 16), inv.z, -oi.z);
+	if (OCT == 8) {
+		const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.f));
+		const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlim));
+		return tn <= tf;
+	}
+	const float nx = (OCT & 1) ? tx0 : tx1, fx = (OCT & 1) ? tx1 : tx0;
+	const float ny = (OCT & 2) ? ty0 : ty1, fy = (OCT & 2) ? ty1 : ty0;
+	const float nz = (OCT & 4) ? tz0 : tz1, fz = (OCT & 4) ? tz1 : tz0;
+	const float tn = fmaxf(fmaxf(nx, ny), fmaxf(nz, 0.f));
+	/* min with the segment end in asm: tlim is loop-carried and the compiler would
+	 * canonicalise it before every fminf; no NaN reaches here */
+	float tf = fminf(fminf(fx, fy), fz);
+	asm("v_min_f32 %0, %0, %1" : "+v"(tf) : "v"(tlim));
+	return tn <= tf;
+}
+
+/* moller_trumbore (object.c:422-441) as a branch-free any-hit test on (eps, tlim), with the
+ * same accept set for finite inputs:
+ *   reject |a| < eps;  reject u < 0, v < 0, u + v > 1 (u > 1 is implied);  accept eps < t < tlim.
+ * Whenever t is finite, f = 1/a and u, v are finite too, so the three sign conditions fold into
+ * one max3 compare and the t window into one min compare (a NaN or infinite t fails it).
+ * Products are fused and 1/a comes from v_rcp_f32 (1 ulp): only hit/miss decisions at exact
+ * edges can differ from the IEEE test (KAT: RTX_KAT_ANY_TRI). */
+__device__ __forceinline__ f3 cross3_fma(f3 a, f3 b)
+{
+	return mk3(fmaf(a.y, b.z, -a.z * b.y), fmaf(a.z, b.x, -a.x * b.z), fmaf(a.x, b.y, -a.y * b.x));
+}
+__device__ __forceinline__ float dot3_fma(f3 a, f3 b) { return fmaf(a.x, b.x, fmaf(a.y, b.y, a.z * b.z)); }
+
+__device__ __forceinline__ bool any_tri(f3 v0, f3 e1, f3 e2, f3 o, f3 d, float eps, float tlim)
+{
+	const f3 h = cross3_fma(d, e2);
+	const float a = dot3_fma(e1, h);
+	const float f = __builtin_amdgcn_rcpf(a);
+	const f3 s = sub3(o, v0);
+	const float u = f * dot3_fma(s, h);
+	const f3 q = cross3_fma(s, e1);
+	const float v = f * dot3_fma(d, q);
+	const float t = f * dot3_fma(e2, q);
+	const float out = fmaxf(fmaxf(-u, -v), (u + v) - 1.f); /* > 0: outside the triangle */
+	return ((int)(fabsf(a) >= eps) & (int)(out <= 0.f) & (int)(fminf(t - eps, tlim - t) > 0.f)) != 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* one shadow ray per lane                                                  */
+/* ------------------------------------------------------------------------ */
+struct ShadowCount {
+	u64 boxes;     /* box tests (records stepped through), summed over lanes */
+	u64 gboxes;    /* ... of which from the DQNode array (not the LDS top) */
+	u64 tris, sph; /* primitive tests */
+	u64 pln;       /* plane tests */
+	u64 steps;     /* walk-loop iterations of the waves (a wave runs until its longest ray ends) */
+	u64 walks;     /* wave walks (64 rays each) */
+};
+
+/* one primitive record (a, b, c = its first 48 bytes) against this lane's shadow ray
+ * (accel.c:362-373): the target emitter skipped; transparent hit -> li *= kt; opaque hit ->
+ * true (blocked) */
+template <bool COUNT>
+__device__ __forceinline__ bool shadow_prim(float4 a, float4 b, float4 c, const DMaterial *__restrict__ mats, f3 o, f3 d,
+					    float tl, uint32_t emit_obj, f3 &li, uint32_t &ntri, uint32_t &nsph)
+{
+	const uint32_t meta = __float_as_uint(c.w), obj = __float_as_uint(b.w);
+	if (obj == emit_obj)
+		return false;
+	bool h;
+	if ((meta >> 24) == RTX_SPHERE) {
+		if (COUNT)
+			nsph++;
+		float t = 0.f;
+		h = hit_sphere(mk3(a.x, a.y, a.z), b.x, o, d, a.w, t) && t < tl;
+	} else {
+		if (COUNT)
+			ntri++;
+		h = any_tri(mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z), mk3(c.x, c.y, c.z), o, d, a.w, tl);
+	}
+	if (!h)
+		return false;
+	if (meta & RTX_META_TRANSPARENT) {
+		const auto *m = gptr(mats) + (meta & RTX_META_MAT);
+		li = mul3v(li, mk3(m->kt[0], m->kt[1], m->kt[2]));
+		return false;
+	}
+	return true;
+}
+
+/* the quantised threaded BVH and its frame (rtx_device.h DQNode) */
+struct QBvh {
+	const DQNode *q;
+	f3 qo, qs;
+	const uint4 *top;     /* the workgroup's LDS copy of the top records */
+	const uint32_t *tend; /* ... and of the cut records' range ends */
+	uint32_t nt;
+};
+
+/* is_light_blocked's BVH part (accel.c:360-387) for this lane's ray.  The walk starts in the
+ * workgroup's LDS copy of the tree's top levels: a cut record whose box is hit hands the lane
+ * to the DQNode array for the index range of its children's subtrees, and the lane returns to
+ * the top copy at the next top record when the range ends.  tl < 0 on entry: inactive lane.
+ * On an opaque hit tl becomes -1. */
+template <bool COUNT, int OCT>
+__device__ __forceinline__ void shadow_walk(const QBvh &Q, const char *__restrict__ recs, const DMaterial *__restrict__ mats,
+					    f3 o, f3 d, f3 inv, float &tl, uint32_t emit_obj, f3 &li, ShadowCount &sc)
+{
+	const f3 invq = mk3(inv.x / Q.qs.x, inv.y / Q.qs.y, inv.z / Q.qs.z);
+	const f3 oq = mk3((o.x - Q.qo.x) * Q.qs.x, (o.y - Q.qo.y) * Q.qs.y, (o.z - Q.qo.z) * Q.qs.z);
+	const f3 oi = mul3v(oq, invq);
+	const uint32_t nt = Q.nt;
+	uint32_t t = tl >= 0.f ? 0u : nt, g = 0, ge = 0;
+	uint32_t nbox = 0, nglob = 0, ntri = 0, nsph = 0, nstep = 0;
+	while (t < nt || g < ge) {
+		const bool ing = g < ge;
+		uint4 nd;
+		if (ing)
+			nd = ldg4u(Q.q + g);
+		else
+			nd = lds4u(Q.top + t);
+		if (COUNT) {
+			nbox++;
+			nglob += ing ? 1u : 0u;
+		}
+		const bool hit = box_hit_q<OCT>(nd, oi, invq, tl);
+		const uint32_t L = nd.w;
+		if (L & RTX_REF_LEAF) {
+			if (ing)
+				g++;
+			else
+				t++;
+			if (hit) {
+				const char *p = recs + (L & RTX_REF_OFF);
+				const uint32_t cnt = (L & RTX_REF_CNT) + 1;
+				for (uint32_t k = 0; k < cnt; k++) {
+					const char *pr = p + k * (uint32_t)sizeof(DPrim);
+					if (shadow_prim<COUNT>(ldg4(pr, 0), ldg4(pr, 16), ldg4(pr, 32), mats, o, d, tl, emit_obj, li,
+							       ntri, nsph)) {
+						tl = -1.f;
+						t = nt;
+						ge = 0;
+						break;
+					}
+				}
+			}
+		} else if (ing) {
+			g = hit ? g + 1 : L >> 6;
+		} else if (L & RTX_QTOP_CUT) {
+			if (hit) {
+				g = L >> 6;
+				ge = lds1u(Q.tend + t);
+			}
+			t++;
+		} else {
+			t = hit ? t + 1 : L >> 6;
+		}
+	}
+	if (COUNT) {
+		nstep = nbox;
+		uint32_t a = nbox, b = ntri, c = nsph, gq = nglob;
+#pragma unroll
+		for (int s = 32; s > 0; s >>= 1) {
+			a += __shfl_xor(a, s, WAVE);
+			b += __shfl_xor(b, s, WAVE);
+			c += __shfl_xor(c, s, WAVE);
+			gq += __shfl_xor(gq, s, WAVE);
+			nstep = max(nstep, (uint32_t)__shfl_xor(nstep, s, WAVE));
+		}
+		sc.boxes += uni(a);
+		sc.gboxes += uni(gq);
+		sc.tris += uni(b);
+		sc.sph += uni(c);
+		sc.steps += uni(nstep);
+		sc.walks++;
+	}
+}
+
+/* is_light_blocked (render.c:126-134): planes first (unbound_objects_is_light_blocked,
+ * object.c:183-197), then the BVH walk, specialised on the direction octant when every live
+ * lane shares it.  Returns the lane's blocked flag; li carries the transmittance product. */
+template <bool COUNT>
+__device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restrict__ recs, const DMaterial *__restrict__ mats,
+					     const DPlane *__restrict__ planes, uint32_t num_planes, bool have_tree, bool act,
+					     f3 o, f3 d, float dist, uint32_t emit_obj, f3 &li, ShadowCount &sc)
+{
+	float tl = act ? dist : -1.f;
+	for (uint32_t i = 0; i < num_planes; i++) { /* plane records are wave-uniform: s_load */
+		const auto *pl = cptr(planes) + i;
+		const auto *m = cptr(mats) + pl->mat;
+		float t;
+		const bool h = hit_plane(mk3(pl->n[0], pl->n[1], pl->n[2]), pl->d, o, d, pl->eps, t) && t < dist && tl >= 0.f;
+		if (m->flags & RTX_MF_TRANSPARENT) {
+			if (h)
+				li = mul3v(li, mk3(m->kt[0], m->kt[1], m->kt[2]));
+		} else if (h) {
+			tl = -1.f;
+		}
+	}
+	if (COUNT)
+		sc.pln += (u64)popc64(ballot(act)) * num_planes;
+	const bool alive = tl >= 0.f;
+	const u64 live = ballot(alive);
+	if (!live || !have_tree)
+		return act && !alive;
+	const f3 inv = safe_inv_fast(d); /* boxes are padded 2e-6 relative: a 1-ulp 1/d keeps the test conservative */
+	const uint32_t oct = ((~__float_as_uint(inv.x)) >> 31) | (((~__float_as_uint(inv.y)) >> 31) << 1) |
+			     (((~__float_as_uint(inv.z)) >> 31) << 2);
+	const uint32_t lead = readlane(oct, (uint32_t)__ffsll((long long)live) - 1);
+	const uint32_t sel = ballot(alive & (oct != lead)) ? 8u : lead;
+	switch (sel) {
+#define RTX_WALK(K)                                                                  \
+	case K:                                                                      \
+		shadow_walk<COUNT, K>(Q, recs, mats, o, d, inv, tl, emit_obj, li, sc); \
+		break;
+		RTX_WALK(0) RTX_WALK(1) RTX_WALK(2) RTX_WALK(3) RTX_WALK(4) RTX_WALK(5) RTX_WALK(6) RTX_WALK(7)
+#undef RTX_WALK
+	default:
+		shadow_walk<COUNT, 8>(Q, recs, mats, o, d, inv, tl, emit_obj, li, sc);
+		break;
+	}
+	return act && tl < 0.f;
+}
+
+/* ------------------------------------------------------------------------ */
+/* light sampling and shading                                               */
+/* ------------------------------------------------------------------------ */
+/* k_shadow arguments.  Lane 0 copies them to LDS; the loops re-read them from there behind a
+ * compiler memory barrier, so none stays live in registers across the walk. */
+struct KShadow {
+	const DPrim *prims;   /* primitive records (DQNode leaf refs are byte offsets from `recs`) */
+	const char *recs;     /* base of the record array the leaf refs point into */
+	const DQNode *qnodes; /* threaded quantised BVH */
+	float qo[3], qs[3];
+	const uint32_t *top; /* its top levels (rtx_device.h RTX_QTOP_CUT), copied to LDS per workgroup */
+	uint32_t ntop;
+	const DMaterial *mats;
+	const DPlane *planes;
+	const DEmitter *emitters;
+	const float4 *sp;
+	const uint32_t *perm; /* shade points in processing (Morton) order, or null */
+	float4 *contrib;
+	unsigned long long *ctr;
+	uint32_t have_tree, num_planes, num_emitters;
+	uint32_t n_sp, per_wave, slot_b, slot_lg;
+	int32_t rng, attenuation, reflection;
+	float att_offset;
+};
+
+__device__ __forceinline__ void reread_barrier() { asm volatile("" ::: "memory"); }
+
+/* a pointer read from LDS, made wave-uniform (SGPRs) so accesses through it stay scalar */
+template <typename T> __device__ __forceinline__ T *unip(T *p)
+{
+	const uint64_t v = (uint64_t)p;
+	return (T *)(((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v));
+}
+
+__device__ __forceinline__ float sh_rcp(float x) { return RTX_SH_FASTDIV ? __builtin_amdgcn_rcpf(x) : 1.f / x; }
+
+/* light_point (object.c:293-304, 403-419) as k_shadow evaluates it (RTX_SH_FASTTRIG) */
+__device__ __forceinline__ f3 light_point_sh(const DEmitter &e, f3 p, float u1, float u2)
+{
+	if (RTX_SH_FASTTRIG && e.type == RTX_SPHERE) {
+		const f3 c = ld3(e.p0);
+		const f3 nrm = sub3(c, p);
+		const float si = __builtin_amdgcn_sinf(u1), ci = __builtin_amdgcn_cosf(u1);
+		const float sa = __builtin_amdgcn_sinf(u2), ca = __builtin_amdgcn_cosf(u2);
+		f3 ld = mk3(e.radius * ca * si, e.radius * sa * si, e.radius * ci);
+		if (dot3(nrm, ld) != 0.f)
+			ld = mul3s(ld, -1.f);
+		return add3(c, ld);
+	}
+	return light_point(e, p, u1, u2);
+}
+
+/* direct-lighting terms of one unblocked light sample (render.c:199-228), read after the walk */
+__device__ __forceinline__ f3 shade_light(const KShadow &ks, const float4 *rec, f3 ldir, f3 li, float ldist, float dsq)
+{
+	const float4 q1 = rec[1], q2 = rec[2], q3 = rec[3];
+	const f3 n = mk3(q1.x, q1.y, q1.z), dir = mk3(q2.x, q2.y, q2.z);
+	const float a = dot3(ldir, n);
+	const int32_t att = (int32_t)uni((uint32_t)ks.attenuation);
+	if (att == RTX_ATT_LIN)
+		li = mul3s(li, sh_rcp(ks.att_offset + ldist));
+	else if (att == RTX_ATT_SQR)
+		li = mul3s(li, sh_rcp(ks.att_offset + dsq));
+	const DMaterial &m = unip(ks.mats)[__float_as_uint(q3.w)];
+	const f3 diff = mul3s(mul3v(mk3(q3.x, q3.y, q3.z), li), fmaxf(0.f, a));
+	float sm;
+	if ((int32_t)uni((uint32_t)ks.reflection) == RTX_BLINN)
+		sm = -dot3(n, norm3(add3(mul3s(ldir, -1.f), dir)));
+	else
+		sm = -dot3(sub3(mul3s(n, 2.f * a), ldir), dir);
+	const f3 spec = mul3s(mul3v(ld3(m.ks), li), fmaxf(0.f, powf(sm, m.shininess)));
+	return add3(diff, spec);
+}
+
+/* one light sample per lane of the shade point `rec` (render.c:170-229): the light point of
+ * sample idx (emitters in scene order, the hit object skipped), its shadow ray, attenuation
+ * and Phong / Blinn.  Argument-block fields are read from LDS behind reread barriers. */
+template <bool COUNT>
+__device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec, uint32_t idx, bool act, ShadowCount &sc,
+					   const uint4 *top_q, const uint32_t *top_e)
+{
+	reread_barrier();
+	const float4 q0 = rec[0], q4 = rec[4];
+	const f3 p = mk3(q0.x, q0.y, q0.z);
+	const uint32_t obj = __float_as_uint(q4.x);
+	const DEmitter *emitters = unip(ks.emitters);
+	const uint32_t num_emitters = uni(ks.num_emitters);
+	uint32_t j = idx;
+	uint32_t e = 0;
+	for (; e < num_emitters; e++) {
+		const uint32_t eo = emitters[e].obj, enl = emitters[e].num_lights;
+		if (eo == obj)
+			continue;
+		if (j < enl)
+			break;
+		j -= enl;
+	}
+	if (e >= num_emitters)
+		e = 0;
+	const DEmitter &E = emitters[e];
+	float u1 = 0.5f, u2 = 0.5f;
+	if (uni(ks.rng) != RTX_RNG_CONST) /* the key already carries the seed (rtx_key_pixel) */
+		rtx_draw2(key_of(__float_as_uint(q4.y), __float_as_uint(q4.z)), e, j, &u1, &u2);
+	const f3 lp = light_point_sh(E, p, u1, u2);
+	const f3 dv = sub3(lp, p);
+	const float ldist = mag3(dv);
+	const float dsq = magsqr3(dv);
+	const f3 ldir = mul3s(dv, sh_rcp(ldist));
+	f3 li = ld3(E.li);
+	QBvh Q;
+	Q.q = unip(ks.qnodes);
+	Q.qo = mk3(ks.qo[0], ks.qo[1], ks.qo[2]);
+	Q.qs = mk3(ks.qs[0], ks.qs[1], ks.qs[2]);
+	Q.top = top_q;
+	Q.tend = top_e;
+	Q.nt = uni(ks.ntop);
+	const bool have_tree = uni(ks.have_tree) != 0 && !RTX_DEBUG_NOWALK;
+	const bool blocked = shadow_query<COUNT>(Q, unip(ks.recs), unip(ks.mats), unip(ks.planes), uni(ks.num_planes),
+						 have_tree, act, p, ldir, ldist, E.obj, li, sc);
+	reread_barrier();
+	f3 contribution = mk3(0.f, 0.f, 0.f);
+	if (act && !blocked)
+		contribution = shade_light(ks, rec, ldir, li, ldist, dsq);
+	return contribution;
+}
+
+/* ------------------------------------------------------------------------ */
+/* the kernel                                                               */
+/* ------------------------------------------------------------------------ */
+/* Persistent workgroups of RTX_SH_NW waves.  A workgroup copies the threaded BVH's top levels
+ * to LDS once; then each wave takes per_wave shade points at a time from a global queue
+ * (RTX_C_SPQUEUE), in processing (Morton) order, until the points run out. */
+template <bool COUNT, int OCC>
+__global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
+{
+	__shared__ uint4 top_q[RTX_TOP_MAX];            /* the top records (rtx_device.h RTX_QTOP_CUT) */
+	__shared__ uint32_t top_e[RTX_TOP_MAX];         /* cut records: the DQNode index after the subtree */
+	__shared__ KShadow ks_w[RTX_SH_NW];
+	__shared__ uint32_t off_w[RTX_SH_NW][WAVE + 1]; /* first lane slot of each shade point, total */
+	__shared__ uint32_t nls_w[RTX_SH_NW][WAVE];     /* shadow rays of each shade point */
+	__shared__ uint32_t sid_w[RTX_SH_NW][WAVE];     /* each shade point's index in the record array */
+	__shared__ float Ls_w[RTX_SH_NW][3][WAVE];      /* per shade point light sum, in packet order */
+	const uint32_t ntop = ka.ntop;
+	for (uint32_t i = threadIdx.x; i < ntop; i += WAVE * RTX_SH_NW) {
+		top_q[i] = ldg4u(ka.top + 4 * i);
+		top_e[i] = gptr(ka.top)[4 * ntop + i];
+	}
+	const uint32_t wv = uni(threadIdx.x / WAVE);
+	if (lane_id() == 0)
+		ks_w[wv] = ka;
+	__syncthreads();
+	KShadow &ks = ks_w[wv];
+	uint32_t *off = off_w[wv], *nls = nls_w[wv], *sid = sid_w[wv];
+	float(*Ls)[WAVE] = Ls_w[wv];
+	ShadowCount sc = { 0, 0, 0, 0, 0, 0, 0 };
+	u64 rays_total = 0;
+	for (;;) {
+		reread_barrier();
+		uint32_t j0 = 0;
+		if (lane_id() == 0)
+			j0 = (uint32_t)atomicAdd(unip(ks.ctr) + RTX_C_SPQUEUE, (unsigned long long)uni(ks.per_wave));
+		j0 = readlane(j0, 0);
+		const uint32_t n_sp = uni(ks.n_sp);
+		if (j0 >= n_sp)
+			break;
+		const uint32_t cnt = min(uni(ks.per_wave), n_sp - j0);
+		const bool own = lane_id() < cnt;
+		const uint32_t *perm = unip(ks.perm);
+		const uint32_t my_sid = own ? (perm ? perm[j0 + lane_id()] : j0 + lane_id()) : 0u;
+		const uint32_t nl_mine = own ? __float_as_uint(unip(ks.sp)[(size_t)my_sid * SPREC + 4].w) : 0u;
+		/* each point's samples occupy whole lane slots of B lanes (B = power of two), so a point's
+		 * packet partial sums never depend on which other points share its wave: deterministic */
+		uint32_t total;
+		const uint32_t ex = wave_excl_scan((nl_mine + uni(ks.slot_b) - 1) >> uni(ks.slot_lg), &total);
+		off[lane_id()] = ex;
+		nls[lane_id()] = nl_mine;
+		sid[lane_id()] = my_sid;
+		Ls[0][lane_id()] = 0.f;
+		Ls[1][lane_id()] = 0.f;
+		Ls[2][lane_id()] = 0.f;
+		if (lane_id() == 0)
+			off[WAVE] = total;
+		lds_sync();
+		if (uni(ks.slot_b) == WAVE) {
+			/* >= 64 lights: every packet is 64 samples of ONE shade point.  The point is wave-uniform
+			 * (its record is read once per packet through one address, no owner search), each lane
+			 * sums its samples over the point's packets, and one butterfly per point reduces them. */
+			for (uint32_t k = 0; k < cnt; k++) {
+				reread_barrier();
+				const uint32_t nl = uni(nls[k]);
+				const float4 *rec = unip(ks.sp) + (size_t)uni(sid[k]) * SPREC;
+				f3 acc = mk3(0.f, 0.f, 0.f);
+				for (uint32_t base = 0; base < nl; base += WAVE) {
+					const uint32_t idx = base + lane_id();
+					acc = add3(acc, light_sample<COUNT>(ks, rec, idx, idx < nl, sc, top_q, top_e));
+				}
+				const float sx = wave_sum(acc.x), sy = wave_sum(acc.y), sz = wave_sum(acc.z);
+				if (lane_id() == 0) {
+					Ls[0][k] = sx;
+					Ls[1][k] = sy;
+					Ls[2][k] = sz;
+				}
+			}
+			lds_sync();
+		} else {
+			/* fewer lights: several points share a packet, each in its own power-of-two lane slot */
+			for (uint32_t base = 0;;) {
+				reread_barrier();
+				const uint32_t tot = uni(off[WAVE]), slot_b = uni(ks.slot_b), slot_lg = uni(ks.slot_lg);
+				if (base >= tot)
+					break;
+				const uint32_t slot = base + (lane_id() >> slot_lg);
+				const uint32_t k = slot < tot ? owner_of(off, slot) : 0u;
+				const uint32_t idx = ((slot - off[k]) << slot_lg) + (lane_id() & (slot_b - 1));
+				const bool act = slot < tot && idx < nls[k];
+				const float4 *rec = unip(ks.sp) + (size_t)sid[k] * SPREC;
+				const f3 contribution = light_sample<COUNT>(ks, rec, idx, act, sc, top_q, top_e);
+				/* per-shade-point sums; lanes are ordered by k */
+				const uint32_t t2 = uni(off[WAVE]), sb = uni(ks.slot_b), spp = WAVE / sb;
+				const uint32_t last_slot_lane = (min(t2 - base, spp) - 1) * sb;
+				const uint32_t k0 = readlane(k, 0), k1 = readlane(k, last_slot_lane);
+				for (uint32_t kk = k0; kk <= k1; kk++) {
+					const bool in = act && k == kk;
+					if (!ballot(in))
+						continue;
+					const float sx = wave_sum(in ? contribution.x : 0.f);
+					const float sy = wave_sum(in ? contribution.y : 0.f);
+					const float sz = wave_sum(in ? contribution.z : 0.f);
+					if (lane_id() == 0) {
+						Ls[0][kk] += sx;
+						Ls[1][kk] += sy;
+						Ls[2][kk] += sz;
+					}
+				}
+				lds_sync();
+				base += spp;
+			}
+		}
+		reread_barrier();
+		if (own) {
+			const float4 *my = unip(ks.sp) + (size_t)my_sid * SPREC;
+			const float4 q0 = my[0], q1 = my[1], q2 = my[2], q5 = my[5];
+			const f3 w = mk3(q0.w, q1.w, q2.w);
+			const f3 c = mul3v(w, mk3(Ls[0][lane_id()], Ls[1][lane_id()], Ls[2][lane_id()]));
+			unip(ks.contrib)[my_sid] = make_float4(c.x, c.y, c.z, q5.x);
+		}
+		uint32_t n_rays = own ? nls[lane_id()] : 0u;
+#pragma unroll
+		for (int o = 32; o > 0; o >>= 1)
+			n_rays += __shfl_xor(n_rays, o, WAVE);
+		rays_total += uni(n_rays);
+	}
+	if (lane_id() == 0) {
+		unsigned long long *ctr = unip(ks.ctr);
+		atomicAdd(&ctr[RTX_C_SHADOW], rays_total);
+		if (COUNT) {
+			atomicAdd(&ctr[RTX_C_SBOXES], sc.boxes);
+			atomicAdd(&ctr[RTX_C_SGBOXES], sc.gboxes);
+			atomicAdd(&ctr[RTX_C_STRIS], sc.tris);
+			atomicAdd(&ctr[RTX_C_SSPHERES], sc.sph);
+			atomicAdd(&ctr[RTX_C_SPLANES], sc.pln);
+			atomicAdd(&ctr[RTX_C_SSTEPS], sc.steps);
+			atomicAdd(&ctr[RTX_C_SWALKS], sc.walks);
+		}
+	}
+}
+
+/* ------------------------------------------------------------------------ */
+/* known answers of the fast device functions k_shadow runs (rtx_kat.h)     */
+/* ------------------------------------------------------------------------ */
+__global__ void k_kat_shadow(int kind, uint32_t n, const float *__restrict__ in, float *__restrict__ out)
+{
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n)
+		return;
+	const float *x = in + (size_t)i * rtx_kat_in_width[kind];
+	float *y = out + (size_t)i * rtx_kat_out_width[kind];
+	switch (kind) {
+	case RTX_KAT_ANY_TRI:
+		y[0] = any_tri(ld3(x + 6), ld3(x + 9), ld3(x + 12), ld3(x), ld3(x + 3), x[15], x[16]) ? 1.f : 0.f;
+		break;
+	case RTX_KAT_SPH_LIGHT_SH: {
+		DEmitter e;
+		e.type = RTX_SPHERE;
+		for (int k = 0; k < 3; k++)
+			e.p0[k] = x[k];
+		e.radius = x[3];
+		const f3 l = light_point_sh(e, ld3(x + 4), x[7], x[8]);
+		y[0] = l.x;
+		y[1] = l.y;
+		y[2] = l.z;
+	} break;
+	case RTX_KAT_BOX_Q: {
+		/* the walk's setup (shadow_query / shadow_walk) and its box test on the quantised box */
+		const f3 o = ld3(x), d = ld3(x + 3), qo = ld3(x + 12), qs = ld3(x + 15);
+		const uint4 nd = make_uint4(rtx_quantise(x[6], x[9], qo.x, qs.x), rtx_quantise(x[7], x[10], qo.y, qs.y),
+					    rtx_quantise(x[8], x[11], qo.z, qs.z), 0u);
+		const f3 inv = safe_inv_fast(d);
+		const f3 invq = mk3(inv.x / qs.x, inv.y / qs.y, inv.z / qs.z);
+		const f3 oq = mk3((o.x - qo.x) * qs.x, (o.y - qo.y) * qs.y, (o.z - qo.z) * qs.z);
+		const f3 oi = mul3v(oq, invq);
+		const uint32_t oct = ((~__float_as_uint(inv.x)) >> 31) | (((~__float_as_uint(inv.y)) >> 31) << 1) |
+				     (((~__float_as_uint(inv.z)) >> 31) << 2);
+		bool ho = false;
+		switch (oct) {
+#define RTX_KATOCT(K)                                      \
+	case K:                                                \
+		ho = box_hit_q<K>(nd, oi, invq, x[18]);            \
+		break;
+			RTX_KATOCT(0) RTX_KATOCT(1) RTX_KATOCT(2) RTX_KATOCT(3) RTX_KATOCT(4) RTX_KATOCT(5) RTX_KATOCT(6)
+			RTX_KATOCT(7)
+#undef RTX_KATOCT
+		}
+		y[0] = box_hit_q<8>(nd, oi, invq, x[18]) ? 1.f : 0.f;
+		y[1] = ho ? 1.f : 0.f;
+	} break;
+	}
+}
+
+extern "C" hipError_t rtx_launch_kat_shadow(int kind, uint32_t n, const float *in, float *out, hipStream_t stream)
+{
+	if (kind < RTX_KAT_FIRST_SHADOW || kind >= RTX_KAT_NKINDS)
+		return hipErrorInvalidValue;
+	hipLaunchKernelGGL(k_kat_shadow, dim3((n + 255) / 256), dim3(256), 0, stream, kind, n, in, out);
+	return hipGetLastError();
+}
+
+/* ------------------------------------------------------------------------ */
+/* launcher (called from rtx_api.cpp)                                       */
+/* ------------------------------------------------------------------------ */
+/* the persistent grid: as many workgroups as are resident on the device at once (no more than
+ * the work needs); the waves then share the shade points through RTX_C_SPQUEUE */
+template <bool C, int O> static hipError_t launch_shadow(const KShadow &ka, uint32_t nw, uint32_t cus, hipStream_t stream)
+{
+	int per_cu = 0;
+	hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(&k_shadow<C, O>),
+								   WAVE * RTX_SH_NW, 0);
+	if (e != hipSuccess)
+		return e;
+	const uint32_t slots = per_cu > 0 && cus > 0 ? (uint32_t)per_cu * cus : 1024u;
+	const uint32_t need = (nw + RTX_SH_NW - 1) / RTX_SH_NW;
+	hipLaunchKernelGGL((k_shadow<C, O>), dim3(need < slots ? need : slots), dim3(WAVE * RTX_SH_NW), 0, stream, ka);
+	return hipGetLastError();
+}
+
+extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const float4 *sp, const uint32_t *perm,
+					uint32_t n_sp, uint32_t per_wave, uint32_t slot_b, float4 *contrib,
+					unsigned long long *ctr, int count, uint32_t cus, hipStream_t stream)
+{
+	const uint32_t nw = per_wave ? (n_sp + per_wave - 1) / per_wave : 0u;
+	if (!slot_b || (slot_b & (slot_b - 1)) || slot_b > WAVE || !per_wave || per_wave > WAVE)
+		return hipErrorInvalidValue;
+	if (!nw)
+		return hipSuccess;
+	if (S->num_top > RTX_TOP_MAX)
+		return hipErrorInvalidValue;
+	KShadow ka;
+	ka.prims = S->prims;
+	ka.recs = (const char *)S->nodes;
+	ka.qnodes = S->qnodes;
+	ka.top = S->top;
+	ka.ntop = S->num_top;
+	for (int a = 0; a < 3; a++) {
+		ka.qo[a] = S->qo[a];
+		ka.qs[a] = S->qs[a];
+	}
+	ka.mats = S->mats;
+	ka.planes = S->planes;
+	ka.emitters = S->emitters;
+	ka.sp = sp;
+	ka.perm = perm;
+	ka.contrib = contrib;
+	ka.ctr = ctr;
+	ka.have_tree = S->root_ref != RTX_EMPTY_REF && S->qnodes;
+	ka.num_planes = S->num_planes;
+	ka.num_emitters = S->num_emitters;
+	ka.n_sp = n_sp;
+	ka.per_wave = per_wave;
+	ka.slot_b = slot_b;
+	ka.slot_lg = (uint32_t)__builtin_ctz(slot_b);
+	ka.rng = P->rng;
+	ka.attenuation = P->attenuation;
+	ka.reflection = P->reflection;
+	ka.att_offset = P->att_offset;
+	if (count)
+		return launch_shadow<true, 1>(ka, nw, cus, stream);
+	/* occupancy variant (measurement): RTX_SHADOW_OCC = 1 (compiler's choice), 6, 7 or 8 waves/SIMD */
+	const char *env = getenv("RTX_SHADOW_OCC");
+	const int occ = env ? atoi(env) : RTX_SHADOW_OCC_DEFAULT;
+	switch (occ) {
+	case 8: return launch_shadow<false, 8>(ka, nw, cus, stream);
+	case 7: return launch_shadow<false, 7>(ka, nw, cus, stream);
+	case 6: return launch_shadow<false, 6>(ka, nw, cus, stream);
+	default: return launch_shadow<false, 1>(ka, nw, cus, stream);
+	}
+}

@@ -1,0 +1,773 @@
+/*
+ * MI355X (gfx950) closest-hit kernels for C-Raytracer's trace/shade path.
+ *
+ * The reference's cast_ray() recursion (render.c:136-343) runs per chunk of 8x8
+ * pixel tiles as k_trace -> [shade-point sort] -> k_shadow (rtx_shadow.hip) -> k_accum:
+ *
+ *  k_trace  (persistent, one wave per workgroup; tiles from a device queue) every
+ *           closest-hit query of the tile's ray trees: primaries, then
+ *           reflection/refraction children from a per-wave LIFO task stack in HBM
+ *           (__ballot/mbcnt compaction on push), and the path-GI samples of each
+ *           batch flattened over (hit, sample) 64 at a time.  Per-lane BVH2
+ *           traversal with the stack in LDS ([entry][lane], conflict-free).  Local
+ *           terms (ke, ambient) go straight to the tile's pixels; every hit that
+ *           sees lights becomes a 96-byte shade point (rtx_wave.h), appended in a
+ *           fixed order to a per-wave staging region and moved to the chunk's
+ *           contiguous array at tile end.
+ *  k_accum  (one wave per tile) adds the shade points' light terms, computed by
+ *           k_shadow, to their pixels in emission order.
+ *  k_kat    per-function known answers of the device intersectors/samplers.
+ *
+ * No float atomics anywhere: a pixel's value is bit-identical whichever wave,
+ * GPU or tile order renders it.
+ */
+#include <hip/hip_runtime.h>
+#include <float.h>
+#include <stdlib.h>
+
+#include "rtx_kat.h"
+#include "rtx_wave.h"
+
+/* ------------------------------------------------------------------------ */
+/* closest hit: inside-object shortcut, planes, then BVH (render.c:118-147)  */
+/* per-lane traversal, stack in LDS laid out [entry][lane]                  */
+/* ------------------------------------------------------------------------ */
+struct TraceCount {
+	uint32_t nodes, tris, sph, pln;
+};
+
+template <bool COUNT>
+__device__ void trace_closest(const DScene &S, uint32_t *stk, bool act, f3 o, f3 d, uint32_t inside, float &t_out,
+			      uint32_t &hid_out, TraceCount &tc)
+{
+	float tbest = FLT_MAX;
+	uint32_t hid = RTX_NONE;
+	if (act && isnan3(d)) /* TIR / degenerate directions hit nothing */
+		act = false;
+	if (act && inside != RTX_NONE) {
+		float t;
+		bool h;
+		if (inside & RTX_PLANE_BIT) {
+			const DPlane &pl = S.planes[inside & ~RTX_PLANE_BIT];
+			h = hit_plane(ld3(pl.n), pl.d, o, d, pl.eps, t);
+		} else {
+			const DPrim &pr = S.prims[inside];
+			if ((__float_as_uint(pr.c[3]) >> 24) == RTX_SPHERE)
+				h = hit_sphere(mk3(pr.a[0], pr.a[1], pr.a[2]), pr.b[0], o, d, pr.a[3], t);
+			else
+				h = hit_triangle(mk3(pr.a[0], pr.a[1], pr.a[2]), mk3(pr.b[0], pr.b[1], pr.b[2]),
+						 mk3(pr.c[0], pr.c[1], pr.c[2]), o, d, pr.a[3], t);
+		}
+		if (h) {
+			tbest = t;
+			hid = inside;
+			act = false;
+		}
+	}
+	if (act) {
+		for (uint32_t i = 0; i < S.num_planes; i++) {
+			const DPlane &pl = S.planes[i];
+			float t;
+			if (COUNT)
+				tc.pln++;
+			if (hit_plane(ld3(pl.n), pl.d, o, d, pl.eps, t) && t < tbest) {
+				tbest = t;
+				hid = RTX_PLANE_BIT | i;
+			}
+		}
+	}
+	if (act && S.root_ref != RTX_EMPTY_REF) {
+		const f3 inv = safe_inv(d);
+		const f3 oi = mul3v(o, inv);
+		uint32_t ref = S.root_ref;
+		uint32_t sp = 0;
+		stk += lane_id();
+		for (;;) {
+			if (ref & RTX_REF_LEAF) {
+				const uint32_t first = (ref & RTX_REF_OFF) / (uint32_t)sizeof(DNode) - S.num_nodes,
+					       cnt = (ref & RTX_REF_CNT) + 1;
+				for (uint32_t k = 0; k < cnt; k++) {
+					const float4 *pr = (const float4 *)(S.prims + first + k);
+					const float4 a = pr[0], b = pr[1], c = pr[2];
+					float t;
+					bool h;
+					if ((__float_as_uint(c.w) >> 24) == RTX_SPHERE) {
+						if (COUNT)
+							tc.sph++;
+						h = hit_sphere(mk3(a.x, a.y, a.z), b.x, o, d, a.w, t);
+					} else {
+						if (COUNT)
+							tc.tris++;
+						h = hit_triangle(mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z), mk3(c.x, c.y, c.z), o, d,
+								 a.w, t);
+					}
+					if (h && t < tbest) {
+						tbest = t;
+						hid = first + k;
+					}
+				}
+				if (sp == 0)
+					break;
+				ref = stk[--sp * WAVE];
+			} else {
+				const float4 *nd = (const float4 *)((const char *)S.nodes + (ref & RTX_REF_OFF));
+				const float4 n0 = nd[0], n1 = nd[1], n2 = nd[2];
+				const uint4 n3 = *(const uint4 *)(nd + 3);
+				if (COUNT)
+					tc.nodes++;
+				float tn0, tn1;
+				const bool h0 = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, oi, inv, tbest, tn0) && tn0 < tbest;
+				const bool h1 = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, oi, inv, tbest, tn1) && tn1 < tbest;
+				if (h0 && h1) {
+					/* nearer child first; tie -> right first (accel.c:341-345) */
+					const bool l_first = tn0 < tn1;
+					stk[sp++ * WAVE] = l_first ? n3.y : n3.x;
+					ref = l_first ? n3.x : n3.y;
+				} else if (h0) {
+					ref = n3.x;
+				} else if (h1) {
+					ref = n3.y;
+				} else {
+					if (sp == 0)
+						break;
+					ref = stk[--sp * WAVE];
+				}
+			}
+		}
+	}
+	t_out = tbest;
+	hid_out = hid;
+}
+
+struct HitInfo {
+	f3 p, n;
+	float b;
+	bool outside;
+	uint32_t obj, mat;
+	float eps;
+};
+
+/* hit record of hid for ray (o,d) at t (object.c sphere 254-265, triangle 356-365, plane 473-488) */
+__device__ __forceinline__ HitInfo hit_info(const DScene &S, uint32_t hid, f3 o, f3 d, float t)
+{
+	HitInfo h;
+	h.p = add3(mul3s(d, t), o);
+	if (hid & RTX_PLANE_BIT) {
+		const DPlane &pl = S.planes[hid & ~RTX_PLANE_BIT];
+		const f3 n = ld3(pl.n);
+		h.n = signbit(dot3(n, d)) ? n : mul3s(n, -1.f);
+		h.obj = pl.obj;
+		h.mat = pl.mat;
+		h.eps = pl.eps;
+	} else {
+		const DPrim &pr = S.prims[hid];
+		const uint32_t meta = __float_as_uint(pr.c[3]);
+		if ((meta >> 24) == RTX_SPHERE)
+			h.n = mul3s(sub3(add3(mul3s(d, t), o), mk3(pr.a[0], pr.a[1], pr.a[2])), 1.f / pr.b[0]);
+		else
+			h.n = mk3(pr.d[0], pr.d[1], pr.d[2]);
+		h.obj = __float_as_uint(pr.b[3]);
+		h.mat = meta & RTX_META_MAT;
+		h.eps = pr.a[3];
+	}
+	h.b = dot3(h.n, d);
+	h.outside = signbit(h.b);
+	return h;
+}
+
+/* ------------------------------------------------------------------------ */
+/* shade points                                                             */
+/*  - GI parents live in an LDS table inside k_trace (SPW floats each)      */
+/*  - every shade point with lights is emitted as a 96-byte record          */
+/*    (6 x float4) for k_shadow:                                            */
+/*      q0 = P, W.x   q1 = n, W.y   q2 = d, W.z   q3 = tex, mat             */
+/*      q4 = obj, key_lo, key_hi, nl   q5 = slot, -, -, -                   */
+/* ------------------------------------------------------------------------ */
+#define SPW 16
+
+struct GiParent {
+	f3 p;
+	float eps;
+	f3 n;
+	float delta;
+	f3 w;
+	uint32_t slot;
+	uint32_t key_lo, key_hi, ngi, pad;
+};
+
+__device__ __forceinline__ void gp_store(float *tab, uint32_t k, const GiParent &g)
+{
+	float4 *q = (float4 *)(tab + k * SPW);
+	q[0] = make_float4(g.p.x, g.p.y, g.p.z, g.eps);
+	q[1] = make_float4(g.n.x, g.n.y, g.n.z, g.delta);
+	q[2] = make_float4(g.w.x, g.w.y, g.w.z, __uint_as_float(g.slot));
+	q[3] = make_float4(__uint_as_float(g.key_lo), __uint_as_float(g.key_hi), __uint_as_float(g.ngi), 0.f);
+}
+
+__device__ __forceinline__ GiParent gp_load(const float *tab, uint32_t k)
+{
+	const float4 *q = (const float4 *)(tab + k * SPW);
+	const float4 a = q[0], b = q[1], c = q[2], e = q[3];
+	GiParent g;
+	g.p = mk3(a.x, a.y, a.z);
+	g.eps = a.w;
+	g.n = mk3(b.x, b.y, b.z);
+	g.delta = b.w;
+	g.w = mk3(c.x, c.y, c.z);
+	g.slot = __float_as_uint(c.w);
+	g.key_lo = __float_as_uint(e.x);
+	g.key_hi = __float_as_uint(e.y);
+	g.ngi = __float_as_uint(e.z);
+	return g;
+}
+
+struct ShadePt {
+	f3 p, n, d, w, tex;
+	uint32_t mat, obj, key_lo, key_hi, nl, slot;
+};
+
+__device__ __forceinline__ void spr_store(float4 *rec, const ShadePt &s)
+{
+	rec[0] = make_float4(s.p.x, s.p.y, s.p.z, s.w.x);
+	rec[1] = make_float4(s.n.x, s.n.y, s.n.z, s.w.y);
+	rec[2] = make_float4(s.d.x, s.d.y, s.d.z, s.w.z);
+	rec[3] = make_float4(s.tex.x, s.tex.y, s.tex.z, __uint_as_float(s.mat));
+	rec[4] = make_float4(__uint_as_float(s.obj), __uint_as_float(s.key_lo), __uint_as_float(s.key_hi),
+			     __uint_as_float(s.nl));
+	rec[5] = make_float4(__uint_as_float(s.slot), 0.f, 0.f, 0.f);
+}
+
+
+/* ------------------------------------------------------------------------ */
+/* k_trace: per 8x8 tile, every cast_ray() of the tile's ray trees          */
+/* ------------------------------------------------------------------------ */
+struct TraceOut {
+	float4 *staging; /* this wave's staging region */
+	uint32_t cap;    /* records */
+	uint32_t n;      /* records written for the current tile (uniform) */
+	bool overflow;
+};
+
+/* append the lanes' shade points (has) to the staging region, order = lane order */
+__device__ __forceinline__ void emit_sp(TraceOut &T, bool has, const ShadePt &s)
+{
+	const u64 m = ballot(has);
+	if (!m)
+		return;
+	const uint32_t pos = T.n + mbcnt(m);
+	if (has && pos < T.cap)
+		spr_store(T.staging + (size_t)pos * SPREC, s);
+	T.n += popc64(m);
+	if (T.n > T.cap)
+		T.overflow = true;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void gi_batch(const DScene &S, const DParams &P, uint32_t total_lights, uint32_t *stk,
+					 float *gp_tab, uint32_t *off, uint32_t ngi_mine, f3 &acc, TraceOut &T,
+					 TraceCount &tc, u64 &n_closest)
+{
+	uint32_t total;
+	const uint32_t ex = wave_excl_scan(ngi_mine, &total);
+	if (total == 0)
+		return;
+	lds_sync();
+	off[lane_id()] = ex;
+	if (lane_id() == 0)
+		off[WAVE] = total;
+	lds_sync();
+	for (uint32_t base = 0; base < total; base += WAVE) {
+		const uint32_t idx = base + lane_id();
+		const bool act = idx < total;
+		const uint32_t h = act ? owner_of(off, idx) : 0u;
+		const GiParent par = gp_load(gp_tab, h);
+		const uint32_t s = idx - off[h];
+		const uint64_t pkey = key_of(par.key_lo, par.key_hi);
+		float u1, u2;
+		draw(P, pkey, RTX_STREAM_GI, s, u1, u2);
+		/* render.c:270-286: uniform hemisphere sample about n, weight delta * (n . dir) */
+		const f3 dir = gi_direction(par.n, par.eps, u1, u2);
+		const f3 kr = mul3s(par.w, par.delta * dot3(par.n, dir));
+		const uint64_t ckey = rtx_key_child(pkey, RTX_CHILD_GI0 + s);
+		float t;
+		uint32_t hid;
+		trace_closest<COUNT>(S, stk, act, par.p, dir, RTX_NONE, t, hid, tc);
+		n_closest += popc64(ballot(act));
+		const bool hit = act && hid != RTX_NONE;
+		ShadePt cs = ShadePt();
+		f3 cc = mk3(0.f, 0.f, 0.f);
+		bool has = false;
+		if (hit) {
+			/* child cast_ray(..., 0 bounces): ke + direct light only (path mode has no ambient term) */
+			const HitInfo hi = hit_info(S, hid, par.p, dir, t);
+			const DMaterial &m = S.mats[hi.mat];
+			const f3 w = mul3s(kr, att_factor(P, t));
+			cc = mul3v(w, ld3(m.ke));
+			cs.nl = hi.outside ? lights_for(S, total_lights, hi.obj) : 0u;
+			has = cs.nl != 0;
+			cs.p = hi.p;
+			cs.n = hi.n;
+			cs.d = dir;
+			cs.w = w;
+			cs.mat = hi.mat;
+			cs.obj = hi.obj;
+			cs.slot = par.slot;
+			cs.tex = has ? texture_color(m, hi.p, P.u32conv) : mk3(0.f, 0.f, 0.f);
+			cs.key_lo = (uint32_t)ckey;
+			cs.key_hi = (uint32_t)(ckey >> 32);
+		}
+		route_add(acc, hit, par.slot, cc);
+		emit_sp(T, has, cs);
+		lds_sync();
+	}
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(WAVE) void k_trace(DScene S, DFrame F, DParams P, float *__restrict__ rgb,
+						float *__restrict__ zbuf, DTask *__restrict__ tasks, uint32_t task_cap,
+						float4 *__restrict__ staging, uint32_t staging_cap,
+						float4 *__restrict__ sp_out, uint32_t sp_cap, uint2 *__restrict__ tile_rec,
+						uint32_t tile_begin, uint32_t tile_end, unsigned long long *__restrict__ ctr)
+{
+	extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+	float *gp_tab = (float *)lds_raw;
+	uint32_t *off = (uint32_t *)(lds_raw + WAVE * SPW * 4);
+	uint32_t *stk = (uint32_t *)(lds_raw + WAVE * SPW * 4 + 80 * 4);
+
+	uint32_t total_lights = 0;
+	for (uint32_t e = 0; e < S.num_emitters; e++)
+		total_lights += S.emitters[e].num_lights;
+	u64 n_closest = 0;
+	TraceCount tc = { 0, 0, 0, 0 };
+	DTask *my_tasks = tasks + (size_t)blockIdx.x * task_cap;
+	TraceOut T;
+	T.staging = staging + (size_t)blockIdx.x * staging_cap * SPREC;
+	T.cap = staging_cap;
+	bool overflow = false, task_overflow = false, sp_overflow = false;
+
+	for (;;) {
+		uint32_t tile = 0;
+		if (lane_id() == 0)
+			tile = (uint32_t)atomicAdd(&ctr[RTX_C_TILE], 1ull);
+		tile = uni(__shfl(tile, 0, WAVE)) + tile_begin;
+		if (tile >= tile_end)
+			break;
+		const uint32_t g = P.tile_offset + tile * P.tile_stride;
+		const uint32_t tx = g % P.tiles_x, ty = g / P.tiles_x;
+		const uint32_t px = tx * RTX_TILE_W + (lane_id() & 7), py = ty * RTX_TILE_H + (lane_id() >> 3);
+		const bool valid_px = px < F.width && py < F.height;
+		T.n = 0;
+		T.overflow = false;
+
+		f3 acc = mk3(0.f, 0.f, 0.f);
+		float zval = 0.f;
+
+		/* primary ray (render.c:353-363): P = corner + row*vy, then += vx (col+1) times, sequentially */
+		bool act = valid_px;
+		f3 o = ld3(F.origin), d = mk3(0.f, 0.f, 1.f), kr = mk3(1.f, 1.f, 1.f);
+		uint32_t rb = P.max_bounces, inside = RTX_NONE, slot = lane_id();
+		uint64_t key = 0;
+		bool primary = true;
+		if (act) {
+			f3 pp = add3(mul3s(ld3(F.step_y), (float)py), ld3(F.corner));
+			const f3 sx = ld3(F.step_x);
+			for (uint32_t c = 0; c <= px; c++)
+				pp = add3(pp, sx);
+			d = norm3(sub3(pp, o));
+			key = rtx_key_pixel(P.seed, py * F.width + px);
+		}
+		uint32_t top = 0;
+		for (;;) {
+			float t;
+			uint32_t hid;
+			lds_sync();
+			trace_closest<COUNT>(S, stk, act, o, d, inside, t, hid, tc);
+			n_closest += popc64(ballot(act));
+			const bool hit = act && hid != RTX_NONE;
+			ShadePt sp = ShadePt();
+			GiParent gp = GiParent();
+			f3 cc = mk3(0.f, 0.f, 0.f);
+			bool has = false, want_refl = false, want_refr = false;
+			f3 rkr = mk3(0.f, 0.f, 0.f), rkt = rkr, rdir = rkr, tdir = rkr;
+			if (hit) {
+				const HitInfo h = hit_info(S, hid, o, d, t);
+				const DMaterial &m = S.mats[h.mat];
+				const f3 w = mul3s(kr, att_factor(P, t));
+				f3 local = ld3(m.ke);
+				if (P.gi == RTX_GI_AMBIENT)
+					local = add3(local, mul3v(ld3(m.ka), ld3(S.ambient)));
+				cc = mul3v(w, local);
+				if (primary)
+					zval = rb ? t : 0.f; /* render.c:304-305, 342 */
+				if (rb) {
+					if (inside != hid && (m.flags & RTX_MF_REFLECTIVE)) { /* render.c:308-317 */
+						rkr = mul3v(kr, ld3(m.kr));
+						if (P.min_intensity_sqr < magsqr3(rkr)) {
+							want_refl = true;
+							rdir = sub3(d, mul3s(h.n, 2.f * h.b));
+						}
+					}
+					if (m.flags & RTX_MF_TRANSPARENT) { /* render.c:320-340 */
+						rkt = mul3v(kr, ld3(m.kt));
+						if (P.min_intensity_sqr < magsqr3(rkt)) {
+							want_refr = true;
+							tdir = refract_dir(d, h.n, h.b, h.outside, m.ior);
+						}
+					}
+				}
+				sp.nl = h.outside ? lights_for(S, total_lights, h.obj) : 0u;
+				has = sp.nl != 0;
+				sp.p = h.p;
+				sp.n = h.n;
+				sp.d = d;
+				sp.w = w;
+				sp.mat = h.mat;
+				sp.obj = h.obj;
+				sp.slot = slot;
+				sp.tex = has ? texture_color(m, h.p, P.u32conv) : mk3(0.f, 0.f, 0.f);
+				sp.key_lo = (uint32_t)key;
+				sp.key_hi = (uint32_t)(key >> 32);
+				gp.p = h.p;
+				gp.eps = h.eps;
+				gp.n = h.n;
+				gp.w = w;
+				gp.slot = slot;
+				gp.key_lo = sp.key_lo;
+				gp.key_hi = sp.key_hi;
+				gp.ngi = (P.gi == RTX_GI_PATH && rb && h.outside) ? (rb == P.max_bounces ? P.samples : 1u) : 0u;
+				gp.delta = (rb == P.max_bounces) ? 1.f / (float)P.samples : 1.f;
+			}
+			route_add(acc, hit, slot, cc);
+			emit_sp(T, has, sp);
+			/* push reflection / refraction children (compacted, LIFO) */
+			{
+				const u64 mr = ballot(want_refl), mt = ballot(want_refr);
+				const uint32_t nr = popc64(mr), nt = popc64(mt);
+				if (nr + nt) {
+					if (top + nr + nt > task_cap) {
+						task_overflow = true;
+					} else {
+						const uint32_t pos_r = top + mbcnt(mr), pos_t = top + nr + mbcnt(mt);
+						if (want_refl) {
+							const uint64_t k2 = rtx_key_child(key, RTX_CHILD_REFLECT);
+							DTask tk;
+							tk.o[0] = sp.p.x; tk.o[1] = sp.p.y; tk.o[2] = sp.p.z;
+							tk.d[0] = rdir.x; tk.d[1] = rdir.y; tk.d[2] = rdir.z;
+							tk.kr[0] = rkr.x; tk.kr[1] = rkr.y; tk.kr[2] = rkr.z;
+							tk.rb = rb - 1;
+							tk.inside = RTX_NONE;
+							tk.key_lo = (uint32_t)k2;
+							tk.key_hi = (uint32_t)(k2 >> 32);
+							tk.slot = slot;
+							my_tasks[pos_r] = tk;
+						}
+						if (want_refr) {
+							const uint64_t k2 = rtx_key_child(key, RTX_CHILD_REFRACT);
+							DTask tk;
+							tk.o[0] = sp.p.x; tk.o[1] = sp.p.y; tk.o[2] = sp.p.z;
+							tk.d[0] = tdir.x; tk.d[1] = tdir.y; tk.d[2] = tdir.z;
+							tk.kr[0] = rkt.x; tk.kr[1] = rkt.y; tk.kr[2] = rkt.z;
+							tk.rb = rb - 1;
+							tk.inside = hid;
+							tk.key_lo = (uint32_t)k2;
+							tk.key_hi = (uint32_t)(k2 >> 32);
+							tk.slot = slot;
+							my_tasks[pos_t] = tk;
+						}
+						top += nr + nt;
+					}
+				}
+			}
+			/* path-traced GI children of this batch's hits (render.c:238-288) */
+			if (P.gi == RTX_GI_PATH) {
+				lds_sync();
+				if (hit)
+					gp_store(gp_tab, lane_id(), gp);
+				gi_batch<COUNT>(S, P, total_lights, stk, gp_tab, off, hit ? gp.ngi : 0u, acc, T, tc,
+						n_closest);
+			}
+			if (top == 0)
+				break;
+			/* next batch: pop up to 64 tasks */
+			__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+			const uint32_t n = min(top, (uint32_t)WAVE);
+			top -= n;
+			act = lane_id() < n;
+			primary = false;
+			if (act) {
+				const DTask tk = my_tasks[top + lane_id()];
+				o = ld3(tk.o);
+				d = ld3(tk.d);
+				kr = ld3(tk.kr);
+				rb = tk.rb;
+				inside = tk.inside;
+				key = key_of(tk.key_lo, tk.key_hi);
+				slot = tk.slot;
+			}
+			__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+		}
+		/* local terms + z of the tile; light terms are added by k_accum */
+		if (valid_px) {
+			const size_t pix = (size_t)py * F.width + px;
+			if (rgb) {
+				rgb[pix * 3 + 0] = acc.x;
+				rgb[pix * 3 + 1] = acc.y;
+				rgb[pix * 3 + 2] = acc.z;
+			}
+			if (zbuf)
+				zbuf[pix] = zval;
+		}
+		/* move the tile's shade points to the chunk's contiguous array */
+		uint32_t n = T.n;
+		uint32_t start = 0;
+		if (T.overflow) {
+			overflow = true;
+			n = 0;
+		}
+		if (lane_id() == 0)
+			start = n ? (uint32_t)atomicAdd(&ctr[RTX_C_SPCOUNT], (unsigned long long)n) : 0u;
+		start = uni(__shfl(start, 0, WAVE));
+		if ((uint64_t)start + n > sp_cap) {
+			sp_overflow = true;
+			n = 0;
+		}
+		__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+		for (uint32_t i = lane_id(); i < n * SPREC; i += WAVE)
+			sp_out[(size_t)start * SPREC + i] = T.staging[i];
+		if (lane_id() == 0)
+			tile_rec[tile - tile_begin] = make_uint2(start, n);
+	}
+	if (COUNT) {
+		u64 a = tc.nodes, b = tc.tris, c = tc.sph, d2 = tc.pln;
+#pragma unroll
+		for (int o2 = 32; o2 > 0; o2 >>= 1) {
+			a += __shfl_xor(a, o2, WAVE);
+			b += __shfl_xor(b, o2, WAVE);
+			c += __shfl_xor(c, o2, WAVE);
+			d2 += __shfl_xor(d2, o2, WAVE);
+		}
+		if (lane_id() == 0) {
+			atomicAdd(&ctr[RTX_C_NODES], a);
+			atomicAdd(&ctr[RTX_C_TRIS], b);
+			atomicAdd(&ctr[RTX_C_SPHERES], c);
+			atomicAdd(&ctr[RTX_C_PLANES], d2);
+		}
+	}
+	if (lane_id() == 0) {
+		atomicAdd(&ctr[RTX_C_CLOSEST], n_closest);
+		if (overflow)
+			atomicAdd(&ctr[RTX_C_OVERFLOW], 1ull);
+		if (task_overflow)
+			atomicAdd(&ctr[RTX_C_TASKOVERFLOW], 1ull);
+		if (sp_overflow)
+			atomicAdd(&ctr[RTX_C_SPOVERFLOW], 1ull);
+	}
+}
+
+/* ------------------------------------------------------------------------ */
+/* k_accum: one wave per tile adds its shade points' light terms to the     */
+/* tile's pixels in emission order (deterministic, no float atomics)        */
+/* ------------------------------------------------------------------------ */
+__global__ __launch_bounds__(WAVE) void k_accum(DFrame F, DParams P, const uint2 *__restrict__ tile_rec,
+						 const float4 *__restrict__ contrib, uint32_t tile_begin,
+						 float *__restrict__ rgb)
+{
+	const uint32_t t = blockIdx.x;
+	const uint2 rec = tile_rec[t];
+	f3 acc = mk3(0.f, 0.f, 0.f);
+	for (uint32_t base = 0; base < rec.y; base += WAVE) {
+		const bool valid = base + lane_id() < rec.y;
+		float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
+		if (valid)
+			c = contrib[rec.x + base + lane_id()];
+		route_add(acc, valid, valid ? __float_as_uint(c.w) : 0u, mk3(c.x, c.y, c.z));
+	}
+	const uint32_t g = P.tile_offset + (tile_begin + t) * P.tile_stride;
+	const uint32_t px = (g % P.tiles_x) * RTX_TILE_W + (lane_id() & 7), py = (g / P.tiles_x) * RTX_TILE_H + (lane_id() >> 3);
+	if (px < F.width && py < F.height) {
+		const size_t pix = (size_t)py * F.width + px;
+		rgb[pix * 3 + 0] += acc.x;
+		rgb[pix * 3 + 1] += acc.y;
+		rgb[pix * 3 + 2] += acc.z;
+	}
+}
+
+__global__ void k_kat(int kind, uint32_t n, const float *__restrict__ in, float *__restrict__ out, int u32mode)
+{
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n)
+		return;
+	const int wi = rtx_kat_in_width[kind], wo = rtx_kat_out_width[kind];
+	const float *x = in + (size_t)i * wi;
+	float *y = out + (size_t)i * wo;
+	for (int k = 0; k < wo; k++)
+		y[k] = 0.f;
+	switch (kind) {
+	case RTX_KAT_MOLLER: {
+		float t = 0.f;
+		bool h = hit_triangle(ld3(x + 6), ld3(x + 9), ld3(x + 12), ld3(x), ld3(x + 3), x[15], t);
+		y[0] = h;
+		y[1] = h ? t : 0.f;
+	} break;
+	case RTX_KAT_SPHERE: {
+		float t = 0.f;
+		f3 o = ld3(x), d = ld3(x + 3), c = ld3(x + 6);
+		bool h = hit_sphere(c, x[9], o, d, x[10], t);
+		y[0] = h;
+		if (h) {
+			y[1] = t;
+			f3 n = mul3s(sub3(add3(mul3s(d, t), o), c), 1.f / x[9]);
+			y[2] = n.x;
+			y[3] = n.y;
+			y[4] = n.z;
+		}
+	} break;
+	case RTX_KAT_PLANE: {
+		float t = 0.f;
+		f3 o = ld3(x), d = ld3(x + 3), nn = ld3(x + 6);
+		bool h = hit_plane(nn, x[9], o, d, x[10], t);
+		y[0] = h;
+		if (h) {
+			y[1] = t;
+			f3 n = signbit(dot3(nn, d)) ? nn : mul3s(nn, -1.f);
+			y[2] = n.x;
+			y[3] = n.y;
+			y[4] = n.z;
+		}
+	} break;
+	case RTX_KAT_SLAB: {
+		float tmin = 0.f, tmax = 0.f;
+		bool h = slab_ref(ld3(x + 6), ld3(x + 9), x[12], ld3(x), ld3(x + 3), tmin, tmax);
+		y[0] = h;
+		y[1] = h ? tmin : 0.f;
+		y[2] = h ? tmax : 0.f;
+	} break;
+	case RTX_KAT_NOISE:
+		y[0] = simplex3(x[0], x[1], x[2]);
+		break;
+	case RTX_KAT_TEXTURE: {
+		DMaterial m;
+		m.tex = (int)x[0];
+		m.periodic = (int)x[1];
+		for (int k = 0; k < 3; k++) {
+			m.color[0][k] = x[2 + k];
+			m.color[1][k] = x[5 + k];
+		}
+		m.scale = x[8];
+		m.mortar = x[9];
+		m.nfs = x[10];
+		m.ns = x[11];
+		m.fs = x[12];
+		f3 c = texture_color(m, ld3(x + 13), u32mode);
+		y[0] = c.x;
+		y[1] = c.y;
+		y[2] = c.z;
+	} break;
+	case RTX_KAT_SPH_LIGHT:
+	case RTX_KAT_TRI_LIGHT: {
+		DEmitter e;
+		f3 p = mk3(0.f, 0.f, 0.f);
+		float u1, u2;
+		if (kind == RTX_KAT_SPH_LIGHT) {
+			e.type = RTX_SPHERE;
+			for (int k = 0; k < 3; k++)
+				e.p0[k] = x[k];
+			e.radius = x[3];
+			p = ld3(x + 4);
+			u1 = x[7];
+			u2 = x[8];
+		} else {
+			e.type = RTX_TRIANGLE;
+			for (int k = 0; k < 3; k++) {
+				e.p0[k] = x[k];
+				e.p1[k] = x[3 + k];
+				e.p2[k] = x[6 + k];
+			}
+			u1 = x[9];
+			u2 = x[10];
+		}
+		f3 l = light_point(e, p, u1, u2);
+		y[0] = l.x;
+		y[1] = l.y;
+		y[2] = l.z;
+	} break;
+	case RTX_KAT_MORTON: {
+		/* accel.c:72-88 (used by the reference's BVH build; kept for parity of the KAT suite) */
+		uint32_t c = 0;
+		for (int a = 0; a < 3; a++) {
+			uint32_t v = (uint32_t)(1023.f * x[a]);
+			v = (v * 0x00010001u) & 0xFF0000FFu;
+			v = (v * 0x00000101u) & 0x0F00F00Fu;
+			v = (v * 0x00000011u) & 0xC30C30C3u;
+			v = (v * 0x00000005u) & 0x49249249u;
+			c += v * (a == 0 ? 4u : a == 1 ? 2u : 1u);
+		}
+		y[0] = __uint_as_float(c);
+	} break;
+	case RTX_KAT_U32:
+		y[0] = __uint_as_float(to_u32(x[0], RTX_U32_SAT));
+		y[1] = __uint_as_float(to_u32(x[0], RTX_U32_WRAP));
+		break;
+	case RTX_KAT_GI_DIR: {
+		f3 dd = gi_direction(ld3(x), x[3], x[4], x[5]);
+		y[0] = dd.x;
+		y[1] = dd.y;
+		y[2] = dd.z;
+	} break;
+	case RTX_KAT_REFRACT: {
+		f3 dd = ld3(x), nn = ld3(x + 3);
+		float b = dot3(nn, dd);
+		f3 r = refract_dir(dd, nn, b, signbit(b), x[6]);
+		y[0] = r.x;
+		y[1] = r.y;
+		y[2] = r.z;
+	} break;
+	}
+}
+
+/* ------------------------------------------------------------------------ */
+/* launchers (called from rtx_api.cpp)                                      */
+/* ------------------------------------------------------------------------ */
+extern "C" size_t rtx_trace_lds_bytes(uint32_t stack_size)
+{
+	return (size_t)WAVE * SPW * 4 + 80 * 4 + (size_t)stack_size * WAVE * 4;
+}
+
+extern "C" hipError_t rtx_trace_occupancy(uint32_t stack_size, int *blocks_per_cu)
+{
+	return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_trace<false>, WAVE,
+							     rtx_trace_lds_bytes(stack_size));
+}
+
+extern "C" hipError_t rtx_launch_trace(const DScene *S, const DFrame *F, const DParams *P, float *rgb, float *z,
+				       DTask *tasks, uint32_t task_cap, float4 *staging, uint32_t staging_cap,
+				       float4 *sp_out, uint32_t sp_cap, uint2 *tile_rec, uint32_t tile_begin,
+				       uint32_t tile_end, unsigned long long *ctr, uint32_t waves, int count,
+				       hipStream_t stream)
+{
+	const size_t lds = rtx_trace_lds_bytes(S->stack_size);
+	if (count)
+		hipLaunchKernelGGL(k_trace<true>, dim3(waves), dim3(WAVE), lds, stream, *S, *F, *P, rgb, z, tasks, task_cap,
+				   staging, staging_cap, sp_out, sp_cap, tile_rec, tile_begin, tile_end, ctr);
+	else
+		hipLaunchKernelGGL(k_trace<false>, dim3(waves), dim3(WAVE), lds, stream, *S, *F, *P, rgb, z, tasks,
+				   task_cap, staging, staging_cap, sp_out, sp_cap, tile_rec, tile_begin, tile_end, ctr);
+	return hipGetLastError();
+}
+
+extern "C" hipError_t rtx_launch_accum(const DFrame *F, const DParams *P, const uint2 *tile_rec,
+				       const float4 *contrib, uint32_t tile_begin, uint32_t ntiles, float *rgb,
+				       hipStream_t stream)
+{
+	if (!ntiles || !rgb)
+		return hipSuccess;
+	hipLaunchKernelGGL(k_accum, dim3(ntiles), dim3(WAVE), 0, stream, *F, *P, tile_rec, contrib, tile_begin, rgb);
+	return hipGetLastError();
+}
+
+extern "C" hipError_t rtx_launch_kat(int kind, uint32_t n, const float *in, float *out, int u32mode,
+				     hipStream_t stream)
+{
+	hipLaunchKernelGGL(k_kat, dim3((n + 255) / 256), dim3(256), 0, stream, kind, n, in, out, u32mode);
+	return hipGetLastError();
+}

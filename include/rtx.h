@@ -178,7 +178,7 @@ typedef struct rtx_stats {
 	uint64_t tri_tests;
 	uint64_t sphere_tests;
 	uint64_t plane_tests;
-	/* ... of which by shadow rays */
+	/* ... of which by shadow rays (node visits in BVH2 units: shadow_box_tests / 2) */
 	uint64_t shadow_node_visits;
 	uint64_t shadow_tri_tests;
 	uint64_t shadow_sphere_tests;
@@ -196,15 +196,11 @@ typedef struct rtx_stats {
 	uint32_t waves;              /* persistent waves of the closest-hit kernel */
 	uint32_t chunks;             /* tile chunks the frame was split into */
 	uint32_t builder;            /* RTX_BUILD_* used by the last upload */
-	/* only with count_traversal: records a shadow packet walk fetched, summed over packets
-	 * (a packet = the 64 or 64*R shadow rays walking the BVH together) */
-	uint64_t shadow_packet_nodes;
-	uint64_t shadow_packet_prims;
-	/* only with count_traversal: what a ray-by-ray walk would fetch, summed over shadow rays:
-	 * inner nodes (root + children whose box the ray hits) and primitives in leaves whose
-	 * box the ray hits.  shadow_node_visits / shadow_ray_nodes = the packets' overhead */
-	uint64_t shadow_ray_nodes;
-	uint64_t shadow_ray_prims;
+	/* only with count_traversal: the shadow walk (k_shadow) */
+	uint64_t shadow_box_tests;        /* box tests (threaded-BVH records stepped through), summed over shadow rays */
+	uint64_t shadow_global_box_tests; /* ... of which read from the DQNode array (the rest from the LDS top copy) */
+	uint64_t shadow_wave_steps;       /* walk-loop iterations summed over waves (a wave steps until its longest ray ends) */
+	uint64_t shadow_wave_walks;       /* wave walks (64 lane slots each): steps / walks = the waves' mean walk length */
 } rtx_stats;
 
 typedef struct rtx_ctx rtx_ctx;

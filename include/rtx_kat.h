@@ -17,6 +17,12 @@
  * KAT_U32    (9)     x                                 = 1           sat(bits) wrap(bits)   = 2  material.c:164
  * KAT_GI_DIR (10)    n3 eps u1 u2                      = 6           dir3                   = 3  render.c:240-281
  * KAT_REFRACT(11)    d3 n3 ior                         = 7           dir3                   = 3  render.c:320-335
+ * -- the fast forms k_shadow actually runs (rtx_shadow.hip), checked against the exact ones --
+ * KAT_ANY_TRI(12)    o3 d3 v0_3 e1_3 e2_3 eps tlim     = 17          hit                    = 1  object.c:422-441 (t < tlim)
+ * KAT_SPH_LIGHT_SH(13) c3 r P3 u1 u2                   = 9           L3                     = 3  object.c:293-304
+ * KAT_BOX_Q  (14)    o3 d3 lo3 hi3 qo3 qs3 tlim        = 19          hit(generic) hit(octant) = 2  accel.c:112-158
+ *                    (the box is quantised on the device exactly as rtx_upload_scene quantises the
+ *                     threaded BVH, rtx_quant.h, then tested by box_hit_q on the segment (0, tlim))
  * Texture records use the params' u32conv for the float->uint32 conversion.
  */
 #ifndef RTX_KAT_H
@@ -35,10 +41,14 @@ enum rtx_kat_kind {
 	RTX_KAT_U32 = 9,
 	RTX_KAT_GI_DIR = 10,
 	RTX_KAT_REFRACT = 11,
-	RTX_KAT_NKINDS = 12,
+	RTX_KAT_ANY_TRI = 12,
+	RTX_KAT_SPH_LIGHT_SH = 13,
+	RTX_KAT_BOX_Q = 14,
+	RTX_KAT_NKINDS = 15,
 };
+#define RTX_KAT_FIRST_SHADOW RTX_KAT_ANY_TRI /* kinds >= this run in rtx_shadow.hip */
 
-static const int rtx_kat_in_width[RTX_KAT_NKINDS] = { 16, 11, 11, 13, 3, 16, 9, 11, 3, 1, 6, 7 };
-static const int rtx_kat_out_width[RTX_KAT_NKINDS] = { 2, 5, 5, 3, 1, 3, 3, 3, 1, 2, 3, 3 };
+static const int rtx_kat_in_width[RTX_KAT_NKINDS] = { 16, 11, 11, 13, 3, 16, 9, 11, 3, 1, 6, 7, 17, 9, 19 };
+static const int rtx_kat_out_width[RTX_KAT_NKINDS] = { 2, 5, 5, 3, 1, 3, 3, 3, 1, 2, 3, 3, 1, 3, 2 };
 
 #endif

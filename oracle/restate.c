@@ -1020,6 +1020,41 @@ int rtx_oracle_kat(int kind, uint32_t n, const float *in, float *out, const rtx_
 			float b = dot3(x + 3, x);
 			refract_dir(x, x + 3, b, signbit(b) != 0, x[6], y);
 		} break;
+		case RTX_KAT_ANY_TRI: { /* the exact any-hit decision: moller_trumbore hit with t < tlim */
+			float t = 0.f;
+			int h = hit_triangle(x + 6, x + 9, x + 12, x, x + 3, x[15], &t);
+			y[0] = (float)(h && t < x[16]);
+		} break;
+		case RTX_KAT_SPH_LIGHT_SH: { /* exact light_point; the device runs the fast-trig form */
+			rtx_object o;
+			memset(&o, 0, sizeof(o));
+			o.type = RTX_SPHERE;
+			assign3(o.p0, x);
+			o.radius = x[3];
+			light_point(&o, x + 4, x[7], x[8], y);
+		} break;
+		case RTX_KAT_BOX_Q: { /* the exact answer in double: does the segment (0, tlim) of the ray meet
+				       * the (unquantised) box?  A conservative quantised test must say hit
+				       * wherever this does (the frame fields are unused here). */
+			double tn = 0.0, tf = x[18];
+			for (int a = 0; a < 3 && tn <= tf; a++) {
+				const double o = x[a], d = x[3 + a], lo = x[6 + a], hi = x[9 + a];
+				if (d == 0.0) {
+					if (o < lo || o > hi)
+						tn = 1.0, tf = 0.0;
+					continue;
+				}
+				double t0 = (lo - o) / d, t1 = (hi - o) / d;
+				if (t0 > t1) {
+					const double s = t0;
+					t0 = t1;
+					t1 = s;
+				}
+				tn = t0 > tn ? t0 : tn;
+				tf = t1 < tf ? t1 : tf;
+			}
+			y[0] = y[1] = (float)(tn <= tf);
+		} break;
 		}
 	}
 	return RTX_OK;

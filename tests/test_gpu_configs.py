@@ -1,0 +1,121 @@
+"""Parity at the BASELINE.json workloads themselves (the frames bench.py and the scaling runs time).
+
+Each config renders on the GPU through the C-ABI at its full size, flags and spp, with the
+counter RNG (seed 1, as bench.py).  The oracle (oracle/restate.c, bit-exact with the reference
+built at -O2, tests/test_oracle.py) renders an evenly spaced sample of the same frame's 8x8
+tiles with the same RNG stream, and the GPU pixels of those tiles must agree within SURVEY
+§8(c)'s tolerances (conftest.compare_const):
+    hit mask <= 0.01 % of pixels (+1 px); |dz| <= 1e-4*max(z,1) on >= 99.9 % of hit pixels;
+    per-channel |d rgb| <= 1e-4*max(ref) on >= 99.5 % of pixels; relL1 <= 1e-2.
+A second GPU render of only the sampled tiles (the multi-GPU sharding path) must reproduce the
+full-frame pixels bit for bit and count exactly the oracle's cast_ray / is_light_blocked calls
+for those tiles.
+
+  configs[1]  scene3 1920x1080 -g path -n 16
+  configs[2]  scene5 (dragon stand-in) 1920x1080 -g path -n 64    (bench.py's workload)
+  configs[3]  scene5 1920x1080 -n 256, one rank's tile shard of an 8-GPU split
+  configs[4]  scene6 (Menger stand-in) 3840x2160 -g path -n 128 on one GPU
+(configs[0], scene1 512x512 ambient, is the reference's CPU case: test_cpu_config0 below and
+ the 512x512 frame in test_gpu_config0.)
+"""
+import os
+
+import numpy as np
+import pytest
+
+import conftest as C
+import rtxpy
+from rtxpy import abi, oracle
+from rtxpy.dist import rank_tiles, tile_pixel_index
+
+CONFIGS = {
+    # name: (scene, width, height, spp, oracle tile stride, GPU shard (offset, stride) or None)
+    "k2_scene3_1080p_n16": ("scene3", 1920, 1080, 16, 131, None),
+    "k3_scene5_1080p_n64": ("scene5", 1920, 1080, 64, 263, None),
+    "k4_scene5_1080p_n256_shard0of8": ("scene5", 1920, 1080, 256, 8 * 131, (0, 8)),
+    "k5_scene6_2160p_n128": ("scene6", 3840, 2160, 128, 2003, None),
+}
+
+
+def load(name):
+    import standins
+    if name in ("scene5", "scene6"):
+        standins.ensure_scene(name)
+        return rtxpy.Scene.load(os.path.join(C.SCENES, f"{name}_standin.json"), base_dir=C.GOLDEN)
+    return rtxpy.Scene.load(os.path.join(C.SCENES, f"{name}.json"), base_dir=C.GOLDEN)
+
+
+def params_for(spp, offset=0, stride=1):
+    p = rtxpy.params_from_args(["-g", "path", "-n", str(spp)], seed=1)
+    p.rng = abi.RTX_RNG_COUNTER
+    p.tile_offset, p.tile_stride = offset, stride
+    return p
+
+
+def sample_index(w, h, offset, stride):
+    idx = tile_pixel_index(w, h, rank_tiles(w, h, offset, stride)).reshape(-1)
+    return idx[idx >= 0]
+
+
+@pytest.fixture(scope="module")
+def renderer():
+    r = rtxpy.Renderer(0)
+    yield r
+    r.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", list(CONFIGS))
+def test_gpu_baseline_config_vs_oracle(renderer, cfg):
+    scene_name, w, h, spp, ostride, shard = CONFIGS[cfg]
+    scene = load(scene_name)
+    frame = scene.frame(w, h)
+    off, stride = shard or (0, 1)
+    renderer.upload(scene)
+    rgb = np.zeros((h, w, 3), np.float32)
+    z = np.zeros((h, w), np.float32)
+    rgb, z = renderer.render(frame, params_for(spp, off, stride), rgb, z)
+    full = renderer.stats()
+    assert np.isfinite(rgb).all() and (rgb >= 0).all()
+    if shard is None:
+        assert (z > 0).any()
+    # the oracle's sample: tiles t = off (mod ostride), a subset of the GPU's shard
+    assert ostride % stride == 0
+    o_rgb, o_z, (nc, ns) = oracle.render(scene, frame, params_for(spp, off, ostride))
+    idx = sample_index(w, h, off, ostride)
+    g_rgb, g_z = rgb.reshape(-1, 3)[idx], z.reshape(-1)[idx]
+    r_rgb, r_z = o_rgb.reshape(-1, 3)[idx], o_z.reshape(-1)[idx]
+    ok, info = C.compare_const(g_rgb[:, None, :], g_z[:, None], r_rgb[:, None, :], r_z[:, None])
+    info["sample_px"] = int(idx.size)
+    print(cfg, info, "gpu rays", full.closest_rays, full.shadow_rays, "ms", round(full.kernel_ms, 1))
+    assert ok, info
+    # the sharded render of exactly the oracle's tiles: bit-identical pixels, exact ray counts
+    s_rgb, s_z = renderer.render(frame, params_for(spp, off, ostride))
+    st = renderer.stats()
+    assert np.array_equal(s_rgb.reshape(-1, 3)[idx], g_rgb) and np.array_equal(s_z.reshape(-1)[idx], g_z)
+    assert (st.closest_rays, st.shadow_rays) == (nc, ns)
+
+
+@pytest.mark.gpu
+def test_gpu_config0_scene1_512(renderer):
+    """configs[0]: scene1 512x512 ambient, const RNG: the whole frame against the oracle."""
+    scene = load("scene1")
+    frame = scene.frame(512, 512)
+    p = rtxpy.params_from_args([])
+    p.rng = abi.RTX_RNG_CONST
+    renderer.upload(scene)
+    rgb, z = renderer.render(frame, p)
+    st = renderer.stats()
+    o_rgb, o_z, (nc, ns) = oracle.render(scene, frame, p)
+    ok, info = C.compare_const(rgb, z, o_rgb, o_z)
+    assert ok, info
+    assert (st.closest_rays, st.shadow_rays) == (nc, ns)
+
+
+def test_cpu_config_sample_indices():
+    """The oracle samples are subsets of the GPU shards they are compared with."""
+    for cfg, (_, w, h, _, ostride, shard) in CONFIGS.items():
+        off, stride = shard or (0, 1)
+        a = set(sample_index(w, h, off, ostride).tolist())
+        b = set(sample_index(w, h, off, stride).tolist())
+        assert a and a <= b, cfg

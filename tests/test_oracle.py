@@ -171,3 +171,19 @@ def test_oracle_tile_sharding_is_exact():
         tot[1] += c[1]
     assert (parts == full).all() and (zp == zf).all()
     assert tuple(tot) == cf
+
+
+def test_kat_fast_forms_oracle_side():
+    """The oracle's exact answers for the fast-form KATs (rtx_kat.h 12-14), pinned to the
+    reference's own known answers: any-hit = moller_trumbore hit with t < tlim; the sphere light
+    = light_point; the box answer is the double-precision slab test."""
+    import kat_fast
+    kat = np.load(os.path.join(C.GOLDEN, "kat.npz"))
+    recs, want = kat_fast.any_tri_records(kat)
+    got = oracle.kat(abi.KAT_ANY_TRI, recs)[:, 0] > 0
+    assert (got == want).mean() >= 0.999
+    x, ref = kat["sph_light_in"], kat["sph_light_out"]
+    assert np.allclose(oracle.kat(abi.KAT_SPH_LIGHT_SH, x), ref, rtol=1e-4, atol=2e-6)
+    b = kat_fast.box_q_records(2000)
+    out = oracle.kat(abi.KAT_BOX_Q, b)
+    assert out.shape == (2000, 2) and 0.05 < out[:, 0].mean() < 0.95

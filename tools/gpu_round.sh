@@ -23,7 +23,7 @@ python3 tools/standins.py scene5 scene6 > /dev/null
 for s in $STEPS; do
   case $s in
     smoke) run smoke 240 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) run tests 1500 python3 -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    tests) run tests 1500 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     testsall) run testsall 1500 python3 -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) run bench 900 python3 bench.py --verbose ;;
     benchq) run benchq 600 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --verbose ;;
@@ -34,7 +34,8 @@ for s in $STEPS; do
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-count --no-post ;;
     pmcf) run pmcf 900 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post ;;
     pmcw) run pmcw 900 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post ;;
-    pmcv) run pmcv 900 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES -d "$OUT/pmc_valu" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post ;;
+    pmcv) run pmcv 900 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$OUT/pmc_valu" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post ;;
+    pmcsum) python3 tools/pmc_summary.py ${PMCKEY:-scene5_1920x1080_n64_g1} "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_valu" > "$OUT/pmcsum.log" 2>&1; cp profiles/pmc_k_shadow.json "$OUT/" ;;
   esac
 done
 echo done
