@@ -93,7 +93,12 @@ def test_gpu_baseline_config_vs_oracle(renderer, cfg):
     s_rgb, s_z = renderer.render(frame, params_for(spp, off, ostride))
     st = renderer.stats()
     assert np.array_equal(s_rgb.reshape(-1, 3)[idx], g_rgb) and np.array_equal(s_z.reshape(-1)[idx], g_z)
-    assert (st.closest_rays, st.shadow_rays) == (nc, ns)
+    # cast_ray calls are exact; is_light_blocked calls may differ by a few shade points' lights:
+    # a path-GI direction (acosf / sinf / cosf, render.c:281-283) rounded 1 ulp apart by OCML and
+    # glibc can flip a grazing hit or the is_outside sign of one child in ~1e6 (measured: one
+    # point of 300 lights in 80.5 M shadow rays on k3).  Bound: 2e-5 of the count.
+    assert st.closest_rays == nc
+    assert abs(st.shadow_rays - ns) <= 2e-5 * ns, (st.shadow_rays, ns)
 
 
 @pytest.mark.gpu
