@@ -394,8 +394,8 @@ def main():
     t0 = time.perf_counter()
     r.upload(scene)
     st = r.stats()
-    log(f"scene {os.path.basename(path)}: {scene.num_objects} objects, BVH {st.bvh_nodes} nodes depth {st.bvh_depth} "
-        f"({time.perf_counter() - t0:.2f}s build+upload)")
+    log(f"scene {os.path.basename(path)}: {scene.num_objects} objects, BVH {st.bvh_nodes} nodes depth {st.bvh_depth}, "
+        f"shadow BVH4 {st.wide_nodes} nodes depth {st.wide_depth} ({time.perf_counter() - t0:.2f}s build+upload)")
 
     npx = a.width * a.height
     d_rgb = torch.zeros((npx, 3), dtype=torch.float32, device=dev)

@@ -79,6 +79,7 @@ struct rtx_ctx {
 	DEmitter *d_emitters = nullptr;
 	DQNode *d_qnodes = nullptr;
 	uint32_t *d_top = nullptr;
+	DQNode *d_wnodes = nullptr;
 	DScene scene{};
 	bool have_scene = false;
 	/* work buffers (grow-only) */
@@ -157,6 +158,7 @@ static void free_scene(rtx_ctx *c)
 	dfree(c->d_emitters);
 	dfree(c->d_qnodes);
 	dfree(c->d_top);
+	dfree(c->d_wnodes);
 	c->have_scene = false;
 }
 
@@ -345,6 +347,98 @@ static uint32_t thread_top(const std::vector<DQNode> &q, const std::vector<uint3
 		}
 	}
 	return nt;
+}
+
+/* The 4-wide shadow-walk BVH (rtx_device.h RTX_W_STACK): each wide node collapses its BVH2
+ * node's subtree top, repeatedly opening the inner child of largest surface area until it has
+ * four children (the usual SAH-driven collapse).  Inner children come first in a node's slots
+ * and are allocated as consecutive nodes, depth first.  Returns the wide tree's depth. */
+struct WKid {
+	uint32_t ref;
+	float lo[3], hi[3];
+};
+
+static float half_area(const WKid &k)
+{
+	const float dx = k.hi[0] - k.lo[0], dy = k.hi[1] - k.lo[1], dz = k.hi[2] - k.lo[2];
+	return dx * dy + dy * dz + dz * dx;
+}
+
+static void wide_kids(const std::vector<DNode> &recs, uint32_t ref, WKid kids[4], uint32_t &n)
+{
+	auto open = [&](uint32_t r, WKid &a, WKid &b) {
+		const DNode &d = recs[(r & RTX_REF_OFF) / (uint32_t)sizeof(DNode)];
+		a = WKid{ d.ref0, { d.lo0x, d.lo0y, d.lo0z }, { d.hi0x, d.hi0y, d.hi0z } };
+		b = WKid{ d.ref1, { d.lo1x, d.lo1y, d.lo1z }, { d.hi1x, d.hi1y, d.hi1z } };
+	};
+	open(ref, kids[0], kids[1]);
+	n = 2;
+	while (n < 4) {
+		int best = -1;
+		float ba = -1.f;
+		for (uint32_t i = 0; i < n; i++)
+			if (!(kids[i].ref & RTX_REF_LEAF) && half_area(kids[i]) > ba) {
+				ba = half_area(kids[i]);
+				best = (int)i;
+			}
+		if (best < 0)
+			break;
+		const uint32_t r = kids[best].ref;
+		open(r, kids[best], kids[n]);
+		n++;
+	}
+	/* inner children first (stable), so slot c's child node is slot 0's + c */
+	std::stable_partition(kids, kids + n, [](const WKid &k) { return !(k.ref & RTX_REF_LEAF); });
+}
+
+static uint32_t wide_emit(const std::vector<DNode> &recs, const QFrame &F, uint32_t ref, uint32_t me,
+			  std::vector<DQNode> &out)
+{
+	WKid kids[4];
+	uint32_t n = 0;
+	wide_kids(recs, ref, kids, n);
+	uint32_t ninner = 0;
+	while (ninner < n && !(kids[ninner].ref & RTX_REF_LEAF))
+		ninner++;
+	const uint32_t base = (uint32_t)(out.size() / 4);
+	out.resize(out.size() + 4 * (size_t)ninner);
+	for (uint32_t c = 0; c < 4; c++) {
+		DQNode &t = out[4 * (size_t)me + c];
+		if (c >= n) {
+			t.x = t.y = t.z = RTX_W_EMPTY_BOX;
+			t.link = RTX_EMPTY_REF;
+			continue;
+		}
+		t.x = rtx_quantise(kids[c].lo[0], kids[c].hi[0], F.qo[0], F.qs[0]);
+		t.y = rtx_quantise(kids[c].lo[1], kids[c].hi[1], F.qo[1], F.qs[1]);
+		t.z = rtx_quantise(kids[c].lo[2], kids[c].hi[2], F.qo[2], F.qs[2]);
+		t.link = c < ninner ? (base + c) << 6 : kids[c].ref;
+	}
+	uint32_t dep = 1;
+	for (uint32_t c = 0; c < ninner; c++)
+		dep = std::max(dep, 1 + wide_emit(recs, F, kids[c].ref, base + c, out));
+	return dep;
+}
+
+static uint32_t wide_bvh(const std::vector<DNode> &inner, uint32_t root_ref, const float lo[3], const float hi[3],
+			 const QFrame &F, std::vector<DQNode> &out)
+{
+	out.clear();
+	if (root_ref == RTX_EMPTY_REF)
+		return 0;
+	out.resize(4);
+	if (root_ref & RTX_REF_LEAF) { /* a single leaf: one node, one slot with the scene box */
+		for (uint32_t c = 0; c < 4; c++) {
+			out[c].x = out[c].y = out[c].z = RTX_W_EMPTY_BOX;
+			out[c].link = RTX_EMPTY_REF;
+		}
+		out[0].x = rtx_quantise(lo[0], hi[0], F.qo[0], F.qs[0]);
+		out[0].y = rtx_quantise(lo[1], hi[1], F.qo[1], F.qs[1]);
+		out[0].z = rtx_quantise(lo[2], hi[2], F.qo[2], F.qs[2]);
+		out[0].link = root_ref;
+		return 1;
+	}
+	return wide_emit(inner, F, root_ref, 0, out);
 }
 
 static inline float pad_lo(float x, float ext) { return x - (std::fabs(x) + ext) * 2e-6f - 1e-30f; }
@@ -595,6 +689,16 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 	const uint32_t ntop = thread_top(qnodes, qdepth, qtop);
 	if ((rc = upload(c->d_top, qtop)))
 		return rc;
+	std::vector<DQNode> wnodes;
+	uint32_t wdepth = 0;
+	const char *we = getenv("RTX_WIDE"); /* measurement: RTX_WIDE=0 keeps the threaded BVH2 walk */
+	if (!(we && atoi(we) == 0)) {
+		wdepth = wide_bvh(inner, nb ? root_ref : RTX_EMPTY_REF, c->bound_lo, c->bound_hi, qf, wnodes);
+		if (wdepth > RTX_W_STACK + 1 || wnodes.size() / 4 >= (1u << 26)) /* the lane stacks would overflow */
+			wnodes.clear();
+	}
+	if ((rc = upload(c->d_wnodes, wnodes)))
+		return rc;
 	c->stats.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count();
 	if ((rc = upload(c->d_planes, planes)) || (rc = upload(c->d_mats, mats)) || (rc = upload(c->d_emitters, emit)))
 		return rc;
@@ -613,6 +717,9 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 	memcpy(S.qs, qf.qs, 12);
 	S.top = ntop ? c->d_top : nullptr;
 	S.num_top = ntop;
+	S.wnodes = wnodes.empty() ? nullptr : c->d_wnodes;
+	S.num_wnodes = (uint32_t)(wnodes.size() / 4);
+	S.wdepth = wnodes.empty() ? 0 : wdepth;
 	S.root_ref = nb ? root_ref : RTX_EMPTY_REF;
 	S.num_prims = nb;
 	S.num_planes = (uint32_t)planes.size();
@@ -627,6 +734,8 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 	c->stats.bvh_depth = depth;
 	c->stats.builder = (uint32_t)c->builder;
 	c->stats.bvh_prims = nb;
+	c->stats.wide_nodes = S.num_wnodes;
+	c->stats.wide_depth = S.wdepth;
 	return RTX_OK;
 }
 

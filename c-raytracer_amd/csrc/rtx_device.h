@@ -97,6 +97,20 @@ typedef struct __attribute__((aligned(16))) DQNode {
 #define RTX_SH_NW 16 /* waves per k_shadow workgroup (they share the top copy) */
 #endif
 
+/* 4-wide copy of the BVH for the shadow walk (rtx_shadow.hip shadow_walk4): node i is four
+ * 16-byte child slots (DQNode records 4i .. 4i+3, one 64-byte line), each {x, y, z, ref} with the
+ * child's box quantised as in DQNode.  The slots hold the inner children first (ref = child node
+ * index << 6; a node's inner children are consecutive nodes, so slot c's child is slot 0's + c),
+ * then the leaves (ref = device leaf ref, RTX_REF_LEAF set), then empty slots (ref =
+ * RTX_EMPTY_REF, quantised box lo > hi on every axis, never hit).  Node 0 is the root.  A lane
+ * keeps its pending siblings as groups (first child << 4 | slot mask), one per tree level, in
+ * an LDS stack of RTX_W_STACK entries: the uploader builds the wide tree only when its depth
+ * fits (num_wnodes = 0 otherwise, and k_shadow walks the threaded BVH2). */
+#ifndef RTX_W_STACK
+#define RTX_W_STACK 12
+#endif
+#define RTX_W_EMPTY_BOX 0x0000FFFFu
+
 typedef struct DPlane {
 	float n[3];
 	float d;
@@ -138,6 +152,8 @@ typedef struct DScene {
 	float qo[3], qs[3];     /* its quantisation frame: q = (x - qo) * qs */
 	const uint32_t *top;    /* its top levels (num_top records + num_top words, see RTX_QTOP_CUT) */
 	uint32_t num_top;
+	const DQNode *wnodes;   /* 4-wide BVH (4 records per node, same frame), null when not built */
+	uint32_t num_wnodes, wdepth;
 	uint32_t root_ref;
 	uint32_t num_nodes;    /* prims == (const DPrim *)(nodes + num_nodes) */
 	uint32_t num_prims;

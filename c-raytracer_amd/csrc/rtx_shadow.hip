@@ -30,6 +30,12 @@
 #ifndef RTX_DEBUG_NOWALK
 #define RTX_DEBUG_NOWALK 0 /* measurement only: skip the BVH walk (everything else in k_shadow stays) */
 #endif
+#ifndef RTX_SH_NOTOP
+#define RTX_SH_NOTOP 0 /* measurement: walk the DQNode array only, no LDS top */
+#endif
+#ifndef RTX_SH_DEFER
+#define RTX_SH_DEFER 0 /* leaf tests deferred until >= 1/N of the live lanes hold a leaf (0: test at once) */
+#endif
 #ifndef RTX_SHADOW_OCC_DEFAULT
 #define RTX_SHADOW_OCC_DEFAULT 8 /* waves per SIMD the walk is register-capped for */
 #endif
@@ -82,6 +88,7 @@ __device__ __forceinline__ uint32_t lds1u(const uint32_t *p)
 {
 	return *(const __attribute__((address_space(3))) uint32_t *)p;
 }
+__device__ __forceinline__ void lds1st(uint32_t *p, uint32_t v) { *(__attribute__((address_space(3))) uint32_t *)p = v; }
 
 /* ------------------------------------------------------------------------ */
 /* intersection tests of the any-hit walk                                   */
@@ -184,13 +191,30 @@ __device__ __forceinline__ bool shadow_prim(float4 a, float4 b, float4 c, const 
 	return true;
 }
 
+/* every primitive of the leaf with device ref L, in order; true at the first opaque hit */
+template <bool COUNT>
+__device__ __forceinline__ bool shadow_leaf(uint32_t L, const char *__restrict__ recs, const DMaterial *__restrict__ mats, f3 o,
+					    f3 d, float tl, uint32_t emit_obj, f3 &li, uint32_t &ntri, uint32_t &nsph)
+{
+	const char *p = recs + (L & RTX_REF_OFF);
+	const uint32_t cnt = (L & RTX_REF_CNT) + 1;
+	for (uint32_t k = 0; k < cnt; k++) {
+		const char *pr = p + k * (uint32_t)sizeof(DPrim);
+		if (shadow_prim<COUNT>(ldg4(pr, 0), ldg4(pr, 16), ldg4(pr, 32), mats, o, d, tl, emit_obj, li, ntri, nsph))
+			return true;
+	}
+	return false;
+}
+
 /* the quantised threaded BVH and its frame (rtx_device.h DQNode) */
 struct QBvh {
 	const DQNode *q;
 	f3 qo, qs;
 	const uint4 *top;     /* the workgroup's LDS copy of the top records */
 	const uint32_t *tend; /* ... and of the cut records' range ends */
-	uint32_t nt;
+	uint32_t nt, nq;      /* top records, DQNode records */
+	const DQNode *w;      /* the 4-wide BVH (rtx_device.h RTX_W_STACK), WIDE walks */
+	uint32_t *stk;        /* this lane's LDS stack of sibling groups: entry k at stk[k * WAVE] */
 };
 
 /* is_light_blocked's BVH part (accel.c:360-387) for this lane's ray.  The walk starts in the
@@ -208,7 +232,55 @@ __device__ __forceinline__ void shadow_walk(const QBvh &Q, const char *__restric
 	const uint32_t nt = Q.nt;
 	uint32_t t = tl >= 0.f ? 0u : nt, g = 0, ge = 0;
 	uint32_t nbox = 0, nglob = 0, ntri = 0, nsph = 0, nstep = 0;
-	while (t < nt || g < ge) {
+#if RTX_SH_NOTOP
+	/* measurement variant: the whole walk over the DQNode array (no LDS top copy) */
+	const uint32_t nq = Q.nq;
+	(void)t;
+	(void)ge;
+	for (g = tl >= 0.f ? 0u : nq; g < nq;) {
+		const uint4 nd = ldg4u(Q.q + g);
+		if (COUNT) {
+			nbox++;
+			nglob++;
+		}
+		const bool hit = box_hit_q<OCT>(nd, oi, invq, tl);
+		const uint32_t L = nd.w;
+		const bool leaf = (L & RTX_REF_LEAF) != 0;
+		g = (hit || leaf) ? g + 1 : L >> 6;
+		if (leaf && hit && shadow_leaf<COUNT>(L, recs, mats, o, d, tl, emit_obj, li, ntri, nsph)) {
+			tl = -1.f;
+			g = nq;
+		}
+	}
+	if (COUNT)
+		nstep = nbox;
+#elif RTX_SH_DEFER
+	/* Deferred leaves: a lane whose leaf box is hit records the leaf (p1, then p2) and walks on;
+	 * the wave runs the primitive tests for all its recorded leaves at once, when at least
+	 * 1/RTX_SH_DEFER of its live lanes hold one or no lane can step (a lane holding two waits).
+	 * Each lane still tests its leaves in walk order, so transmittance products are unchanged. */
+	uint32_t p1 = 0, p2 = 0;
+	for (;;) {
+		const bool more = t < nt || g < ge;
+		const bool stepping = more && p2 == 0;
+		const u64 sm = ballot(stepping), pm = ballot(p1 != 0);
+		if (COUNT)
+			nstep++;
+		if (!(sm | pm))
+			break;
+		if (pm && (!sm || popc64(pm) * RTX_SH_DEFER >= popc64(sm | pm))) {
+			if (p1 && shadow_leaf<COUNT>(p1, recs, mats, o, d, tl, emit_obj, li, ntri, nsph)) {
+				tl = -1.f;
+				t = nt;
+				ge = 0;
+				p2 = 0;
+			}
+			p1 = p2;
+			p2 = 0;
+			continue;
+		}
+		if (!stepping)
+			continue;
 		const bool ing = g < ge;
 		uint4 nd;
 		if (ing)
@@ -227,18 +299,10 @@ __device__ __forceinline__ void shadow_walk(const QBvh &Q, const char *__restric
 			else
 				t++;
 			if (hit) {
-				const char *p = recs + (L & RTX_REF_OFF);
-				const uint32_t cnt = (L & RTX_REF_CNT) + 1;
-				for (uint32_t k = 0; k < cnt; k++) {
-					const char *pr = p + k * (uint32_t)sizeof(DPrim);
-					if (shadow_prim<COUNT>(ldg4(pr, 0), ldg4(pr, 16), ldg4(pr, 32), mats, o, d, tl, emit_obj, li,
-							       ntri, nsph)) {
-						tl = -1.f;
-						t = nt;
-						ge = 0;
-						break;
-					}
-				}
+				if (p1)
+					p2 = L;
+				else
+					p1 = L;
 			}
 		} else if (ing) {
 			g = hit ? g + 1 : L >> 6;
@@ -252,8 +316,46 @@ __device__ __forceinline__ void shadow_walk(const QBvh &Q, const char *__restric
 			t = hit ? t + 1 : L >> 6;
 		}
 	}
-	if (COUNT) {
+#else
+	while (t < nt || g < ge) {
+		const bool ing = g < ge;
+		uint4 nd;
+		if (ing)
+			nd = ldg4u(Q.q + g);
+		else
+			nd = lds4u(Q.top + t);
+		if (COUNT) {
+			nbox++;
+			nglob += ing ? 1u : 0u;
+		}
+		const bool hit = box_hit_q<OCT>(nd, oi, invq, tl);
+		const uint32_t L = nd.w;
+		if (L & RTX_REF_LEAF) {
+			if (ing)
+				g++;
+			else
+				t++;
+			if (hit && shadow_leaf<COUNT>(L, recs, mats, o, d, tl, emit_obj, li, ntri, nsph)) {
+				tl = -1.f;
+				t = nt;
+				ge = 0;
+			}
+		} else if (ing) {
+			g = hit ? g + 1 : L >> 6;
+		} else if (L & RTX_QTOP_CUT) {
+			if (hit) {
+				g = L >> 6;
+				ge = lds1u(Q.tend + t);
+			}
+			t++;
+		} else {
+			t = hit ? t + 1 : L >> 6;
+		}
+	}
+	if (COUNT)
 		nstep = nbox;
+#endif
+	if (COUNT) {
 		uint32_t a = nbox, b = ntri, c = nsph, gq = nglob;
 #pragma unroll
 		for (int s = 32; s > 0; s >>= 1) {
@@ -272,10 +374,102 @@ __device__ __forceinline__ void shadow_walk(const QBvh &Q, const char *__restric
 	}
 }
 
+/* is_light_blocked's BVH part (accel.c:360-387) over the 4-wide BVH (rtx_device.h
+ * RTX_W_STACK): one 64-byte node per step (four 16-byte loads issued together, one memory
+ * latency for four box tests).  Hit leaves are tested at once, in slot order; of the hit inner
+ * children the first is visited next and the rest are kept as one group (first child << 4 |
+ * slot mask) in a register, the older groups in the lane's LDS stack.  Any-hit needs no visit
+ * order.  tl < 0 on entry: inactive lane.  On an opaque hit tl becomes -1. */
+template <bool COUNT, int OCT>
+__device__ __forceinline__ void shadow_walk4(const QBvh &Q, const char *__restrict__ recs, const DMaterial *__restrict__ mats,
+					     f3 o, f3 d, f3 inv, float &tl, uint32_t emit_obj, f3 &li, ShadowCount &sc)
+{
+	const f3 invq = mk3(inv.x / Q.qs.x, inv.y / Q.qs.y, inv.z / Q.qs.z);
+	const f3 oq = mk3((o.x - Q.qo.x) * Q.qs.x, (o.y - Q.qo.y) * Q.qs.y, (o.z - Q.qo.z) * Q.qs.z);
+	const f3 oi = mul3v(oq, invq);
+	uint32_t *stk = Q.stk;
+	uint32_t node = tl >= 0.f ? 0u : RTX_NONE, grp = 0, sp = 0;
+	uint32_t nbox = 0, ntri = 0, nsph = 0, nstep = 0;
+	while (node != RTX_NONE) {
+		const DQNode *N = Q.w + 4 * (size_t)node;
+		const uint4 s0 = ldg4u(N), s1 = ldg4u(N + 1), s2 = ldg4u(N + 2), s3 = ldg4u(N + 3);
+		bool h0 = box_hit_q<OCT>(s0, oi, invq, tl), h1 = box_hit_q<OCT>(s1, oi, invq, tl);
+		bool h2 = box_hit_q<OCT>(s2, oi, invq, tl), h3 = box_hit_q<OCT>(s3, oi, invq, tl);
+		if (OCT == 8) { /* the min/max slab form would turn an empty slot's inverted box around */
+			h1 = h1 && s1.w != RTX_EMPTY_REF;
+			h2 = h2 && s2.w != RTX_EMPTY_REF;
+			h3 = h3 && s3.w != RTX_EMPTY_REF;
+		}
+		if (COUNT) {
+			nstep++;
+			nbox += 1u + (s1.w != RTX_EMPTY_REF) + (s2.w != RTX_EMPTY_REF) + (s3.w != RTX_EMPTY_REF);
+		}
+		const uint32_t hm = (uint32_t)h0 | ((uint32_t)h1 << 1) | ((uint32_t)h2 << 2) | ((uint32_t)h3 << 3);
+		const uint32_t lf = ((s0.w & RTX_REF_LEAF) | ((s1.w & RTX_REF_LEAF) << 1) | ((s2.w & RTX_REF_LEAF) << 2) |
+				     ((s3.w & RTX_REF_LEAF) << 3)) >> 5;
+		uint32_t lm = hm & lf, im = hm & ~lf;
+		bool blocked = false;
+		while (lm) {
+			const uint32_t c = __builtin_ctz(lm);
+			lm &= lm - 1;
+			const uint32_t L = c == 0 ? s0.w : c == 1 ? s1.w : c == 2 ? s2.w : s3.w;
+			if (shadow_leaf<COUNT>(L, recs, mats, o, d, tl, emit_obj, li, ntri, nsph)) {
+				blocked = true;
+				break;
+			}
+		}
+		if (blocked) {
+			tl = -1.f;
+			break;
+		}
+		if (im) {
+			const uint32_t c = __builtin_ctz(im), base = s0.w >> 6;
+			im &= im - 1;
+			node = base + c;
+			if (im) {
+				if (grp) {
+					lds1st(stk + sp * WAVE, grp);
+					sp++;
+				}
+				grp = (base << 4) | im;
+			}
+		} else if (grp) {
+			const uint32_t c = __builtin_ctz(grp & 15u);
+			node = (grp >> 4) + c;
+			grp &= ~(1u << c);
+			if (!(grp & 15u)) {
+				grp = 0;
+				if (sp) {
+					sp--;
+					grp = lds1u(stk + sp * WAVE);
+				}
+			}
+		} else {
+			node = RTX_NONE;
+		}
+	}
+	if (COUNT) {
+		uint32_t a = nbox, b = ntri, c = nsph;
+#pragma unroll
+		for (int s = 32; s > 0; s >>= 1) {
+			a += __shfl_xor(a, s, WAVE);
+			b += __shfl_xor(b, s, WAVE);
+			c += __shfl_xor(c, s, WAVE);
+			nstep = max(nstep, (uint32_t)__shfl_xor(nstep, s, WAVE));
+		}
+		sc.boxes += uni(a);
+		sc.gboxes += uni(a);
+		sc.tris += uni(b);
+		sc.sph += uni(c);
+		sc.steps += uni(nstep);
+		sc.walks++;
+	}
+}
+
 /* is_light_blocked (render.c:126-134): planes first (unbound_objects_is_light_blocked,
  * object.c:183-197), then the BVH walk, specialised on the direction octant when every live
  * lane shares it.  Returns the lane's blocked flag; li carries the transmittance product. */
-template <bool COUNT>
+template <bool COUNT, bool WIDE>
 __device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restrict__ recs, const DMaterial *__restrict__ mats,
 					     const DPlane *__restrict__ planes, uint32_t num_planes, bool have_tree, bool act,
 					     f3 o, f3 d, float dist, uint32_t emit_obj, f3 &li, ShadowCount &sc)
@@ -305,14 +499,20 @@ __device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restri
 	const uint32_t lead = readlane(oct, (uint32_t)__ffsll((long long)live) - 1);
 	const uint32_t sel = ballot(alive & (oct != lead)) ? 8u : lead;
 	switch (sel) {
-#define RTX_WALK(K)                                                                  \
-	case K:                                                                      \
-		shadow_walk<COUNT, K>(Q, recs, mats, o, d, inv, tl, emit_obj, li, sc); \
+#define RTX_WALK(K)                                                                       \
+	case K:                                                                           \
+		if (WIDE)                                                                 \
+			shadow_walk4<COUNT, K>(Q, recs, mats, o, d, inv, tl, emit_obj, li, sc); \
+		else                                                                      \
+			shadow_walk<COUNT, K>(Q, recs, mats, o, d, inv, tl, emit_obj, li, sc);  \
 		break;
 		RTX_WALK(0) RTX_WALK(1) RTX_WALK(2) RTX_WALK(3) RTX_WALK(4) RTX_WALK(5) RTX_WALK(6) RTX_WALK(7)
 #undef RTX_WALK
 	default:
-		shadow_walk<COUNT, 8>(Q, recs, mats, o, d, inv, tl, emit_obj, li, sc);
+		if (WIDE)
+			shadow_walk4<COUNT, 8>(Q, recs, mats, o, d, inv, tl, emit_obj, li, sc);
+		else
+			shadow_walk<COUNT, 8>(Q, recs, mats, o, d, inv, tl, emit_obj, li, sc);
 		break;
 	}
 	return act && tl < 0.f;
@@ -327,9 +527,10 @@ struct KShadow {
 	const DPrim *prims;   /* primitive records (DQNode leaf refs are byte offsets from `recs`) */
 	const char *recs;     /* base of the record array the leaf refs point into */
 	const DQNode *qnodes; /* threaded quantised BVH */
+	const DQNode *wnodes; /* 4-wide quantised BVH (WIDE instances) */
 	float qo[3], qs[3];
 	const uint32_t *top; /* its top levels (rtx_device.h RTX_QTOP_CUT), copied to LDS per workgroup */
-	uint32_t ntop;
+	uint32_t ntop, nq;
 	const DMaterial *mats;
 	const DPlane *planes;
 	const DEmitter *emitters;
@@ -395,9 +596,9 @@ __device__ __forceinline__ f3 shade_light(const KShadow &ks, const float4 *rec, 
 /* one light sample per lane of the shade point `rec` (render.c:170-229): the light point of
  * sample idx (emitters in scene order, the hit object skipped), its shadow ray, attenuation
  * and Phong / Blinn.  Argument-block fields are read from LDS behind reread barriers. */
-template <bool COUNT>
+template <bool COUNT, bool WIDE>
 __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec, uint32_t idx, bool act, ShadowCount &sc,
-					   const uint4 *top_q, const uint32_t *top_e)
+					   const uint4 *top_q, const uint32_t *top_e, uint32_t *stk)
 {
 	reread_barrier();
 	const float4 q0 = rec[0], q4 = rec[4];
@@ -434,8 +635,11 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	Q.top = top_q;
 	Q.tend = top_e;
 	Q.nt = uni(ks.ntop);
+	Q.nq = uni(ks.nq);
 	const bool have_tree = uni(ks.have_tree) != 0 && !RTX_DEBUG_NOWALK;
-	const bool blocked = shadow_query<COUNT>(Q, unip(ks.recs), unip(ks.mats), unip(ks.planes), uni(ks.num_planes),
+	Q.w = WIDE ? unip(ks.wnodes) : nullptr;
+	Q.stk = stk;
+	const bool blocked = shadow_query<COUNT, WIDE>(Q, unip(ks.recs), unip(ks.mats), unip(ks.planes), uni(ks.num_planes),
 						 have_tree, act, p, ldir, ldist, E.obj, li, sc);
 	reread_barrier();
 	f3 contribution = mk3(0.f, 0.f, 0.f);
@@ -450,17 +654,18 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 /* Persistent workgroups of RTX_SH_NW waves.  A workgroup copies the threaded BVH's top levels
  * to LDS once; then each wave takes per_wave shade points at a time from a global queue
  * (RTX_C_SPQUEUE), in processing (Morton) order, until the points run out. */
-template <bool COUNT, int OCC>
+template <bool COUNT, int OCC, bool WIDE>
 __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 {
-	__shared__ uint4 top_q[RTX_TOP_MAX];            /* the top records (rtx_device.h RTX_QTOP_CUT) */
-	__shared__ uint32_t top_e[RTX_TOP_MAX];         /* cut records: the DQNode index after the subtree */
+	__shared__ uint4 top_q[WIDE ? 1 : RTX_TOP_MAX];    /* the top records (rtx_device.h RTX_QTOP_CUT) */
+	__shared__ uint32_t top_e[WIDE ? 1 : RTX_TOP_MAX]; /* cut records: the DQNode index after the subtree */
+	__shared__ uint32_t wstk[RTX_SH_NW][WIDE ? RTX_W_STACK : 1][WAVE]; /* the wide walk's lane stacks */
 	__shared__ KShadow ks_w[RTX_SH_NW];
 	__shared__ uint32_t off_w[RTX_SH_NW][WAVE + 1]; /* first lane slot of each shade point, total */
 	__shared__ uint32_t nls_w[RTX_SH_NW][WAVE];     /* shadow rays of each shade point */
 	__shared__ uint32_t sid_w[RTX_SH_NW][WAVE];     /* each shade point's index in the record array */
 	__shared__ float Ls_w[RTX_SH_NW][3][WAVE];      /* per shade point light sum, in packet order */
-	const uint32_t ntop = ka.ntop;
+	const uint32_t ntop = WIDE ? 0u : ka.ntop;
 	for (uint32_t i = threadIdx.x; i < ntop; i += WAVE * RTX_SH_NW) {
 		top_q[i] = ldg4u(ka.top + 4 * i);
 		top_e[i] = gptr(ka.top)[4 * ntop + i];
@@ -472,6 +677,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 	KShadow &ks = ks_w[wv];
 	uint32_t *off = off_w[wv], *nls = nls_w[wv], *sid = sid_w[wv];
 	float(*Ls)[WAVE] = Ls_w[wv];
+	uint32_t *stk = &wstk[wv][0][lane_id()];
 	ShadowCount sc = { 0, 0, 0, 0, 0, 0, 0 };
 	u64 rays_total = 0;
 	for (;;) {
@@ -512,7 +718,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 				f3 acc = mk3(0.f, 0.f, 0.f);
 				for (uint32_t base = 0; base < nl; base += WAVE) {
 					const uint32_t idx = base + lane_id();
-					acc = add3(acc, light_sample<COUNT>(ks, rec, idx, idx < nl, sc, top_q, top_e));
+					acc = add3(acc, light_sample<COUNT, WIDE>(ks, rec, idx, idx < nl, sc, top_q, top_e, stk));
 				}
 				const float sx = wave_sum(acc.x), sy = wave_sum(acc.y), sz = wave_sum(acc.z);
 				if (lane_id() == 0) {
@@ -534,7 +740,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 				const uint32_t idx = ((slot - off[k]) << slot_lg) + (lane_id() & (slot_b - 1));
 				const bool act = slot < tot && idx < nls[k];
 				const float4 *rec = unip(ks.sp) + (size_t)sid[k] * SPREC;
-				const f3 contribution = light_sample<COUNT>(ks, rec, idx, act, sc, top_q, top_e);
+				const f3 contribution = light_sample<COUNT, WIDE>(ks, rec, idx, act, sc, top_q, top_e, stk);
 				/* per-shade-point sums; lanes are ordered by k */
 				const uint32_t t2 = uni(off[WAVE]), sb = uni(ks.slot_b), spp = WAVE / sb;
 				const uint32_t last_slot_lane = (min(t2 - base, spp) - 1) * sb;
@@ -650,16 +856,16 @@ extern "C" hipError_t rtx_launch_kat_shadow(int kind, uint32_t n, const float *i
 /* ------------------------------------------------------------------------ */
 /* the persistent grid: as many workgroups as are resident on the device at once (no more than
  * the work needs); the waves then share the shade points through RTX_C_SPQUEUE */
-template <bool C, int O> static hipError_t launch_shadow(const KShadow &ka, uint32_t nw, uint32_t cus, hipStream_t stream)
+template <bool C, int O, bool W> static hipError_t launch_shadow(const KShadow &ka, uint32_t nw, uint32_t cus, hipStream_t stream)
 {
 	int per_cu = 0;
-	hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(&k_shadow<C, O>),
+	hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(&k_shadow<C, O, W>),
 								   WAVE * RTX_SH_NW, 0);
 	if (e != hipSuccess)
 		return e;
 	const uint32_t slots = per_cu > 0 && cus > 0 ? (uint32_t)per_cu * cus : 1024u;
 	const uint32_t need = (nw + RTX_SH_NW - 1) / RTX_SH_NW;
-	hipLaunchKernelGGL((k_shadow<C, O>), dim3(need < slots ? need : slots), dim3(WAVE * RTX_SH_NW), 0, stream, ka);
+	hipLaunchKernelGGL((k_shadow<C, O, W>), dim3(need < slots ? need : slots), dim3(WAVE * RTX_SH_NW), 0, stream, ka);
 	return hipGetLastError();
 }
 
@@ -680,6 +886,7 @@ extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const
 	ka.qnodes = S->qnodes;
 	ka.top = S->top;
 	ka.ntop = S->num_top;
+	ka.nq = S->num_qnodes;
 	for (int a = 0; a < 3; a++) {
 		ka.qo[a] = S->qo[a];
 		ka.qs[a] = S->qs[a];
@@ -702,15 +909,14 @@ extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const
 	ka.attenuation = P->attenuation;
 	ka.reflection = P->reflection;
 	ka.att_offset = P->att_offset;
+	ka.wnodes = S->wnodes;
+	const bool wide = S->wnodes != nullptr;
 	if (count)
-		return launch_shadow<true, 1>(ka, nw, cus, stream);
-	/* occupancy variant (measurement): RTX_SHADOW_OCC = 1 (compiler's choice), 6, 7 or 8 waves/SIMD */
+		return wide ? launch_shadow<true, 1, true>(ka, nw, cus, stream) : launch_shadow<true, 1, false>(ka, nw, cus, stream);
+	/* occupancy variant (measurement): RTX_SHADOW_OCC = 1 (the compiler's choice) or 8 waves/SIMD */
 	const char *env = getenv("RTX_SHADOW_OCC");
 	const int occ = env ? atoi(env) : RTX_SHADOW_OCC_DEFAULT;
-	switch (occ) {
-	case 8: return launch_shadow<false, 8>(ka, nw, cus, stream);
-	case 7: return launch_shadow<false, 7>(ka, nw, cus, stream);
-	case 6: return launch_shadow<false, 6>(ka, nw, cus, stream);
-	default: return launch_shadow<false, 1>(ka, nw, cus, stream);
-	}
+	if (occ == 8)
+		return wide ? launch_shadow<false, 8, true>(ka, nw, cus, stream) : launch_shadow<false, 8, false>(ka, nw, cus, stream);
+	return wide ? launch_shadow<false, 1, true>(ka, nw, cus, stream) : launch_shadow<false, 1, false>(ka, nw, cus, stream);
 }

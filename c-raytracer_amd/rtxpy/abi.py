@@ -67,7 +67,8 @@ class Stats(C.Structure):
                 ("bvh_depth", C.c_uint32), ("bvh_prims", C.c_uint32), ("waves", C.c_uint32),
                 ("chunks", C.c_uint32), ("builder", C.c_uint32),
                 ("shadow_box_tests", C.c_uint64), ("shadow_global_box_tests", C.c_uint64),
-                ("shadow_wave_steps", C.c_uint64), ("shadow_wave_walks", C.c_uint64)]
+                ("shadow_wave_steps", C.c_uint64), ("shadow_wave_walks", C.c_uint64),
+                ("wide_nodes", C.c_uint32), ("wide_depth", C.c_uint32)]
 
 
 RTX_BUILD_SAH_HOST, RTX_BUILD_LBVH_GPU = 0, 1

@@ -201,6 +201,8 @@ typedef struct rtx_stats {
 	uint64_t shadow_global_box_tests; /* ... of which read from the DQNode array (the rest from the LDS top copy) */
 	uint64_t shadow_wave_steps;       /* walk-loop iterations summed over waves (a wave steps until its longest ray ends) */
 	uint64_t shadow_wave_walks;       /* wave walks (64 lane slots each): steps / walks = the waves' mean walk length */
+	uint32_t wide_nodes;              /* 4-wide shadow-walk BVH nodes (0: k_shadow walks the threaded BVH2) */
+	uint32_t wide_depth;
 } rtx_stats;
 
 typedef struct rtx_ctx rtx_ctx;
