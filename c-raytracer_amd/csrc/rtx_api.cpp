@@ -20,6 +20,7 @@
 #include "rtx_device.h"
 #include "rtx_kat.h"
 #include "rtx_quant.h"
+#include "rtx_internal.h"
 
 extern "C" size_t rtx_trace_lds_bytes(uint32_t stack_size);
 extern "C" size_t rtx_shadow_lds_bytes(uint32_t stack_size);
@@ -50,7 +51,7 @@ extern "C" hipError_t rtx_launch_kat_shadow(int kind, uint32_t n, const float *i
 
 static thread_local char g_err[512] = "";
 
-static int fail(int code, const char *fmt, ...)
+int rtx_fail(int code, const char *fmt, ...)
 {
 	va_list ap;
 	va_start(ap, fmt);
@@ -59,56 +60,6 @@ static int fail(int code, const char *fmt, ...)
 	return code;
 }
 
-#define HIP_TRY(expr)                                                                                   \
-	do {                                                                                            \
-		hipError_t e_ = (expr);                                                                 \
-		if (e_ != hipSuccess)                                                                   \
-			return fail(RTX_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));        \
-	} while (0)
-
-struct rtx_ctx {
-	int device = 0;
-	int builder = RTX_BUILD_SAH_HOST;
-	hipStream_t stream = nullptr;
-	hipEvent_t ev0 = nullptr, ev1 = nullptr;
-	int cus = 0;
-	/* scene */
-	DNode *d_nodes = nullptr;
-	DPlane *d_planes = nullptr;
-	DMaterial *d_mats = nullptr;
-	DEmitter *d_emitters = nullptr;
-	DQNode *d_qnodes = nullptr;
-	uint32_t *d_top = nullptr;
-	DQNode *d_wnodes = nullptr;
-	DScene scene{};
-	bool have_scene = false;
-	/* work buffers (grow-only) */
-	DTask *d_tasks = nullptr;
-	size_t task_bytes = 0;
-	float4 *d_staging = nullptr;
-	size_t staging_bytes = 0;
-	float4 *d_sp = nullptr;
-	size_t sp_bytes = 0;
-	float4 *d_contrib = nullptr;
-	size_t contrib_bytes = 0;
-	uint2 *d_tile_rec = nullptr;
-	size_t tile_rec_bytes = 0;
-	uint32_t *d_sortbuf = nullptr; /* keys0 | keys1 | vals0 | vals1 (shade-point sort) */
-	size_t sortbuf_bytes = 0;
-	void *d_sorttmp = nullptr;
-	size_t sorttmp_bytes = 0;
-	int *d_post_rad = nullptr; /* postprocess: per-pixel DoF radius, pv, scratch */
-	float4 *d_post_pv = nullptr;
-	size_t post_pixels = 0;
-	unsigned *d_post_scratch = nullptr;
-	float bound_lo[3] = { 0, 0, 0 }, bound_hi[3] = { 0, 0, 0 }; /* bounded objects' box */
-	hipEvent_t ev[5] = { nullptr, nullptr, nullptr, nullptr, nullptr };
-	uint32_t total_lights = 0;
-	unsigned long long *d_ctr = nullptr;
-	float *d_rgb = nullptr, *d_z = nullptr;
-	size_t fb_pixels = 0;
-	rtx_stats stats{};
-};
 
 extern "C" const char *rtx_last_error(void)
 {
@@ -143,12 +94,6 @@ extern "C" int rtx_device_count(int *count)
 	return RTX_OK;
 }
 
-template <class T> static void dfree(T *&p)
-{
-	if (p)
-		(void)hipFree(p);
-	p = nullptr;
-}
 
 static void free_scene(rtx_ctx *c)
 {
@@ -226,15 +171,6 @@ extern "C" int rtx_open(int device, rtx_ctx **out)
 	return RTX_OK;
 }
 
-template <class T> static int upload(T *&dst, const std::vector<T> &v)
-{
-	dfree(dst);
-	size_t n = std::max<size_t>(v.size(), 1);
-	HIP_TRY(hipMalloc(&dst, n * sizeof(T)));
-	if (!v.empty())
-		HIP_TRY(hipMemcpy(dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
-	return RTX_OK;
-}
 
 /* DQNode preorder of the subtree at device ref `ref` (rtx_device.h): the node itself with the
  * box it has in its parent, then its left and right subtrees.  An inner node's link is the
@@ -250,9 +186,6 @@ static uint32_t thread_sizes(const std::vector<DNode> &recs, uint32_t ref, std::
 	return size[i];
 }
 
-struct QFrame {
-	float qo[3], qs[3];
-};
 
 /* one plane pair quantised conservatively (rtx_quant.h) */
 static uint32_t quantise(float lo, float hi, float qo, float qs) { return rtx_quantise(lo, hi, qo, qs); }
@@ -441,13 +374,12 @@ static uint32_t wide_bvh(const std::vector<DNode> &inner, uint32_t root_ref, con
 	return wide_emit(inner, F, root_ref, 0, out);
 }
 
+
 static inline float pad_lo(float x, float ext) { return x - (std::fabs(x) + ext) * 2e-6f - 1e-30f; }
 static inline float pad_hi(float x, float ext) { return x + (std::fabs(x) + ext) * 2e-6f + 1e-30f; }
 
-extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
+int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 {
-	if (!c || !sc)
-		return fail(RTX_ERR_ARG, "null argument");
 	if (!sc->num_materials || !sc->materials)
 		return fail(RTX_ERR_SCENE, "scene has no materials");
 	if (sc->num_objects && !sc->objects)
@@ -456,6 +388,7 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 		return fail(RTX_ERR_ARG, "emitters pointer is null");
 	HIP_TRY(hipSetDevice(c->device));
 	free_scene(c);
+	hs.builder = c->builder;
 
 	if (sc->num_materials > RTX_META_MAT)
 		return fail(RTX_ERR_SCENE, "too many materials (%u)", sc->num_materials);
@@ -629,6 +562,7 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 		if (e != hipSuccess)
 			return fail(RTX_ERR_HIP, "GPU BVH build failed: %s", hipGetErrorString(e));
 		c->d_nodes = recs;
+		hs.recs_on_device = true;
 		if (root_ref == RTX_EMPTY_REF) /* nb <= max_leaf: a single leaf */
 			root_ref = RTX_REF_LEAF | sph | (nb - 1);
 		if (((uint64_t)nnodes + nb) * sizeof(DNode) > 0xFFFFFFC0ull)
@@ -637,6 +571,10 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 		inner.resize(nnodes);
 		if (nnodes)
 			HIP_TRY(hipMemcpy(inner.data(), recs, nnodes * sizeof(DNode), hipMemcpyDeviceToHost));
+		if (hs.want_host_recs) { /* the other devices of a group get the records from the host */
+			hs.recs.resize((size_t)nnodes + nb);
+			HIP_TRY(hipMemcpy(hs.recs.data(), recs, hs.recs.size() * sizeof(DNode), hipMemcpyDeviceToHost));
+		}
 	} else {
 		BvhOutput bvh;
 		bvh_build(BvhInput{ nb, lo.data(), hi.data() }, cfg, bvh);
@@ -671,75 +609,101 @@ extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
 		}
 		if (nb)
 			memcpy(recs.data() + nnodes, prims.data(), nb * sizeof(DPrim));
-		if ((rc = upload(c->d_nodes, recs)))
-			return rc;
 		root_ref = dref(bvh.root_ref);
 		depth = bvh.depth;
 		inner.assign(recs.begin(), recs.begin() + nnodes);
+		hs.recs = std::move(recs);
 	}
-	std::vector<DQNode> qnodes;
 	std::vector<uint32_t> qdepth;
-	QFrame qf;
-	thread_bvh(inner, nb ? root_ref : RTX_EMPTY_REF, c->bound_lo, c->bound_hi, qnodes, qf, qdepth);
-	if (qnodes.size() >= (1u << 26))
-		return fail(RTX_ERR_SCENE, "scene too large: %zu threaded BVH nodes (max 2^26)", qnodes.size());
-	if ((rc = upload(c->d_qnodes, qnodes)))
-		return rc;
-	std::vector<uint32_t> qtop;
-	const uint32_t ntop = thread_top(qnodes, qdepth, qtop);
-	if ((rc = upload(c->d_top, qtop)))
-		return rc;
-	std::vector<DQNode> wnodes;
-	uint32_t wdepth = 0;
+	thread_bvh(inner, nb ? root_ref : RTX_EMPTY_REF, c->bound_lo, c->bound_hi, hs.qnodes, hs.qf, qdepth);
+	if (hs.qnodes.size() >= (1u << 26))
+		return fail(RTX_ERR_SCENE, "scene too large: %zu threaded BVH nodes (max 2^26)", hs.qnodes.size());
+	hs.ntop = thread_top(hs.qnodes, qdepth, hs.qtop);
 	const char *we = getenv("RTX_WIDE"); /* measurement: RTX_WIDE=0 keeps the threaded BVH2 walk */
 	if (!(we && atoi(we) == 0)) {
-		wdepth = wide_bvh(inner, nb ? root_ref : RTX_EMPTY_REF, c->bound_lo, c->bound_hi, qf, wnodes);
-		if (wdepth > RTX_W_STACK + 1 || wnodes.size() / 4 >= (1u << 26)) /* the lane stacks would overflow */
-			wnodes.clear();
+		hs.wdepth = wide_bvh(inner, nb ? root_ref : RTX_EMPTY_REF, c->bound_lo, c->bound_hi, hs.qf, hs.wnodes);
+		if (hs.wdepth > RTX_W_STACK + 1 || hs.wnodes.size() / 4 >= (1u << 26)) /* the lane stacks would overflow */
+			hs.wnodes.clear();
 	}
-	if ((rc = upload(c->d_wnodes, wnodes)))
-		return rc;
-	c->stats.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count();
-	if ((rc = upload(c->d_planes, planes)) || (rc = upload(c->d_mats, mats)) || (rc = upload(c->d_emitters, emit)))
-		return rc;
+	if (hs.wnodes.empty())
+		hs.wdepth = 0;
+	hs.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count();
+	hs.mats = std::move(mats);
+	hs.planes = std::move(planes);
+	hs.emit = std::move(emit);
+	hs.nnodes = nnodes;
+	hs.nb = nb;
+	hs.root_ref = nb ? root_ref : RTX_EMPTY_REF;
+	hs.depth = depth;
+	memcpy(hs.bound_lo, c->bound_lo, 12);
+	memcpy(hs.bound_hi, c->bound_hi, 12);
+	memcpy(hs.ambient, sc->ambient, 12);
+	hs.num_emitters = sc->num_emitters;
+	return RTX_OK;
+}
 
+/* the built scene onto c's device (c->d_nodes already holds the records when the device
+ * builder ran on c) */
+int rtx_upload_built(rtx_ctx *c, const HostScene &hs)
+{
+	int rc;
+	HIP_TRY(hipSetDevice(c->device));
+	if (!(hs.recs_on_device && c->d_nodes) && (rc = upload(c->d_nodes, hs.recs)))
+		return rc;
+	if ((rc = upload(c->d_qnodes, hs.qnodes)) || (rc = upload(c->d_top, hs.qtop)) || (rc = upload(c->d_wnodes, hs.wnodes)) ||
+	    (rc = upload(c->d_planes, hs.planes)) || (rc = upload(c->d_mats, hs.mats)) || (rc = upload(c->d_emitters, hs.emit)))
+		return rc;
+	memcpy(c->bound_lo, hs.bound_lo, 12);
+	memcpy(c->bound_hi, hs.bound_hi, 12);
 	DScene &S = c->scene;
 	memset(&S, 0, sizeof(S));
 	S.nodes = c->d_nodes;
-	S.num_nodes = nnodes;
-	S.prims = (const DPrim *)(c->d_nodes + nnodes);
+	S.num_nodes = hs.nnodes;
+	S.prims = (const DPrim *)(c->d_nodes + hs.nnodes);
 	S.planes = c->d_planes;
 	S.mats = c->d_mats;
 	S.emitters = c->d_emitters;
-	S.qnodes = qnodes.empty() ? nullptr : c->d_qnodes;
-	S.num_qnodes = (uint32_t)qnodes.size();
-	memcpy(S.qo, qf.qo, 12);
-	memcpy(S.qs, qf.qs, 12);
-	S.top = ntop ? c->d_top : nullptr;
-	S.num_top = ntop;
-	S.wnodes = wnodes.empty() ? nullptr : c->d_wnodes;
-	S.num_wnodes = (uint32_t)(wnodes.size() / 4);
-	S.wdepth = wnodes.empty() ? 0 : wdepth;
-	S.root_ref = nb ? root_ref : RTX_EMPTY_REF;
-	S.num_prims = nb;
-	S.num_planes = (uint32_t)planes.size();
-	S.num_emitters = sc->num_emitters;
-	S.stack_size = std::max<uint32_t>(depth + 1, 4);
+	S.qnodes = hs.qnodes.empty() ? nullptr : c->d_qnodes;
+	S.num_qnodes = (uint32_t)hs.qnodes.size();
+	memcpy(S.qo, hs.qf.qo, 12);
+	memcpy(S.qs, hs.qf.qs, 12);
+	S.top = hs.ntop ? c->d_top : nullptr;
+	S.num_top = hs.ntop;
+	S.wnodes = hs.wnodes.empty() ? nullptr : c->d_wnodes;
+	S.num_wnodes = (uint32_t)(hs.wnodes.size() / 4);
+	S.wdepth = hs.wdepth;
+	S.root_ref = hs.root_ref;
+	S.num_prims = hs.nb;
+	S.num_planes = (uint32_t)hs.planes.size();
+	S.num_emitters = hs.num_emitters;
+	S.stack_size = std::max<uint32_t>(hs.depth + 1, 4);
 	c->total_lights = 0;
-	for (const DEmitter &e : emit)
+	for (const DEmitter &e : hs.emit)
 		c->total_lights += e.num_lights;
-	memcpy(S.ambient, sc->ambient, 12);
+	memcpy(S.ambient, hs.ambient, 12);
 	c->have_scene = true;
-	c->stats.bvh_nodes = nnodes;
-	c->stats.bvh_depth = depth;
-	c->stats.builder = (uint32_t)c->builder;
-	c->stats.bvh_prims = nb;
+	c->stats.build_ms = hs.build_ms;
+	c->stats.bvh_nodes = hs.nnodes;
+	c->stats.bvh_depth = hs.depth;
+	c->stats.builder = (uint32_t)hs.builder;
+	c->stats.bvh_prims = hs.nb;
 	c->stats.wide_nodes = S.num_wnodes;
 	c->stats.wide_depth = S.wdepth;
 	return RTX_OK;
 }
 
-static int render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, float *d_rgb, float *d_z,
+extern "C" int rtx_upload_scene(rtx_ctx *c, const rtx_scene_desc *sc)
+{
+	if (!c || !sc)
+		return fail(RTX_ERR_ARG, "null argument");
+	HostScene hs;
+	int rc = rtx_build_scene(c, sc, hs);
+	if (rc)
+		return rc;
+	return rtx_upload_built(c, hs);
+}
+
+int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, float *d_rgb, float *d_z,
 			 hipStream_t stream)
 {
 	if (!c->have_scene)
@@ -816,7 +780,10 @@ static int render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, f
 	while (slot_b < 64 && slot_b < c->total_lights)
 		slot_b <<= 1;
 	const uint32_t slots_per_point = (std::max<uint32_t>(c->total_lights, 1) + slot_b - 1) / slot_b;
-	const uint32_t per_wave = std::max<uint32_t>(1, std::min<uint32_t>(64, 1024 / (slot_b * slots_per_point)));
+	uint32_t grab = 4096; /* lane slots per k_shadow queue grab (RTX_SH_LANES: measurement; 1024 -> 4096: 903 -> 885 ms) */
+	if (const char *ge = getenv("RTX_SH_LANES"))
+		grab = (uint32_t)std::max(1, atoi(ge));
+	const uint32_t per_wave = std::max<uint32_t>(1, std::min<uint32_t>(64, grab / (slot_b * slots_per_point)));
 	const char *se = getenv("RTX_SPSORT");
 	const bool spsort = !(se && se[0] == '0');
 	for (uint32_t begin = 0; begin < P.ntiles;) {
@@ -903,6 +870,7 @@ static int render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, f
 	st.shadow_global_box_tests = ctr[RTX_C_SGBOXES];
 	st.shadow_wave_steps = ctr[RTX_C_SSTEPS];
 	st.shadow_wave_walks = ctr[RTX_C_SWALKS];
+	st.shadow_leaf_rounds = ctr[RTX_C_SLEAFR];
 	st.node_visits = ctr[RTX_C_NODES] + st.shadow_node_visits;
 	st.tri_tests = ctr[RTX_C_TRIS] + ctr[RTX_C_STRIS];
 	st.sphere_tests = ctr[RTX_C_SPHERES] + ctr[RTX_C_SSPHERES];
@@ -924,7 +892,7 @@ extern "C" int rtx_render_device(rtx_ctx *c, const rtx_frame *fr, const rtx_para
 	if (!c)
 		return fail(RTX_ERR_ARG, "null context");
 	HIP_TRY(hipSetDevice(c->device));
-	return render_common(c, fr, p, (float *)d_rgb, (float *)d_z, stream ? (hipStream_t)stream : c->stream);
+	return rtx_render_common(c, fr, p, (float *)d_rgb, (float *)d_z, stream ? (hipStream_t)stream : c->stream);
 }
 
 extern "C" int rtx_render(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, float *rgb, float *z)
@@ -947,7 +915,7 @@ extern "C" int rtx_render(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, 
 		if (z)
 			HIP_TRY(hipMemcpyAsync(c->d_z, z, px * 4, hipMemcpyHostToDevice, c->stream));
 	}
-	int rc = render_common(c, fr, p, rgb ? c->d_rgb : nullptr, z ? c->d_z : nullptr, c->stream);
+	int rc = rtx_render_common(c, fr, p, rgb ? c->d_rgb : nullptr, z ? c->d_z : nullptr, c->stream);
 	if (rc)
 		return rc;
 	if (rgb)

@@ -216,6 +216,7 @@ enum {
 	RTX_C_SPLANES,
 	RTX_C_SSTEPS,       /* ... walk-loop iterations of the waves */
 	RTX_C_SWALKS,       /* ... wave walks (64 shadow rays each) */
+	RTX_C_SLEAFR,       /* ... 4-wide walk: wave iterations of the leaf loop (rounds of primitive fetches) */
 	RTX_C_N
 };
 

@@ -1,0 +1,384 @@
+/*
+ * Multi-device C-ABI (include/rtx.h rtx_group_*): one frame rendered by n MI355X devices of
+ * one process.  Replaces the reference's parallel point, the OpenMP row loop of render()
+ * (render.c:349-352), with a tile deal over devices:
+ *
+ *   upload   the scene is flattened and its BVHs built ONCE on the host (rtx_build_scene,
+ *            the work of accel_init, accel.c:266-315), then uploaded to every device
+ *   render   device r renders tiles t = r (mod n) on its own host thread (rtx_render_common
+ *            with tile_offset r, tile_stride n), into its own HBM framebuffer
+ *   gather   devices r > 0 pack their shard into 16-byte {r, g, b, z} tile records
+ *            (rtx_gather.hip), and one grouped ncclSend / ncclRecv moves them to device 0
+ *            over xGMI (RCCL, one communicator per device, ncclCommInitAll); device 0
+ *            unpacks them into its frame, which is copied to the caller.
+ *
+ * At 1080p a shard is 4.1 MB / n per device; the gather is a few tens of microseconds of
+ * link time.  With n = 1 no communicator is created.
+ */
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <string.h>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "rtx_internal.h"
+#include "rtx_tiles.h"
+
+extern "C" hipError_t rtx_launch_tile_pack(const float *rgb, const float *z, uint32_t w, uint32_t h, uint32_t off,
+					   uint32_t stride, float4 *out, hipStream_t stream);
+extern "C" hipError_t rtx_launch_tile_unpack(const float4 *in, uint32_t w, uint32_t h, uint32_t off, uint32_t stride,
+					     float *rgb, float *z, hipStream_t stream);
+
+#define NCCL_TRY(expr)                                                                                  \
+	do {                                                                                            \
+		ncclResult_t r_ = (expr);                                                               \
+		if (r_ != ncclSuccess)                                                                  \
+			return fail(RTX_ERR_HIP, "%s failed: %s", #expr, ncclGetErrorString(r_));       \
+	} while (0)
+
+struct rtx_group {
+	int n = 0;
+	std::vector<rtx_ctx *> ctx;
+	std::vector<ncclComm_t> comm;  /* n > 1: one per device, rank r = ctx[r] */
+	std::vector<float4 *> d_buf;   /* r > 0: shard r's packed records on device r */
+	std::vector<float4 *> d_recv;  /* r > 0: shard r's records received on device 0 */
+	std::vector<size_t> buf_recs;  /* capacity of d_buf[r] / d_recv[r] in records */
+	rtx_stats stats{};
+};
+
+extern "C" void rtx_group_close(rtx_group *g)
+{
+	if (!g)
+		return;
+	for (int r = 0; r < (int)g->ctx.size(); r++) {
+		if (!g->ctx[r])
+			continue;
+		(void)hipSetDevice(g->ctx[r]->device);
+		if (r < (int)g->d_buf.size())
+			dfree(g->d_buf[r]);
+	}
+	if (!g->ctx.empty() && g->ctx[0]) {
+		(void)hipSetDevice(g->ctx[0]->device);
+		for (auto &p : g->d_recv)
+			dfree(p);
+	}
+	for (ncclComm_t c : g->comm)
+		if (c)
+			(void)ncclCommDestroy(c);
+	for (rtx_ctx *c : g->ctx)
+		rtx_close(c);
+	delete g;
+}
+
+extern "C" int rtx_group_open(int n, const int *devices, rtx_group **out)
+{
+	if (!out)
+		return fail(RTX_ERR_ARG, "null out");
+	*out = nullptr;
+	if (n < 1 || n > 64)
+		return fail(RTX_ERR_ARG, "group of %d devices (1..64)", n);
+	std::vector<int> dev(n);
+	for (int r = 0; r < n; r++) {
+		dev[r] = devices ? devices[r] : r;
+		for (int q = 0; q < r; q++)
+			if (dev[q] == dev[r])
+				return fail(RTX_ERR_ARG, "device %d listed twice", dev[r]);
+	}
+	rtx_group *g = new rtx_group();
+	g->n = n;
+	g->ctx.assign(n, nullptr);
+	g->d_buf.assign(n, nullptr);
+	g->d_recv.assign(n, nullptr);
+	g->buf_recs.assign(n, 0);
+	for (int r = 0; r < n; r++) {
+		int rc = rtx_open(dev[r], &g->ctx[r]);
+		if (rc) {
+			rtx_group_close(g);
+			return rc;
+		}
+	}
+	if (n > 1) {
+		g->comm.assign(n, nullptr);
+		ncclResult_t e = ncclCommInitAll(g->comm.data(), n, dev.data());
+		if (e != ncclSuccess) {
+			g->comm.assign(n, nullptr);
+			rtx_group_close(g);
+			return fail(RTX_ERR_HIP, "ncclCommInitAll over %d devices failed: %s", n, ncclGetErrorString(e));
+		}
+	}
+	*out = g;
+	return RTX_OK;
+}
+
+extern "C" int rtx_group_size(const rtx_group *g) { return g ? g->n : 0; }
+
+extern "C" int rtx_group_set_builder(rtx_group *g, int builder)
+{
+	if (!g)
+		return fail(RTX_ERR_ARG, "null group");
+	for (rtx_ctx *c : g->ctx) {
+		int rc = rtx_set_builder(c, builder);
+		if (rc)
+			return rc;
+	}
+	return RTX_OK;
+}
+
+extern "C" int rtx_group_upload_scene(rtx_group *g, const rtx_scene_desc *sc)
+{
+	if (!g || !sc)
+		return fail(RTX_ERR_ARG, "null argument");
+	HostScene hs;
+	hs.want_host_recs = g->n > 1;
+	int rc = rtx_build_scene(g->ctx[0], sc, hs);
+	if (rc)
+		return rc;
+	const bool built_on_device = hs.recs_on_device;
+	for (int r = 0; r < g->n; r++) {
+		/* only the building device (ctx[0]) holds device-built records; the others take the
+		 * host copy (hs.want_host_recs) */
+		hs.recs_on_device = built_on_device && r == 0;
+		if ((rc = rtx_upload_built(g->ctx[r], hs)))
+			return rc;
+	}
+	return RTX_OK;
+}
+
+static int grow_recs(float4 *&p, size_t &have, size_t need)
+{
+	if (need <= have)
+		return RTX_OK;
+	dfree(p);
+	have = 0;
+	HIP_TRY(hipMalloc(&p, need * sizeof(float4)));
+	have = need;
+	return RTX_OK;
+}
+
+static int ensure_fb(rtx_ctx *c, size_t px)
+{
+	if (px <= c->fb_pixels)
+		return RTX_OK;
+	dfree(c->d_rgb);
+	dfree(c->d_z);
+	HIP_TRY(hipMalloc(&c->d_rgb, px * 3 * sizeof(float)));
+	HIP_TRY(hipMalloc(&c->d_z, px * sizeof(float)));
+	c->fb_pixels = px;
+	return RTX_OK;
+}
+
+extern "C" int rtx_group_render(rtx_group *g, const rtx_frame *fr, const rtx_params *p, float *rgb, float *z)
+{
+	if (!g || !fr || !p)
+		return fail(RTX_ERR_ARG, "null argument");
+	if (p->tile_offset != 0 || p->tile_stride != 1)
+		return fail(RTX_ERR_ARG, "rtx_group_render shards the frame itself (tile_offset 0, tile_stride 1 expected)");
+	for (rtx_ctx *c : g->ctx)
+		if (!c->have_scene)
+			return fail(RTX_ERR_STATE, "render before rtx_group_upload_scene");
+	const int n = g->n;
+	const uint32_t w = fr->width, h = fr->height;
+	const size_t px = (size_t)w * h;
+	for (rtx_ctx *c : g->ctx) {
+		HIP_TRY(hipSetDevice(c->device));
+		int rc = ensure_fb(c, px);
+		if (rc)
+			return rc;
+	}
+	/* every shard on its own host thread (rtx_render_common synchronises its stream) */
+	std::vector<int> rcs(n, RTX_OK);
+	std::vector<std::string> errs(n);
+	auto shard = [&](int r) {
+		rtx_ctx *c = g->ctx[r];
+		if (hipSetDevice(c->device) != hipSuccess) {
+			rcs[r] = RTX_ERR_HIP;
+			errs[r] = "hipSetDevice failed";
+			return;
+		}
+		rtx_params pr = *p;
+		pr.tile_offset = (uint32_t)r;
+		pr.tile_stride = (uint32_t)n;
+		rcs[r] = rtx_render_common(c, fr, &pr, c->d_rgb, c->d_z, c->stream);
+		if (rcs[r])
+			errs[r] = rtx_last_error();
+	};
+	if (n == 1) {
+		shard(0);
+	} else {
+		std::vector<std::thread> th;
+		for (int r = 0; r < n; r++)
+			th.emplace_back(shard, r);
+		for (auto &t : th)
+			t.join();
+	}
+	for (int r = 0; r < n; r++)
+		if (rcs[r])
+			return fail(rcs[r], "device %d: %s", g->ctx[r]->device, errs[r].c_str());
+
+	const auto tg0 = std::chrono::steady_clock::now();
+	rtx_ctx *c0 = g->ctx[0];
+	if (n > 1) {
+		/* pack on every shard device, then one grouped send/recv to device 0 */
+		for (int r = 1; r < n; r++) {
+			rtx_ctx *c = g->ctx[r];
+			const size_t recs = rtx_tile_pack_count(w, h, (uint32_t)r, (uint32_t)n);
+			size_t cap = g->buf_recs[r], cap0 = g->buf_recs[r];
+			HIP_TRY(hipSetDevice(c->device));
+			int rc = grow_recs(g->d_buf[r], cap, recs);
+			if (rc)
+				return rc;
+			HIP_TRY(hipSetDevice(c0->device));
+			if ((rc = grow_recs(g->d_recv[r], cap0, recs)))
+				return rc;
+			g->buf_recs[r] = std::min(cap, cap0);
+			HIP_TRY(hipSetDevice(c->device));
+			HIP_TRY(rtx_launch_tile_pack(c->d_rgb, c->d_z, w, h, (uint32_t)r, (uint32_t)n, g->d_buf[r], c->stream));
+		}
+		NCCL_TRY(ncclGroupStart());
+		for (int r = 1; r < n; r++) {
+			const size_t floats = rtx_tile_pack_count(w, h, (uint32_t)r, (uint32_t)n) * 4;
+			if (!floats)
+				continue;
+			NCCL_TRY(ncclSend(g->d_buf[r], floats, ncclFloat, 0, g->comm[r], g->ctx[r]->stream));
+			NCCL_TRY(ncclRecv(g->d_recv[r], floats, ncclFloat, r, g->comm[0], c0->stream));
+		}
+		NCCL_TRY(ncclGroupEnd());
+		HIP_TRY(hipSetDevice(c0->device));
+		for (int r = 1; r < n; r++)
+			HIP_TRY(rtx_launch_tile_unpack(g->d_recv[r], w, h, (uint32_t)r, (uint32_t)n, c0->d_rgb, c0->d_z, c0->stream));
+		for (int r = 1; r < n; r++) {
+			HIP_TRY(hipSetDevice(g->ctx[r]->device));
+			HIP_TRY(hipStreamSynchronize(g->ctx[r]->stream));
+		}
+		HIP_TRY(hipSetDevice(c0->device));
+		HIP_TRY(hipStreamSynchronize(c0->stream));
+	}
+	const double gather_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tg0).count();
+	HIP_TRY(hipSetDevice(c0->device));
+	if (rgb)
+		HIP_TRY(hipMemcpy(rgb, c0->d_rgb, px * 12, hipMemcpyDeviceToHost));
+	if (z)
+		HIP_TRY(hipMemcpy(z, c0->d_z, px * 4, hipMemcpyDeviceToHost));
+
+	/* statistics: counts summed, times of the slowest device */
+	rtx_stats s = c0->stats;
+	for (int r = 1; r < n; r++) {
+		const rtx_stats &o = g->ctx[r]->stats;
+		s.closest_rays += o.closest_rays;
+		s.shadow_rays += o.shadow_rays;
+		s.node_visits += o.node_visits;
+		s.tri_tests += o.tri_tests;
+		s.sphere_tests += o.sphere_tests;
+		s.plane_tests += o.plane_tests;
+		s.shadow_node_visits += o.shadow_node_visits;
+		s.shadow_tri_tests += o.shadow_tri_tests;
+		s.shadow_sphere_tests += o.shadow_sphere_tests;
+		s.shadow_plane_tests += o.shadow_plane_tests;
+		s.shade_points += o.shade_points;
+		s.shadow_box_tests += o.shadow_box_tests;
+		s.shadow_global_box_tests += o.shadow_global_box_tests;
+		s.shadow_wave_steps += o.shadow_wave_steps;
+		s.shadow_wave_walks += o.shadow_wave_walks;
+		s.shadow_leaf_rounds += o.shadow_leaf_rounds;
+		s.waves += o.waves;
+		s.chunks += o.chunks;
+		s.kernel_ms = std::max(s.kernel_ms, o.kernel_ms);
+		s.trace_ms = std::max(s.trace_ms, o.trace_ms);
+		s.shadow_ms = std::max(s.shadow_ms, o.shadow_ms);
+		s.accum_ms = std::max(s.accum_ms, o.accum_ms);
+		s.sort_ms = std::max(s.sort_ms, o.sort_ms);
+	}
+	s.gather_ms = n > 1 ? gather_ms : 0.0;
+	s.devices = (uint32_t)n;
+	g->stats = s;
+	return RTX_OK;
+}
+
+extern "C" int rtx_group_get_stats(const rtx_group *g, rtx_stats *out)
+{
+	if (!g || !out)
+		return fail(RTX_ERR_ARG, "null argument");
+	*out = g->stats;
+	return RTX_OK;
+}
+
+/* ---- tile records: host reference and device entry points (rtx_tiles.h) ---- */
+
+extern "C" size_t rtx_tile_pack_count(uint32_t w, uint32_t h, uint32_t off, uint32_t stride)
+{
+	if (!stride || off >= stride)
+		return 0;
+	return (size_t)rtx_shard_tiles(w, h, off, stride) * RTX_TILE_PX;
+}
+
+extern "C" int rtx_tile_pack_host(const float *rgb, const float *z, uint32_t w, uint32_t h, uint32_t off, uint32_t stride,
+				  float *out)
+{
+	if (!rgb || !z || !out || !stride || off >= stride)
+		return fail(RTX_ERR_ARG, "bad tile pack arguments");
+	const size_t nrec = rtx_tile_pack_count(w, h, off, stride);
+	const uint32_t tx = rtx_tiles_x(w);
+	for (size_t i = 0; i < nrec; i++) {
+		uint32_t x, y;
+		rtx_shard_pixel((uint32_t)i, tx, off, stride, &x, &y);
+		float *o = out + 4 * i;
+		if (x < w && y < h) {
+			const size_t p = (size_t)y * w + x;
+			o[0] = rgb[3 * p];
+			o[1] = rgb[3 * p + 1];
+			o[2] = rgb[3 * p + 2];
+			o[3] = z[p];
+		} else {
+			o[0] = o[1] = o[2] = o[3] = 0.f;
+		}
+	}
+	return RTX_OK;
+}
+
+extern "C" int rtx_tile_unpack_host(const float *in, uint32_t w, uint32_t h, uint32_t off, uint32_t stride, float *rgb,
+				    float *z)
+{
+	if (!in || !rgb || !z || !stride || off >= stride)
+		return fail(RTX_ERR_ARG, "bad tile unpack arguments");
+	const size_t nrec = rtx_tile_pack_count(w, h, off, stride);
+	const uint32_t tx = rtx_tiles_x(w);
+	for (size_t i = 0; i < nrec; i++) {
+		uint32_t x, y;
+		rtx_shard_pixel((uint32_t)i, tx, off, stride, &x, &y);
+		if (x >= w || y >= h)
+			continue;
+		const size_t p = (size_t)y * w + x;
+		rgb[3 * p] = in[4 * i];
+		rgb[3 * p + 1] = in[4 * i + 1];
+		rgb[3 * p + 2] = in[4 * i + 2];
+		z[p] = in[4 * i + 3];
+	}
+	return RTX_OK;
+}
+
+extern "C" int rtx_tile_pack_device(rtx_ctx *c, const void *d_rgb, const void *d_z, uint32_t w, uint32_t h, uint32_t off,
+				    uint32_t stride, void *d_out, void *stream)
+{
+	if (!c || !d_rgb || !d_z || !d_out || !stride || off >= stride)
+		return fail(RTX_ERR_ARG, "bad tile pack arguments");
+	HIP_TRY(hipSetDevice(c->device));
+	hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+	HIP_TRY(rtx_launch_tile_pack((const float *)d_rgb, (const float *)d_z, w, h, off, stride, (float4 *)d_out, s));
+	HIP_TRY(hipStreamSynchronize(s));
+	return RTX_OK;
+}
+
+extern "C" int rtx_tile_unpack_device(rtx_ctx *c, const void *d_in, uint32_t w, uint32_t h, uint32_t off, uint32_t stride,
+				      void *d_rgb, void *d_z, void *stream)
+{
+	if (!c || !d_in || !d_rgb || !d_z || !stride || off >= stride)
+		return fail(RTX_ERR_ARG, "bad tile unpack arguments");
+	HIP_TRY(hipSetDevice(c->device));
+	hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+	HIP_TRY(rtx_launch_tile_unpack((const float4 *)d_in, w, h, off, stride, (float *)d_rgb, (float *)d_z, s));
+	HIP_TRY(hipStreamSynchronize(s));
+	return RTX_OK;
+}

@@ -1,0 +1,120 @@
+/*
+ * Library-internal declarations shared by rtx_api.cpp (single-device C-ABI) and rtx_group.cpp
+ * (multi-device C-ABI): the device context, a host-built scene, and the render entry.
+ * Not installed; nothing outside librtx includes it.
+ */
+#ifndef RTX_INTERNAL_H
+#define RTX_INTERNAL_H
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "rtx.h"
+#include "rtx_device.h"
+
+/* sets the calling thread's rtx_last_error() message, returns code */
+int rtx_fail(int code, const char *fmt, ...);
+#define fail rtx_fail
+
+#define HIP_TRY(expr)                                                                                   \
+	do {                                                                                            \
+		hipError_t e_ = (expr);                                                                 \
+		if (e_ != hipSuccess)                                                                   \
+			return fail(RTX_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));        \
+	} while (0)
+
+template <class T> static inline void dfree(T *&p)
+{
+	if (p)
+		(void)hipFree(p);
+	p = nullptr;
+}
+
+template <class T> static inline int upload(T *&dst, const std::vector<T> &v)
+{
+	dfree(dst);
+	size_t n = std::max<size_t>(v.size(), 1);
+	HIP_TRY(hipMalloc(&dst, n * sizeof(T)));
+	if (!v.empty())
+		HIP_TRY(hipMemcpy(dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+	return RTX_OK;
+}
+
+struct rtx_ctx {
+	int device = 0;
+	int builder = RTX_BUILD_SAH_HOST;
+	hipStream_t stream = nullptr;
+	hipEvent_t ev0 = nullptr, ev1 = nullptr;
+	int cus = 0;
+	/* scene */
+	DNode *d_nodes = nullptr;
+	DPlane *d_planes = nullptr;
+	DMaterial *d_mats = nullptr;
+	DEmitter *d_emitters = nullptr;
+	DQNode *d_qnodes = nullptr;
+	uint32_t *d_top = nullptr;
+	DQNode *d_wnodes = nullptr;
+	DScene scene{};
+	bool have_scene = false;
+	/* work buffers (grow-only) */
+	DTask *d_tasks = nullptr;
+	size_t task_bytes = 0;
+	float4 *d_staging = nullptr;
+	size_t staging_bytes = 0;
+	float4 *d_sp = nullptr;
+	size_t sp_bytes = 0;
+	float4 *d_contrib = nullptr;
+	size_t contrib_bytes = 0;
+	uint2 *d_tile_rec = nullptr;
+	size_t tile_rec_bytes = 0;
+	uint32_t *d_sortbuf = nullptr; /* keys0 | keys1 | vals0 | vals1 (shade-point sort) */
+	size_t sortbuf_bytes = 0;
+	void *d_sorttmp = nullptr;
+	size_t sorttmp_bytes = 0;
+	int *d_post_rad = nullptr; /* postprocess: per-pixel DoF radius, pv, scratch */
+	float4 *d_post_pv = nullptr;
+	size_t post_pixels = 0;
+	unsigned *d_post_scratch = nullptr;
+	float bound_lo[3] = { 0, 0, 0 }, bound_hi[3] = { 0, 0, 0 }; /* bounded objects' box */
+	hipEvent_t ev[5] = { nullptr, nullptr, nullptr, nullptr, nullptr };
+	uint32_t total_lights = 0;
+	unsigned long long *d_ctr = nullptr;
+	float *d_rgb = nullptr, *d_z = nullptr;
+	size_t fb_pixels = 0;
+	rtx_stats stats{};
+};
+
+struct QFrame {
+	float qo[3], qs[3];
+};
+
+/* a scene flattened and its BVHs built on the host, ready to upload to one or more devices */
+struct HostScene {
+	int builder = RTX_BUILD_SAH_HOST;
+	bool want_host_recs = false;  /* device builder: copy the records back for other devices */
+	bool recs_on_device = false;  /* device builder: the building context holds the records */
+	std::vector<DNode> recs;      /* inner nodes then primitives (64-byte records) */
+	uint32_t nnodes = 0, nb = 0, root_ref = RTX_EMPTY_REF, depth = 0;
+	std::vector<DQNode> qnodes;   /* threaded BVH2 */
+	QFrame qf{};
+	std::vector<uint32_t> qtop;
+	uint32_t ntop = 0;
+	std::vector<DQNode> wnodes;   /* 4-wide BVH */
+	uint32_t wdepth = 0;
+	std::vector<DPlane> planes;
+	std::vector<DMaterial> mats;
+	std::vector<DEmitter> emit;
+	float bound_lo[3] = { 0, 0, 0 }, bound_hi[3] = { 0, 0, 0 }, ambient[3] = { 0, 0, 0 };
+	uint32_t num_emitters = 0;
+	double build_ms = 0;
+};
+
+/* flatten sc and build its BVHs (on c's device for the device builder), then upload to c */
+int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs);
+int rtx_upload_built(rtx_ctx *c, const HostScene &hs);
+/* one frame (or tile shard) into device buffers on stream */
+int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, float *d_rgb, float *d_z, hipStream_t stream);
+
+#endif

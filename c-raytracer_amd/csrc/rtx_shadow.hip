@@ -7,11 +7,12 @@
  * unbound planes, walks the BVH for any opaque blocker (multiplying the
  * transmittance of transparent ones), then evaluates Phong / Blinn.
  *
- * The walk: every lane walks its own shadow ray over the threaded, quantised
- * BVH (rtx_device.h DQNode), one 16-byte record per step and no stack (any-hit
- * needs no visit order: a hit box continues at the next record, a missed one
- * jumps to its skip link).  The top levels of the tree sit in LDS, copied once
- * per persistent 16-wave workgroup (DScene.top).
+ * The walk: every lane walks its own shadow ray over the 4-wide quantised BVH
+ * (rtx_device.h RTX_W_STACK, shadow_walk4): one 64-byte node per step, four box
+ * tests per memory round trip, pending siblings as (first child, slot mask)
+ * groups in a register and an LDS stack.  Scenes whose wide tree is too deep
+ * for the stack walk the threaded BVH2 instead (shadow_walk: one 16-byte
+ * record per step, no stack, the top levels in LDS).
  *
  * Scheduling: persistent workgroups; each wave takes `per_wave` shade points at
  * a time from a global queue in Morton order of their position (rtx_sort.hip),
@@ -29,12 +30,6 @@
 
 #ifndef RTX_DEBUG_NOWALK
 #define RTX_DEBUG_NOWALK 0 /* measurement only: skip the BVH walk (everything else in k_shadow stays) */
-#endif
-#ifndef RTX_SH_NOTOP
-#define RTX_SH_NOTOP 0 /* measurement: walk the DQNode array only, no LDS top */
-#endif
-#ifndef RTX_SH_DEFER
-#define RTX_SH_DEFER 0 /* leaf tests deferred until >= 1/N of the live lanes hold a leaf (0: test at once) */
 #endif
 #ifndef RTX_SHADOW_OCC_DEFAULT
 #define RTX_SHADOW_OCC_DEFAULT 8 /* waves per SIMD the walk is register-capped for */
@@ -158,6 +153,7 @@ struct ShadowCount {
 	u64 pln;       /* plane tests */
 	u64 steps;     /* walk-loop iterations of the waves (a wave runs until its longest ray ends) */
 	u64 walks;     /* wave walks (64 rays each) */
+	u64 lrounds;   /* 4-wide walk: wave iterations of the leaf loop */
 };
 
 /* one primitive record (a, b, c = its first 48 bytes) against this lane's shadow ray
@@ -232,91 +228,6 @@ __device__ __forceinline__ void shadow_walk(const QBvh &Q, const char *__restric
 	const uint32_t nt = Q.nt;
 	uint32_t t = tl >= 0.f ? 0u : nt, g = 0, ge = 0;
 	uint32_t nbox = 0, nglob = 0, ntri = 0, nsph = 0, nstep = 0;
-#if RTX_SH_NOTOP
-	/* measurement variant: the whole walk over the DQNode array (no LDS top copy) */
-	const uint32_t nq = Q.nq;
-	(void)t;
-	(void)ge;
-	for (g = tl >= 0.f ? 0u : nq; g < nq;) {
-		const uint4 nd = ldg4u(Q.q + g);
-		if (COUNT) {
-			nbox++;
-			nglob++;
-		}
-		const bool hit = box_hit_q<OCT>(nd, oi, invq, tl);
-		const uint32_t L = nd.w;
-		const bool leaf = (L & RTX_REF_LEAF) != 0;
-		g = (hit || leaf) ? g + 1 : L >> 6;
-		if (leaf && hit && shadow_leaf<COUNT>(L, recs, mats, o, d, tl, emit_obj, li, ntri, nsph)) {
-			tl = -1.f;
-			g = nq;
-		}
-	}
-	if (COUNT)
-		nstep = nbox;
-#elif RTX_SH_DEFER
-	/* Deferred leaves: a lane whose leaf box is hit records the leaf (p1, then p2) and walks on;
-	 * the wave runs the primitive tests for all its recorded leaves at once, when at least
-	 * 1/RTX_SH_DEFER of its live lanes hold one or no lane can step (a lane holding two waits).
-	 * Each lane still tests its leaves in walk order, so transmittance products are unchanged. */
-	uint32_t p1 = 0, p2 = 0;
-	for (;;) {
-		const bool more = t < nt || g < ge;
-		const bool stepping = more && p2 == 0;
-		const u64 sm = ballot(stepping), pm = ballot(p1 != 0);
-		if (COUNT)
-			nstep++;
-		if (!(sm | pm))
-			break;
-		if (pm && (!sm || popc64(pm) * RTX_SH_DEFER >= popc64(sm | pm))) {
-			if (p1 && shadow_leaf<COUNT>(p1, recs, mats, o, d, tl, emit_obj, li, ntri, nsph)) {
-				tl = -1.f;
-				t = nt;
-				ge = 0;
-				p2 = 0;
-			}
-			p1 = p2;
-			p2 = 0;
-			continue;
-		}
-		if (!stepping)
-			continue;
-		const bool ing = g < ge;
-		uint4 nd;
-		if (ing)
-			nd = ldg4u(Q.q + g);
-		else
-			nd = lds4u(Q.top + t);
-		if (COUNT) {
-			nbox++;
-			nglob += ing ? 1u : 0u;
-		}
-		const bool hit = box_hit_q<OCT>(nd, oi, invq, tl);
-		const uint32_t L = nd.w;
-		if (L & RTX_REF_LEAF) {
-			if (ing)
-				g++;
-			else
-				t++;
-			if (hit) {
-				if (p1)
-					p2 = L;
-				else
-					p1 = L;
-			}
-		} else if (ing) {
-			g = hit ? g + 1 : L >> 6;
-		} else if (L & RTX_QTOP_CUT) {
-			if (hit) {
-				g = L >> 6;
-				ge = lds1u(Q.tend + t);
-			}
-			t++;
-		} else {
-			t = hit ? t + 1 : L >> 6;
-		}
-	}
-#else
 	while (t < nt || g < ge) {
 		const bool ing = g < ge;
 		uint4 nd;
@@ -354,7 +265,6 @@ __device__ __forceinline__ void shadow_walk(const QBvh &Q, const char *__restric
 	}
 	if (COUNT)
 		nstep = nbox;
-#endif
 	if (COUNT) {
 		uint32_t a = nbox, b = ntri, c = nsph, gq = nglob;
 #pragma unroll
@@ -389,7 +299,7 @@ __device__ __forceinline__ void shadow_walk4(const QBvh &Q, const char *__restri
 	const f3 oi = mul3v(oq, invq);
 	uint32_t *stk = Q.stk;
 	uint32_t node = tl >= 0.f ? 0u : RTX_NONE, grp = 0, sp = 0;
-	uint32_t nbox = 0, ntri = 0, nsph = 0, nstep = 0;
+	uint32_t nbox = 0, ntri = 0, nsph = 0, nstep = 0, nlr = 0;
 	while (node != RTX_NONE) {
 		const DQNode *N = Q.w + 4 * (size_t)node;
 		const uint4 s0 = ldg4u(N), s1 = ldg4u(N + 1), s2 = ldg4u(N + 2), s3 = ldg4u(N + 3);
@@ -409,6 +319,15 @@ __device__ __forceinline__ void shadow_walk4(const QBvh &Q, const char *__restri
 				     ((s3.w & RTX_REF_LEAF) << 3)) >> 5;
 		uint32_t lm = hm & lf, im = hm & ~lf;
 		bool blocked = false;
+		if (COUNT) {
+			uint32_t r = 0;
+			for (uint32_t m = lm;; m &= m - 1) { /* rounds = the wave's largest leaf-hit count */
+				if (!ballot(m != 0))
+					break;
+				r++;
+			}
+			nlr += r;
+		}
 		while (lm) {
 			const uint32_t c = __builtin_ctz(lm);
 			lm &= lm - 1;
@@ -459,6 +378,7 @@ __device__ __forceinline__ void shadow_walk4(const QBvh &Q, const char *__restri
 		}
 		sc.boxes += uni(a);
 		sc.gboxes += uni(a);
+		sc.lrounds += uni(nlr);
 		sc.tris += uni(b);
 		sc.sph += uni(c);
 		sc.steps += uni(nstep);
@@ -678,7 +598,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 	uint32_t *off = off_w[wv], *nls = nls_w[wv], *sid = sid_w[wv];
 	float(*Ls)[WAVE] = Ls_w[wv];
 	uint32_t *stk = &wstk[wv][0][lane_id()];
-	ShadowCount sc = { 0, 0, 0, 0, 0, 0, 0 };
+	ShadowCount sc = { 0, 0, 0, 0, 0, 0, 0, 0 };
 	u64 rays_total = 0;
 	for (;;) {
 		reread_barrier();
@@ -787,6 +707,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 			atomicAdd(&ctr[RTX_C_SPLANES], sc.pln);
 			atomicAdd(&ctr[RTX_C_SSTEPS], sc.steps);
 			atomicAdd(&ctr[RTX_C_SWALKS], sc.walks);
+			atomicAdd(&ctr[RTX_C_SLEAFR], sc.lrounds);
 		}
 	}
 }
@@ -913,10 +834,11 @@ extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const
 	const bool wide = S->wnodes != nullptr;
 	if (count)
 		return wide ? launch_shadow<true, 1, true>(ka, nw, cus, stream) : launch_shadow<true, 1, false>(ka, nw, cus, stream);
-	/* occupancy variant (measurement): RTX_SHADOW_OCC = 1 (the compiler's choice) or 8 waves/SIMD */
+	/* occupancy variant (measurement): RTX_SHADOW_OCC = 1 (the compiler's choice) */
 	const char *env = getenv("RTX_SHADOW_OCC");
 	const int occ = env ? atoi(env) : RTX_SHADOW_OCC_DEFAULT;
-	if (occ == 8)
-		return wide ? launch_shadow<false, 8, true>(ka, nw, cus, stream) : launch_shadow<false, 8, false>(ka, nw, cus, stream);
+	constexpr int O = RTX_SHADOW_OCC_DEFAULT;
+	if (occ == O)
+		return wide ? launch_shadow<false, O, true>(ka, nw, cus, stream) : launch_shadow<false, O, false>(ka, nw, cus, stream);
 	return wide ? launch_shadow<false, 1, true>(ka, nw, cus, stream) : launch_shadow<false, 1, false>(ka, nw, cus, stream);
 }

@@ -8,14 +8,14 @@
  * MI355X path (rtx_upload_scene / rtx_render) and the host glue from
  * librtxscene.  Reference flags: -m -b -a -s -n -r -l -o -p -g -f (HELPTEXT,
  * main.c:23-53; -o is undocumented there).  Extensions:
- *   --gpus N     render tile shards on N devices (one thread each)
+ *   --gpus N     render on N devices (rtx_group: BVH built once, tiles dealt round-robin,
+ *                shards gathered to the first device over RCCL)
  *   --device D   first device (default 0)
  *   --seed S     counter-RNG seed (default 1)
  *   --rng const  every rand_flt() draw = 0.5 (the oracle's REF_CONST_RNG)
  *   --u32 wrap   float->uint32 texture conversion of a generic x86-64 build
  *                (default: AVX-512 saturating, like -march=native on AVX-512 hosts)
  */
-#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -67,34 +67,6 @@ static int argv_find(int argc, char **argv, const char *flag, int nargs)
 		if (rtx_hash_djb(argv[i]) == h)
 			return (i + nargs < argc) ? i : 0;
 	return 0;
-}
-
-typedef struct {
-	int device;
-	const rtx_scene_desc *desc;
-	const rtx_frame *frame;
-	rtx_params params;
-	float *rgb, *z;
-	int rc;
-	char err[512];
-	rtx_stats stats;
-} shard_job;
-
-static void *shard_main(void *arg)
-{
-	shard_job *j = (shard_job *)arg;
-	rtx_ctx *ctx = NULL;
-	j->rc = rtx_open(j->device, &ctx);
-	if (!j->rc)
-		j->rc = rtx_upload_scene(ctx, j->desc);
-	if (!j->rc)
-		j->rc = rtx_render(ctx, j->frame, &j->params, j->rgb, j->z);
-	if (!j->rc)
-		rtx_get_stats(ctx, &j->stats);
-	if (j->rc)
-		snprintf(j->err, sizeof(j->err), "%s", rtx_last_error());
-	rtx_close(ctx);
-	return NULL;
 }
 
 int main(int argc, char **argv)
@@ -149,53 +121,27 @@ int main(int argc, char **argv)
 	}
 	size_t px = (size_t)w * h;
 	float *rgb = calloc(px * 3, sizeof(float)), *z = calloc(px, sizeof(float));
-	shard_job *jobs = calloc((size_t)ngpu, sizeof(shard_job));
-	pthread_t *th = calloc((size_t)ngpu, sizeof(pthread_t));
-	if (!rgb || !z || !jobs || !th) {
+	int *devs = calloc((size_t)ngpu, sizeof(int));
+	if (!rgb || !z || !devs) {
 		LOG("Unable to allocate the framebuffer.");
 		return 1;
 	}
+	for (int g = 0; g < ngpu; g++)
+		devs[g] = dev0 + g;
 	LOG("Commencing raytracing on %d GPU(s).", ngpu);
-	for (int g = 0; g < ngpu; g++) {
-		jobs[g].device = dev0 + g;
-		jobs[g].desc = desc;
-		jobs[g].frame = &fr;
-		jobs[g].params = p;
-		jobs[g].params.tile_offset = (uint32_t)g;
-		jobs[g].params.tile_stride = (uint32_t)ngpu;
-		jobs[g].rgb = ngpu == 1 ? rgb : calloc(px * 3, sizeof(float));
-		jobs[g].z = ngpu == 1 ? z : calloc(px, sizeof(float));
-		if (!jobs[g].rgb || !jobs[g].z) {
-			LOG("Unable to allocate shard buffers.");
-			return 1;
-		}
-		pthread_create(&th[g], NULL, shard_main, &jobs[g]);
+	rtx_group *grp = NULL;
+	rtx_stats st;
+	if (rtx_group_open(ngpu, devs, &grp) || rtx_group_upload_scene(grp, desc) ||
+	    rtx_group_render(grp, &fr, &p, rgb, z) || rtx_group_get_stats(grp, &st)) {
+		LOG("%s", rtx_last_error());
+		rtx_group_close(grp);
+		return 1;
 	}
-	uint64_t closest = 0, shadow = 0;
-	double kms = 0;
-	for (int g = 0; g < ngpu; g++) {
-		pthread_join(th[g], NULL);
-		if (jobs[g].rc) {
-			LOG("GPU %d: %s", jobs[g].device, jobs[g].err);
-			return 1;
-		}
-		closest += jobs[g].stats.closest_rays;
-		shadow += jobs[g].stats.shadow_rays;
-		if (jobs[g].stats.kernel_ms > kms)
-			kms = jobs[g].stats.kernel_ms;
-	}
-	if (ngpu > 1) {
-		/* gather: tile t belongs to shard t % ngpu */
-		uint32_t tiles_x = (w + 7) / 8;
-		for (uint32_t y = 0; y < h; y++)
-			for (uint32_t x = 0; x < w; x++) {
-				uint32_t t = (y / 8) * tiles_x + x / 8;
-				const shard_job *j = &jobs[t % (uint32_t)ngpu];
-				size_t i = (size_t)y * w + x;
-				memcpy(rgb + 3 * i, j->rgb + 3 * i, 12);
-				z[i] = j->z[i];
-			}
-	}
+	rtx_group_close(grp);
+	const uint64_t closest = st.closest_rays, shadow = st.shadow_rays;
+	const double kms = st.kernel_ms;
+	if (ngpu > 1)
+		LOG("Gathered %d shards in %.3f ms.", ngpu, st.gather_ms);
 	LOG("Rays: %llu closest + %llu shadow in %.3f ms device time (%.1f Mrays/s).", (unsigned long long)closest,
 	    (unsigned long long)shadow, kms, kms > 0 ? (closest + shadow) / (kms * 1e3) : 0.0);
 

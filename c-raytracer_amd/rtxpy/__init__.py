@@ -270,3 +270,64 @@ def gpu_kat(kind, records, params=None):
     p = params or default_params()
     _check(rtx_lib().rtx_kat(kind, records.shape[0], records.ctypes.data, out.ctypes.data, C.byref(p)))
     return out
+
+
+class Group:
+    """Several HIP devices rendering one frame (rtx_group_open .. rtx_group_close): tiles dealt
+    round-robin over the devices, gathered to the first one over RCCL."""
+
+    def __init__(self, devices):
+        self.lib = rtx_lib()
+        self._g = C.c_void_p()
+        devs = (C.c_int * len(devices))(*devices)
+        _check(self.lib.rtx_group_open(len(devices), devs, C.byref(self._g)))
+        self.devices = list(devices)
+
+    def set_builder(self, builder):
+        _check(self.lib.rtx_group_set_builder(self._g, builder))
+
+    def upload(self, scene):
+        _check(self.lib.rtx_group_upload_scene(self._g, C.byref(scene.desc)))
+
+    def render(self, frame, params):
+        w, h = frame.width, frame.height
+        rgb = np.zeros((h, w, 3), np.float32)
+        z = np.zeros((h, w), np.float32)
+        _check(self.lib.rtx_group_render(self._g, C.byref(frame), C.byref(params), rgb.ctypes.data, z.ctypes.data))
+        return rgb, z
+
+    def stats(self):
+        s = Stats()
+        _check(self.lib.rtx_group_get_stats(self._g, C.byref(s)))
+        return s
+
+    def close(self):
+        if self._g:
+            self.lib.rtx_group_close(self._g)
+            self._g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def tile_pack(rgb, z, offset, stride):
+    """rtx_tile_pack_host: the shard's (N, 4) float32 tile records {r, g, b, z}."""
+    rgb = np.ascontiguousarray(rgb, dtype=np.float32)
+    z = np.ascontiguousarray(z, dtype=np.float32)
+    h, w = z.shape
+    lib = rtx_lib()
+    n = lib.rtx_tile_pack_count(w, h, offset, stride)
+    out = np.zeros((n, 4), np.float32)
+    _check(lib.rtx_tile_pack_host(rgb.ctypes.data, z.ctypes.data, w, h, offset, stride, out.ctypes.data))
+    return out
+
+
+def tile_unpack(records, rgb, z, offset, stride):
+    """rtx_tile_unpack_host: writes the shard's pixels of records into rgb / z in place."""
+    records = np.ascontiguousarray(records, dtype=np.float32)
+    assert rgb.dtype == np.float32 and rgb.flags.c_contiguous and z.dtype == np.float32 and z.flags.c_contiguous
+    h, w = z.shape
+    _check(rtx_lib().rtx_tile_unpack_host(records.ctypes.data, w, h, offset, stride, rgb.ctypes.data, z.ctypes.data))

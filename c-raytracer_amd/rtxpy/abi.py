@@ -68,7 +68,8 @@ class Stats(C.Structure):
                 ("chunks", C.c_uint32), ("builder", C.c_uint32),
                 ("shadow_box_tests", C.c_uint64), ("shadow_global_box_tests", C.c_uint64),
                 ("shadow_wave_steps", C.c_uint64), ("shadow_wave_walks", C.c_uint64),
-                ("wide_nodes", C.c_uint32), ("wide_depth", C.c_uint32)]
+                ("wide_nodes", C.c_uint32), ("wide_depth", C.c_uint32), ("shadow_leaf_rounds", C.c_uint64),
+                ("gather_ms", C.c_double), ("devices", C.c_uint32), ("pad_", C.c_uint32)]
 
 
 RTX_BUILD_SAH_HOST, RTX_BUILD_LBVH_GPU = 0, 1
@@ -95,7 +96,10 @@ KAT_NAMES = ["moller", "sphere", "plane", "slab", "noise", "texture", "sph_light
 # symbols include/rtx.h declares (checked by tests/test_abi.py)
 RTX_SYMBOLS = ["rtx_params_default", "rtx_device_count", "rtx_open", "rtx_upload_scene", "rtx_render",
                "rtx_render_device", "rtx_get_stats", "rtx_close", "rtx_last_error", "rtx_kat", "rtx_postprocess",
-               "rtx_postprocess_device", "rtx_set_builder"]
+               "rtx_postprocess_device", "rtx_set_builder", "rtx_group_open", "rtx_group_size",
+               "rtx_group_set_builder", "rtx_group_upload_scene", "rtx_group_render", "rtx_group_get_stats",
+               "rtx_group_close", "rtx_tile_pack_count", "rtx_tile_pack_host", "rtx_tile_unpack_host",
+               "rtx_tile_pack_device", "rtx_tile_unpack_device"]
 RTX_SCENE_SYMBOLS = ["rtx_scene_load", "rtx_scene_parse", "rtx_scene_desc_of", "rtx_scene_num_json_objects",
                      "rtx_scene_free", "rtx_scene_last_error", "rtx_frame_setup", "rtx_tiff_write", "rtx_hash_djb",
                      "rtx_params_from_argv", "rtx_stl_write", "rtx_tiff_read_raw", "rtx_buffer_free",
@@ -164,6 +168,34 @@ def declare_rtx(lib):
     lib.rtx_postprocess_device.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(Post), C.c_void_p,
                                            C.c_void_p, C.c_void_p]
     lib.rtx_postprocess_device.restype = C.c_int
+    lib.rtx_group_open.argtypes = [C.c_int, C.c_void_p, C.POINTER(C.c_void_p)]
+    lib.rtx_group_open.restype = C.c_int
+    lib.rtx_group_size.argtypes = [C.c_void_p]
+    lib.rtx_group_size.restype = C.c_int
+    lib.rtx_group_set_builder.argtypes = [C.c_void_p, C.c_int]
+    lib.rtx_group_set_builder.restype = C.c_int
+    lib.rtx_group_upload_scene.argtypes = [C.c_void_p, C.POINTER(SceneDesc)]
+    lib.rtx_group_upload_scene.restype = C.c_int
+    lib.rtx_group_render.argtypes = [C.c_void_p, C.POINTER(Frame), C.POINTER(Params), C.c_void_p, C.c_void_p]
+    lib.rtx_group_render.restype = C.c_int
+    lib.rtx_group_get_stats.argtypes = [C.c_void_p, C.POINTER(Stats)]
+    lib.rtx_group_get_stats.restype = C.c_int
+    lib.rtx_group_close.argtypes = [C.c_void_p]
+    lib.rtx_group_close.restype = None
+    lib.rtx_tile_pack_count.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
+    lib.rtx_tile_pack_count.restype = C.c_size_t
+    lib.rtx_tile_pack_host.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                       C.c_void_p]
+    lib.rtx_tile_pack_host.restype = C.c_int
+    lib.rtx_tile_unpack_host.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
+                                         C.c_void_p]
+    lib.rtx_tile_unpack_host.restype = C.c_int
+    lib.rtx_tile_pack_device.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
+                                         C.c_uint32, C.c_void_p, C.c_void_p]
+    lib.rtx_tile_pack_device.restype = C.c_int
+    lib.rtx_tile_unpack_device.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                           C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.rtx_tile_unpack_device.restype = C.c_int
 
 
 def declare_oracle(lib):

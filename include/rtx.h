@@ -203,6 +203,10 @@ typedef struct rtx_stats {
 	uint64_t shadow_wave_walks;       /* wave walks (64 lane slots each): steps / walks = the waves' mean walk length */
 	uint32_t wide_nodes;              /* 4-wide shadow-walk BVH nodes (0: k_shadow walks the threaded BVH2) */
 	uint32_t wide_depth;
+	uint64_t shadow_leaf_rounds;      /* only with count_traversal, 4-wide walk: wave iterations of its leaf loop */
+	double gather_ms;                 /* rtx_group_render: shard pack + RCCL gather + unpack (0 on one device) */
+	uint32_t devices;                 /* devices that rendered the last frame */
+	uint32_t pad_;
 } rtx_stats;
 
 typedef struct rtx_ctx rtx_ctx;
@@ -231,6 +235,43 @@ int rtx_get_stats(const rtx_ctx *ctx, rtx_stats *out);
 int rtx_set_builder(rtx_ctx *ctx, int builder);
 void rtx_close(rtx_ctx *ctx);
 const char *rtx_last_error(void);
+
+/*
+ * Several devices rendering one frame (the reference's own parallel point is
+ * the OpenMP row loop of render.c:349-352).  The group builds the scene's BVHs once on the
+ * host (rtx_upload_scene's work) and uploads them to every device; rtx_group_render deals the
+ * frame's 8x8 tiles round-robin (tile t -> device t % n), renders every shard on its own host
+ * thread, packs each shard into 16-byte {r, g, b, z} records (64 per tile) and gathers them
+ * to the first device over RCCL (grouped ncclSend / ncclRecv on xGMI), which unpacks the frame
+ * and copies it to the caller.  Pixels are independent and the RNG is counter-based, so the
+ * frame is bit-identical for any n.  One host thread calls the group; it must not be shared.
+ */
+typedef struct rtx_group rtx_group;
+
+/* n devices: devices[0..n-1], or 0..n-1 when devices is NULL (each must be gfx950, distinct) */
+int rtx_group_open(int n, const int *devices, rtx_group **out);
+int rtx_group_size(const rtx_group *g);
+int rtx_group_set_builder(rtx_group *g, int builder);
+int rtx_group_upload_scene(rtx_group *g, const rtx_scene_desc *scene);
+/* params->tile_offset / tile_stride must be 0 / 1: the group shards the frame itself.
+ * rgb / z: HOST buffers as for rtx_render (either may be NULL). */
+int rtx_group_render(rtx_group *g, const rtx_frame *frame, const rtx_params *params, float *rgb, float *z);
+/* ray and traversal counts summed over the devices, kernel times the slowest device's,
+ * gather_ms the pack + RCCL + unpack time */
+int rtx_group_get_stats(const rtx_group *g, rtx_stats *out);
+void rtx_group_close(rtx_group *g);
+
+/* The gather's tile records (rtx_tiles.h): shard `offset` of `stride` of a W x H frame packs
+ * to rtx_tile_pack_count() records of 4 floats.  Host reference and device versions. */
+size_t rtx_tile_pack_count(uint32_t width, uint32_t height, uint32_t offset, uint32_t stride);
+int rtx_tile_pack_host(const float *rgb, const float *z, uint32_t width, uint32_t height, uint32_t offset,
+		       uint32_t stride, float *out);
+int rtx_tile_unpack_host(const float *in, uint32_t width, uint32_t height, uint32_t offset, uint32_t stride,
+			 float *rgb, float *z);
+int rtx_tile_pack_device(rtx_ctx *ctx, const void *d_rgb, const void *d_z, uint32_t width, uint32_t height,
+			 uint32_t offset, uint32_t stride, void *d_out, void *stream);
+int rtx_tile_unpack_device(rtx_ctx *ctx, const void *d_in, uint32_t width, uint32_t height, uint32_t offset,
+			   uint32_t stride, void *d_rgb, void *d_z, void *stream);
 
 /*
  * Postprocess: the reference's separate `postprocess` binary

@@ -11,7 +11,7 @@ INCLUDE = os.path.join(rtxpy.REPO_ROOT, "include")
 
 def declared(header):
     text = open(os.path.join(INCLUDE, header)).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|const char \*|uint32_t|const rtx_scene_desc \*)\s*\*?(rtx_\w+)\(",
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char \*|uint32_t|size_t|const rtx_scene_desc \*)\s*\*?(rtx_\w+)\(",
                                  text, re.M)))
 
 
@@ -58,4 +58,4 @@ def test_struct_sizes_match_c():
     assert ctypes.sizeof(abi.Object) == 4 * (4 + 18 + 2)
     assert ctypes.sizeof(abi.Frame) == 4 * (2 + 12)
     assert ctypes.sizeof(abi.Params) == 56
-    assert ctypes.sizeof(abi.Stats) == 11 * 8 + 6 * 8 + 6 * 4 + 4 * 8
+    assert ctypes.sizeof(abi.Stats) == 11 * 8 + 6 * 8 + 6 * 4 + 4 * 8 + 2 * 4 + 8 + 8 + 2 * 4
