@@ -273,6 +273,7 @@ def shadow_roofline(r, frame, params, d_rgb, d_z, stream, shadow_ms, a, world):
            "tri_tests": int(c.shadow_tri_tests), "sphere_tests": int(c.shadow_sphere_tests),
            "plane_tests": int(c.shadow_plane_tests), "wave_steps": int(c.shadow_wave_steps),
            "wave_walks": int(c.shadow_wave_walks), "leaf_rounds": int(c.shadow_leaf_rounds),
+           "uniform_steps": int(c.shadow_uniform_steps),
            "wide_nodes": int(c.wide_nodes), "wide_depth": int(c.wide_depth),
            "hbm": {"algorithmic_bytes_per_launch": int(algo_bytes), "lds_bytes_per_launch": 16 * lds_box,
                    "achieved": round(algo_bytes / dur / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -871,6 +871,7 @@ int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, floa
 	st.shadow_wave_steps = ctr[RTX_C_SSTEPS];
 	st.shadow_wave_walks = ctr[RTX_C_SWALKS];
 	st.shadow_leaf_rounds = ctr[RTX_C_SLEAFR];
+	st.shadow_uniform_steps = ctr[RTX_C_SUNIF];
 	st.node_visits = ctr[RTX_C_NODES] + st.shadow_node_visits;
 	st.tri_tests = ctr[RTX_C_TRIS] + ctr[RTX_C_STRIS];
 	st.sphere_tests = ctr[RTX_C_SPHERES] + ctr[RTX_C_SSPHERES];

@@ -217,6 +217,7 @@ enum {
 	RTX_C_SSTEPS,       /* ... walk-loop iterations of the waves */
 	RTX_C_SWALKS,       /* ... wave walks (64 shadow rays each) */
 	RTX_C_SLEAFR,       /* ... 4-wide walk: wave iterations of the leaf loop (rounds of primitive fetches) */
+	RTX_C_SUNIF,        /* ... 4-wide walk: wave steps whose active lanes all fetched the same node */
 	RTX_C_N
 };
 

@@ -283,6 +283,7 @@ extern "C" int rtx_group_render(rtx_group *g, const rtx_frame *fr, const rtx_par
 		s.shadow_wave_steps += o.shadow_wave_steps;
 		s.shadow_wave_walks += o.shadow_wave_walks;
 		s.shadow_leaf_rounds += o.shadow_leaf_rounds;
+		s.shadow_uniform_steps += o.shadow_uniform_steps;
 		s.waves += o.waves;
 		s.chunks += o.chunks;
 		s.kernel_ms = std::max(s.kernel_ms, o.kernel_ms);

@@ -154,6 +154,7 @@ struct ShadowCount {
 	u64 steps;     /* walk-loop iterations of the waves (a wave runs until its longest ray ends) */
 	u64 walks;     /* wave walks (64 rays each) */
 	u64 lrounds;   /* 4-wide walk: wave iterations of the leaf loop */
+	u64 unif;      /* 4-wide walk: wave steps with one node for all active lanes */
 };
 
 /* one primitive record (a, b, c = its first 48 bytes) against this lane's shadow ray
@@ -299,7 +300,7 @@ __device__ __forceinline__ void shadow_walk4(const QBvh &Q, const char *__restri
 	const f3 oi = mul3v(oq, invq);
 	uint32_t *stk = Q.stk;
 	uint32_t node = tl >= 0.f ? 0u : RTX_NONE, grp = 0, sp = 0;
-	uint32_t nbox = 0, ntri = 0, nsph = 0, nstep = 0, nlr = 0;
+	uint32_t nbox = 0, ntri = 0, nsph = 0, nstep = 0, nlr = 0, nun = 0;
 	while (node != RTX_NONE) {
 		const DQNode *N = Q.w + 4 * (size_t)node;
 		const uint4 s0 = ldg4u(N), s1 = ldg4u(N + 1), s2 = ldg4u(N + 2), s3 = ldg4u(N + 3);
@@ -313,6 +314,7 @@ __device__ __forceinline__ void shadow_walk4(const QBvh &Q, const char *__restri
 		if (COUNT) {
 			nstep++;
 			nbox += 1u + (s1.w != RTX_EMPTY_REF) + (s2.w != RTX_EMPTY_REF) + (s3.w != RTX_EMPTY_REF);
+			nun += ballot(node != uni(node)) ? 0u : 1u;
 		}
 		const uint32_t hm = (uint32_t)h0 | ((uint32_t)h1 << 1) | ((uint32_t)h2 << 2) | ((uint32_t)h3 << 3);
 		const uint32_t lf = ((s0.w & RTX_REF_LEAF) | ((s1.w & RTX_REF_LEAF) << 1) | ((s2.w & RTX_REF_LEAF) << 2) |
@@ -375,10 +377,13 @@ __device__ __forceinline__ void shadow_walk4(const QBvh &Q, const char *__restri
 			b += __shfl_xor(b, s, WAVE);
 			c += __shfl_xor(c, s, WAVE);
 			nstep = max(nstep, (uint32_t)__shfl_xor(nstep, s, WAVE));
+			nun = max(nun, (uint32_t)__shfl_xor(nun, s, WAVE));
+			nlr = max(nlr, (uint32_t)__shfl_xor(nlr, s, WAVE));
 		}
 		sc.boxes += uni(a);
 		sc.gboxes += uni(a);
 		sc.lrounds += uni(nlr);
+		sc.unif += uni(nun);
 		sc.tris += uni(b);
 		sc.sph += uni(c);
 		sc.steps += uni(nstep);
@@ -598,7 +603,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 	uint32_t *off = off_w[wv], *nls = nls_w[wv], *sid = sid_w[wv];
 	float(*Ls)[WAVE] = Ls_w[wv];
 	uint32_t *stk = &wstk[wv][0][lane_id()];
-	ShadowCount sc = { 0, 0, 0, 0, 0, 0, 0, 0 };
+	ShadowCount sc = { 0, 0, 0, 0, 0, 0, 0, 0, 0 };
 	u64 rays_total = 0;
 	for (;;) {
 		reread_barrier();
@@ -708,6 +713,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 			atomicAdd(&ctr[RTX_C_SSTEPS], sc.steps);
 			atomicAdd(&ctr[RTX_C_SWALKS], sc.walks);
 			atomicAdd(&ctr[RTX_C_SLEAFR], sc.lrounds);
+			atomicAdd(&ctr[RTX_C_SUNIF], sc.unif);
 		}
 	}
 }

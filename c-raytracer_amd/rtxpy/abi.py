@@ -69,7 +69,8 @@ class Stats(C.Structure):
                 ("shadow_box_tests", C.c_uint64), ("shadow_global_box_tests", C.c_uint64),
                 ("shadow_wave_steps", C.c_uint64), ("shadow_wave_walks", C.c_uint64),
                 ("wide_nodes", C.c_uint32), ("wide_depth", C.c_uint32), ("shadow_leaf_rounds", C.c_uint64),
-                ("gather_ms", C.c_double), ("devices", C.c_uint32), ("pad_", C.c_uint32)]
+                ("gather_ms", C.c_double), ("devices", C.c_uint32), ("pad_", C.c_uint32),
+                ("shadow_uniform_steps", C.c_uint64)]
 
 
 RTX_BUILD_SAH_HOST, RTX_BUILD_LBVH_GPU = 0, 1

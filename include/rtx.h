@@ -207,6 +207,7 @@ typedef struct rtx_stats {
 	double gather_ms;                 /* rtx_group_render: shard pack + RCCL gather + unpack (0 on one device) */
 	uint32_t devices;                 /* devices that rendered the last frame */
 	uint32_t pad_;
+	uint64_t shadow_uniform_steps;    /* only with count_traversal, 4-wide walk: wave steps whose active lanes all fetched one node */
 } rtx_stats;
 
 typedef struct rtx_ctx rtx_ctx;
