@@ -47,6 +47,7 @@ extern "C" hipError_t rtx_launch_accum(const DFrame *F, const DParams *P, const 
 				       hipStream_t stream);
 extern "C" hipError_t rtx_launch_kat(int kind, uint32_t n, const float *in, float *out, int u32mode,
 				     hipStream_t stream);
+extern "C" hipError_t rtx_launch_pack_tris(const DPrim *prims, uint32_t n, float4 *out, hipStream_t stream);
 extern "C" hipError_t rtx_launch_kat_shadow(int kind, uint32_t n, const float *in, float *out, hipStream_t stream);
 
 static thread_local char g_err[512] = "";
@@ -104,6 +105,7 @@ static void free_scene(rtx_ctx *c)
 	dfree(c->d_qnodes);
 	dfree(c->d_top);
 	dfree(c->d_wnodes);
+	dfree(c->d_wtris);
 	c->have_scene = false;
 }
 
@@ -324,6 +326,13 @@ static void wide_kids(const std::vector<DNode> &recs, uint32_t ref, WKid kids[4]
 	std::stable_partition(kids, kids + n, [](const WKid &k) { return !(k.ref & RTX_REF_LEAF); });
 }
 
+/* a device leaf ref (record byte offset | flags) as the wide walk's leaf ref: primitive index
+ * << 6 | flags, the index into the compact 48-byte triangle records (DScene.wtris) */
+static uint32_t wide_leaf_ref(uint32_t ref, uint32_t nnodes)
+{
+	return ((((ref & RTX_REF_OFF) / (uint32_t)sizeof(DNode)) - nnodes) << 6) | (ref & ~RTX_REF_OFF);
+}
+
 static uint32_t wide_emit(const std::vector<DNode> &recs, const QFrame &F, uint32_t ref, uint32_t me,
 			  std::vector<DQNode> &out)
 {
@@ -345,7 +354,7 @@ static uint32_t wide_emit(const std::vector<DNode> &recs, const QFrame &F, uint3
 		t.x = rtx_quantise(kids[c].lo[0], kids[c].hi[0], F.qo[0], F.qs[0]);
 		t.y = rtx_quantise(kids[c].lo[1], kids[c].hi[1], F.qo[1], F.qs[1]);
 		t.z = rtx_quantise(kids[c].lo[2], kids[c].hi[2], F.qo[2], F.qs[2]);
-		t.link = c < ninner ? (base + c) << 6 : kids[c].ref;
+		t.link = c < ninner ? (base + c) << 6 : wide_leaf_ref(kids[c].ref, (uint32_t)recs.size());
 	}
 	uint32_t dep = 1;
 	for (uint32_t c = 0; c < ninner; c++)
@@ -368,7 +377,7 @@ static uint32_t wide_bvh(const std::vector<DNode> &inner, uint32_t root_ref, con
 		out[0].x = rtx_quantise(lo[0], hi[0], F.qo[0], F.qs[0]);
 		out[0].y = rtx_quantise(lo[1], hi[1], F.qo[1], F.qs[1]);
 		out[0].z = rtx_quantise(lo[2], hi[2], F.qo[2], F.qs[2]);
-		out[0].link = root_ref;
+		out[0].link = wide_leaf_ref(root_ref, (uint32_t)inner.size());
 		return 1;
 	}
 	return wide_emit(inner, F, root_ref, 0, out);
@@ -653,6 +662,12 @@ int rtx_upload_built(rtx_ctx *c, const HostScene &hs)
 	if ((rc = upload(c->d_qnodes, hs.qnodes)) || (rc = upload(c->d_top, hs.qtop)) || (rc = upload(c->d_wnodes, hs.wnodes)) ||
 	    (rc = upload(c->d_planes, hs.planes)) || (rc = upload(c->d_mats, hs.mats)) || (rc = upload(c->d_emitters, hs.emit)))
 		return rc;
+	dfree(c->d_wtris);
+	if (!hs.wnodes.empty() && hs.nb) { /* the wide walk's compact triangle records, from the primitives */
+		HIP_TRY(hipMalloc(&c->d_wtris, (size_t)hs.nb * 3 * sizeof(float4)));
+		HIP_TRY(rtx_launch_pack_tris((const DPrim *)(c->d_nodes + hs.nnodes), hs.nb, c->d_wtris, c->stream));
+		HIP_TRY(hipStreamSynchronize(c->stream));
+	}
 	memcpy(c->bound_lo, hs.bound_lo, 12);
 	memcpy(c->bound_hi, hs.bound_hi, 12);
 	DScene &S = c->scene;
@@ -671,6 +686,7 @@ int rtx_upload_built(rtx_ctx *c, const HostScene &hs)
 	S.num_top = hs.ntop;
 	S.wnodes = hs.wnodes.empty() ? nullptr : c->d_wnodes;
 	S.num_wnodes = (uint32_t)(hs.wnodes.size() / 4);
+	S.wtris = (const float *)c->d_wtris;
 	S.wdepth = hs.wdepth;
 	S.root_ref = hs.root_ref;
 	S.num_prims = hs.nb;

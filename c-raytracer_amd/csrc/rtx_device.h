@@ -101,7 +101,8 @@ typedef struct __attribute__((aligned(16))) DQNode {
  * 16-byte child slots (DQNode records 4i .. 4i+3, one 64-byte line), each {x, y, z, ref} with the
  * child's box quantised as in DQNode.  The slots hold the inner children first (ref = child node
  * index << 6; a node's inner children are consecutive nodes, so slot c's child is slot 0's + c),
- * then the leaves (ref = device leaf ref, RTX_REF_LEAF set), then empty slots (ref =
+ * then the leaves (ref = primitive index << 6 | RTX_REF_LEAF | RTX_REF_SPH | count-1, indexing
+ * the compact 48-byte records DScene.wtris), then empty slots (ref =
  * RTX_EMPTY_REF, quantised box lo > hi on every axis, never hit).  Node 0 is the root.  A lane
  * keeps its pending siblings as groups (first child << 4 | slot mask), one per tree level, in
  * an LDS stack of RTX_W_STACK entries: the uploader builds the wide tree only when its depth
@@ -153,6 +154,7 @@ typedef struct DScene {
 	const uint32_t *top;    /* its top levels (num_top records + num_top words, see RTX_QTOP_CUT) */
 	uint32_t num_top;
 	const DQNode *wnodes;   /* 4-wide BVH (4 records per node, same frame), null when not built */
+	const float *wtris;     /* its leaves' primitives as 48-byte records (the first 48 B of each DPrim) */
 	uint32_t num_wnodes, wdepth;
 	uint32_t root_ref;
 	uint32_t num_nodes;    /* prims == (const DPrim *)(nodes + num_nodes) */

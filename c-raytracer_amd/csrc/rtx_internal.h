@@ -56,6 +56,7 @@ struct rtx_ctx {
 	DQNode *d_qnodes = nullptr;
 	uint32_t *d_top = nullptr;
 	DQNode *d_wnodes = nullptr;
+	float4 *d_wtris = nullptr;
 	DScene scene{};
 	bool have_scene = false;
 	/* work buffers (grow-only) */

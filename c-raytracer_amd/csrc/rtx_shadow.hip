@@ -188,15 +188,16 @@ __device__ __forceinline__ bool shadow_prim(float4 a, float4 b, float4 c, const 
 	return true;
 }
 
-/* every primitive of the leaf with device ref L, in order; true at the first opaque hit */
-template <bool COUNT>
-__device__ __forceinline__ bool shadow_leaf(uint32_t L, const char *__restrict__ recs, const DMaterial *__restrict__ mats, f3 o,
+/* every primitive of the leaf with ref L, in order, its records REC bytes apart from p (64-byte
+ * DPrims for the BVH2 walk, 48-byte triangle records for the wide walk); true at the first
+ * opaque hit */
+template <bool COUNT, uint32_t REC>
+__device__ __forceinline__ bool shadow_leaf(uint32_t L, const char *__restrict__ p, const DMaterial *__restrict__ mats, f3 o,
 					    f3 d, float tl, uint32_t emit_obj, f3 &li, uint32_t &ntri, uint32_t &nsph)
 {
-	const char *p = recs + (L & RTX_REF_OFF);
 	const uint32_t cnt = (L & RTX_REF_CNT) + 1;
 	for (uint32_t k = 0; k < cnt; k++) {
-		const char *pr = p + k * (uint32_t)sizeof(DPrim);
+		const char *pr = p + k * REC;
 		if (shadow_prim<COUNT>(ldg4(pr, 0), ldg4(pr, 16), ldg4(pr, 32), mats, o, d, tl, emit_obj, li, ntri, nsph))
 			return true;
 	}
@@ -211,6 +212,7 @@ struct QBvh {
 	const uint32_t *tend; /* ... and of the cut records' range ends */
 	uint32_t nt, nq;      /* top records, DQNode records */
 	const DQNode *w;      /* the 4-wide BVH (rtx_device.h RTX_W_STACK), WIDE walks */
+	const char *wt;       /* ... and its 48-byte leaf triangle records */
 	uint32_t *stk;        /* this lane's LDS stack of sibling groups: entry k at stk[k * WAVE] */
 };
 
@@ -247,7 +249,7 @@ __device__ __forceinline__ void shadow_walk(const QBvh &Q, const char *__restric
 				g++;
 			else
 				t++;
-			if (hit && shadow_leaf<COUNT>(L, recs, mats, o, d, tl, emit_obj, li, ntri, nsph)) {
+			if (hit && shadow_leaf<COUNT, sizeof(DPrim)>(L, recs + (L & RTX_REF_OFF), mats, o, d, tl, emit_obj, li, ntri, nsph)) {
 				tl = -1.f;
 				t = nt;
 				ge = 0;
@@ -334,7 +336,7 @@ __device__ __forceinline__ void shadow_walk4(const QBvh &Q, const char *__restri
 			const uint32_t c = __builtin_ctz(lm);
 			lm &= lm - 1;
 			const uint32_t L = c == 0 ? s0.w : c == 1 ? s1.w : c == 2 ? s2.w : s3.w;
-			if (shadow_leaf<COUNT>(L, recs, mats, o, d, tl, emit_obj, li, ntri, nsph)) {
+			if (shadow_leaf<COUNT, 48>(L, Q.wt + (size_t)(L >> 6) * 48, mats, o, d, tl, emit_obj, li, ntri, nsph)) {
 				blocked = true;
 				break;
 			}
@@ -453,6 +455,7 @@ struct KShadow {
 	const char *recs;     /* base of the record array the leaf refs point into */
 	const DQNode *qnodes; /* threaded quantised BVH */
 	const DQNode *wnodes; /* 4-wide quantised BVH (WIDE instances) */
+	const char *wtris;    /* its leaves' 48-byte triangle records */
 	float qo[3], qs[3];
 	const uint32_t *top; /* its top levels (rtx_device.h RTX_QTOP_CUT), copied to LDS per workgroup */
 	uint32_t ntop, nq;
@@ -563,6 +566,7 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	Q.nq = uni(ks.nq);
 	const bool have_tree = uni(ks.have_tree) != 0 && !RTX_DEBUG_NOWALK;
 	Q.w = WIDE ? unip(ks.wnodes) : nullptr;
+	Q.wt = WIDE ? unip(ks.wtris) : nullptr;
 	Q.stk = stk;
 	const bool blocked = shadow_query<COUNT, WIDE>(Q, unip(ks.recs), unip(ks.mats), unip(ks.planes), uni(ks.num_planes),
 						 have_tree, act, p, ldir, ldist, E.obj, li, sc);
@@ -718,6 +722,24 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 	}
 }
 
+/* the wide walk's 48-byte triangle records (DScene.wtris): the first three float4 of every
+ * DPrim (v0 | centre + eps, e1 | radius + object id, e2 + meta), 2.67 per 128-byte line */
+__global__ void k_pack_tris(const DPrim *__restrict__ prims, uint32_t n, float4 *__restrict__ out)
+{
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= 3 * n)
+		return;
+	out[i] = ldg4((const char *)(prims + i / 3), 16 * (i % 3));
+}
+
+extern "C" hipError_t rtx_launch_pack_tris(const DPrim *prims, uint32_t n, float4 *out, hipStream_t stream)
+{
+	if (!n)
+		return hipSuccess;
+	hipLaunchKernelGGL(k_pack_tris, dim3((3 * n + 255) / 256), dim3(256), 0, stream, prims, n, out);
+	return hipGetLastError();
+}
+
 /* ------------------------------------------------------------------------ */
 /* known answers of the fast device functions k_shadow runs (rtx_kat.h)     */
 /* ------------------------------------------------------------------------ */
@@ -837,6 +859,7 @@ extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const
 	ka.reflection = P->reflection;
 	ka.att_offset = P->att_offset;
 	ka.wnodes = S->wnodes;
+	ka.wtris = (const char *)S->wtris;
 	const bool wide = S->wnodes != nullptr;
 	if (count)
 		return wide ? launch_shadow<true, 1, true>(ka, nw, cus, stream) : launch_shadow<true, 1, false>(ka, nw, cus, stream);
