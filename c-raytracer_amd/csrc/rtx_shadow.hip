@@ -31,6 +31,12 @@
 #ifndef RTX_DEBUG_NOWALK
 #define RTX_DEBUG_NOWALK 0 /* measurement only: skip the BVH walk (everything else in k_shadow stays) */
 #endif
+#ifndef RTX_SH_FASTPOW
+#define RTX_SH_FASTPOW 1 /* specular powf from v_log_f32 / v_exp_f32 (sh_pow) */
+#endif
+#ifndef RTX_SH_SPUNI
+#define RTX_SH_SPUNI 1 /* >= 64 lights: the shade-point record through scalar loads */
+#endif
 #ifndef RTX_SHADOW_OCC_DEFAULT
 #define RTX_SHADOW_OCC_DEFAULT 8 /* waves per SIMD the walk is register-capped for */
 #endif
@@ -499,10 +505,45 @@ __device__ __forceinline__ f3 light_point_sh(const DEmitter &e, f3 p, float u1, 
 	return light_point(e, p, u1, u2);
 }
 
+/* field k of a shade-point record: UNI (>= 64 lights, the record is wave-uniform) through
+ * scalar loads, else per lane */
+template <bool UNI> __device__ __forceinline__ float4 sp_field(const float4 *rec, int k)
+{
+	if (UNI) {
+		const auto *r = (const __attribute__((address_space(4))) f4v *)rec;
+		const f4v v = r[k];
+		return make_float4(v.x, v.y, v.z, v.w);
+	}
+	return ldg4(rec, 16 * k);
+}
+
+/* powf(x, y) of the specular term (render.c:224, fmaxf(0, powf(specular_mul, shininess))).
+ * RTX_SH_FASTPOW: exp2(y * log2|x|) from v_log_f32 / v_exp_f32, with powf's y = 0 -> 1 and its
+ * sign rule for x < 0 (odd integer y negative, even positive, otherwise NaN, which fmaxf
+ * turns into 0).  Relative error about |y log2 x| * 2^-24 (< 2e-6 for results above 1e-9). */
+__device__ __forceinline__ float sh_pow(float x, float y)
+{
+	if (!RTX_SH_FASTPOW)
+		return powf(x, y);
+	if (y == 0.f)
+		return 1.f;
+	const float ax = fabsf(x);
+	const bool den = ax < 1.17549435e-38f; /* v_log_f32 flushes denormal inputs: scale by 2^32 */
+	const float lx = __builtin_amdgcn_logf(den ? ax * 4294967296.f : ax) - (den ? 32.f : 0.f);
+	const float r = __builtin_amdgcn_exp2f(y * lx);
+	if (!(x < 0.f))
+		return r;
+	if (rintf(y) != y)
+		return __builtin_nanf("");
+	const float h = 0.5f * y; /* exact; an integer iff y is even */
+	return rintf(h) != h ? -r : r;
+}
+
 /* direct-lighting terms of one unblocked light sample (render.c:199-228), read after the walk */
+template <bool UNI>
 __device__ __forceinline__ f3 shade_light(const KShadow &ks, const float4 *rec, f3 ldir, f3 li, float ldist, float dsq)
 {
-	const float4 q1 = rec[1], q2 = rec[2], q3 = rec[3];
+	const float4 q1 = sp_field<UNI>(rec, 1), q2 = sp_field<UNI>(rec, 2), q3 = sp_field<UNI>(rec, 3);
 	const f3 n = mk3(q1.x, q1.y, q1.z), dir = mk3(q2.x, q2.y, q2.z);
 	const float a = dot3(ldir, n);
 	const int32_t att = (int32_t)uni((uint32_t)ks.attenuation);
@@ -517,19 +558,19 @@ __device__ __forceinline__ f3 shade_light(const KShadow &ks, const float4 *rec, 
 		sm = -dot3(n, norm3(add3(mul3s(ldir, -1.f), dir)));
 	else
 		sm = -dot3(sub3(mul3s(n, 2.f * a), ldir), dir);
-	const f3 spec = mul3s(mul3v(ld3(m.ks), li), fmaxf(0.f, powf(sm, m.shininess)));
+	const f3 spec = mul3s(mul3v(ld3(m.ks), li), fmaxf(0.f, sh_pow(sm, m.shininess)));
 	return add3(diff, spec);
 }
 
 /* one light sample per lane of the shade point `rec` (render.c:170-229): the light point of
  * sample idx (emitters in scene order, the hit object skipped), its shadow ray, attenuation
  * and Phong / Blinn.  Argument-block fields are read from LDS behind reread barriers. */
-template <bool COUNT, bool WIDE>
+template <bool COUNT, bool WIDE, bool UNI>
 __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec, uint32_t idx, bool act, ShadowCount &sc,
 					   const uint4 *top_q, const uint32_t *top_e, uint32_t *stk)
 {
 	reread_barrier();
-	const float4 q0 = rec[0], q4 = rec[4];
+	const float4 q0 = sp_field<UNI && RTX_SH_SPUNI>(rec, 0), q4 = sp_field<UNI && RTX_SH_SPUNI>(rec, 4);
 	const f3 p = mk3(q0.x, q0.y, q0.z);
 	const uint32_t obj = __float_as_uint(q4.x);
 	const DEmitter *emitters = unip(ks.emitters);
@@ -573,7 +614,7 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	reread_barrier();
 	f3 contribution = mk3(0.f, 0.f, 0.f);
 	if (act && !blocked)
-		contribution = shade_light(ks, rec, ldir, li, ldist, dsq);
+		contribution = shade_light<UNI && RTX_SH_SPUNI>(ks, rec, ldir, li, ldist, dsq);
 	return contribution;
 }
 
@@ -647,7 +688,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 				f3 acc = mk3(0.f, 0.f, 0.f);
 				for (uint32_t base = 0; base < nl; base += WAVE) {
 					const uint32_t idx = base + lane_id();
-					acc = add3(acc, light_sample<COUNT, WIDE>(ks, rec, idx, idx < nl, sc, top_q, top_e, stk));
+					acc = add3(acc, light_sample<COUNT, WIDE, true>(ks, rec, idx, idx < nl, sc, top_q, top_e, stk));
 				}
 				const float sx = wave_sum(acc.x), sy = wave_sum(acc.y), sz = wave_sum(acc.z);
 				if (lane_id() == 0) {
@@ -669,7 +710,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 				const uint32_t idx = ((slot - off[k]) << slot_lg) + (lane_id() & (slot_b - 1));
 				const bool act = slot < tot && idx < nls[k];
 				const float4 *rec = unip(ks.sp) + (size_t)sid[k] * SPREC;
-				const f3 contribution = light_sample<COUNT, WIDE>(ks, rec, idx, act, sc, top_q, top_e, stk);
+				const f3 contribution = light_sample<COUNT, WIDE, false>(ks, rec, idx, act, sc, top_q, top_e, stk);
 				/* per-shade-point sums; lanes are ordered by k */
 				const uint32_t t2 = uni(off[WAVE]), sb = uni(ks.slot_b), spp = WAVE / sb;
 				const uint32_t last_slot_lane = (min(t2 - base, spp) - 1) * sb;
@@ -765,6 +806,9 @@ __global__ void k_kat_shadow(int kind, uint32_t n, const float *__restrict__ in,
 		y[1] = l.y;
 		y[2] = l.z;
 	} break;
+	case RTX_KAT_SPEC_POW:
+		y[0] = fmaxf(0.f, sh_pow(x[0], x[1]));
+		break;
 	case RTX_KAT_BOX_Q: {
 		/* the walk's setup (shadow_query / shadow_walk) and its box test on the quantised box */
 		const f3 o = ld3(x), d = ld3(x + 3), qo = ld3(x + 12), qs = ld3(x + 15);

@@ -88,11 +88,11 @@ class Post(C.Structure):
 
 # include/rtx_kat.h
 KAT_MOLLER, KAT_SPHERE, KAT_PLANE, KAT_SLAB, KAT_NOISE, KAT_TEXTURE, KAT_SPH_LIGHT, KAT_TRI_LIGHT, \
-    KAT_MORTON, KAT_U32, KAT_GI_DIR, KAT_REFRACT, KAT_ANY_TRI, KAT_SPH_LIGHT_SH, KAT_BOX_Q = range(15)
-KAT_IN = [16, 11, 11, 13, 3, 16, 9, 11, 3, 1, 6, 7, 17, 9, 19]
-KAT_OUT = [2, 5, 5, 3, 1, 3, 3, 3, 1, 2, 3, 3, 1, 3, 2]
+    KAT_MORTON, KAT_U32, KAT_GI_DIR, KAT_REFRACT, KAT_ANY_TRI, KAT_SPH_LIGHT_SH, KAT_BOX_Q, KAT_SPEC_POW = range(16)
+KAT_IN = [16, 11, 11, 13, 3, 16, 9, 11, 3, 1, 6, 7, 17, 9, 19, 2]
+KAT_OUT = [2, 5, 5, 3, 1, 3, 3, 3, 1, 2, 3, 3, 1, 3, 2, 1]
 KAT_NAMES = ["moller", "sphere", "plane", "slab", "noise", "texture", "sph_light", "tri_light", "morton", "u32",
-             "gi_dir", "refract", "any_tri", "sph_light_sh", "box_q"]
+             "gi_dir", "refract", "any_tri", "sph_light_sh", "box_q", "spec_pow"]
 
 # symbols include/rtx.h declares (checked by tests/test_abi.py)
 RTX_SYMBOLS = ["rtx_params_default", "rtx_device_count", "rtx_open", "rtx_upload_scene", "rtx_render",

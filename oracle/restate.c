@@ -1033,6 +1033,9 @@ int rtx_oracle_kat(int kind, uint32_t n, const float *in, float *out, const rtx_
 			o.radius = x[3];
 			light_point(&o, x + 4, x[7], x[8], y);
 		} break;
+		case RTX_KAT_SPEC_POW: /* render.c:224 fmaxf(0., powf(specular_mul, shininess)) */
+			y[0] = fmaxf(0.f, powf(x[0], x[1]));
+			break;
 		case RTX_KAT_BOX_Q: { /* the exact answer in double: does the segment (0, tlim) of the ray meet
 				       * the (unquantised) box?  A conservative quantised test must say hit
 				       * wherever this does (the frame fields are unused here). */

@@ -72,3 +72,37 @@ def box_q_records(n=20000, seed=11):
     tl[rng.random(n) < 0.1] = FLT_MAX
     recs = np.concatenate([o, d, lo, hi, np.tile(flo, (n, 1)), np.tile(qs, (n, 1)), tl[:, None]], 1)
     return recs.astype(np.float32)
+
+
+def spec_pow_records(n=40000, seed=5):
+    """(specular_mul, shininess) pairs for the specular power (render.c:224): specular_mul over
+    [-1, 1] with 0, +-1, denormals and values a few ulp from +-1; shininess from the scenes'
+    values (0, 0.1, 1, 5, 10, 15, 20, 35), odd and even integers up to 1000 and uniform reals."""
+    rng = np.random.default_rng(seed)
+    x = rng.uniform(-1.0, 1.0, n)
+    k = rng.random(n)
+    x[k < 0.05] = 0.0
+    x[(k >= 0.05) & (k < 0.08)] = 1.0
+    x[(k >= 0.08) & (k < 0.10)] = -1.0
+    near = (k >= 0.10) & (k < 0.20)
+    x[near] = np.sign(rng.normal(size=near.sum())) * (1.0 - rng.integers(1, 64, near.sum()) * 2.0 ** -24)
+    tiny = (k >= 0.20) & (k < 0.23)
+    x[tiny] = rng.uniform(-1, 1, tiny.sum()) * 1e-38
+    y = rng.choice(np.array([0.0, 0.1, 1.0, 5.0, 10.0, 15.0, 20.0, 35.0]), n)
+    j = rng.random(n)
+    y[j < 0.3] = rng.integers(0, 1000, (j < 0.3).sum())
+    y[(j >= 0.3) & (j < 0.5)] = rng.uniform(0, 200, ((j >= 0.3) & (j < 0.5)).sum())
+    return np.stack([x, y], 1).astype(np.float32)
+
+
+def libm_spec_pow(recs):
+    """fmaxf(0, powf(x, y)) with the C library's powf (the reference's libm)."""
+    import ctypes
+    libm = ctypes.CDLL("libm.so.6")
+    libm.powf.argtypes = [ctypes.c_float, ctypes.c_float]
+    libm.powf.restype = ctypes.c_float
+    out = np.empty(len(recs), np.float32)
+    for i, (x, y) in enumerate(recs):
+        p = libm.powf(float(x), float(y))
+        out[i] = p if p > 0.0 else 0.0  # fmaxf(0, NaN) = 0
+    return out

@@ -148,6 +148,27 @@ def test_gpu_kat_quantised_box_is_conservative():
     assert got[~exact].mean() <= 0.05  # padding admits few extra boxes
 
 
+def test_gpu_kat_spec_pow_fast():
+    """sh_pow (exp2(y log2|x|) from v_log_f32 / v_exp_f32 with powf's sign and zero rules)
+    against glibc powf through the reference's fmaxf(0, powf(specular_mul, shininess)):
+    relative error <= 2e-6 * max(1, |y log2 |x||) where the reference value is above 1e-30,
+    below that both are at most 1e-30; zero exactly where the reference is zero (x <= 0 with
+    non-integer or odd y, x = 0, NaN) apart from underflow."""
+    import kat_fast
+    recs = kat_fast.spec_pow_records()
+    want = oracle.kat(abi.KAT_SPEC_POW, recs)[:, 0].astype(np.float64)
+    got = rtxpy.gpu_kat(abi.KAT_SPEC_POW, recs)[:, 0].astype(np.float64)
+    x, y = recs[:, 0].astype(np.float64), recs[:, 1].astype(np.float64)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        e = np.abs(y * np.log2(np.abs(x)))
+    e = np.where(np.isfinite(e), e, 0.0)
+    big = want > 1e-30
+    rel = np.abs(got[big] - want[big]) / want[big]
+    assert (rel <= 2e-6 * np.maximum(1.0, e[big])).all(), float(rel.max())
+    assert (got[~big] <= 1e-30).all()
+    assert (got[want == 0] == 0).all()
+
+
 # ---------------------------------------------------------------- frames
 CONST = [k for k, v in C.manifest().items() if v["rng"] == "const"]
 

@@ -187,3 +187,11 @@ def test_kat_fast_forms_oracle_side():
     b = kat_fast.box_q_records(2000)
     out = oracle.kat(abi.KAT_BOX_Q, b)
     assert out.shape == (2000, 2) and 0.05 < out[:, 0].mean() < 0.95
+
+
+def test_kat_spec_pow_oracle_is_libm():
+    """The oracle's specular power is the reference's expression (render.c:224) on glibc powf."""
+    import kat_fast
+    recs = kat_fast.spec_pow_records(4000)
+    out = oracle.kat(abi.KAT_SPEC_POW, recs)[:, 0]
+    assert np.array_equal(out, kat_fast.libm_spec_pow(recs))
