@@ -440,6 +440,8 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 			p.eps = o.epsilon;
 			p.obj = i;
 			p.mat = (uint32_t)o.material;
+			p.transparent = (mats[o.material].flags & RTX_MF_TRANSPARENT) ? 1u : 0u;
+			memcpy(p.kt, mats[o.material].kt, 12);
 			plane_of[i] = (uint32_t)planes.size();
 			planes.push_back(p);
 		} else if (o.type == RTX_SPHERE || o.type == RTX_TRIANGLE) {

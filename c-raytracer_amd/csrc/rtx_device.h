@@ -118,6 +118,8 @@ typedef struct DPlane {
 	float eps;
 	uint32_t obj;
 	uint32_t mat;
+	uint32_t transparent; /* its material's RTX_MF_TRANSPARENT, copied for the shadow test */
+	float kt[3];          /* its material's kt (shadow transmittance), copied likewise */
 	uint32_t pad;
 } DPlane;
 

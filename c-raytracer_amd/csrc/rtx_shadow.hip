@@ -213,7 +213,7 @@ __device__ __forceinline__ bool shadow_leaf(uint32_t L, const char *__restrict__
 /* the quantised threaded BVH and its frame (rtx_device.h DQNode) */
 struct QBvh {
 	const DQNode *q;
-	f3 qo, qs;
+	f3 qo, qs, qsi; /* qsi = 1 / qs (IEEE, per component) */
 	const uint4 *top;     /* the workgroup's LDS copy of the top records */
 	const uint32_t *tend; /* ... and of the cut records' range ends */
 	uint32_t nt, nq;      /* top records, DQNode records */
@@ -231,7 +231,7 @@ template <bool COUNT, int OCT>
 __device__ __forceinline__ void shadow_walk(const QBvh &Q, const char *__restrict__ recs, const DMaterial *__restrict__ mats,
 					    f3 o, f3 d, f3 inv, float &tl, uint32_t emit_obj, f3 &li, ShadowCount &sc)
 {
-	const f3 invq = mk3(inv.x / Q.qs.x, inv.y / Q.qs.y, inv.z / Q.qs.z);
+	const f3 invq = mk3(inv.x * Q.qsi.x, inv.y * Q.qsi.y, inv.z * Q.qsi.z);
 	const f3 oq = mk3((o.x - Q.qo.x) * Q.qs.x, (o.y - Q.qo.y) * Q.qs.y, (o.z - Q.qo.z) * Q.qs.z);
 	const f3 oi = mul3v(oq, invq);
 	const uint32_t nt = Q.nt;
@@ -303,7 +303,7 @@ template <bool COUNT, int OCT>
 __device__ __forceinline__ void shadow_walk4(const QBvh &Q, const char *__restrict__ recs, const DMaterial *__restrict__ mats,
 					     f3 o, f3 d, f3 inv, float &tl, uint32_t emit_obj, f3 &li, ShadowCount &sc)
 {
-	const f3 invq = mk3(inv.x / Q.qs.x, inv.y / Q.qs.y, inv.z / Q.qs.z);
+	const f3 invq = mk3(inv.x * Q.qsi.x, inv.y * Q.qsi.y, inv.z * Q.qsi.z);
 	const f3 oq = mk3((o.x - Q.qo.x) * Q.qs.x, (o.y - Q.qo.y) * Q.qs.y, (o.z - Q.qo.z) * Q.qs.z);
 	const f3 oi = mul3v(oq, invq);
 	uint32_t *stk = Q.stk;
@@ -410,12 +410,11 @@ __device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restri
 	float tl = act ? dist : -1.f;
 	for (uint32_t i = 0; i < num_planes; i++) { /* plane records are wave-uniform: s_load */
 		const auto *pl = cptr(planes) + i;
-		const auto *m = cptr(mats) + pl->mat;
 		float t;
 		const bool h = hit_plane(mk3(pl->n[0], pl->n[1], pl->n[2]), pl->d, o, d, pl->eps, t) && t < dist && tl >= 0.f;
-		if (m->flags & RTX_MF_TRANSPARENT) {
+		if (pl->transparent) {
 			if (h)
-				li = mul3v(li, mk3(m->kt[0], m->kt[1], m->kt[2]));
+				li = mul3v(li, mk3(pl->kt[0], pl->kt[1], pl->kt[2]));
 		} else if (h) {
 			tl = -1.f;
 		}
@@ -462,7 +461,7 @@ struct KShadow {
 	const DQNode *qnodes; /* threaded quantised BVH */
 	const DQNode *wnodes; /* 4-wide quantised BVH (WIDE instances) */
 	const char *wtris;    /* its leaves' 48-byte triangle records */
-	float qo[3], qs[3];
+	float qo[3], qs[3], qsi[3];
 	const uint32_t *top; /* its top levels (rtx_device.h RTX_QTOP_CUT), copied to LDS per workgroup */
 	uint32_t ntop, nq;
 	const DMaterial *mats;
@@ -601,6 +600,7 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	Q.q = unip(ks.qnodes);
 	Q.qo = mk3(ks.qo[0], ks.qo[1], ks.qo[2]);
 	Q.qs = mk3(ks.qs[0], ks.qs[1], ks.qs[2]);
+	Q.qsi = mk3(ks.qsi[0], ks.qsi[1], ks.qsi[2]);
 	Q.top = top_q;
 	Q.tend = top_e;
 	Q.nt = uni(ks.ntop);
@@ -815,7 +815,7 @@ __global__ void k_kat_shadow(int kind, uint32_t n, const float *__restrict__ in,
 		const uint4 nd = make_uint4(rtx_quantise(x[6], x[9], qo.x, qs.x), rtx_quantise(x[7], x[10], qo.y, qs.y),
 					    rtx_quantise(x[8], x[11], qo.z, qs.z), 0u);
 		const f3 inv = safe_inv_fast(d);
-		const f3 invq = mk3(inv.x / qs.x, inv.y / qs.y, inv.z / qs.z);
+		const f3 invq = mk3(inv.x * (1.f / qs.x), inv.y * (1.f / qs.y), inv.z * (1.f / qs.z));
 		const f3 oq = mk3((o.x - qo.x) * qs.x, (o.y - qo.y) * qs.y, (o.z - qo.z) * qs.z);
 		const f3 oi = mul3v(oq, invq);
 		const uint32_t oct = ((~__float_as_uint(inv.x)) >> 31) | (((~__float_as_uint(inv.y)) >> 31) << 1) |
@@ -883,6 +883,7 @@ extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const
 	for (int a = 0; a < 3; a++) {
 		ka.qo[a] = S->qo[a];
 		ka.qs[a] = S->qs[a];
+		ka.qsi[a] = 1.f / S->qs[a];
 	}
 	ka.mats = S->mats;
 	ka.planes = S->planes;
