@@ -492,6 +492,8 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 		cfg.c_trav = (float)atof(e);
 	if (const char *e = getenv("RTX_BVH_CI"))
 		cfg.c_isect = (float)atof(e);
+	if (const char *e = getenv("RTX_BVH_BINS"))
+		cfg.bins = (uint32_t)std::min(64, std::max(2, atoi(e)));
 
 	/* one 64-byte primitive record (rtx_device.h DPrim) of bounded object oi */
 	auto make_prim = [&](uint32_t oi) {

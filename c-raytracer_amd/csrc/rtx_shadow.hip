@@ -90,6 +90,8 @@ __device__ __forceinline__ uint32_t lds1u(const uint32_t *p)
 	return *(const __attribute__((address_space(3))) uint32_t *)p;
 }
 __device__ __forceinline__ void lds1st(uint32_t *p, uint32_t v) { *(__attribute__((address_space(3))) uint32_t *)p = v; }
+/* a 32-bit LDS pointer (the lane stacks): one VGPR instead of a 64-bit generic pointer */
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
 /* ------------------------------------------------------------------------ */
 /* intersection tests of the any-hit walk                                   */
@@ -219,7 +221,7 @@ struct QBvh {
 	uint32_t nt, nq;      /* top records, DQNode records */
 	const DQNode *w;      /* the 4-wide BVH (rtx_device.h RTX_W_STACK), WIDE walks */
 	const char *wt;       /* ... and its 48-byte leaf triangle records */
-	uint32_t *stk;        /* this lane's LDS stack of sibling groups: entry k at stk[k * WAVE] */
+	lds_u32 *stk;         /* this lane's LDS stack of sibling groups: entry k at stk[k * WAVE] */
 };
 
 /* is_light_blocked's BVH part (accel.c:360-387) for this lane's ray.  The walk starts in the
@@ -306,7 +308,7 @@ __device__ __forceinline__ void shadow_walk4(const QBvh &Q, const char *__restri
 	const f3 invq = mk3(inv.x * Q.qsi.x, inv.y * Q.qsi.y, inv.z * Q.qsi.z);
 	const f3 oq = mk3((o.x - Q.qo.x) * Q.qs.x, (o.y - Q.qo.y) * Q.qs.y, (o.z - Q.qo.z) * Q.qs.z);
 	const f3 oi = mul3v(oq, invq);
-	uint32_t *stk = Q.stk;
+	lds_u32 *stk = Q.stk;
 	uint32_t node = tl >= 0.f ? 0u : RTX_NONE, grp = 0, sp = 0;
 	uint32_t nbox = 0, ntri = 0, nsph = 0, nstep = 0, nlr = 0, nun = 0;
 	while (node != RTX_NONE) {
@@ -357,7 +359,7 @@ __device__ __forceinline__ void shadow_walk4(const QBvh &Q, const char *__restri
 			node = base + c;
 			if (im) {
 				if (grp) {
-					lds1st(stk + sp * WAVE, grp);
+					stk[sp * WAVE] = grp;
 					sp++;
 				}
 				grp = (base << 4) | im;
@@ -370,7 +372,7 @@ __device__ __forceinline__ void shadow_walk4(const QBvh &Q, const char *__restri
 				grp = 0;
 				if (sp) {
 					sp--;
-					grp = lds1u(stk + sp * WAVE);
+					grp = stk[sp * WAVE];
 				}
 			}
 		} else {
@@ -566,7 +568,7 @@ __device__ __forceinline__ f3 shade_light(const KShadow &ks, const float4 *rec, 
  * and Phong / Blinn.  Argument-block fields are read from LDS behind reread barriers. */
 template <bool COUNT, bool WIDE, bool UNI>
 __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec, uint32_t idx, bool act, ShadowCount &sc,
-					   const uint4 *top_q, const uint32_t *top_e, uint32_t *stk)
+					   const uint4 *top_q, const uint32_t *top_e, lds_u32 *stk)
 {
 	reread_barrier();
 	const float4 q0 = sp_field<UNI && RTX_SH_SPUNI>(rec, 0), q4 = sp_field<UNI && RTX_SH_SPUNI>(rec, 4);
@@ -631,10 +633,14 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 	__shared__ uint32_t top_e[WIDE ? 1 : RTX_TOP_MAX]; /* cut records: the DQNode index after the subtree */
 	__shared__ uint32_t wstk[RTX_SH_NW][WIDE ? RTX_W_STACK : 1][WAVE]; /* the wide walk's lane stacks */
 	__shared__ KShadow ks_w[RTX_SH_NW];
-	__shared__ uint32_t off_w[RTX_SH_NW][WAVE + 1]; /* first lane slot of each shade point, total */
-	__shared__ uint32_t nls_w[RTX_SH_NW][WAVE];     /* shadow rays of each shade point */
-	__shared__ uint32_t sid_w[RTX_SH_NW][WAVE];     /* each shade point's index in the record array */
-	__shared__ float Ls_w[RTX_SH_NW][3][WAVE];      /* per shade point light sum, in packet order */
+	/* one wave's tables in one struct, so every lane addresses them from one base register */
+	struct WaveTables {
+		uint32_t off[WAVE + 1]; /* first lane slot of each shade point, total */
+		uint32_t nls[WAVE];     /* shadow rays of each shade point */
+		uint32_t sid[WAVE];     /* each shade point's index in the record array */
+		float Ls[3][WAVE];      /* per shade point light sum, in packet order */
+	};
+	__shared__ WaveTables wt_w[RTX_SH_NW];
 	const uint32_t ntop = WIDE ? 0u : ka.ntop;
 	for (uint32_t i = threadIdx.x; i < ntop; i += WAVE * RTX_SH_NW) {
 		top_q[i] = ldg4u(ka.top + 4 * i);
@@ -645,9 +651,9 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 		ks_w[wv] = ka;
 	__syncthreads();
 	KShadow &ks = ks_w[wv];
-	uint32_t *off = off_w[wv], *nls = nls_w[wv], *sid = sid_w[wv];
-	float(*Ls)[WAVE] = Ls_w[wv];
-	uint32_t *stk = &wstk[wv][0][lane_id()];
+	uint32_t *off = wt_w[wv].off, *nls = wt_w[wv].nls, *sid = wt_w[wv].sid;
+	float(*Ls)[WAVE] = wt_w[wv].Ls;
+	lds_u32 *stk = (lds_u32 *)&wstk[wv][0][lane_id()];
 	ShadowCount sc = { 0, 0, 0, 0, 0, 0, 0, 0, 0 };
 	u64 rays_total = 0;
 	for (;;) {
@@ -733,18 +739,15 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 			}
 		}
 		reread_barrier();
-		if (own) {
-			const float4 *my = unip(ks.sp) + (size_t)my_sid * SPREC;
+		if (lane_id() < cnt) {
+			const uint32_t me = sid[lane_id()]; /* re-read: my_sid need not stay live across the walks */
+			const float4 *my = unip(ks.sp) + (size_t)me * SPREC;
 			const float4 q0 = my[0], q1 = my[1], q2 = my[2], q5 = my[5];
 			const f3 w = mk3(q0.w, q1.w, q2.w);
 			const f3 c = mul3v(w, mk3(Ls[0][lane_id()], Ls[1][lane_id()], Ls[2][lane_id()]));
-			unip(ks.contrib)[my_sid] = make_float4(c.x, c.y, c.z, q5.x);
+			unip(ks.contrib)[me] = make_float4(c.x, c.y, c.z, q5.x);
 		}
-		uint32_t n_rays = own ? nls[lane_id()] : 0u;
-#pragma unroll
-		for (int o = 32; o > 0; o >>= 1)
-			n_rays += __shfl_xor(n_rays, o, WAVE);
-		rays_total += uni(n_rays);
+		rays_total += uni(wave_sum_u(lane_id() < cnt ? nls[lane_id()] : 0u));
 	}
 	if (lane_id() == 0) {
 		unsigned long long *ctr = unip(ks.ctr);

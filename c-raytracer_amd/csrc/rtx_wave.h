@@ -35,27 +35,60 @@ __device__ __forceinline__ float readlanef(float v, uint32_t l)
 }
 __device__ __forceinline__ bool lane_in(u64 m) { return (m >> lane_id()) & 1ull; }
 
-/* deterministic butterfly sum: every lane gets the same total */
+/* The value of lane (lane ^ M), from immediate lane patterns only (no per-lane address registers,
+ * which __shfl_xor's ds_bpermute needs and the compiler keeps live across whole kernels):
+ * M = 1, 2 DPP quad_perm, M = 4, 8, 16 ds_swizzle (xor mode within 32 lanes). */
+template <int M> __device__ __forceinline__ uint32_t lane_xor_u(uint32_t v)
+{
+	if (M == 1)
+		return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false); /* quad_perm [1,0,3,2] */
+	if (M == 2)
+		return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false); /* quad_perm [2,3,0,1] */
+	return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (M << 10) | 0x1F);
+}
+template <int M> __device__ __forceinline__ float lane_xor_f(float v) { return __uint_as_float(lane_xor_u<M>(__float_as_uint(v))); }
+
+/* deterministic butterfly sum: every lane gets the same total.  Step M adds lane ^ M's value,
+ * M = 32, 16, ..., 1; the cross-half step is v_permlane32_swap (both halves' values in every
+ * lane; the two operand orders of lanes i and i ^ 32 give the same IEEE sum). */
 __device__ __forceinline__ float wave_sum(float v)
 {
-#pragma unroll
-	for (int o = 32; o > 0; o >>= 1)
-		v += __shfl_xor(v, o, WAVE);
+	const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+	v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+	v += lane_xor_f<16>(v);
+	v += lane_xor_f<8>(v);
+	v += lane_xor_f<4>(v);
+	v += lane_xor_f<2>(v);
+	v += lane_xor_f<1>(v);
 	return v;
 }
 
-/* exclusive prefix sum over the wave; *tot = total (uniform) */
+__device__ __forceinline__ uint32_t wave_sum_u(uint32_t v)
+{
+	const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+	v = r[0] + r[1];
+	v += lane_xor_u<16>(v);
+	v += lane_xor_u<8>(v);
+	v += lane_xor_u<4>(v);
+	v += lane_xor_u<2>(v);
+	v += lane_xor_u<1>(v);
+	return v;
+}
+
+/* exclusive prefix sum over the wave, bit by bit: the lanes below with bit b set are
+ * mbcnt(ballot(bit b)); *tot = total (uniform).  No shuffles, so no per-lane address registers. */
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t *tot)
 {
-	uint32_t x = v;
-#pragma unroll
-	for (int o = 1; o < WAVE; o <<= 1) {
-		uint32_t y = __shfl_up(x, o, WAVE);
-		if ((int)lane_id() >= o)
-			x += y;
+	uint32_t ex = 0, t = 0;
+	for (uint32_t b = 0; b < 32; b++) {
+		const u64 m = ballot((v >> b) & 1u);
+		if (!ballot((v >> b) != 0u))
+			break;
+		ex += mbcnt(m) << b;
+		t += popc64(m) << b;
 	}
-	*tot = uni(__shfl(x, WAVE - 1, WAVE));
-	return x - v;
+	*tot = t;
+	return ex;
 }
 
 /* largest k in [0,64) with off[k] <= idx, for off[0] = 0 <= idx < off[64] */
