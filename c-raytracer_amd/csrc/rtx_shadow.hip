@@ -31,6 +31,9 @@
 #ifndef RTX_DEBUG_NOWALK
 #define RTX_DEBUG_NOWALK 0 /* measurement only: skip the BVH walk (everything else in k_shadow stays) */
 #endif
+#ifndef RTX_W_NEAR
+#define RTX_W_NEAR 1 /* wide walk: visit the nearest hit inner child first (blockers found sooner) */
+#endif
 #ifndef RTX_SH_FASTPOW
 #define RTX_SH_FASTPOW 1 /* specular powf from v_log_f32 / v_exp_f32 (sh_pow) */
 #endif
@@ -103,7 +106,13 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
  * set: inv[a] >= 0), so each axis' entry plane is known at compile time.  The boxes are
  * widened by one quantisation step on both sides, far more than the transform's rounding, so
  * the test is conservative (KAT: RTX_KAT_BOX_Q). */
+template <int OCT> __device__ __forceinline__ bool box_hit_q(uint4 n, f3 oi, f3 inv, float tlim, float &tn_out);
 template <int OCT> __device__ __forceinline__ bool box_hit_q(uint4 n, f3 oi, f3 inv, float tlim)
+{
+	float tn;
+	return box_hit_q<OCT>(n, oi, inv, tlim, tn);
+}
+template <int OCT> __device__ __forceinline__ bool box_hit_q(uint4 n, f3 oi, f3 inv, float tlim, float &tn_out)
 {
 	const float tx0 = fmaf((float)(n.x & 0xFFFFu), inv.x, -oi.x), tx1 = fmaf((float)(n.x >> 16), inv.x, -oi.x);
 	const float ty0 = fmaf((float)(n.y & 0xFFFFu), inv.y, -oi.y), ty1 = fmaf((float)(n.y >> 16), inv.y, -oi.y);
@@ -111,6 +120,7 @@ template <int OCT> __device__ __forceinline__ bool box_hit_q(uint4 n, f3 oi, f3 
 	if (OCT == 8) {
 		const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.f));
 		const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlim));
+		tn_out = tn;
 		return tn <= tf;
 	}
 	const float nx = (OCT & 1) ? tx0 : tx1, fx = (OCT & 1) ? tx1 : tx0;
@@ -121,6 +131,7 @@ template <int OCT> __device__ __forceinline__ bool box_hit_q(uint4 n, f3 oi, f3 
 	 * canonicalise it before every fminf; no NaN reaches here */
 	float tf = fminf(fminf(fx, fy), fz);
 	asm("v_min_f32 %0, %0, %1" : "+v"(tf) : "v"(tlim));
+	tn_out = tn;
 	return tn <= tf;
 }
 
@@ -314,8 +325,9 @@ __device__ __forceinline__ void shadow_walk4(const QBvh &Q, const char *__restri
 	while (node != RTX_NONE) {
 		const DQNode *N = Q.w + 4 * (size_t)node;
 		const uint4 s0 = ldg4u(N), s1 = ldg4u(N + 1), s2 = ldg4u(N + 2), s3 = ldg4u(N + 3);
-		bool h0 = box_hit_q<OCT>(s0, oi, invq, tl), h1 = box_hit_q<OCT>(s1, oi, invq, tl);
-		bool h2 = box_hit_q<OCT>(s2, oi, invq, tl), h3 = box_hit_q<OCT>(s3, oi, invq, tl);
+		float n0, n1, n2, n3; /* entry distances: the nearest hit inner child is visited next */
+		bool h0 = box_hit_q<OCT>(s0, oi, invq, tl, n0), h1 = box_hit_q<OCT>(s1, oi, invq, tl, n1);
+		bool h2 = box_hit_q<OCT>(s2, oi, invq, tl, n2), h3 = box_hit_q<OCT>(s3, oi, invq, tl, n3);
 		if (OCT == 8) { /* the min/max slab form would turn an empty slot's inverted box around */
 			h1 = h1 && s1.w != RTX_EMPTY_REF;
 			h2 = h2 && s2.w != RTX_EMPTY_REF;
@@ -354,8 +366,22 @@ __device__ __forceinline__ void shadow_walk4(const QBvh &Q, const char *__restri
 			break;
 		}
 		if (im) {
-			const uint32_t c = __builtin_ctz(im), base = s0.w >> 6;
-			im &= im - 1;
+			uint32_t c = __builtin_ctz(im);
+			if (RTX_W_NEAR) { /* inner children occupy the first slots */
+				float best = c == 0 ? n0 : c == 1 ? n1 : c == 2 ? n2 : n3;
+				if ((im & 2u) && n1 < best) {
+					best = n1;
+					c = 1;
+				}
+				if ((im & 4u) && n2 < best) {
+					best = n2;
+					c = 2;
+				}
+				if ((im & 8u) && n3 < best)
+					c = 3;
+			}
+			const uint32_t base = s0.w >> 6;
+			im &= ~(1u << c);
 			node = base + c;
 			if (im) {
 				if (grp) {
