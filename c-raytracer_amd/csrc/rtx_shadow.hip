@@ -618,6 +618,8 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	float u1 = 0.5f, u2 = 0.5f;
 	if (uni(ks.rng) != RTX_RNG_CONST) /* the key already carries the seed (rtx_key_pixel) */
 		rtx_draw2(key_of(__float_as_uint(q4.y), __float_as_uint(q4.z)), e, j, &u1, &u2);
+	if (uni(ks.rng) == RTX_RNG_STRAT) /* stratum j of the emitter's lights (IEEE, as the oracle) */
+		u1 = ((float)j + u1) / (float)E.num_lights;
 	const f3 lp = light_point_sh(E, p, u1, u2);
 	const f3 dv = sub3(lp, p);
 	const float ldist = mag3(dv);

@@ -13,6 +13,7 @@
  *   --device D   first device (default 0)
  *   --seed S     counter-RNG seed (default 1)
  *   --rng const  every rand_flt() draw = 0.5 (the oracle's REF_CONST_RNG)
+ *   --rng counter  counter-based draws without the light-sample stratification (default: strat)
  *   --u32 wrap   float->uint32 texture conversion of a generic x86-64 build
  *                (default: AVX-512 saturating, like -march=native on AVX-512 hosts)
  */
@@ -44,7 +45,7 @@ static const char *HELPTEXT =
 	"[-p] (\"real\" | \"cpu\")            : DEFAULT = real    : time to print with status messages.\n"
 	"[-g] (string)                    : DEFAULT = ambient : global illumination model (ambient | path).\n"
 	"[-f]                             : DEFAULT = OFF     : save raw output for post-processing.\n"
-	"[--gpus N] [--device D] [--seed S] [--rng counter|const] [--u32 sat|wrap]\n";
+	"[--gpus N] [--device D] [--seed S] [--rng strat|counter|const] [--u32 sat|wrap]\n";
 
 static struct timespec t0;
 static int log_cpu = 0;
@@ -95,6 +96,8 @@ int main(int argc, char **argv)
 		p.seed = strtoull(argv[idx + 1], NULL, 10);
 	if ((idx = argv_find(argc, argv, "--rng", 1)) && !strcmp(argv[idx + 1], "const"))
 		p.rng = RTX_RNG_CONST;
+	if ((idx = argv_find(argc, argv, "--rng", 1)) && !strcmp(argv[idx + 1], "counter"))
+		p.rng = RTX_RNG_COUNTER;
 	if ((idx = argv_find(argc, argv, "--u32", 1)) && !strcmp(argv[idx + 1], "wrap"))
 		p.u32conv = RTX_U32_WRAP;
 	if (ngpu < 1)

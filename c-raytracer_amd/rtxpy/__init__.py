@@ -129,7 +129,7 @@ def default_params(**kw):
     p.samples = 1
     p.attenuation = abi.RTX_ATT_SQR
     p.attenuation_offset = 1.0
-    p.rng = abi.RTX_RNG_COUNTER
+    p.rng = abi.RTX_RNG_STRAT
     p.seed = 1
     p.u32conv = abi.RTX_U32_SAT
     p.tile_offset = 0

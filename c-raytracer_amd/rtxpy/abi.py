@@ -13,7 +13,7 @@ RTX_TEX_UNIFORM, RTX_TEX_CHECKERBOARD, RTX_TEX_BRICK, RTX_TEX_NOISY_PERIODIC = 0
 RTX_PHONG, RTX_BLINN = 0, 1
 RTX_GI_AMBIENT, RTX_GI_PATH = 0, 1
 RTX_ATT_NONE, RTX_ATT_LIN, RTX_ATT_SQR = 0, 1, 2
-RTX_RNG_COUNTER, RTX_RNG_CONST = 0, 1
+RTX_RNG_COUNTER, RTX_RNG_CONST, RTX_RNG_STRAT = 0, 1, 2
 RTX_U32_SAT, RTX_U32_WRAP = 0, 1
 
 F3 = C.c_float * 3

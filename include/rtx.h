@@ -139,6 +139,10 @@ enum rtx_attenuation { RTX_ATT_NONE = 0, RTX_ATT_LIN = 1, RTX_ATT_SQR = 2 }; /* 
 enum rtx_rng {
 	RTX_RNG_COUNTER = 0,  /* counter-based hash of (seed, pixel, ray-tree node, draw) */
 	RTX_RNG_CONST = 1,    /* every draw == 0.5f (the oracle's REF_CONST_RNG) */
+	RTX_RNG_STRAT = 2,    /* RTX_RNG_COUNTER with the light samples stratified (the default): sample j
+	                       * of an emitter's n draws its first number (the sphere's inclination, the
+	                       * triangle's p) from [j/n, (j+1)/n) as ((float)j + u) / n; each stratum is
+	                       * sampled uniformly, so the estimator keeps render.c:170-229's expectation */
 };
 /* (uint32_t)float in texture_get_color_checkerboard/brick (material.c:164,173)
  * is UB for negatives; its result depends on the host ISA. */

@@ -733,6 +733,8 @@ static float cast_ray(tctx *T, const ray_t *ray, const float *kr, float *color, 
 			v3 lp, inl;
 			float u1, u2;
 			draw2(P, key, i, j, &u1, &u2);
+			if (P->rng == RTX_RNG_STRAT) /* stratified light samples (include/rtx.h RTX_RNG_STRAT) */
+				u1 = ((float)j + u1) / (float)e->num_lights;
 			light_point(e, out.point, u1, u2, lp);
 			assign3(inl, li);
 			sub3v(lp, out.point, out.dir);
@@ -836,7 +838,7 @@ void rtx_oracle_params_default(rtx_params *p)
 	p->samples = 1;
 	p->attenuation = RTX_ATT_SQR;
 	p->attenuation_offset = 1.f;
-	p->rng = RTX_RNG_COUNTER;
+	p->rng = RTX_RNG_STRAT;
 	p->seed = 1;
 	p->u32conv = RTX_U32_SAT;
 	p->tile_offset = 0;

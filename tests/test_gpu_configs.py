@@ -1,8 +1,8 @@
 """Parity at the BASELINE.json workloads themselves (the frames bench.py and the scaling runs time).
 
 Each config renders on the GPU through the C-ABI at its full size, flags and spp, with the
-counter RNG (seed 1, as bench.py).  The oracle (oracle/restate.c, bit-exact with the reference
-built at -O2, tests/test_oracle.py) renders an evenly spaced sample of the same frame's 8x8
+default RNG (counter-based, stratified light samples, seed 1, as bench.py).  The oracle
+(oracle/restate.c, bit-exact with the reference built at -O2, tests/test_oracle.py) renders an evenly spaced sample of the same frame's 8x8
 tiles with the same RNG stream, and the GPU pixels of those tiles must agree within SURVEY
 §8(c)'s tolerances (conftest.compare_const):
     hit mask <= 0.01 % of pixels (+1 px); |dz| <= 1e-4*max(z,1) on >= 99.9 % of hit pixels;
@@ -47,7 +47,7 @@ def load(name):
 
 def params_for(spp, offset=0, stride=1):
     p = rtxpy.params_from_args(["-g", "path", "-n", str(spp)], seed=1)
-    p.rng = abi.RTX_RNG_COUNTER
+    p.rng = abi.RTX_RNG_STRAT  # bench.py's mode (the library default)
     p.tile_offset, p.tile_stride = offset, stride
     return p
 

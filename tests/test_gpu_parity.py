@@ -193,11 +193,13 @@ def test_gpu_frame_vs_reference_ofast(renderer, name):
     assert ok, (info, m["floor"])
 
 
+@pytest.mark.parametrize("rng", [abi.RTX_RNG_COUNTER, abi.RTX_RNG_STRAT])
 @pytest.mark.parametrize("name", ["s1_path2", "s3_path2", "s4_path2_blinn", "s5_path2", "s6_path2", "s2_amb"])
-def test_gpu_vs_oracle_counter_rng(renderer, name):
-    """Same counter-RNG stream on both sides: sample-for-sample agreement, not just statistics."""
+def test_gpu_vs_oracle_counter_rng(renderer, name, rng):
+    """Same counter-RNG stream on both sides (plain, and with the light samples stratified,
+    include/rtx.h RTX_RNG_STRAT): sample-for-sample agreement, not just statistics."""
     scene, frame, params, m = C.load_config(name)
-    params.rng = abi.RTX_RNG_COUNTER
+    params.rng = rng
     params.seed = 12345
     if params.gi == abi.RTX_GI_PATH:
         params.samples = 8
@@ -212,9 +214,13 @@ def test_gpu_vs_oracle_counter_rng(renderer, name):
 SEEDED = [k for k, v in C.manifest().items() if v["rng"].startswith("seed") and not k.endswith("_s2")]
 
 
+@pytest.mark.parametrize("rng", [abi.RTX_RNG_COUNTER, abi.RTX_RNG_STRAT])
 @pytest.mark.parametrize("name", SEEDED)
-def test_gpu_statistical_vs_reference_seeded(renderer, name):
+def test_gpu_statistical_vs_reference_seeded(renderer, name, rng):
+    """Against the reference's own glibc rand() stream (seeded): the same expectation, for the
+    plain counter RNG and for stratified light samples (RTX_RNG_STRAT, the default)."""
     scene, frame, params, m = C.load_config(name)
+    params.rng = rng
     rgb, z, _ = render(renderer, scene, frame, params)
     ref_rgb, ref_z = C.golden_frame(name)
     assert ((z > 0) != (ref_z > 0)).mean() <= 1e-3

@@ -195,3 +195,18 @@ def test_kat_spec_pow_oracle_is_libm():
     recs = kat_fast.spec_pow_records(4000)
     out = oracle.kat(abi.KAT_SPEC_POW, recs)[:, 0]
     assert np.array_equal(out, kat_fast.libm_spec_pow(recs))
+
+
+def test_oracle_stratified_light_samples_keep_the_expectation():
+    """RTX_RNG_STRAT (include/rtx.h) only moves each light sample inside its stratum: the image
+    differs sample for sample from the plain counter RNG but keeps its mean, with less noise."""
+    scene, frame, params, _ = C.load_config("s3_path2")
+    params.seed = 7
+    params.rng = abi.RTX_RNG_COUNTER
+    a, za, (ca, sa) = oracle.render(scene, frame, params)
+    params.rng = abi.RTX_RNG_STRAT
+    b, zb, (cb, sb) = oracle.render(scene, frame, params)
+    assert np.array_equal(za, zb) and (ca, sa) == (cb, sb)  # same rays, same primary hits
+    assert not np.array_equal(a, b)
+    ma, mb = a.reshape(-1, 3).mean(0), b.reshape(-1, 3).mean(0)
+    assert np.all(np.abs(ma - mb) <= 0.02 * np.abs(ma) + 1e-7), (ma, mb)
