@@ -130,6 +130,12 @@ def flags_for(which, spp):
     return ["-g", "path", "-n", str(spp)]
 
 
+def _rng_name(mode):
+    from rtxpy import abi
+    return {abi.RTX_RNG_CONST: "const", abi.RTX_RNG_COUNTER: "counter",
+            abi.RTX_RNG_STRAT: "counter, stratified light samples"}.get(mode, str(mode))
+
+
 def _omp_threads():
     return int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
 
@@ -159,7 +165,7 @@ def cpu_port(scene, frame, params, target_s, log):
     log(f"cpu port: {n_tiles} tiles, {c}+{s} rays in {dt:.2f}s on {threads} threads")
     return {"value": round((c + s) / dt / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"{n_tiles} of {total} 8x8 tiles (every {stride}th) of the same {frame.width}x{frame.height} "
-                      f"frame and flags, counter RNG", "seconds": round(dt, 2), "rays": c + s}
+                      f"frame and flags, {_rng_name(p.rng)} RNG", "seconds": round(dt, 2), "rays": c + s}
 
 
 def cpu_reference(scene_file, flags, width, height, target_s, log):
