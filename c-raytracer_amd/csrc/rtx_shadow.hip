@@ -31,6 +31,9 @@
 #ifndef RTX_DEBUG_NOWALK
 #define RTX_DEBUG_NOWALK 0 /* measurement only: skip the BVH walk (everything else in k_shadow stays) */
 #endif
+#ifndef RTX_SH_OCT
+#define RTX_SH_OCT 1 /* walks specialised on a wave-uniform direction octant */
+#endif
 #ifndef RTX_W_NEAR
 #define RTX_W_NEAR 1 /* wide walk: visit the nearest hit inner child first (blockers found sooner) */
 #endif
@@ -457,7 +460,7 @@ __device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restri
 	const uint32_t oct = ((~__float_as_uint(inv.x)) >> 31) | (((~__float_as_uint(inv.y)) >> 31) << 1) |
 			     (((~__float_as_uint(inv.z)) >> 31) << 2);
 	const uint32_t lead = readlane(oct, (uint32_t)__ffsll((long long)live) - 1);
-	const uint32_t sel = ballot(alive & (oct != lead)) ? 8u : lead;
+	const uint32_t sel = (!RTX_SH_OCT || ballot(alive & (oct != lead))) ? 8u : lead;
 	switch (sel) {
 #define RTX_WALK(K)                                                                       \
 	case K:                                                                           \
