@@ -34,6 +34,9 @@
 #ifndef RTX_SH_OCT
 #define RTX_SH_OCT 1 /* walks specialised on a wave-uniform direction octant */
 #endif
+#ifndef RTX_W_SUNI
+#define RTX_W_SUNI 1 /* wide walk: a node all live lanes share is read with scalar loads */
+#endif
 #ifndef RTX_W_NEAR
 #define RTX_W_NEAR 1 /* wide walk: visit the nearest hit inner child first (blockers found sooner) */
 #endif
@@ -326,8 +329,24 @@ __device__ __forceinline__ void shadow_walk4(const QBvh &Q, const char *__restri
 	uint32_t node = tl >= 0.f ? 0u : RTX_NONE, grp = 0, sp = 0;
 	uint32_t nbox = 0, ntri = 0, nsph = 0, nstep = 0, nlr = 0, nun = 0;
 	while (node != RTX_NONE) {
-		const DQNode *N = Q.w + 4 * (size_t)node;
-		const uint4 s0 = ldg4u(N), s1 = ldg4u(N + 1), s2 = ldg4u(N + 2), s3 = ldg4u(N + 3);
+		uint4 s0, s1, s2, s3;
+		const uint32_t un = uni(node);
+		if (RTX_W_SUNI && !ballot(node != un)) {
+			/* every live lane is at one node: read it through the scalar cache (no vector-memory
+			 * address / data cycles, which the divergent steps keep busy) */
+			const auto *U = (const __attribute__((address_space(4))) u4v *)(Q.w + 4 * (size_t)un);
+			const u4v a = U[0], b = U[1], c = U[2], e = U[3];
+			s0 = make_uint4(a.x, a.y, a.z, a.w);
+			s1 = make_uint4(b.x, b.y, b.z, b.w);
+			s2 = make_uint4(c.x, c.y, c.z, c.w);
+			s3 = make_uint4(e.x, e.y, e.z, e.w);
+		} else {
+			const DQNode *N = Q.w + 4 * (size_t)node;
+			s0 = ldg4u(N);
+			s1 = ldg4u(N + 1);
+			s2 = ldg4u(N + 2);
+			s3 = ldg4u(N + 3);
+		}
 		float n0, n1, n2, n3; /* entry distances: the nearest hit inner child is visited next */
 		bool h0 = box_hit_q<OCT>(s0, oi, invq, tl, n0), h1 = box_hit_q<OCT>(s1, oi, invq, tl, n1);
 		bool h2 = box_hit_q<OCT>(s2, oi, invq, tl, n2), h3 = box_hit_q<OCT>(s3, oi, invq, tl, n3);
