@@ -307,6 +307,10 @@ def shadow_roofline(r, frame, params, d_rgb, d_z, stream, shadow_ms, a, world):
             out["issued"] = round(issued, 1)
             out["issued_frac"] = round(issued / VALU_PEAK_GINST, 4)
             out["useful_over_issued"] = round(useful / rec["sq_insts_valu"], 4)
+        if "ta_busy_frac" in rec:
+            out["vmem"] = {"ta_busy_frac": rec["ta_busy_frac"], "td_busy_frac": rec.get("td_busy_frac"),
+                           "note": "PMC TA_TA_BUSY / TD_TD_BUSY per CU cycle: the vector-memory address / data "
+                                   "path, the walk's second limit beside VALU issue (DESIGN.md section 5)"}
     return out
 
 

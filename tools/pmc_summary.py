@@ -2,13 +2,16 @@
 """profiles/pmc_k_shadow.json from rocprofv3 --pmc passes over `bench.py --steps 1` (one k_shadow
 launch per pass; gpu_round.sh steps pmcf / pmcw / pmcv).
 
-usage: pmc_summary.py <key> <fetch_dir> <write_dir> <sq_dir> [kernel-substring]
+usage: pmc_summary.py <key> <fetch_dir> <write_dir> <sq_dir> [ta_dir] [kernel-substring]
 Per launch of the kernel (default k_shadow):
   hbm_bytes_per_launch = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes; on gfx950 FETCH_SIZE counts
   128-B fabric read requests at 64 B, hence the 2: MI355X_MICROARCH.md, HBM section).  Both come
   from the L2's memory-side request counters, which include Infinity-Cache hits: L2-miss traffic,
   an upper bound on HBM bytes.
   sq_*: the SQ counters of the sq pass (SQ_INSTS_VALU = wave-level VALU instructions issued).
+  ta_busy_frac (optional ta pass, gpu_round.sh pmcta): TA_TA_BUSY_sum / (256 CUs x GRBM_GUI_ACTIVE / 8
+  XCDs), the share of the kernel's cycles the texture-address units (vector-memory address
+  path, one per CU) were busy; td_busy_frac likewise for TD_TD_BUSY_sum.
 kernel_src_sha ties the entry to the k_shadow sources it measured (bench.py shadow_src_sha).
 """
 import csv
@@ -39,7 +42,9 @@ def per_launch(d, kern):
 
 def main():
     key, fdir, wdir, sdir = sys.argv[1:5]
-    kern = sys.argv[5] if len(sys.argv) > 5 else "k_shadow"
+    rest = sys.argv[5:]
+    tdir = rest.pop(0) if rest and os.path.isdir(rest[0]) else None
+    kern = rest[0] if rest else "k_shadow"
     import bench
     f, nf = per_launch(fdir, kern)
     w, nw = per_launch(wdir, kern)
@@ -54,6 +59,14 @@ def main():
                     "Infinity-Cache hits included)"}
     for k, v in sq.items():
         e[k.lower()] = v
+    if tdir:
+        ta, nt = per_launch(tdir, kern)
+        cyc = ta["GRBM_GUI_ACTIVE"] / 8.0  # summed over the 8 XCDs
+        e["ta_busy_frac"] = round(ta["TA_TA_BUSY_sum"] / (256 * cyc), 4)
+        e["td_busy_frac"] = round(ta["TD_TD_BUSY_sum"] / (256 * cyc), 4)
+        e["tcp_cache_accesses"] = ta["TCP_TOTAL_CACHE_ACCESSES_sum"]
+        e["source"].append(os.path.relpath(tdir, ROOT))
+        e["launches"].append(nt)
     data[key] = e
     with open(out_path, "w") as fh:
         json.dump(data, fh, indent=1)
