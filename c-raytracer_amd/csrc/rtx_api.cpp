@@ -799,6 +799,21 @@ int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, floa
 	uint32_t slot_b = 1;
 	while (slot_b < 64 && slot_b < c->total_lights)
 		slot_b <<= 1;
+	{
+		/* a point's lanes in slots of pow2ceil(lights) (one point per 64-lane packet from 64 lights
+		 * up) leave lanes idle when the count is awkward (100 lights: 64 + 36 of 128 lanes); below
+		 * 90 % use, points take consecutive 4-lane slots and straddle packets instead (k_shadow
+		 * sums a point's slots in slot order, so the result does not depend on its neighbours) */
+		const uint32_t n = std::max<uint32_t>(c->total_lights, 1);
+		const uint32_t used = slot_b * ((n + slot_b - 1) / slot_b);
+		if (n > 4 && (double)n / used < 0.9)
+			slot_b = 4;
+	}
+	if (const char *e = getenv("RTX_SH_SLOT")) { /* measurement: lanes per slot (a power of two <= 64) */
+		const uint32_t v = (uint32_t)atoi(e);
+		if (v && v <= 64 && !(v & (v - 1)))
+			slot_b = v;
+	}
 	const uint32_t slots_per_point = (std::max<uint32_t>(c->total_lights, 1) + slot_b - 1) / slot_b;
 	uint32_t grab = 4096; /* lane slots per k_shadow queue grab (RTX_SH_LANES: measurement; 1024 -> 4096: 903 -> 885 ms) */
 	if (const char *ge = getenv("RTX_SH_LANES"))

@@ -755,7 +755,8 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 			}
 			lds_sync();
 		} else {
-			/* fewer lights: several points share a packet, each in its own power-of-two lane slot */
+			/* several points share a packet: each point's samples fill consecutive slots of B
+			 * (power of two) lanes, B = slot_b; a point may straddle packets */
 			for (uint32_t base = 0;;) {
 				reread_barrier();
 				const uint32_t tot = uni(off[WAVE]), slot_b = uni(ks.slot_b), slot_lg = uni(ks.slot_lg);
@@ -767,22 +768,61 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 				const bool act = slot < tot && idx < nls[k];
 				const float4 *rec = unip(ks.sp) + (size_t)sid[k] * SPREC;
 				const f3 contribution = light_sample<COUNT, WIDE, false>(ks, rec, idx, act, sc, top_q, top_e, stk);
-				/* per-shade-point sums; lanes are ordered by k */
+				/* per-shade-point sums.  Each slot's B lanes reduce in a fixed butterfly (masks B/2 .. 1),
+				 * then the slot sums are added to their point's total one slot at a time in slot order, so a
+				 * point whose slots straddle packets gets the same sum whatever its neighbours (with one slot
+				 * per point this is the 64-lane butterfly over zeros and one slot it replaced, bit for bit) */
 				const uint32_t t2 = uni(off[WAVE]), sb = uni(ks.slot_b), spp = WAVE / sb;
-				const uint32_t last_slot_lane = (min(t2 - base, spp) - 1) * sb;
-				const uint32_t k0 = readlane(k, 0), k1 = readlane(k, last_slot_lane);
-				for (uint32_t kk = k0; kk <= k1; kk++) {
-					const bool in = act && k == kk;
-					if (!ballot(in))
-						continue;
-					const float sx = wave_sum(in ? contribution.x : 0.f);
-					const float sy = wave_sum(in ? contribution.y : 0.f);
-					const float sz = wave_sum(in ? contribution.z : 0.f);
-					if (lane_id() == 0) {
-						Ls[0][kk] += sx;
-						Ls[1][kk] += sy;
-						Ls[2][kk] += sz;
+				f3 v = act ? contribution : mk3(0.f, 0.f, 0.f);
+				if (sb > 16) {
+					v.x += lane_xor_f<16>(v.x);
+					v.y += lane_xor_f<16>(v.y);
+					v.z += lane_xor_f<16>(v.z);
+				}
+				if (sb > 8) {
+					v.x += lane_xor_f<8>(v.x);
+					v.y += lane_xor_f<8>(v.y);
+					v.z += lane_xor_f<8>(v.z);
+				}
+				if (sb > 4) {
+					v.x += lane_xor_f<4>(v.x);
+					v.y += lane_xor_f<4>(v.y);
+					v.z += lane_xor_f<4>(v.z);
+				}
+				if (sb > 2) {
+					v.x += lane_xor_f<2>(v.x);
+					v.y += lane_xor_f<2>(v.y);
+					v.z += lane_xor_f<2>(v.z);
+				}
+				if (sb > 1) {
+					v.x += lane_xor_f<1>(v.x);
+					v.y += lane_xor_f<1>(v.y);
+					v.z += lane_xor_f<1>(v.z);
+				}
+				const uint32_t ns = min(t2 - base, spp);
+				uint32_t kc = readlane(k, 0);
+				float rx = Ls[0][kc], ry = Ls[1][kc], rz = Ls[2][kc];
+				for (uint32_t j = 0; j < ns; j++) {
+					const uint32_t kj = readlane(k, j * sb);
+					if (kj != kc) {
+						if (lane_id() == 0) {
+							Ls[0][kc] = rx;
+							Ls[1][kc] = ry;
+							Ls[2][kc] = rz;
+						}
+						kc = kj;
+						rx = Ls[0][kc];
+						ry = Ls[1][kc];
+						rz = Ls[2][kc];
 					}
+					rx += readlanef(v.x, j * sb);
+					ry += readlanef(v.y, j * sb);
+					rz += readlanef(v.z, j * sb);
+				}
+				if (lane_id() == 0) {
+					Ls[0][kc] = rx;
+					Ls[1][kc] = ry;
+					Ls[2][kc] = rz;
 				}
 				lds_sync();
 				base += spp;
