@@ -344,13 +344,16 @@ def test_gpu_errors():
 
 @pytest.mark.slow
 def test_gpu_full_size_scene5_properties(renderer):
-    """BASELINE config 3 size (1920x1080, path GI) on the dragon stand-in: hit mask / z against the
-    oracle on a tile sample, ray accounting consistent, finite non-negative image."""
+    """BASELINE configs[2] size (1920x1080, path GI) on the dragon stand-in at -n 2 with the
+    counter RNG on both sides: the GPU frame against the oracle on an evenly spaced tile sample
+    within SURVEY §8(c)'s tolerances (C.compare_const; the same check at -n 64 is
+    test_gpu_configs.py's k3 case), ray accounting consistent, finite non-negative image."""
     import standins
     standins.ensure_scene("scene5")
     scene = rtxpy.Scene.load(os.path.join(C.SCENES, "scene5_standin.json"), base_dir=C.GOLDEN)
     frame = scene.frame(1920, 1080)
     params = rtxpy.params_from_args(["-g", "path", "-n", "2"], seed=1)
+    params.rng = abi.RTX_RNG_COUNTER
     rgb, z, st = render(renderer, scene, frame, params)
     assert np.isfinite(rgb).all() and (rgb >= 0).all()
     p = rtxpy.default_params(**{f: getattr(params, f) for f, _ in abi.Params._fields_})
@@ -360,11 +363,8 @@ def test_gpu_full_size_scene5_properties(renderer):
     idx = tile_pixel_index(1920, 1080, rank_tiles(1920, 1080, 0, 131)).reshape(-1)
     idx = idx[idx >= 0]
     zz, oz = z.reshape(-1)[idx], o_z.reshape(-1)[idx]
-    assert ((zz > 0) != (oz > 0)).mean() <= 1e-3
-    both = (zz > 0) & (oz > 0)
-    assert (np.abs(zz[both] - oz[both]) <= 1e-4 * np.maximum(oz[both], 1)).mean() >= 0.999
     rr, orr = rgb.reshape(-1, 3)[idx], o_rgb.reshape(-1, 3)[idx]
-    rel = np.abs(rr - orr).sum() / np.abs(orr).sum()
-    assert rel <= 0.3  # same RNG; checker-wall parity flips (see floor of s5_amb) dominate
+    ok, info = C.compare_const(rr[:, None, :], zz[:, None], orr[:, None, :], oz[:, None])
+    assert ok, info
     # every hit pixel casts 1 primary + spp GI rays at least
     assert st.closest_rays >= (z > 0).sum() * 3
