@@ -730,7 +730,10 @@ __global__ void k_kat(int kind, uint32_t n, const float *__restrict__ in, float 
 /* ------------------------------------------------------------------------ */
 extern "C" size_t rtx_trace_lds_bytes(uint32_t stack_size)
 {
-	return (size_t)WAVE * SPW * 4 + 80 * 4 + (size_t)stack_size * WAVE * 4;
+	/* RTX_TRACE_LDS_PAD (measurement): extra bytes per wave, to read k_trace's occupancy slope */
+	const char *e = getenv("RTX_TRACE_LDS_PAD");
+	const size_t pad = e ? (size_t)atoi(e) : 0;
+	return (size_t)WAVE * SPW * 4 + 80 * 4 + (size_t)stack_size * WAVE * 4 + pad;
 }
 
 extern "C" hipError_t rtx_trace_occupancy(uint32_t stack_size, int *blocks_per_cu)
