@@ -118,6 +118,8 @@ extern "C" void rtx_close(rtx_ctx *c)
 		(void)hipStreamSynchronize(c->stream);
 	free_scene(c);
 	dfree(c->d_tasks);
+	dfree(c->d_ostk);
+	c->ostk_bytes = 0;
 	dfree(c->d_sortbuf);
 	dfree(c->d_sorttmp);
 	dfree(c->d_post_rad);
@@ -789,6 +791,10 @@ int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, floa
 		return e;
 	};
 	HIP_TRY(grow(c->d_tasks, c->task_bytes, (size_t)waves * task_cap * sizeof(DTask)));
+	if (c->scene.stack_size > RTX_TRACE_LSTK) /* the closest-hit stack entries beyond the LDS part */
+		HIP_TRY(grow(c->d_ostk, c->ostk_bytes,
+			     (size_t)waves * 64 * (c->scene.stack_size - RTX_TRACE_LSTK) * sizeof(uint32_t)));
+	c->scene.ostk = c->d_ostk;
 
 	HIP_TRY(hipEventRecord(c->ev0, stream));
 	double t_trace = 0, t_sort = 0, t_shadow = 0, t_accum = 0;

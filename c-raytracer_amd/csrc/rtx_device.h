@@ -165,7 +165,15 @@ typedef struct DScene {
 	uint32_t num_emitters;
 	uint32_t stack_size;   /* per-lane closest-hit stack entries (>= BVH depth) */
 	float ambient[3];
+	uint32_t *ostk;        /* k_trace: lane-stack entries from RTX_TRACE_LSTK on, [entry][grid lane] in HBM */
 } DScene;
+
+/* k_trace keeps the first RTX_TRACE_LSTK entries of a lane's closest-hit stack in LDS and the
+ * deeper ones (rare) in HBM (DScene.ostk): the LDS per wave, not the tree depth, sets how many
+ * waves a CU holds, and the kernel is latency-bound */
+#ifndef RTX_TRACE_LSTK
+#define RTX_TRACE_LSTK 14
+#endif
 
 typedef struct DFrame {
 	uint32_t width, height;

@@ -62,6 +62,8 @@ struct rtx_ctx {
 	/* work buffers (grow-only) */
 	DTask *d_tasks = nullptr;
 	size_t task_bytes = 0;
+	uint32_t *d_ostk = nullptr; /* k_trace lane-stack overflow (DScene.ostk) */
+	size_t ostk_bytes = 0;
 	float4 *d_staging = nullptr;
 	size_t staging_bytes = 0;
 	float4 *d_sp = nullptr;

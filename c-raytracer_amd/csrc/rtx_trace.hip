@@ -82,6 +82,20 @@ __device__ void trace_closest(const DScene &S, uint32_t *stk, bool act, f3 o, f3
 		uint32_t ref = S.root_ref;
 		uint32_t sp = 0;
 		stk += lane_id();
+		/* entries from RTX_TRACE_LSTK on live in HBM, [entry][grid lane] */
+		uint32_t *ostk = S.ostk + (size_t)blockIdx.x * WAVE + lane_id();
+		const size_t ostride = (size_t)gridDim.x * WAVE;
+		auto push = [&](uint32_t v) {
+			if (sp < RTX_TRACE_LSTK)
+				stk[sp * WAVE] = v;
+			else
+				ostk[(sp - RTX_TRACE_LSTK) * ostride] = v;
+			sp++;
+		};
+		auto pop = [&]() -> uint32_t {
+			sp--;
+			return sp < RTX_TRACE_LSTK ? stk[sp * WAVE] : ostk[(sp - RTX_TRACE_LSTK) * ostride];
+		};
 		for (;;) {
 			if (ref & RTX_REF_LEAF) {
 				const uint32_t first = (ref & RTX_REF_OFF) / (uint32_t)sizeof(DNode) - S.num_nodes,
@@ -108,7 +122,7 @@ __device__ void trace_closest(const DScene &S, uint32_t *stk, bool act, f3 o, f3
 				}
 				if (sp == 0)
 					break;
-				ref = stk[--sp * WAVE];
+				ref = pop();
 			} else {
 				const float4 *nd = (const float4 *)((const char *)S.nodes + (ref & RTX_REF_OFF));
 				const float4 n0 = nd[0], n1 = nd[1], n2 = nd[2];
@@ -121,7 +135,7 @@ __device__ void trace_closest(const DScene &S, uint32_t *stk, bool act, f3 o, f3
 				if (h0 && h1) {
 					/* nearer child first; tie -> right first (accel.c:341-345) */
 					const bool l_first = tn0 < tn1;
-					stk[sp++ * WAVE] = l_first ? n3.y : n3.x;
+					push(l_first ? n3.y : n3.x);
 					ref = l_first ? n3.x : n3.y;
 				} else if (h0) {
 					ref = n3.x;
@@ -130,7 +144,7 @@ __device__ void trace_closest(const DScene &S, uint32_t *stk, bool act, f3 o, f3
 				} else {
 					if (sp == 0)
 						break;
-					ref = stk[--sp * WAVE];
+					ref = pop();
 				}
 			}
 		}
@@ -323,7 +337,10 @@ __device__ __forceinline__ void gi_batch(const DScene &S, const DParams &P, uint
 }
 
 template <bool COUNT>
-__global__ __launch_bounds__(WAVE) void k_trace(DScene S, DFrame F, DParams P, float *__restrict__ rgb,
+#ifndef RTX_TRACE_OCC
+#define RTX_TRACE_OCC 5 /* waves per SIMD k_trace is register-capped for (96 VGPRs; with 14 LDS stack entries, 20 waves per CU) */
+#endif
+__global__ __launch_bounds__(WAVE, RTX_TRACE_OCC) void k_trace(DScene S, DFrame F, DParams P, float *__restrict__ rgb,
 						float *__restrict__ zbuf, DTask *__restrict__ tasks, uint32_t task_cap,
 						float4 *__restrict__ staging, uint32_t staging_cap,
 						float4 *__restrict__ sp_out, uint32_t sp_cap, uint2 *__restrict__ tile_rec,
@@ -733,7 +750,8 @@ extern "C" size_t rtx_trace_lds_bytes(uint32_t stack_size)
 	/* RTX_TRACE_LDS_PAD (measurement): extra bytes per wave, to read k_trace's occupancy slope */
 	const char *e = getenv("RTX_TRACE_LDS_PAD");
 	const size_t pad = e ? (size_t)atoi(e) : 0;
-	return (size_t)WAVE * SPW * 4 + 80 * 4 + (size_t)stack_size * WAVE * 4 + pad;
+	const size_t lstk = stack_size < RTX_TRACE_LSTK ? stack_size : RTX_TRACE_LSTK;
+	return (size_t)WAVE * SPW * 4 + 80 * 4 + lstk * WAVE * 4 + pad;
 }
 
 extern "C" hipError_t rtx_trace_occupancy(uint32_t stack_size, int *blocks_per_cu)
