@@ -172,7 +172,7 @@ typedef struct DScene {
  * deeper ones (rare) in HBM (DScene.ostk): the LDS per wave, not the tree depth, sets how many
  * waves a CU holds, and the kernel is latency-bound */
 #ifndef RTX_TRACE_LSTK
-#define RTX_TRACE_LSTK 14
+#define RTX_TRACE_LSTK 9
 #endif
 
 typedef struct DFrame {

@@ -338,7 +338,7 @@ __device__ __forceinline__ void gi_batch(const DScene &S, const DParams &P, uint
 
 template <bool COUNT>
 #ifndef RTX_TRACE_OCC
-#define RTX_TRACE_OCC 5 /* waves per SIMD k_trace is register-capped for (96 VGPRs; with 14 LDS stack entries, 20 waves per CU) */
+#define RTX_TRACE_OCC 6 /* waves per SIMD k_trace is register-capped for (80 VGPRs; with 9 LDS stack entries, 24 waves per CU) */
 #endif
 __global__ __launch_bounds__(WAVE, RTX_TRACE_OCC) void k_trace(DScene S, DFrame F, DParams P, float *__restrict__ rgb,
 						float *__restrict__ zbuf, DTask *__restrict__ tasks, uint32_t task_cap,
