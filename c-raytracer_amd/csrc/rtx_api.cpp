@@ -49,6 +49,8 @@ extern "C" hipError_t rtx_launch_kat(int kind, uint32_t n, const float *in, floa
 				     hipStream_t stream);
 extern "C" hipError_t rtx_launch_pack_tris(const DPrim *prims, uint32_t n, float4 *out, hipStream_t stream);
 extern "C" hipError_t rtx_launch_kat_shadow(int kind, uint32_t n, const float *in, float *out, hipStream_t stream);
+extern "C" hipError_t rtx_launch_w8_fill(const DPrim *prims, const uint32_t *leafmap, uint32_t n, DW8 *out, hipStream_t stream);
+extern "C" hipError_t rtx_shadow_grid_lanes(uint32_t cus, uint32_t *lanes);
 
 static thread_local char g_err[512] = "";
 
@@ -106,6 +108,7 @@ static void free_scene(rtx_ctx *c)
 	dfree(c->d_top);
 	dfree(c->d_wnodes);
 	dfree(c->d_wtris);
+	dfree(c->d_w8);
 	c->have_scene = false;
 }
 
@@ -120,6 +123,8 @@ extern "C" void rtx_close(rtx_ctx *c)
 	dfree(c->d_tasks);
 	dfree(c->d_ostk);
 	c->ostk_bytes = 0;
+	dfree(c->d_w8spill);
+	c->w8spill_bytes = 0;
 	dfree(c->d_sortbuf);
 	dfree(c->d_sorttmp);
 	dfree(c->d_post_rad);
@@ -487,15 +492,7 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 			c->bound_hi[a] = std::max(c->bound_hi[a], hi[3 * (size_t)k + a]);
 		}
 	BvhConfig cfg;
-	/* builder knobs for measurement (defaults are the tuned values) */
-	if (const char *e = getenv("RTX_BVH_LEAF"))
-		cfg.max_leaf = (uint32_t)std::min(16, std::max(1, atoi(e)));
-	if (const char *e = getenv("RTX_BVH_CT"))
-		cfg.c_trav = (float)atof(e);
-	if (const char *e = getenv("RTX_BVH_CI"))
-		cfg.c_isect = (float)atof(e);
-	if (const char *e = getenv("RTX_BVH_BINS"))
-		cfg.bins = (uint32_t)std::min(64, std::max(2, atoi(e)));
+	cfg.max_leaf = c->opt_leaf; /* RTX_OPT_BVH_LEAF (default 1) */
 
 	/* one 64-byte primitive record (rtx_device.h DPrim) of bounded object oi */
 	auto make_prim = [&](uint32_t oi) {
@@ -634,14 +631,22 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 	if (hs.qnodes.size() >= (1u << 26))
 		return fail(RTX_ERR_SCENE, "scene too large: %zu threaded BVH nodes (max 2^26)", hs.qnodes.size());
 	hs.ntop = thread_top(hs.qnodes, qdepth, hs.qtop);
-	const char *we = getenv("RTX_WIDE"); /* measurement: RTX_WIDE=0 keeps the threaded BVH2 walk */
-	if (!(we && atoi(we) == 0)) {
+	/* the shadow walk's BVH (RTX_OPT_SHADOW_WALK): the 8-wide compressed tree by default, which
+	 * walks any depth; the 4-wide tree (depth-limited by its LDS stacks) and the threaded BVH2 for
+	 * measurement, and the BVH2 when the 8-wide tree cannot be built (over 2^24 entries) */
+	if (c->opt_walk == RTX_WALK_AUTO || c->opt_walk == RTX_WALK_W8) {
+		const DPrim *hp = hs.recs.size() >= (size_t)nnodes + nb ? (const DPrim *)(hs.recs.data() + nnodes) : nullptr;
+		hs.w8depth = rtx_wide8_build(inner, nnodes, hp, nb ? root_ref : RTX_EMPTY_REF, c->bound_lo, c->bound_hi, hs.qf,
+					     hs.w8, hs.w8leaf);
+	} else if (c->opt_walk == RTX_WALK_W4) {
 		hs.wdepth = wide_bvh(inner, nb ? root_ref : RTX_EMPTY_REF, c->bound_lo, c->bound_hi, hs.qf, hs.wnodes);
 		if (hs.wdepth > RTX_W_STACK + 1 || hs.wnodes.size() / 4 >= (1u << 26)) /* the lane stacks would overflow */
 			hs.wnodes.clear();
 	}
 	if (hs.wnodes.empty())
 		hs.wdepth = 0;
+	if (hs.w8.empty())
+		hs.w8depth = 0;
 	hs.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count();
 	hs.mats = std::move(mats);
 	hs.planes = std::move(planes);
@@ -662,6 +667,9 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 int rtx_upload_built(rtx_ctx *c, const HostScene &hs)
 {
 	int rc;
+	/* a failure below leaves the context without a scene (RTX_ERR_STATE on render), never with a
+	 * mix of old and new buffers */
+	c->have_scene = false;
 	HIP_TRY(hipSetDevice(c->device));
 	if (!(hs.recs_on_device && c->d_nodes) && (rc = upload(c->d_nodes, hs.recs)))
 		return rc;
@@ -673,6 +681,20 @@ int rtx_upload_built(rtx_ctx *c, const HostScene &hs)
 		HIP_TRY(hipMalloc(&c->d_wtris, (size_t)hs.nb * 3 * sizeof(float4)));
 		HIP_TRY(rtx_launch_pack_tris((const DPrim *)(c->d_nodes + hs.nnodes), hs.nb, c->d_wtris, c->stream));
 		HIP_TRY(hipStreamSynchronize(c->stream));
+	}
+	if ((rc = upload(c->d_w8, hs.w8)))
+		return rc;
+	if (!hs.w8.empty()) { /* the 8-wide tree's leaf entries: copies of their primitive records */
+		uint32_t *d_map = nullptr;
+		if ((rc = upload(d_map, hs.w8leaf)))
+			return rc;
+		hipError_t e = rtx_launch_w8_fill((const DPrim *)(c->d_nodes + hs.nnodes), d_map, (uint32_t)hs.w8.size(), c->d_w8,
+						  c->stream);
+		if (e == hipSuccess)
+			e = hipStreamSynchronize(c->stream);
+		dfree(d_map);
+		if (e != hipSuccess)
+			return fail(RTX_ERR_HIP, "8-wide BVH leaf fill failed: %s", hipGetErrorString(e));
 	}
 	memcpy(c->bound_lo, hs.bound_lo, 12);
 	memcpy(c->bound_hi, hs.bound_hi, 12);
@@ -694,6 +716,9 @@ int rtx_upload_built(rtx_ctx *c, const HostScene &hs)
 	S.num_wnodes = (uint32_t)(hs.wnodes.size() / 4);
 	S.wtris = (const float *)c->d_wtris;
 	S.wdepth = hs.wdepth;
+	S.w8 = hs.w8.empty() ? nullptr : c->d_w8;
+	S.num_w8 = (uint32_t)hs.w8.size();
+	S.w8depth = hs.w8depth;
 	S.root_ref = hs.root_ref;
 	S.num_prims = hs.nb;
 	S.num_planes = (uint32_t)hs.planes.size();
@@ -709,8 +734,19 @@ int rtx_upload_built(rtx_ctx *c, const HostScene &hs)
 	c->stats.bvh_depth = hs.depth;
 	c->stats.builder = (uint32_t)hs.builder;
 	c->stats.bvh_prims = hs.nb;
-	c->stats.wide_nodes = S.num_wnodes;
-	c->stats.wide_depth = S.wdepth;
+	c->stats.shadow_walk = S.w8 ? RTX_WALK_W8 : S.wnodes ? RTX_WALK_W4 : RTX_WALK_BVH2;
+	if (S.w8) {
+		uint32_t inner_nodes = 0;
+		for (const DW8 &e : hs.w8)
+			inner_nodes += e.w[3] != 0;
+		c->stats.wide_nodes = inner_nodes;
+		c->stats.wide_depth = S.w8depth;
+		c->stats.wide_entries = S.num_w8;
+	} else {
+		c->stats.wide_nodes = S.num_wnodes;
+		c->stats.wide_depth = S.wdepth;
+		c->stats.wide_entries = 0;
+	}
 	return RTX_OK;
 }
 
@@ -768,7 +804,9 @@ int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, floa
 		return fail(RTX_ERR_HIP, "trace kernel does not fit (LDS %zu B)", rtx_trace_lds_bytes(c->scene.stack_size));
 	const uint32_t waves = (uint32_t)std::min<uint64_t>((uint64_t)per_cu * c->cus, std::max<uint32_t>(P.ntiles, 1));
 	/* LIFO task stack: each batch pops <= 64 and pushes <= 128, depth <= max_bounces */
-	const uint32_t mb = std::min<uint32_t>(P.max_bounces, 4096u);
+	if (P.max_bounces > RTX_MAX_BOUNCES)
+		return fail(RTX_ERR_ARG, "max_bounces %u above the supported %u", P.max_bounces, RTX_MAX_BOUNCES);
+	const uint32_t mb = P.max_bounces;
 	const uint32_t task_cap = 64u * (mb + 3u);
 	/* shade points per tile: 64 px x (primary + GI samples) + secondary-ray allowance */
 	const uint64_t gi_n = P.gi == RTX_GI_PATH ? (uint64_t)P.samples : 0u;
@@ -795,6 +833,19 @@ int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, floa
 		HIP_TRY(grow(c->d_ostk, c->ostk_bytes,
 			     (size_t)waves * 64 * (c->scene.stack_size - RTX_TRACE_LSTK) * sizeof(uint32_t)));
 	c->scene.ostk = c->d_ostk;
+	c->scene.w8spill = nullptr;
+	c->scene.w8spill_lanes = 0;
+	c->scene.w8lstk = c->opt_lstk;
+	if (c->scene.w8 && c->scene.w8depth > c->scene.w8lstk + 1) {
+		/* 8-wide trees deeper than the LDS lane stacks: the deeper entries of every lane of the
+		 * largest k_shadow grid (one group per level at most) */
+		uint32_t lanes = 0;
+		HIP_TRY(rtx_shadow_grid_lanes((uint32_t)c->cus, &lanes));
+		HIP_TRY(grow(c->d_w8spill, c->w8spill_bytes,
+			     (size_t)lanes * (c->scene.w8depth - 1 - c->scene.w8lstk) * sizeof(uint32_t)));
+		c->scene.w8spill = c->d_w8spill;
+		c->scene.w8spill_lanes = lanes;
+	}
 
 	HIP_TRY(hipEventRecord(c->ev0, stream));
 	double t_trace = 0, t_sort = 0, t_shadow = 0, t_accum = 0;
@@ -815,18 +866,12 @@ int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, floa
 		if (n > 4 && (double)n / used < 0.9)
 			slot_b = 4;
 	}
-	if (const char *e = getenv("RTX_SH_SLOT")) { /* measurement: lanes per slot (a power of two <= 64) */
-		const uint32_t v = (uint32_t)atoi(e);
-		if (v && v <= 64 && !(v & (v - 1)))
-			slot_b = v;
-	}
+	if (c->opt_slot) /* RTX_OPT_SHADOW_SLOT */
+		slot_b = c->opt_slot;
 	const uint32_t slots_per_point = (std::max<uint32_t>(c->total_lights, 1) + slot_b - 1) / slot_b;
-	uint32_t grab = 4096; /* lane slots per k_shadow queue grab (RTX_SH_LANES: measurement; 1024 -> 4096: 903 -> 885 ms) */
-	if (const char *ge = getenv("RTX_SH_LANES"))
-		grab = (uint32_t)std::max(1, atoi(ge));
+	const uint32_t grab = c->opt_grab; /* lane slots per k_shadow queue grab (1024 -> 4096: 903 -> 885 ms) */
 	const uint32_t per_wave = std::max<uint32_t>(1, std::min<uint32_t>(64, grab / (slot_b * slots_per_point)));
-	const char *se = getenv("RTX_SPSORT");
-	const bool spsort = !(se && se[0] == '0');
+	const bool spsort = c->opt_spsort;
 	for (uint32_t begin = 0; begin < P.ntiles;) {
 		const uint32_t end = std::min<uint32_t>(P.ntiles, begin + chunk_tiles);
 		const uint64_t sp_cap64 = std::min<uint64_t>((uint64_t)(end - begin) * avg_tile + staging_cap, 0xFFFFFFF0ull);
@@ -1035,6 +1080,45 @@ extern "C" int rtx_set_builder(rtx_ctx *c, int builder)
 		return fail(RTX_ERR_ARG, "unknown BVH builder %d", builder);
 	c->builder = builder;
 	return RTX_OK;
+}
+
+extern "C" int rtx_set_option(rtx_ctx *c, int option, int64_t value)
+{
+	if (!c)
+		return fail(RTX_ERR_ARG, "null argument");
+	switch (option) {
+	case RTX_OPT_SHADOW_WALK:
+		if (value < RTX_WALK_AUTO || value > RTX_WALK_W8)
+			return fail(RTX_ERR_ARG, "unknown shadow walk %lld", (long long)value);
+		c->opt_walk = (int)value;
+		return RTX_OK;
+	case RTX_OPT_BVH_LEAF:
+		if (value < 1 || value > RTX_MAX_LEAF)
+			return fail(RTX_ERR_ARG, "BVH leaf size %lld outside 1..%d", (long long)value, RTX_MAX_LEAF);
+		c->opt_leaf = (uint32_t)value;
+		return RTX_OK;
+	case RTX_OPT_SPSORT:
+		if (value != 0 && value != 1)
+			return fail(RTX_ERR_ARG, "RTX_OPT_SPSORT takes 0 or 1, not %lld", (long long)value);
+		c->opt_spsort = value != 0;
+		return RTX_OK;
+	case RTX_OPT_SHADOW_SLOT:
+		if (value < 0 || value > 64 || (value & (value - 1)))
+			return fail(RTX_ERR_ARG, "shadow slot %lld is not 0 or a power of two <= 64", (long long)value);
+		c->opt_slot = (uint32_t)value;
+		return RTX_OK;
+	case RTX_OPT_SHADOW_LDS_STACK:
+		if (value < 1 || value > RTX_W8_STACK)
+			return fail(RTX_ERR_ARG, "shadow LDS stack %lld outside 1..%d", (long long)value, RTX_W8_STACK);
+		c->opt_lstk = (uint32_t)value;
+		return RTX_OK;
+	case RTX_OPT_SHADOW_GRAB:
+		if (value < 1 || value > (1 << 24))
+			return fail(RTX_ERR_ARG, "shadow grab %lld outside 1..2^24", (long long)value);
+		c->opt_grab = (uint32_t)value;
+		return RTX_OK;
+	}
+	return fail(RTX_ERR_ARG, "unknown option %d", option);
 }
 
 extern "C" int rtx_get_stats(const rtx_ctx *c, rtx_stats *out)

@@ -29,6 +29,12 @@
 
 #include <stdint.h>
 
+/* Measurement builds (tools/variants.sh EXTRA=-DRTX_MEASURE=1) read a few RTX_* environment knobs
+ * (occupancy, LDS padding); the product library's behaviour never depends on the environment. */
+#ifndef RTX_MEASURE
+#define RTX_MEASURE 0
+#endif
+
 #define RTX_LEAF_BIT 0x80000000u  /* builder-side leaf refs (bvh_build.cpp) */
 #define RTX_REF_LEAF 32u          /* device refs: byte offset | leaf flag | sphere flag | count-1 */
 #define RTX_REF_SPH 16u           /* leaf holds at least one sphere (else triangles only) */
@@ -112,6 +118,32 @@ typedef struct __attribute__((aligned(16))) DQNode {
 #endif
 #define RTX_W_EMPTY_BOX 0x0000FFFFu
 
+/* 8-wide compressed BVH for the shadow walk (rtx_shadow.hip shadow_walk8), in the style of
+ * Ylitie et al.'s compressed wide BVH: an array of 64-byte entries (one 64-byte half line, four
+ * global_load_dwordx4 or one s_load_dwordx16).  A node entry:
+ *   w0 = ox | oy << 16, w1 = oz | ex << 16 | ey << 20 | ez << 24
+ *        the node's frame on the 16-bit grid of DQNode: origin o (grid units) and a per-axis step
+ *        of 2^e grid units (e <= 9)
+ *   w2 = base << 8 | imask      children at entries base + c (c = slot 0..7); imask: inner slots
+ *   w3 = vmask                  slots holding a child
+ *   w4..w15: 8-bit planes, slot c = byte c & 3 of the word:  lo_x w4,w5  hi_x w6,w7  lo_y w8,w9
+ *            hi_y w10,w11  lo_z w12,w13  hi_z w14,w15
+ * Child c's box is [o + lo * 2^e, o + hi * 2^e] on the grid, outward-rounded from its 16-bit box
+ * (rtx_quant.h), so it contains the float box.  An empty slot has lo = 255, hi = 0 on every axis
+ * (never hit by the octant-specialised test; the generic test masks with vmask).  An inner
+ * slot's entry is the child node; a leaf slot's entry is the primitive's 64-byte DPrim record
+ * (one primitive per leaf slot).  A node's eight child entries are contiguous (unused ones are
+ * holes), so a lane's pending siblings are one 32-bit group base << 8 | slot mask.
+ * Slots follow the children's centroid octant about the node centre (bit a: the + side of
+ * axis a), so a ray of direction octant OCT meets them front to back roughly in the order
+ * c ^ (~OCT & 7) = 0, 1, ..., 7; the walk visits hit children in that order.
+ * Entry 0 is the root node, entry 1 a hole (blocks start on 128-byte lines). */
+#define RTX_W8_STACK 8     /* k_shadow lane-stack entries in LDS; deeper ones spill to HBM (DScene.w8spill) */
+#define RTX_W8_MAX_ENTRIES (1u << 24)
+typedef struct __attribute__((aligned(64))) DW8 {
+	uint32_t w[16];
+} DW8;
+
 typedef struct DPlane {
 	float n[3];
 	float d;
@@ -158,6 +190,11 @@ typedef struct DScene {
 	const DQNode *wnodes;   /* 4-wide BVH (4 records per node, same frame), null when not built */
 	const float *wtris;     /* its leaves' primitives as 48-byte records (the first 48 B of each DPrim) */
 	uint32_t num_wnodes, wdepth;
+	const DW8 *w8;          /* 8-wide compressed BVH (num_w8 entries, same frame), null when not built */
+	uint32_t num_w8, w8depth;
+	uint32_t *w8spill;      /* k_shadow lane-stack entries from RTX_W8_STACK on, [entry][grid lane] */
+	uint32_t w8spill_lanes; /* grid lanes the spill area was sized for (0: no spill area) */
+	uint32_t w8lstk;        /* lane-stack entries k_shadow keeps in LDS (<= RTX_W8_STACK) */
 	uint32_t root_ref;
 	uint32_t num_nodes;    /* prims == (const DPrim *)(nodes + num_nodes) */
 	uint32_t num_prims;

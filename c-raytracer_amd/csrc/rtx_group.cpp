@@ -45,7 +45,8 @@ struct rtx_group {
 	std::vector<ncclComm_t> comm;  /* n > 1: one per device, rank r = ctx[r] */
 	std::vector<float4 *> d_buf;   /* r > 0: shard r's packed records on device r */
 	std::vector<float4 *> d_recv;  /* r > 0: shard r's records received on device 0 */
-	std::vector<size_t> buf_recs;  /* capacity of d_buf[r] / d_recv[r] in records */
+	std::vector<size_t> buf_cap;   /* capacity of d_buf[r] in records */
+	std::vector<size_t> recv_cap;  /* capacity of d_recv[r] in records */
 	rtx_stats stats{};
 };
 
@@ -92,7 +93,8 @@ extern "C" int rtx_group_open(int n, const int *devices, rtx_group **out)
 	g->ctx.assign(n, nullptr);
 	g->d_buf.assign(n, nullptr);
 	g->d_recv.assign(n, nullptr);
-	g->buf_recs.assign(n, 0);
+	g->buf_cap.assign(n, 0);
+	g->recv_cap.assign(n, 0);
 	for (int r = 0; r < n; r++) {
 		int rc = rtx_open(dev[r], &g->ctx[r]);
 		if (rc) {
@@ -121,6 +123,18 @@ extern "C" int rtx_group_set_builder(rtx_group *g, int builder)
 		return fail(RTX_ERR_ARG, "null group");
 	for (rtx_ctx *c : g->ctx) {
 		int rc = rtx_set_builder(c, builder);
+		if (rc)
+			return rc;
+	}
+	return RTX_OK;
+}
+
+extern "C" int rtx_group_set_option(rtx_group *g, int option, int64_t value)
+{
+	if (!g)
+		return fail(RTX_ERR_ARG, "null group");
+	for (rtx_ctx *c : g->ctx) {
+		int rc = rtx_set_option(c, option, value);
 		if (rc)
 			return rc;
 	}
@@ -225,15 +239,15 @@ extern "C" int rtx_group_render(rtx_group *g, const rtx_frame *fr, const rtx_par
 		for (int r = 1; r < n; r++) {
 			rtx_ctx *c = g->ctx[r];
 			const size_t recs = rtx_tile_pack_count(w, h, (uint32_t)r, (uint32_t)n);
-			size_t cap = g->buf_recs[r], cap0 = g->buf_recs[r];
+			/* each buffer keeps its own capacity, so a failed allocation (capacity 0, null
+			 * pointer) is retried on the next call instead of being used */
 			HIP_TRY(hipSetDevice(c->device));
-			int rc = grow_recs(g->d_buf[r], cap, recs);
+			int rc = grow_recs(g->d_buf[r], g->buf_cap[r], recs);
 			if (rc)
 				return rc;
 			HIP_TRY(hipSetDevice(c0->device));
-			if ((rc = grow_recs(g->d_recv[r], cap0, recs)))
+			if ((rc = grow_recs(g->d_recv[r], g->recv_cap[r], recs)))
 				return rc;
-			g->buf_recs[r] = std::min(cap, cap0);
 			HIP_TRY(hipSetDevice(c->device));
 			HIP_TRY(rtx_launch_tile_pack(c->d_rgb, c->d_z, w, h, (uint32_t)r, (uint32_t)n, g->d_buf[r], c->stream));
 		}

@@ -57,6 +57,9 @@ struct rtx_ctx {
 	uint32_t *d_top = nullptr;
 	DQNode *d_wnodes = nullptr;
 	float4 *d_wtris = nullptr;
+	DW8 *d_w8 = nullptr;
+	uint32_t *d_w8spill = nullptr; /* k_shadow lane-stack spill of deep 8-wide trees (DScene.w8spill) */
+	size_t w8spill_bytes = 0;
 	DScene scene{};
 	bool have_scene = false;
 	/* work buffers (grow-only) */
@@ -87,6 +90,13 @@ struct rtx_ctx {
 	float *d_rgb = nullptr, *d_z = nullptr;
 	size_t fb_pixels = 0;
 	rtx_stats stats{};
+	/* rtx_set_option (include/rtx.h RTX_OPT_*) */
+	int opt_walk = RTX_WALK_AUTO;
+	uint32_t opt_leaf = 1;
+	bool opt_spsort = true;
+	uint32_t opt_slot = 0;
+	uint32_t opt_grab = 4096;
+	uint32_t opt_lstk = RTX_W8_STACK;
 };
 
 struct QFrame {
@@ -106,6 +116,9 @@ struct HostScene {
 	uint32_t ntop = 0;
 	std::vector<DQNode> wnodes;   /* 4-wide BVH */
 	uint32_t wdepth = 0;
+	std::vector<DW8> w8;          /* 8-wide BVH entries (leaf entries filled on the device) */
+	std::vector<uint32_t> w8leaf; /* entry -> primitive index (RTX_NONE: node or hole) */
+	uint32_t w8depth = 0;
 	std::vector<DPlane> planes;
 	std::vector<DMaterial> mats;
 	std::vector<DEmitter> emit;
@@ -117,6 +130,10 @@ struct HostScene {
 /* flatten sc and build its BVHs (on c's device for the device builder), then upload to c */
 int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs);
 int rtx_upload_built(rtx_ctx *c, const HostScene &hs);
+/* rtx_wide8.cpp: the 8-wide shadow BVH collapsed from the BVH2 (0 = not built) */
+uint32_t rtx_wide8_build(const std::vector<DNode> &inner, uint32_t nnodes, const DPrim *prims, uint32_t root_ref,
+			 const float lo[3], const float hi[3], const QFrame &F, std::vector<DW8> &out,
+			 std::vector<uint32_t> &leafmap);
 /* one frame (or tile shard) into device buffers on stream */
 int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, float *d_rgb, float *d_z, hipStream_t stream);
 

@@ -22,4 +22,14 @@ __host__ __device__ static inline uint32_t rtx_quantise(float lo, float hi, floa
 	return ql | (qh << 16);
 }
 
+/* one axis of a child box in an 8-wide node's frame (rtx_device.h DW8): the 16-bit plane pair
+ * q16 (rtx_quantise) relative to the node origin org (<= its lo) in steps of 2^e, rounded
+ * outward, so [org + lo8 * 2^e, org + hi8 * 2^e] contains [lo16, hi16]; lo8 | hi8 << 8.  The
+ * caller picks e so that hi8 <= 255. */
+__host__ __device__ static inline uint32_t rtx_quantise8(uint32_t q16, uint32_t org, uint32_t e)
+{
+	const uint32_t lo = ((q16 & 0xFFFFu) - org) >> e, hi = ((q16 >> 16) - org + (1u << e) - 1u) >> e;
+	return lo | (hi << 8);
+}
+
 #endif

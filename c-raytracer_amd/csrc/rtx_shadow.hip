@@ -71,6 +71,10 @@ template <typename T> __device__ __forceinline__ const __attribute__((address_sp
 {
 	return (const __attribute__((address_space(1))) T *)p;
 }
+template <typename T> __device__ __forceinline__ __attribute__((address_space(1))) T *gptrw(T *p)
+{
+	return (__attribute__((address_space(1))) T *)p;
+}
 /* wave-uniform reads of read-only scene tables (s_load) */
 template <typename T> __device__ __forceinline__ const __attribute__((address_space(4))) T *cptr(const T *p)
 {
@@ -236,10 +240,17 @@ struct QBvh {
 	const uint4 *top;     /* the workgroup's LDS copy of the top records */
 	const uint32_t *tend; /* ... and of the cut records' range ends */
 	uint32_t nt, nq;      /* top records, DQNode records */
-	const DQNode *w;      /* the 4-wide BVH (rtx_device.h RTX_W_STACK), WIDE walks */
+	const DQNode *w;      /* the 4-wide BVH (rtx_device.h RTX_W_STACK), WALK_W4 */
 	const char *wt;       /* ... and its 48-byte leaf triangle records */
+	const DW8 *w8;        /* the 8-wide BVH (rtx_device.h DW8), WALK_W8 */
+	uint32_t *spill;      /* this lane's stack entries from lstk on: entry k at spill[(k - lstk) * spill_stride] */
+	uint32_t spill_stride;
+	uint32_t lstk;        /* lane-stack entries in LDS (<= RTX_W8_STACK) */
 	lds_u32 *stk;         /* this lane's LDS stack of sibling groups: entry k at stk[k * WAVE] */
 };
+
+/* the shadow walks k_shadow instantiates */
+enum { WALK_BVH2 = 0, WALK_W4 = 1, WALK_W8 = 2 };
 
 /* is_light_blocked's BVH part (accel.c:360-387) for this lane's ray.  The walk starts in the
  * workgroup's LDS copy of the tree's top levels: a cut record whose box is hit hands the lane
@@ -449,10 +460,203 @@ __device__ __forceinline__ void shadow_walk4(const QBvh &Q, const char *__restri
 	}
 }
 
+/* byte B of w as a float (v_cvt_f32_ubyteB) */
+template <int B> __device__ __forceinline__ float ubyte(uint32_t w) { return (float)((w >> (8 * B)) & 0xFFu); }
+
+/* the 8-bit mask m with bit i moved to bit i ^ K (K < 8 a compile-time constant) */
+template <uint32_t K> __device__ __forceinline__ uint32_t perm_xor(uint32_t m)
+{
+	if (K & 1u)
+		m = ((m & 0x55u) << 1) | ((m >> 1) & 0x55u);
+	if (K & 2u)
+		m = ((m & 0x33u) << 2) | ((m >> 2) & 0x33u);
+	if (K & 4u)
+		m = ((m & 0x0Fu) << 4) | ((m >> 4) & 0x0Fu);
+	return m;
+}
+
+/* The slab test (accel.c:112-158) of child C of an 8-wide node (rtx_device.h DW8) on the segment
+ * (0, tl): t = q8 * s + b per plane, with s = invq * 2^e and b = o * invq - oi the node frame's
+ * scale and offset of the walk's ray transform (box_hit_q), so the same conservative grid test
+ * on the box rounded outward to the node's 8-bit frame (KAT: RTX_KAT_BOX_Q8).  OCT < 8: every
+ * live lane's direction lies in octant OCT, entry planes known at compile time; an empty slot
+ * (lo 255 > hi 0) is then never hit. */
+template <int OCT, int C>
+__device__ __forceinline__ bool w8_child(const uint32_t (&w)[16], f3 s, f3 b, float tl)
+{
+	constexpr int W = C >> 2, B = C & 3;
+	const float lx = fmaf(ubyte<B>(w[4 + W]), s.x, b.x), hx = fmaf(ubyte<B>(w[6 + W]), s.x, b.x);
+	const float ly = fmaf(ubyte<B>(w[8 + W]), s.y, b.y), hy = fmaf(ubyte<B>(w[10 + W]), s.y, b.y);
+	const float lz = fmaf(ubyte<B>(w[12 + W]), s.z, b.z), hz = fmaf(ubyte<B>(w[14 + W]), s.z, b.z);
+	if (OCT == 8) {
+		const float tn = fmaxf(fmaxf(fminf(lx, hx), fminf(ly, hy)), fmaxf(fminf(lz, hz), 0.f));
+		const float tf = fminf(fminf(fmaxf(lx, hx), fmaxf(ly, hy)), fminf(fmaxf(lz, hz), tl));
+		return tn <= tf;
+	}
+	const float nx = (OCT & 1) ? lx : hx, fx = (OCT & 1) ? hx : lx;
+	const float ny = (OCT & 2) ? ly : hy, fy = (OCT & 2) ? hy : ly;
+	const float nz = (OCT & 4) ? lz : hz, fz = (OCT & 4) ? hz : lz;
+	const float tn = fmaxf(fmaxf(nx, ny), fmaxf(nz, 0.f));
+	float tf = fminf(fminf(fx, fy), fz);
+	asm("v_min_f32 %0, %0, %1" : "+v"(tf) : "v"(tl));
+	return tn <= tf;
+}
+
+/* the node frame of an 8-wide node: per-axis scale s = invq * 2^e and offset b = o * invq - oi */
+__device__ __forceinline__ void w8_frame(const uint32_t (&w)[16], f3 invq, f3 oi, f3 &s, f3 &b)
+{
+	s = mk3(ldexpf(invq.x, (int)((w[1] >> 16) & 15u)), ldexpf(invq.y, (int)((w[1] >> 20) & 15u)),
+		ldexpf(invq.z, (int)((w[1] >> 24) & 15u)));
+	b = mk3(fmaf((float)(w[0] & 0xFFFFu), invq.x, -oi.x), fmaf((float)(w[0] >> 16), invq.y, -oi.y),
+		fmaf((float)(w[1] & 0xFFFFu), invq.z, -oi.z));
+}
+
+/* hit mask of an 8-wide node's children in visit order: bit p for slot p ^ K */
+template <int OCT, uint32_t K>
+__device__ __forceinline__ uint32_t w8_hits(const uint32_t (&w)[16], f3 s, f3 b, float tl)
+{
+	uint32_t hm = 0;
+	hm |= w8_child<OCT, 0>(w, s, b, tl) ? 1u << (0 ^ K) : 0u;
+	hm |= w8_child<OCT, 1>(w, s, b, tl) ? 1u << (1 ^ K) : 0u;
+	hm |= w8_child<OCT, 2>(w, s, b, tl) ? 1u << (2 ^ K) : 0u;
+	hm |= w8_child<OCT, 3>(w, s, b, tl) ? 1u << (3 ^ K) : 0u;
+	hm |= w8_child<OCT, 4>(w, s, b, tl) ? 1u << (4 ^ K) : 0u;
+	hm |= w8_child<OCT, 5>(w, s, b, tl) ? 1u << (5 ^ K) : 0u;
+	hm |= w8_child<OCT, 6>(w, s, b, tl) ? 1u << (6 ^ K) : 0u;
+	hm |= w8_child<OCT, 7>(w, s, b, tl) ? 1u << (7 ^ K) : 0u;
+	if (OCT == 8)
+		hm &= w[3]; /* K = 0: slot order; the min/max form would turn an empty slot's box around */
+	return hm;
+}
+
+/* is_light_blocked's BVH part (accel.c:360-387) over the 8-wide BVH (rtx_device.h DW8): one
+ * 64-byte node per step (four 16-byte loads, or one s_load_dwordx16 when every live lane is at
+ * the node), eight box tests.  Hit children are taken in the octant's visit order (slot
+ * p ^ K): leaf slots' primitives are tested at once, the first hit inner child is visited
+ * next and the rest are kept as one group (base << 8 | mask in visit order) in a register, the
+ * older groups in the lane's LDS stack (entries from RTX_W8_STACK on in HBM, Q.spill), at most
+ * one per level, so any depth walks.  tl < 0 on entry: inactive lane.  On an opaque hit tl
+ * becomes -1. */
+template <bool COUNT, int OCT>
+__device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__restrict__ mats, f3 o, f3 d, f3 inv,
+					     float &tl, uint32_t emit_obj, f3 &li, ShadowCount &sc)
+{
+	constexpr uint32_t K = OCT == 8 ? 0u : (~(uint32_t)OCT & 7u);
+	const f3 invq = mk3(inv.x * Q.qsi.x, inv.y * Q.qsi.y, inv.z * Q.qsi.z);
+	const f3 oq = mk3((o.x - Q.qo.x) * Q.qs.x, (o.y - Q.qo.y) * Q.qs.y, (o.z - Q.qo.z) * Q.qs.z);
+	const f3 oi = mul3v(oq, invq);
+	lds_u32 *stk = Q.stk;
+	uint32_t node = tl >= 0.f ? 0u : RTX_NONE, grp = 0, sp = 0;
+	uint32_t nbox = 0, ntri = 0, nsph = 0, nstep = 0, nlr = 0, nun = 0;
+	while (node != RTX_NONE) {
+		uint32_t w[16];
+		const uint32_t un = uni(node);
+		if (RTX_W_SUNI && !ballot(node != un)) {
+			/* every live lane is at one node: read it through the scalar cache */
+			const auto *U = (const __attribute__((address_space(4))) u4v *)(Q.w8 + (size_t)un);
+#pragma unroll
+			for (int k = 0; k < 4; k++) {
+				const u4v v = U[k];
+				w[4 * k] = v.x;
+				w[4 * k + 1] = v.y;
+				w[4 * k + 2] = v.z;
+				w[4 * k + 3] = v.w;
+			}
+		} else {
+			const DW8 *N = Q.w8 + (size_t)node;
+#pragma unroll
+			for (int k = 0; k < 4; k++) {
+				const uint4 v = ldg4u((const uint32_t *)N + 4 * k);
+				w[4 * k] = v.x;
+				w[4 * k + 1] = v.y;
+				w[4 * k + 2] = v.z;
+				w[4 * k + 3] = v.w;
+			}
+		}
+		f3 s, b;
+		w8_frame(w, invq, oi, s, b);
+		const uint32_t hm = w8_hits<OCT, K>(w, s, b, tl);
+		const uint32_t base = w[2] >> 8, io = perm_xor<K>(w[2] & 0xFFu);
+		uint32_t lm = hm & ~io, im = hm & io;
+		if (COUNT) {
+			nstep++;
+			nbox += popc64(w[3]);
+			nun += ballot(node != uni(node)) ? 0u : 1u;
+			uint32_t r = 0;
+			for (uint32_t m = lm;; m &= m - 1) {
+				if (!ballot(m != 0))
+					break;
+				r++;
+			}
+			nlr += r;
+		}
+		bool blocked = false;
+		while (lm) {
+			const uint32_t p = __builtin_ctz(lm);
+			lm &= lm - 1;
+			const char *pr = (const char *)(Q.w8 + base + (p ^ K));
+			if (shadow_prim<COUNT>(ldg4(pr, 0), ldg4(pr, 16), ldg4(pr, 32), mats, o, d, tl, emit_obj, li, ntri, nsph)) {
+				blocked = true;
+				break;
+			}
+		}
+		if (blocked) {
+			tl = -1.f;
+			break;
+		}
+		if (im) {
+			node = base + (__builtin_ctz(im) ^ K);
+			im &= im - 1;
+			if (im) {
+				if (grp) {
+					if (sp < Q.lstk)
+						stk[sp * WAVE] = grp;
+					else
+						gptrw(Q.spill)[(size_t)(sp - Q.lstk) * Q.spill_stride] = grp;
+					sp++;
+				}
+				grp = (base << 8) | im;
+			}
+		} else if (grp) {
+			node = (grp >> 8) + (__builtin_ctz(grp) ^ K);
+			grp &= grp - 1;
+			if (!(grp & 0xFFu)) {
+				grp = 0;
+				if (sp) {
+					sp--;
+					grp = sp < Q.lstk ? stk[sp * WAVE] : gptr(Q.spill)[(size_t)(sp - Q.lstk) * Q.spill_stride];
+				}
+			}
+		} else {
+			node = RTX_NONE;
+		}
+	}
+	if (COUNT) {
+		uint32_t a = nbox, bb = ntri, c = nsph;
+#pragma unroll
+		for (int k = 32; k > 0; k >>= 1) {
+			a += __shfl_xor(a, k, WAVE);
+			bb += __shfl_xor(bb, k, WAVE);
+			c += __shfl_xor(c, k, WAVE);
+			nstep = max(nstep, (uint32_t)__shfl_xor(nstep, k, WAVE));
+			nun = max(nun, (uint32_t)__shfl_xor(nun, k, WAVE));
+			nlr = max(nlr, (uint32_t)__shfl_xor(nlr, k, WAVE));
+		}
+		sc.boxes += uni(a);
+		sc.gboxes += uni(a);
+		sc.lrounds += uni(nlr);
+		sc.unif += uni(nun);
+		sc.tris += uni(bb);
+		sc.sph += uni(c);
+		sc.steps += uni(nstep);
+		sc.walks++;
+	}
+}
+
 /* is_light_blocked (render.c:126-134): planes first (unbound_objects_is_light_blocked,
  * object.c:183-197), then the BVH walk, specialised on the direction octant when every live
  * lane shares it.  Returns the lane's blocked flag; li carries the transmittance product. */
-template <bool COUNT, bool WIDE>
+template <bool COUNT, int WALK>
 __device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restrict__ recs, const DMaterial *__restrict__ mats,
 					     const DPlane *__restrict__ planes, uint32_t num_planes, bool have_tree, bool act,
 					     f3 o, f3 d, float dist, uint32_t emit_obj, f3 &li, ShadowCount &sc)
@@ -481,17 +685,21 @@ __device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restri
 	const uint32_t lead = readlane(oct, (uint32_t)__ffsll((long long)live) - 1);
 	const uint32_t sel = (!RTX_SH_OCT || ballot(alive & (oct != lead))) ? 8u : lead;
 	switch (sel) {
-#define RTX_WALK(K)                                                                       \
-	case K:                                                                           \
-		if (WIDE)                                                                 \
+#define RTX_WALK(K)                                                                            \
+	case K:                                                                                \
+		if (WALK == WALK_W8)                                                           \
+			shadow_walk8<COUNT, K>(Q, mats, o, d, inv, tl, emit_obj, li, sc);      \
+		else if (WALK == WALK_W4)                                                      \
 			shadow_walk4<COUNT, K>(Q, recs, mats, o, d, inv, tl, emit_obj, li, sc); \
-		else                                                                      \
+		else                                                                           \
 			shadow_walk<COUNT, K>(Q, recs, mats, o, d, inv, tl, emit_obj, li, sc);  \
 		break;
 		RTX_WALK(0) RTX_WALK(1) RTX_WALK(2) RTX_WALK(3) RTX_WALK(4) RTX_WALK(5) RTX_WALK(6) RTX_WALK(7)
 #undef RTX_WALK
 	default:
-		if (WIDE)
+		if (WALK == WALK_W8)
+			shadow_walk8<COUNT, 8>(Q, mats, o, d, inv, tl, emit_obj, li, sc);
+		else if (WALK == WALK_W4)
 			shadow_walk4<COUNT, 8>(Q, recs, mats, o, d, inv, tl, emit_obj, li, sc);
 		else
 			shadow_walk<COUNT, 8>(Q, recs, mats, o, d, inv, tl, emit_obj, li, sc);
@@ -509,8 +717,11 @@ struct KShadow {
 	const DPrim *prims;   /* primitive records (DQNode leaf refs are byte offsets from `recs`) */
 	const char *recs;     /* base of the record array the leaf refs point into */
 	const DQNode *qnodes; /* threaded quantised BVH */
-	const DQNode *wnodes; /* 4-wide quantised BVH (WIDE instances) */
+	const DQNode *wnodes; /* 4-wide quantised BVH (WALK_W4 instances) */
 	const char *wtris;    /* its leaves' 48-byte triangle records */
+	const DW8 *w8;        /* 8-wide compressed BVH (WALK_W8 instances) */
+	uint32_t *w8spill;    /* lane-stack spill area, [entry][grid lane] */
+	uint32_t w8lstk;      /* lane-stack entries in LDS */
 	float qo[3], qs[3], qsi[3];
 	const uint32_t *top; /* its top levels (rtx_device.h RTX_QTOP_CUT), copied to LDS per workgroup */
 	uint32_t ntop, nq;
@@ -614,7 +825,7 @@ __device__ __forceinline__ f3 shade_light(const KShadow &ks, const float4 *rec, 
 /* one light sample per lane of the shade point `rec` (render.c:170-229): the light point of
  * sample idx (emitters in scene order, the hit object skipped), its shadow ray, attenuation
  * and Phong / Blinn.  Argument-block fields are read from LDS behind reread barriers. */
-template <bool COUNT, bool WIDE, bool UNI>
+template <bool COUNT, int WALK, bool UNI>
 __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec, uint32_t idx, bool act, ShadowCount &sc,
 					   const uint4 *top_q, const uint32_t *top_e, lds_u32 *stk)
 {
@@ -658,10 +869,14 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	Q.nt = uni(ks.ntop);
 	Q.nq = uni(ks.nq);
 	const bool have_tree = uni(ks.have_tree) != 0 && !RTX_DEBUG_NOWALK;
-	Q.w = WIDE ? unip(ks.wnodes) : nullptr;
-	Q.wt = WIDE ? unip(ks.wtris) : nullptr;
+	Q.w = WALK == WALK_W4 ? unip(ks.wnodes) : nullptr;
+	Q.wt = WALK == WALK_W4 ? unip(ks.wtris) : nullptr;
+	Q.w8 = WALK == WALK_W8 ? unip(ks.w8) : nullptr;
+	Q.spill_stride = gridDim.x * blockDim.x;
+	Q.spill = WALK == WALK_W8 ? unip(ks.w8spill) + blockIdx.x * blockDim.x + threadIdx.x : nullptr;
+	Q.lstk = uni(ks.w8lstk);
 	Q.stk = stk;
-	const bool blocked = shadow_query<COUNT, WIDE>(Q, unip(ks.recs), unip(ks.mats), unip(ks.planes), uni(ks.num_planes),
+	const bool blocked = shadow_query<COUNT, WALK>(Q, unip(ks.recs), unip(ks.mats), unip(ks.planes), uni(ks.num_planes),
 						 have_tree, act, p, ldir, ldist, E.obj, li, sc);
 	reread_barrier();
 	f3 contribution = mk3(0.f, 0.f, 0.f);
@@ -676,12 +891,14 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 /* Persistent workgroups of RTX_SH_NW waves.  A workgroup copies the threaded BVH's top levels
  * to LDS once; then each wave takes per_wave shade points at a time from a global queue
  * (RTX_C_SPQUEUE), in processing (Morton) order, until the points run out. */
-template <bool COUNT, int OCC, bool WIDE>
+template <bool COUNT, int OCC, int WALK>
 __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 {
-	__shared__ uint4 top_q[WIDE ? 1 : RTX_TOP_MAX];    /* the top records (rtx_device.h RTX_QTOP_CUT) */
-	__shared__ uint32_t top_e[WIDE ? 1 : RTX_TOP_MAX]; /* cut records: the DQNode index after the subtree */
-	__shared__ uint32_t wstk[RTX_SH_NW][WIDE ? RTX_W_STACK : 1][WAVE]; /* the wide walk's lane stacks */
+	constexpr bool TOP = WALK == WALK_BVH2;
+	__shared__ uint4 top_q[TOP ? RTX_TOP_MAX : 1];    /* the top records (rtx_device.h RTX_QTOP_CUT) */
+	__shared__ uint32_t top_e[TOP ? RTX_TOP_MAX : 1]; /* cut records: the DQNode index after the subtree */
+	/* the wide walks' lane stacks */
+	__shared__ uint32_t wstk[RTX_SH_NW][WALK == WALK_W4 ? RTX_W_STACK : WALK == WALK_W8 ? RTX_W8_STACK : 1][WAVE];
 	__shared__ KShadow ks_w[RTX_SH_NW];
 	/* one wave's tables in one struct, so every lane addresses them from one base register */
 	struct WaveTables {
@@ -691,7 +908,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 		float Ls[3][WAVE];      /* per shade point light sum, in packet order */
 	};
 	__shared__ WaveTables wt_w[RTX_SH_NW];
-	const uint32_t ntop = WIDE ? 0u : ka.ntop;
+	const uint32_t ntop = TOP ? ka.ntop : 0u;
 	for (uint32_t i = threadIdx.x; i < ntop; i += WAVE * RTX_SH_NW) {
 		top_q[i] = ldg4u(ka.top + 4 * i);
 		top_e[i] = gptr(ka.top)[4 * ntop + i];
@@ -744,7 +961,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 				f3 acc = mk3(0.f, 0.f, 0.f);
 				for (uint32_t base = 0; base < nl; base += WAVE) {
 					const uint32_t idx = base + lane_id();
-					acc = add3(acc, light_sample<COUNT, WIDE, true>(ks, rec, idx, idx < nl, sc, top_q, top_e, stk));
+					acc = add3(acc, light_sample<COUNT, WALK, true>(ks, rec, idx, idx < nl, sc, top_q, top_e, stk));
 				}
 				const float sx = wave_sum(acc.x), sy = wave_sum(acc.y), sz = wave_sum(acc.z);
 				if (lane_id() == 0) {
@@ -767,7 +984,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 				const uint32_t idx = ((slot - off[k]) << slot_lg) + (lane_id() & (slot_b - 1));
 				const bool act = slot < tot && idx < nls[k];
 				const float4 *rec = unip(ks.sp) + (size_t)sid[k] * SPREC;
-				const f3 contribution = light_sample<COUNT, WIDE, false>(ks, rec, idx, act, sc, top_q, top_e, stk);
+				const f3 contribution = light_sample<COUNT, WALK, false>(ks, rec, idx, act, sc, top_q, top_e, stk);
 				/* per-shade-point sums.  Each slot's B lanes reduce in a fixed butterfly (masks B/2 .. 1),
 				 * then the slot sums are added to their point's total one slot at a time in slot order, so a
 				 * point whose slots straddle packets gets the same sum whatever its neighbours (with one slot
@@ -926,7 +1143,71 @@ __global__ void k_kat_shadow(int kind, uint32_t n, const float *__restrict__ in,
 		y[0] = box_hit_q<8>(nd, oi, invq, x[18]) ? 1.f : 0.f;
 		y[1] = ho ? 1.f : 0.f;
 	} break;
+	case RTX_KAT_BOX_Q8: {
+		/* the 8-wide walk's setup and child test on the box quantised to 16 bits, then to 8 bits in
+		 * the node frame (org, e) given by the record, exactly as rtx_wide8_build does */
+		const f3 o = ld3(x), d = ld3(x + 3), qo = ld3(x + 12), qs = ld3(x + 15);
+		uint32_t w[16];
+		for (int k = 0; k < 16; k++)
+			w[k] = 0;
+		const uint32_t org[3] = { (uint32_t)x[19], (uint32_t)x[20], (uint32_t)x[21] };
+		const uint32_t ex[3] = { (uint32_t)x[22], (uint32_t)x[23], (uint32_t)x[24] };
+		w[0] = org[0] | (org[1] << 16);
+		w[1] = org[2] | (ex[0] << 16) | (ex[1] << 20) | (ex[2] << 24);
+		w[3] = 1u;
+		for (int a = 0; a < 3; a++) {
+			const uint32_t q8 = rtx_quantise8(rtx_quantise(x[6 + a], x[9 + a], x[12 + a], x[15 + a]), org[a], ex[a]);
+			w[4 + 4 * a] = (q8 & 0xFFu) | 0xFFFFFF00u; /* slot 0 the box, slots 1..7 empty */
+			w[5 + 4 * a] = 0xFFFFFFFFu;
+			w[6 + 4 * a] = q8 >> 8;
+			w[7 + 4 * a] = 0u;
+		}
+		const f3 inv = safe_inv_fast(d);
+		const f3 invq = mk3(inv.x * (1.f / qs.x), inv.y * (1.f / qs.y), inv.z * (1.f / qs.z));
+		const f3 oq = mk3((o.x - qo.x) * qs.x, (o.y - qo.y) * qs.y, (o.z - qo.z) * qs.z);
+		const f3 oi = mul3v(oq, invq);
+		const uint32_t oct = ((~__float_as_uint(inv.x)) >> 31) | (((~__float_as_uint(inv.y)) >> 31) << 1) |
+				     (((~__float_as_uint(inv.z)) >> 31) << 2);
+		f3 sc, bc;
+		w8_frame(w, invq, oi, sc, bc);
+		uint32_t ho = 0;
+		switch (oct) {
+#define RTX_KATOCT8(K)                                                        \
+	case K:                                                                   \
+		ho = w8_hits<K, (~(uint32_t)K & 7u)>(w, sc, bc, x[18]);               \
+		ho = ho == (1u << (~(uint32_t)K & 7u)) ? 1u : ho ? 2u : 0u;           \
+		break;
+			RTX_KATOCT8(0) RTX_KATOCT8(1) RTX_KATOCT8(2) RTX_KATOCT8(3) RTX_KATOCT8(4) RTX_KATOCT8(5) RTX_KATOCT8(6)
+			RTX_KATOCT8(7)
+#undef RTX_KATOCT8
+		}
+		const uint32_t hg = w8_hits<8, 0u>(w, sc, bc, x[18]);
+		/* 1 = slot 0 hit alone; 2 would flag an empty slot hit (never expected) */
+		y[0] = hg == 1u ? 1.f : hg ? 2.f : 0.f;
+		y[1] = (float)ho;
+	} break;
 	}
+}
+
+/* the 8-wide BVH's leaf entries: the primitive records they stand for (leafmap[i] = primitive
+ * index, RTX_NONE for node entries and holes) */
+__global__ void k_w8_fill(const DPrim *__restrict__ prims, const uint32_t *__restrict__ leafmap, uint32_t n, DW8 *__restrict__ out)
+{
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= 4 * n)
+		return;
+	const uint32_t e = i >> 2, p = leafmap[e];
+	if (p == RTX_NONE)
+		return;
+	((float4 *)(out + e))[i & 3] = ldg4((const char *)(prims + p), 16 * (i & 3));
+}
+
+extern "C" hipError_t rtx_launch_w8_fill(const DPrim *prims, const uint32_t *leafmap, uint32_t n, DW8 *out, hipStream_t stream)
+{
+	if (!n)
+		return hipSuccess;
+	hipLaunchKernelGGL(k_w8_fill, dim3((4 * n + 255) / 256), dim3(256), 0, stream, prims, leafmap, n, out);
+	return hipGetLastError();
 }
 
 extern "C" hipError_t rtx_launch_kat_shadow(int kind, uint32_t n, const float *in, float *out, hipStream_t stream)
@@ -940,19 +1221,60 @@ extern "C" hipError_t rtx_launch_kat_shadow(int kind, uint32_t n, const float *i
 /* ------------------------------------------------------------------------ */
 /* launcher (called from rtx_api.cpp)                                       */
 /* ------------------------------------------------------------------------ */
-/* the persistent grid: as many workgroups as are resident on the device at once (no more than
- * the work needs); the waves then share the shade points through RTX_C_SPQUEUE */
-template <bool C, int O, bool W> static hipError_t launch_shadow(const KShadow &ka, uint32_t nw, uint32_t cus, hipStream_t stream)
+template <bool C, int O, int W> static hipError_t shadow_slots(uint32_t cus, uint32_t *slots)
 {
 	int per_cu = 0;
 	hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(&k_shadow<C, O, W>),
 								   WAVE * RTX_SH_NW, 0);
+	*slots = per_cu > 0 && cus > 0 ? (uint32_t)per_cu * cus : 1024u;
+	return e;
+}
+
+/* the persistent grid: as many workgroups as are resident on the device at once (no more than
+ * the work needs); the waves then share the shade points through RTX_C_SPQUEUE */
+template <bool C, int O, int W> static hipError_t launch_shadow(const KShadow &ka, uint32_t nw, uint32_t cus, hipStream_t stream)
+{
+	uint32_t slots = 0;
+	hipError_t e = shadow_slots<C, O, W>(cus, &slots);
 	if (e != hipSuccess)
 		return e;
-	const uint32_t slots = per_cu > 0 && cus > 0 ? (uint32_t)per_cu * cus : 1024u;
 	const uint32_t need = (nw + RTX_SH_NW - 1) / RTX_SH_NW;
 	hipLaunchKernelGGL((k_shadow<C, O, W>), dim3(need < slots ? need : slots), dim3(WAVE * RTX_SH_NW), 0, stream, ka);
 	return hipGetLastError();
+}
+
+template <int W> static hipError_t launch_walk(const KShadow &ka, uint32_t nw, uint32_t cus, int count, hipStream_t stream)
+{
+	if (count)
+		return launch_shadow<true, 1, W>(ka, nw, cus, stream);
+#if RTX_MEASURE
+	/* occupancy variant (measurement builds): RTX_SHADOW_OCC = 1 (the compiler's choice) */
+	const char *env = getenv("RTX_SHADOW_OCC");
+	if (env && atoi(env) != RTX_SHADOW_OCC_DEFAULT)
+		return launch_shadow<false, 1, W>(ka, nw, cus, stream);
+#endif
+	return launch_shadow<false, RTX_SHADOW_OCC_DEFAULT, W>(ka, nw, cus, stream);
+}
+
+/* the walk k_shadow runs for a scene: the 8-wide BVH when built, else the 4-wide one, else the
+ * threaded BVH2 */
+static int walk_of(const DScene *S) { return S->w8 ? WALK_W8 : S->wnodes ? WALK_W4 : WALK_BVH2; }
+
+/* grid lanes of the largest k_shadow launch on `cus` CUs (sizes the 8-wide walk's spill area) */
+extern "C" hipError_t rtx_shadow_grid_lanes(uint32_t cus, uint32_t *lanes)
+{
+	uint32_t a = 0, b = 0;
+	hipError_t e = shadow_slots<false, RTX_SHADOW_OCC_DEFAULT, WALK_W8>(cus, &a);
+	if (e == hipSuccess)
+		e = shadow_slots<true, 1, WALK_W8>(cus, &b);
+#if RTX_MEASURE
+	uint32_t c = 0;
+	if (e == hipSuccess)
+		e = shadow_slots<false, 1, WALK_W8>(cus, &c);
+	b = b > c ? b : c;
+#endif
+	*lanes = (a > b ? a : b) * WAVE * RTX_SH_NW;
+	return e;
 }
 
 extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const float4 *sp, const uint32_t *perm,
@@ -966,6 +1288,18 @@ extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const
 		return hipSuccess;
 	if (S->num_top > RTX_TOP_MAX)
 		return hipErrorInvalidValue;
+	const int walk = walk_of(S);
+	if (walk == WALK_W8 && (S->w8lstk < 1 || S->w8lstk > RTX_W8_STACK))
+		return hipErrorInvalidValue;
+	if (walk == WALK_W8 && S->w8depth > S->w8lstk + 1) {
+		/* deep trees spill lane-stack entries to HBM: the area must cover this launch's grid */
+		uint32_t lanes = 0;
+		hipError_t e = rtx_shadow_grid_lanes(cus, &lanes);
+		if (e != hipSuccess)
+			return e;
+		if (!S->w8spill || S->w8spill_lanes < lanes)
+			return hipErrorInvalidValue;
+	}
 	KShadow ka;
 	ka.prims = S->prims;
 	ka.recs = (const char *)S->nodes;
@@ -998,14 +1332,12 @@ extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const
 	ka.att_offset = P->att_offset;
 	ka.wnodes = S->wnodes;
 	ka.wtris = (const char *)S->wtris;
-	const bool wide = S->wnodes != nullptr;
-	if (count)
-		return wide ? launch_shadow<true, 1, true>(ka, nw, cus, stream) : launch_shadow<true, 1, false>(ka, nw, cus, stream);
-	/* occupancy variant (measurement): RTX_SHADOW_OCC = 1 (the compiler's choice) */
-	const char *env = getenv("RTX_SHADOW_OCC");
-	const int occ = env ? atoi(env) : RTX_SHADOW_OCC_DEFAULT;
-	constexpr int O = RTX_SHADOW_OCC_DEFAULT;
-	if (occ == O)
-		return wide ? launch_shadow<false, O, true>(ka, nw, cus, stream) : launch_shadow<false, O, false>(ka, nw, cus, stream);
-	return wide ? launch_shadow<false, 1, true>(ka, nw, cus, stream) : launch_shadow<false, 1, false>(ka, nw, cus, stream);
+	ka.w8 = S->w8;
+	ka.w8spill = S->w8spill;
+	ka.w8lstk = S->w8lstk;
+	if (walk == WALK_W8)
+		return launch_walk<WALK_W8>(ka, nw, cus, count, stream);
+	if (walk == WALK_W4)
+		return launch_walk<WALK_W4>(ka, nw, cus, count, stream);
+	return launch_walk<WALK_BVH2>(ka, nw, cus, count, stream);
 }

@@ -216,6 +216,11 @@ class Renderer:
         """rtx_set_builder: abi.RTX_BUILD_SAH_HOST (default) or abi.RTX_BUILD_LBVH_GPU."""
         _check(self.lib.rtx_set_builder(self._ctx, builder))
 
+    def set_option(self, option, value):
+        """rtx_set_option: abi.RTX_OPT_* (shadow walk, BVH leaf size, shade-point sort, k_shadow
+        slot and grab sizes); build options take effect at the next upload."""
+        _check(self.lib.rtx_set_option(self._ctx, option, int(value)))
+
     def upload(self, scene):
         _check(self.lib.rtx_upload_scene(self._ctx, C.byref(scene.desc)))
 
@@ -285,6 +290,9 @@ class Group:
 
     def set_builder(self, builder):
         _check(self.lib.rtx_group_set_builder(self._g, builder))
+
+    def set_option(self, option, value):
+        _check(self.lib.rtx_group_set_option(self._g, option, int(value)))
 
     def upload(self, scene):
         _check(self.lib.rtx_group_upload_scene(self._g, C.byref(scene.desc)))

@@ -70,10 +70,13 @@ class Stats(C.Structure):
                 ("shadow_wave_steps", C.c_uint64), ("shadow_wave_walks", C.c_uint64),
                 ("wide_nodes", C.c_uint32), ("wide_depth", C.c_uint32), ("shadow_leaf_rounds", C.c_uint64),
                 ("gather_ms", C.c_double), ("devices", C.c_uint32), ("pad_", C.c_uint32),
-                ("shadow_uniform_steps", C.c_uint64)]
+                ("shadow_uniform_steps", C.c_uint64), ("shadow_walk", C.c_uint32), ("wide_entries", C.c_uint32)]
 
 
 RTX_BUILD_SAH_HOST, RTX_BUILD_LBVH_GPU = 0, 1
+RTX_WALK_AUTO, RTX_WALK_BVH2, RTX_WALK_W4, RTX_WALK_W8 = -1, 0, 1, 2
+RTX_OPT_SHADOW_WALK, RTX_OPT_BVH_LEAF, RTX_OPT_SPSORT, RTX_OPT_SHADOW_SLOT, RTX_OPT_SHADOW_GRAB, \
+    RTX_OPT_SHADOW_LDS_STACK = 1, 2, 3, 4, 5, 6
 RTX_DOF_NONE, RTX_DOF_SCALE_BIAS, RTX_DOF_CAMERA = 0, 1, 2
 RTX_FALLOFF_QUAD, RTX_FALLOFF_LIN, RTX_FALLOFF_INV_QUAD = 0, 1, 2
 
@@ -88,17 +91,18 @@ class Post(C.Structure):
 
 # include/rtx_kat.h
 KAT_MOLLER, KAT_SPHERE, KAT_PLANE, KAT_SLAB, KAT_NOISE, KAT_TEXTURE, KAT_SPH_LIGHT, KAT_TRI_LIGHT, \
-    KAT_MORTON, KAT_U32, KAT_GI_DIR, KAT_REFRACT, KAT_ANY_TRI, KAT_SPH_LIGHT_SH, KAT_BOX_Q, KAT_SPEC_POW = range(16)
-KAT_IN = [16, 11, 11, 13, 3, 16, 9, 11, 3, 1, 6, 7, 17, 9, 19, 2]
-KAT_OUT = [2, 5, 5, 3, 1, 3, 3, 3, 1, 2, 3, 3, 1, 3, 2, 1]
+    KAT_MORTON, KAT_U32, KAT_GI_DIR, KAT_REFRACT, KAT_ANY_TRI, KAT_SPH_LIGHT_SH, KAT_BOX_Q, KAT_SPEC_POW, \
+    KAT_BOX_Q8 = range(17)
+KAT_IN = [16, 11, 11, 13, 3, 16, 9, 11, 3, 1, 6, 7, 17, 9, 19, 2, 25]
+KAT_OUT = [2, 5, 5, 3, 1, 3, 3, 3, 1, 2, 3, 3, 1, 3, 2, 1, 2]
 KAT_NAMES = ["moller", "sphere", "plane", "slab", "noise", "texture", "sph_light", "tri_light", "morton", "u32",
-             "gi_dir", "refract", "any_tri", "sph_light_sh", "box_q", "spec_pow"]
+             "gi_dir", "refract", "any_tri", "sph_light_sh", "box_q", "spec_pow", "box_q8"]
 
 # symbols include/rtx.h declares (checked by tests/test_abi.py)
 RTX_SYMBOLS = ["rtx_params_default", "rtx_device_count", "rtx_open", "rtx_upload_scene", "rtx_render",
                "rtx_render_device", "rtx_get_stats", "rtx_close", "rtx_last_error", "rtx_kat", "rtx_postprocess",
-               "rtx_postprocess_device", "rtx_set_builder", "rtx_group_open", "rtx_group_size",
-               "rtx_group_set_builder", "rtx_group_upload_scene", "rtx_group_render", "rtx_group_get_stats",
+               "rtx_postprocess_device", "rtx_set_builder", "rtx_set_option", "rtx_group_open", "rtx_group_size",
+               "rtx_group_set_builder", "rtx_group_set_option", "rtx_group_upload_scene", "rtx_group_render", "rtx_group_get_stats",
                "rtx_group_close", "rtx_tile_pack_count", "rtx_tile_pack_host", "rtx_tile_unpack_host",
                "rtx_tile_pack_device", "rtx_tile_unpack_device"]
 RTX_SCENE_SYMBOLS = ["rtx_scene_load", "rtx_scene_parse", "rtx_scene_desc_of", "rtx_scene_num_json_objects",
@@ -164,6 +168,10 @@ def declare_rtx(lib):
     lib.rtx_kat.restype = C.c_int
     lib.rtx_set_builder.argtypes = [C.c_void_p, C.c_int]
     lib.rtx_set_builder.restype = C.c_int
+    lib.rtx_set_option.argtypes = [C.c_void_p, C.c_int, C.c_int64]
+    lib.rtx_set_option.restype = C.c_int
+    lib.rtx_group_set_option.argtypes = [C.c_void_p, C.c_int, C.c_int64]
+    lib.rtx_group_set_option.restype = C.c_int
     lib.rtx_postprocess.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(Post), C.c_void_p, C.c_void_p]
     lib.rtx_postprocess.restype = C.c_int
     lib.rtx_postprocess_device.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(Post), C.c_void_p,

@@ -152,8 +152,9 @@ enum rtx_u32conv {
 };
 
 /* render_init() globals (render.c:53-60) + library extensions. */
+#define RTX_MAX_BOUNCES 4096 /* the reflection/refraction task stacks are sized for max_bounces up to this */
 typedef struct rtx_params {
-	uint32_t max_bounces;        /* -b, default 10 */
+	uint32_t max_bounces;        /* -b, default 10, at most RTX_MAX_BOUNCES (RTX_ERR_ARG above) */
 	float min_intensity_sqr;     /* -a squared, default 1e-4 */
 	int32_t reflection;          /* -s, enum rtx_reflection, default phong */
 	int32_t gi;                  /* -g, enum rtx_gi, default ambient */
@@ -211,7 +212,9 @@ typedef struct rtx_stats {
 	double gather_ms;                 /* rtx_group_render: shard pack + RCCL gather + unpack (0 on one device) */
 	uint32_t devices;                 /* devices that rendered the last frame */
 	uint32_t pad_;
-	uint64_t shadow_uniform_steps;    /* only with count_traversal, 4-wide walk: wave steps whose active lanes all fetched one node */
+	uint64_t shadow_uniform_steps;    /* only with count_traversal, wide walks: wave steps whose active lanes all fetched one node */
+	uint32_t shadow_walk;             /* the BVH k_shadow walks: RTX_WALK_W8 / RTX_WALK_W4 / RTX_WALK_BVH2 */
+	uint32_t wide_entries;            /* 8-wide walk: 64-byte entries (nodes, primitive records, holes) */
 } rtx_stats;
 
 typedef struct rtx_ctx rtx_ctx;
@@ -238,6 +241,26 @@ int rtx_render_device(rtx_ctx *ctx, const rtx_frame *frame, const rtx_params *pa
 int rtx_get_stats(const rtx_ctx *ctx, rtx_stats *out);
 /* Builder used by subsequent rtx_upload_scene calls on this context (RTX_BUILD_*). */
 int rtx_set_builder(rtx_ctx *ctx, int builder);
+
+/* Shadow-walk BVH layouts (rtx_stats.shadow_walk, RTX_OPT_SHADOW_WALK) */
+enum {
+	RTX_WALK_AUTO = -1, /* the fastest available: 8-wide when it can be built */
+	RTX_WALK_BVH2 = 0,  /* threaded quantised BVH2 (DQNode), no stack */
+	RTX_WALK_W4 = 1,    /* 4-wide quantised BVH (global 16-bit frame) */
+	RTX_WALK_W8 = 2     /* 8-wide compressed BVH (8-bit child boxes in each node's frame) */
+};
+/* Context options: the defaults are the tuned values; the others exist for A/B measurement and
+ * tests.  Build options take effect at the next rtx_upload_scene. */
+enum rtx_option {
+	RTX_OPT_SHADOW_WALK = 1, /* RTX_WALK_* (build; default RTX_WALK_AUTO) */
+	RTX_OPT_BVH_LEAF = 2,    /* most primitives per BVH2 leaf, 1..16 (build; default 1) */
+	RTX_OPT_SPSORT = 3,      /* 1: shade points in Morton order for k_shadow (default); 0: emission order */
+	RTX_OPT_SHADOW_SLOT = 4, /* k_shadow lanes per shade-point slot: 0 = automatic (default), else a power of two <= 64 */
+	RTX_OPT_SHADOW_GRAB = 5, /* lane slots per k_shadow work-queue grab, >= 1 (default 4096) */
+	RTX_OPT_SHADOW_LDS_STACK = 6 /* 8-wide walk: lane-stack entries kept in LDS, 1..8 (default 8); deeper
+	                              * ones spill to HBM (tests use 1 to exercise the spill on any tree) */
+};
+int rtx_set_option(rtx_ctx *ctx, int option, int64_t value);
 void rtx_close(rtx_ctx *ctx);
 const char *rtx_last_error(void);
 
@@ -257,6 +280,7 @@ typedef struct rtx_group rtx_group;
 int rtx_group_open(int n, const int *devices, rtx_group **out);
 int rtx_group_size(const rtx_group *g);
 int rtx_group_set_builder(rtx_group *g, int builder);
+int rtx_group_set_option(rtx_group *g, int option, int64_t value); /* rtx_set_option on every device */
 int rtx_group_upload_scene(rtx_group *g, const rtx_scene_desc *scene);
 /* params->tile_offset / tile_stride must be 0 / 1: the group shards the frame itself.
  * rgb / z: HOST buffers as for rtx_render (either may be NULL). */

@@ -25,6 +25,10 @@
  *                     threaded BVH, rtx_quant.h, then tested by box_hit_q on the segment (0, tlim))
  * KAT_SPEC_POW(15)   x y                               = 2           fmaxf(0, pow(x, y))    = 1  render.c:224 (specular term,
  *                    x = specular_mul, y = shininess; the device runs sh_pow, the oracle glibc powf)
+ * KAT_BOX_Q8 (16)   o3 d3 lo3 hi3 qo3 qs3 tlim org3 e3 = 25        hit(generic) hit(octant) = 2  accel.c:112-158
+ *                    (the box quantised to 16 bits as for KAT_BOX_Q, then to 8 bits in an 8-wide node frame of
+ *                     origin org (grid units, <= the 16-bit lo) and steps 2^e, rtx_quant.h rtx_quantise8, and
+ *                     tested by the 8-wide walk's child test, rtx_shadow.hip w8_child)
  * Texture records use the params' u32conv for the float->uint32 conversion.
  */
 #ifndef RTX_KAT_H
@@ -47,11 +51,12 @@ enum rtx_kat_kind {
 	RTX_KAT_SPH_LIGHT_SH = 13,
 	RTX_KAT_BOX_Q = 14,
 	RTX_KAT_SPEC_POW = 15,
-	RTX_KAT_NKINDS = 16,
+	RTX_KAT_BOX_Q8 = 16,
+	RTX_KAT_NKINDS = 17,
 };
 #define RTX_KAT_FIRST_SHADOW RTX_KAT_ANY_TRI /* kinds >= this run in rtx_shadow.hip */
 
-static const int rtx_kat_in_width[RTX_KAT_NKINDS] = { 16, 11, 11, 13, 3, 16, 9, 11, 3, 1, 6, 7, 17, 9, 19, 2 };
-static const int rtx_kat_out_width[RTX_KAT_NKINDS] = { 2, 5, 5, 3, 1, 3, 3, 3, 1, 2, 3, 3, 1, 3, 2, 1 };
+static const int rtx_kat_in_width[RTX_KAT_NKINDS] = { 16, 11, 11, 13, 3, 16, 9, 11, 3, 1, 6, 7, 17, 9, 19, 2, 25 };
+static const int rtx_kat_out_width[RTX_KAT_NKINDS] = { 2, 5, 5, 3, 1, 3, 3, 3, 1, 2, 3, 3, 1, 3, 2, 1, 2 };
 
 #endif

@@ -1038,7 +1038,8 @@ int rtx_oracle_kat(int kind, uint32_t n, const float *in, float *out, const rtx_
 		case RTX_KAT_SPEC_POW: /* render.c:224 fmaxf(0., powf(specular_mul, shininess)) */
 			y[0] = fmaxf(0.f, powf(x[0], x[1]));
 			break;
-		case RTX_KAT_BOX_Q: { /* the exact answer in double: does the segment (0, tlim) of the ray meet
+		case RTX_KAT_BOX_Q:
+		case RTX_KAT_BOX_Q8: { /* the exact answer in double: does the segment (0, tlim) of the ray meet
 				       * the (unquantised) box?  A conservative quantised test must say hit
 				       * wherever this does (the frame fields are unused here). */
 			double tn = 0.0, tf = x[18];

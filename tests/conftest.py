@@ -109,3 +109,53 @@ def _torch_hip_first():
     except Exception:
         pass
     yield
+
+
+# ---- multi-seed statistical goldens (tests/golden/seeds, tools/make_seed_goldens.py) ----
+SEEDS = os.path.join(GOLDEN, "seeds")
+STAT_MEAN_TOL = 0.01  # per-channel image means within 1 %
+STAT_BOX_TOL = 0.03   # 8x8-box-filtered relL1 <= 3 %
+
+
+def seed_manifest():
+    with open(os.path.join(SEEDS, "manifest.json")) as fh:
+        return json.load(fh)
+
+
+def load_seedset(name):
+    """(scene, frame, params, manifest entry, golden npz) of a multi-seed reference config"""
+    import rtxpy
+    import standins
+    m = seed_manifest()[name]
+    if "standin" in m["scene"]:
+        standins.ensure_scene(m["scene"].split("_standin")[0])
+    scene = rtxpy.Scene.load(os.path.join(SCENES, m["scene"]), base_dir=GOLDEN)
+    frame = scene.frame(m["width"], m["height"])
+    params = rtxpy.params_from_args(m["flags"])
+    return scene, frame, params, m, np.load(os.path.join(SEEDS, name + ".npz"))
+
+
+def seed_average(render, params, seeds):
+    """average image and z of render(params) over params.seed in seeds (a counter-RNG seed is
+    any 64-bit value; the reference's seeds are glibc srand seeds: the streams are unrelated)"""
+    acc, z0 = None, None
+    for s in seeds:
+        params.seed = 0x5EED0000 + int(s)
+        rgb, z = render(params)
+        acc = rgb.astype(np.float64) if acc is None else acc + rgb
+        z0 = z if z0 is None else z0
+    return acc / len(seeds), z0
+
+
+def compare_stat(avg, z, golden):
+    """SURVEY §8(c) statistical parity of a seed-averaged render against the reference's
+    seed-averaged frame: hit mask, per-channel means within 1 %, box-filtered relL1 <= 3 %"""
+    ref = golden["mean_rgb"].astype(np.float64)
+    info = {"hit_mismatch": float(((z > 0) != (golden["z"] > 0)).mean())}
+    mean, ref_mean = avg.reshape(-1, 3).mean(0), ref.reshape(-1, 3).mean(0)
+    info["mean_rel"] = [float(x) for x in np.abs(mean - ref_mean) / np.maximum(np.abs(ref_mean), 1e-30)]
+    lp, ref_lp = box_filter(avg), box_filter(ref)
+    info["box_rel_l1"] = float(np.abs(lp - ref_lp).sum() / max(float(np.abs(ref_lp).sum()), 1e-30))
+    ok = (info["hit_mismatch"] <= 1e-3 and max(info["mean_rel"]) <= STAT_MEAN_TOL
+          and info["box_rel_l1"] <= STAT_BOX_TOL)
+    return ok, info

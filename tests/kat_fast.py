@@ -106,3 +106,33 @@ def libm_spec_pow(recs):
         p = libm.powf(float(x), float(y))
         out[i] = p if p > 0.0 else 0.0  # fmaxf(0, NaN) = 0
     return out
+
+
+def quantise16(lo, hi, qo, qs):
+    """rtx_quant.h rtx_quantise in float64 on the float32 inputs: (lo16, hi16) grid planes"""
+    lo, hi = lo.astype(np.float32).astype(np.float64), hi.astype(np.float32).astype(np.float64)
+    qo, qs = qo.astype(np.float32).astype(np.float64), qs.astype(np.float32).astype(np.float64)
+    a = np.floor((lo - qo) * qs) - 1.0
+    b = np.ceil((hi - qo) * qs) + 1.0
+    return np.clip(a, 0, 65535).astype(np.int64), np.clip(b, 0, 65535).astype(np.int64)
+
+
+def box_q8_records(n=20000, seed=13):
+    """box_q_records plus an 8-wide node frame per axis (rtx_device.h DW8): an origin at or below
+    the box's 16-bit lo (down to the frame's 0) and a step exponent at or above the smallest one
+    whose 255 steps reach the box's 16-bit hi (up to 3 more), as the 8-wide builder may choose
+    for a box among siblings.  Record: o3 d3 lo3 hi3 qo3 qs3 tlim org3 e3."""
+    rng = np.random.default_rng(seed)
+    base = box_q_records(n, seed)
+    ql, qh = quantise16(base[:, 6:9], base[:, 9:12], base[:, 12:15], base[:, 15:18])
+    org = (ql * rng.random((n, 3)) ** 4).astype(np.int64)  # mostly close to lo, sometimes far below
+    ext = qh - org
+    e = np.zeros((n, 3), np.int64)
+    while True:
+        big = ((ext + (1 << e) - 1) >> e) > 255
+        if not big.any():
+            break
+        e[big] += 1
+    e += rng.integers(0, 4, (n, 3)) * (rng.random((n, 3)) < 0.3)
+    e = np.minimum(e, 15)
+    return np.concatenate([base, org.astype(np.float32), e.astype(np.float32)], 1).astype(np.float32)

@@ -46,16 +46,19 @@ def test_gpu_lbvh_frames_match(renderer, name):
     assert np.abs(a - b).max() <= 1e-5 * max(1.0, float(np.abs(a).max())), name
 
 
-def test_gpu_lbvh_deterministic_and_tiny_scenes(renderer, monkeypatch):
+def test_gpu_lbvh_deterministic_and_tiny_scenes(renderer):
     scene, frame, params, _ = C.load_config("s5_path2")
     a, za, st = render(renderer, abi.RTX_BUILD_LBVH_GPU, scene, frame, params)
     b, zb, _ = render(renderer, abi.RTX_BUILD_LBVH_GPU, scene, frame, params)
     assert np.array_equal(a, b) and np.array_equal(za, zb)
     assert st.bvh_nodes == st.bvh_prims - 1  # single-primitive leaves (the default): a full binary tree
     # scene1: 3 spheres + a light -> with leaves of up to 4 primitives, a single-leaf root
-    monkeypatch.setenv("RTX_BVH_LEAF", "4")
+    renderer.set_option(abi.RTX_OPT_BVH_LEAF, 4)
     scene, frame, params, _ = C.load_config("s1_amb")
-    a, za, st = render(renderer, abi.RTX_BUILD_LBVH_GPU, scene, frame, params)
+    try:
+        a, za, st = render(renderer, abi.RTX_BUILD_LBVH_GPU, scene, frame, params)
+    finally:
+        renderer.set_option(abi.RTX_OPT_BVH_LEAF, 1)
     assert st.bvh_nodes == 0
     o_rgb, o_z = C.golden_frame("s1_amb_o2")
     ok, info = C.compare_const(a, za, o_rgb, o_z)

@@ -1,12 +1,14 @@
-"""The 4-wide shadow-walk BVH (rtx_device.h RTX_W_STACK, rtx_shadow.hip shadow_walk4) against the
-threaded BVH2 walk it replaced (RTX_WIDE=0 keeps the BVH2 walk, the fallback for trees too deep
-for the wide walk's LDS stacks).
+"""The shadow walks over their BVH layouts (include/rtx.h RTX_WALK_*, rtx_shadow.hip):
 
-Both walks answer is_light_blocked (render.c:126-134, accel.c:360-387) exactly: the same boxes,
-quantised the same way, cull the same primitives, and any-hit needs no visit order.  Only the
-order in which transparent blockers multiply a ray's transmittance may differ (leaves are met
-in another order), so z-buffers and ray counts are identical and colours agree to float
-rounding; both stay inside the reference goldens' tolerance.
+  RTX_WALK_W8    8-wide compressed BVH (rtx_device.h DW8, shadow_walk8), the default
+  RTX_WALK_W4    4-wide BVH quantised in the global 16-bit frame (shadow_walk4)
+  RTX_WALK_BVH2  threaded BVH2 (shadow_walk), the fallback for trees the 8-wide layout cannot hold
+
+All answer is_light_blocked (render.c:126-134, accel.c:360-387) exactly: each culls only with
+conservative boxes and any-hit needs no visit order.  Only the order in which transparent
+blockers multiply a ray's transmittance may differ (leaves are met in another order), so
+z-buffers and ray counts are identical and colours agree to float rounding; every walk stays
+inside the reference goldens' tolerance.
 """
 import numpy as np
 import pytest
@@ -27,56 +29,96 @@ def renderer():
     r.close()
 
 
-def render(r, scene, frame, params):
+@pytest.fixture(autouse=True)
+def _defaults(renderer):
+    yield
+    renderer.set_builder(abi.RTX_BUILD_SAH_HOST)
+    renderer.set_option(abi.RTX_OPT_SHADOW_WALK, abi.RTX_WALK_AUTO)
+    renderer.set_option(abi.RTX_OPT_BVH_LEAF, 1)
+    renderer.set_option(abi.RTX_OPT_SHADOW_LDS_STACK, 8)
+
+
+def render(r, scene, frame, params, walk=abi.RTX_WALK_AUTO):
+    r.set_option(abi.RTX_OPT_SHADOW_WALK, walk)
     r.upload(scene)
     rgb, z = r.render(frame, params)
     return rgb, z, r.stats()
 
 
 @pytest.mark.parametrize("name", CONFIGS)
-def test_gpu_wide_walk_matches_bvh2_walk(renderer, name, monkeypatch):
+def test_gpu_walks_agree(renderer, name):
     scene, frame, params, _ = C.load_config(name)
-    renderer.set_builder(abi.RTX_BUILD_SAH_HOST)
     a, za, sa = render(renderer, scene, frame, params)
-    assert sa.wide_nodes > 0 and 1 <= sa.wide_depth <= 13
-    monkeypatch.setenv("RTX_WIDE", "0")
-    b, zb, sb = render(renderer, scene, frame, params)
-    assert sb.wide_nodes == 0 and sb.wide_depth == 0
-    assert np.array_equal(za, zb), name
-    assert (sa.closest_rays, sa.shadow_rays) == (sb.closest_rays, sb.shadow_rays)
-    assert np.abs(a - b).max() <= 1e-5 * max(1.0, float(np.abs(b).max())), name
+    assert sa.shadow_walk == abi.RTX_WALK_W8 and sa.wide_nodes > 0 and sa.wide_depth >= 1
+    assert sa.wide_entries >= 8 * sa.wide_nodes
     ref_rgb, ref_z = C.golden_frame(name + "_o2")
-    for rgb, z in ((a, za), (b, zb)):
-        ok, info = C.compare_const(rgb, z, ref_rgb, ref_z)
-        assert ok, (name, info)
+    for walk in (abi.RTX_WALK_W4, abi.RTX_WALK_BVH2):
+        b, zb, sb = render(renderer, scene, frame, params, walk)
+        assert sb.shadow_walk == walk
+        assert np.array_equal(za, zb), (name, walk)
+        assert (sa.closest_rays, sa.shadow_rays) == (sb.closest_rays, sb.shadow_rays)
+        assert np.abs(a - b).max() <= 1e-5 * max(1.0, float(np.abs(b).max())), (name, walk)
+        ok, info = C.compare_const(b, zb, ref_rgb, ref_z)
+        assert ok, (name, walk, info)
+    ok, info = C.compare_const(a, za, ref_rgb, ref_z)
+    assert ok, (name, info)
 
 
-@pytest.mark.parametrize("leaf", ["2", "5"])
-def test_gpu_wide_walk_multi_primitive_leaves(renderer, leaf, monkeypatch):
-    """Leaves of several primitives (RTX_BVH_LEAF > 1): the wide tree's leaf slots hold the
-    BVH2 leaves whole and the walk tests their primitives in order."""
-    monkeypatch.setenv("RTX_BVH_LEAF", leaf)
+@pytest.mark.parametrize("name", ["s5_path2", "s6_amb", "s3_path2"])
+def test_gpu_w8_lane_stack_spill(renderer, name):
+    """Trees deeper than the LDS lane stack walk on with the deeper entries in HBM: with one LDS
+    entry every wide node below the second level spills (the path the depth-cliff fallback of
+    the 4-wide walk never had); the frame is bit-identical to the all-LDS walk and matches the
+    reference."""
+    scene, frame, params, _ = C.load_config(name)
+    params.rng = abi.RTX_RNG_COUNTER
+    a, za, sa = render(renderer, scene, frame, params)
+    renderer.set_option(abi.RTX_OPT_SHADOW_LDS_STACK, 1)
+    b, zb, sb = render(renderer, scene, frame, params)
+    assert sb.shadow_walk == abi.RTX_WALK_W8 and sb.wide_depth > 2
+    assert np.array_equal(a, b) and np.array_equal(za, zb)
+    assert (sa.closest_rays, sa.shadow_rays) == (sb.closest_rays, sb.shadow_rays)
+    from rtxpy import oracle
+    o_rgb, o_z, _ = oracle.render(scene, frame, params)
+    ok, info = C.compare_const(b, zb, o_rgb, o_z)
+    assert ok, info
+
+
+@pytest.mark.parametrize("leaf", [2, 5])
+def test_gpu_wide_walk_multi_primitive_leaves(renderer, leaf):
+    """BVH2 leaves of several primitives (RTX_OPT_BVH_LEAF > 1): the 8-wide collapse opens them
+    into one slot per primitive (boxes from the records), the 4-wide tree keeps them whole."""
+    renderer.set_option(abi.RTX_OPT_BVH_LEAF, leaf)
     for name in ("s5_path2", "st_amb"):
         scene, frame, params, _ = C.load_config(name)
-        renderer.set_builder(abi.RTX_BUILD_SAH_HOST)
-        a, za, sa = render(renderer, scene, frame, params)
-        assert sa.wide_nodes > 0
         ref_rgb, ref_z = C.golden_frame(name + "_o2")
-        ok, info = C.compare_const(a, za, ref_rgb, ref_z)
-        assert ok, (name, leaf, info)
+        for walk in (abi.RTX_WALK_W8, abi.RTX_WALK_W4):
+            a, za, sa = render(renderer, scene, frame, params, walk)
+            assert sa.shadow_walk == walk and sa.wide_nodes > 0
+            ok, info = C.compare_const(a, za, ref_rgb, ref_z)
+            assert ok, (name, leaf, walk, info)
 
 
-def test_gpu_wide_walk_counts(renderer):
-    """count_traversal on the wide walk: four box tests per node fetch at most, every fetch is a
-    global (no LDS top), and the wave's leaf rounds never exceed its node steps' leaf slots."""
+def test_gpu_w8_walk_counts(renderer):
+    """count_traversal on the 8-wide walk: at most eight box tests per node fetch, and leaf
+    rounds no more than the node steps' leaf slots."""
     scene, frame, params, _ = C.load_config("s5_path2")
-    renderer.set_builder(abi.RTX_BUILD_SAH_HOST)
     renderer.upload(scene)
     p = rtxpy.default_params(**{f: getattr(params, f) for f, _ in abi.Params._fields_})
     p.count_traversal = 1
     renderer.render(frame, p)
     st = renderer.stats()
+    assert st.shadow_walk == abi.RTX_WALK_W8
     assert st.shadow_rays > 0 and st.shadow_box_tests > 0
     assert st.shadow_global_box_tests == st.shadow_box_tests
-    assert st.shadow_wave_steps * 64 * 4 >= st.shadow_box_tests
-    assert 0 < st.shadow_leaf_rounds <= 4 * st.shadow_wave_steps
+    assert st.shadow_wave_steps * 64 * 8 >= st.shadow_box_tests
+    assert 0 < st.shadow_leaf_rounds <= 8 * st.shadow_wave_steps
+
+
+def test_gpu_options_reject_bad_values(renderer):
+    for opt, bad in ((abi.RTX_OPT_SHADOW_WALK, 3), (abi.RTX_OPT_BVH_LEAF, 0), (abi.RTX_OPT_SPSORT, 2),
+                     (abi.RTX_OPT_SHADOW_SLOT, 3), (abi.RTX_OPT_SHADOW_GRAB, 0), (abi.RTX_OPT_SHADOW_LDS_STACK, 9),
+                     (99, 1)):
+        with pytest.raises(rtxpy.RtxError) as e:
+            renderer.set_option(opt, bad)
+        assert e.value.code == abi.RTX_ERR_ARG
