@@ -542,6 +542,11 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 		memcpy(e.p1, o.p1, 12);
 		memcpy(e.p2, o.p2, 12);
 		e.radius = o.radius;
+		memcpy(e.e1, o.e1, 12);
+		memcpy(e.e2, o.e2, 12);
+		e.eps = o.epsilon;
+		e.transparent = (mats[o.material].flags & RTX_MF_TRANSPARENT) ? 1u : 0u;
+		memcpy(e.kt, mats[o.material].kt, 12);
 	}
 
 	const auto tb0 = std::chrono::steady_clock::now();
@@ -635,9 +640,13 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 	 * walks any depth; the 4-wide tree (depth-limited by its LDS stacks) and the threaded BVH2 for
 	 * measurement, and the BVH2 when the 8-wide tree cannot be built (over 2^24 entries) */
 	if (c->opt_walk == RTX_WALK_AUTO || c->opt_walk == RTX_WALK_W8) {
+		/* with the host records the emitters are left out of the tree (k_shadow tests them linearly) */
 		const DPrim *hp = hs.recs.size() >= (size_t)nnodes + nb ? (const DPrim *)(hs.recs.data() + nnodes) : nullptr;
-		hs.w8depth = rtx_wide8_build(inner, nnodes, hp, nb ? root_ref : RTX_EMPTY_REF, c->bound_lo, c->bound_hi, hs.qf,
-					     hs.w8, hs.w8leaf);
+		std::vector<uint32_t> emit_objs;
+		for (const DEmitter &e : emit)
+			emit_objs.push_back(e.obj);
+		hs.w8depth = rtx_wide8_build(inner, nnodes, hp, nb ? root_ref : RTX_EMPTY_REF, c->bound_lo, c->bound_hi, emit_objs,
+					     hs.w8f, hs.w8noemit, hs.w8, hs.w8leaf);
 	} else if (c->opt_walk == RTX_WALK_W4) {
 		hs.wdepth = wide_bvh(inner, nb ? root_ref : RTX_EMPTY_REF, c->bound_lo, c->bound_hi, hs.qf, hs.wnodes);
 		if (hs.wdepth > RTX_W_STACK + 1 || hs.wnodes.size() / 4 >= (1u << 26)) /* the lane stacks would overflow */
@@ -719,6 +728,9 @@ int rtx_upload_built(rtx_ctx *c, const HostScene &hs)
 	S.w8 = hs.w8.empty() ? nullptr : c->d_w8;
 	S.num_w8 = (uint32_t)hs.w8.size();
 	S.w8depth = hs.w8depth;
+	memcpy(S.w8qo, hs.w8f.qo, 12);
+	memcpy(S.w8qs, hs.w8f.qs, 12);
+	S.w8noemit = hs.w8noemit ? 1u : 0u;
 	S.root_ref = hs.root_ref;
 	S.num_prims = hs.nb;
 	S.num_planes = (uint32_t)hs.planes.size();

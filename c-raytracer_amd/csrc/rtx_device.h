@@ -125,7 +125,7 @@ typedef struct __attribute__((aligned(16))) DQNode {
  *        the node's frame on the 16-bit grid of DQNode: origin o (grid units) and a per-axis step
  *        of 2^e grid units (e <= 9)
  *   w2 = base << 8 | imask      children at entries base + c (c = slot 0..7); imask: inner slots
- *   w3 = vmask                  slots holding a child
+ *   w3 = vmask | tmask << 8     slots holding a child; leaf slots of transparent primitives
  *   w4..w15: 8-bit planes, slot c = byte c & 3 of the word:  lo_x w4,w5  hi_x w6,w7  lo_y w8,w9
  *            hi_y w10,w11  lo_z w12,w13  hi_z w14,w15
  * Child c's box is [o + lo * 2^e, o + hi * 2^e] on the grid, outward-rounded from its 16-bit box
@@ -137,7 +137,10 @@ typedef struct __attribute__((aligned(16))) DQNode {
  * Slots follow the children's centroid octant about the node centre (bit a: the + side of
  * axis a), so a ray of direction octant OCT meets them front to back roughly in the order
  * c ^ (~OCT & 7) = 0, 1, ..., 7; the walk visits hit children in that order.
- * Entry 0 is the root node, entry 1 a hole (blocks start on 128-byte lines). */
+ * Entry 0 is the root node, entry 1 a hole (blocks start on 128-byte lines).  The tree has its own
+ * 16-bit frame (DScene.w8qo / w8qs) over its primitives; the emitters are left out of it when the
+ * host has the primitive records (DScene.w8noemit): k_shadow tests them linearly, like planes,
+ * so a shadow ray no longer walks down to the light it was cast to. */
 #define RTX_W8_STACK 8     /* k_shadow lane-stack entries in LDS; deeper ones spill to HBM (DScene.w8spill) */
 #define RTX_W8_MAX_ENTRIES (1u << 24)
 typedef struct __attribute__((aligned(64))) DW8 {
@@ -172,6 +175,10 @@ typedef struct DEmitter {
 	float li[3];       /* ke * (1 / num_lights) */
 	float p0[3], p1[3], p2[3];
 	float radius;
+	float e1[3], e2[3]; /* triangle edges (object.c:331-334), for the shadow test of emitters kept */
+	float eps;          /* out of the 8-wide shadow tree (DScene.w8noemit) */
+	uint32_t transparent;
+	float kt[3];
 } DEmitter;
 
 #define RTX_MAX_EMITTERS 64
@@ -190,8 +197,10 @@ typedef struct DScene {
 	const DQNode *wnodes;   /* 4-wide BVH (4 records per node, same frame), null when not built */
 	const float *wtris;     /* its leaves' primitives as 48-byte records (the first 48 B of each DPrim) */
 	uint32_t num_wnodes, wdepth;
-	const DW8 *w8;          /* 8-wide compressed BVH (num_w8 entries, same frame), null when not built */
+	const DW8 *w8;          /* 8-wide compressed BVH (num_w8 entries), null when not built */
 	uint32_t num_w8, w8depth;
+	float w8qo[3], w8qs[3]; /* its 16-bit frame */
+	uint32_t w8noemit;      /* the emitters are not in it (k_shadow tests them linearly) */
 	uint32_t *w8spill;      /* k_shadow lane-stack entries from RTX_W8_STACK on, [entry][grid lane] */
 	uint32_t w8spill_lanes; /* grid lanes the spill area was sized for (0: no spill area) */
 	uint32_t w8lstk;        /* lane-stack entries k_shadow keeps in LDS (<= RTX_W8_STACK) */

@@ -119,6 +119,8 @@ struct HostScene {
 	std::vector<DW8> w8;          /* 8-wide BVH entries (leaf entries filled on the device) */
 	std::vector<uint32_t> w8leaf; /* entry -> primitive index (RTX_NONE: node or hole) */
 	uint32_t w8depth = 0;
+	QFrame w8f{};                 /* its 16-bit frame */
+	bool w8noemit = false;        /* emitters left out of it */
 	std::vector<DPlane> planes;
 	std::vector<DMaterial> mats;
 	std::vector<DEmitter> emit;
@@ -132,8 +134,8 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs);
 int rtx_upload_built(rtx_ctx *c, const HostScene &hs);
 /* rtx_wide8.cpp: the 8-wide shadow BVH collapsed from the BVH2 (0 = not built) */
 uint32_t rtx_wide8_build(const std::vector<DNode> &inner, uint32_t nnodes, const DPrim *prims, uint32_t root_ref,
-			 const float lo[3], const float hi[3], const QFrame &F, std::vector<DW8> &out,
-			 std::vector<uint32_t> &leafmap);
+			 const float lo[3], const float hi[3], const std::vector<uint32_t> &skip_objs, QFrame &F,
+			 bool &skipped, std::vector<DW8> &out, std::vector<uint32_t> &leafmap);
 /* one frame (or tile shard) into device buffers on stream */
 int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, float *d_rgb, float *d_z, hipStream_t stream);
 

@@ -247,6 +247,7 @@ struct QBvh {
 	uint32_t spill_stride;
 	uint32_t lstk;        /* lane-stack entries in LDS (<= RTX_W8_STACK) */
 	lds_u32 *stk;         /* this lane's LDS stack of sibling groups: entry k at stk[k * WAVE] */
+	lds_u32 *tq;          /* WALK_W8: this lane's LDS queue of deferred leaf groups, entry k at tq[k * WAVE] */
 };
 
 /* the shadow walks k_shadow instantiates */
@@ -531,12 +532,23 @@ __device__ __forceinline__ uint32_t w8_hits(const uint32_t (&w)[16], f3 s, f3 b,
 
 /* is_light_blocked's BVH part (accel.c:360-387) over the 8-wide BVH (rtx_device.h DW8): one
  * 64-byte node per step (four 16-byte loads, or one s_load_dwordx16 when every live lane is at
- * the node), eight box tests.  Hit children are taken in the octant's visit order (slot
- * p ^ K): leaf slots' primitives are tested at once, the first hit inner child is visited
- * next and the rest are kept as one group (base << 8 | mask in visit order) in a register, the
- * older groups in the lane's LDS stack (entries from RTX_W8_STACK on in HBM, Q.spill), at most
- * one per level, so any depth walks.  tl < 0 on entry: inactive lane.  On an opaque hit tl
- * becomes -1. */
+ * the node), eight box tests.  Hit children are taken in the octant's visit order (slot p ^ K):
+ *  - opaque leaf slots are tested at once (an opaque hit ends the ray);
+ *  - transparent leaf slots (tmask) can only multiply the transmittance, so their tests are
+ *    deferred: the lane keeps them as leaf groups (base << 8 | mask) in a register and an LDS
+ *    queue of RTX_W8_TQ, and the wave runs a round of deferred tests only when at least
+ *    RTX_W8_DEFER lanes hold some (or a queue is full, or no lane has node work left), so a
+ *    round tests many lanes' primitives instead of a few;
+ *  - the first hit inner child is visited next and the rest are kept as one group in a
+ *    register, the older groups in the lane's LDS stack (entries from Q.lstk on in HBM,
+ *    Q.spill), at most one per level, so any depth walks.
+ * tl < 0 on entry: inactive lane.  On an opaque hit tl becomes -1. */
+#ifndef RTX_W8_TQ
+#define RTX_W8_TQ 4 /* deferred leaf groups per lane in LDS (besides the one in a register) */
+#endif
+#ifndef RTX_W8_DEFER
+#define RTX_W8_DEFER 32 /* lanes holding deferred leaf tests that trigger a round of them */
+#endif
 template <bool COUNT, int OCT>
 __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__restrict__ mats, f3 o, f3 d, f3 inv,
 					     float &tl, uint32_t emit_obj, f3 &li, ShadowCount &sc)
@@ -545,14 +557,33 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 	const f3 invq = mk3(inv.x * Q.qsi.x, inv.y * Q.qsi.y, inv.z * Q.qsi.z);
 	const f3 oq = mk3((o.x - Q.qo.x) * Q.qs.x, (o.y - Q.qo.y) * Q.qs.y, (o.z - Q.qo.z) * Q.qs.z);
 	const f3 oi = mul3v(oq, invq);
-	lds_u32 *stk = Q.stk;
-	uint32_t node = tl >= 0.f ? 0u : RTX_NONE, grp = 0, sp = 0;
+	lds_u32 *stk = Q.stk, *tq = Q.tq;
+	uint32_t node = tl >= 0.f ? 0u : RTX_NONE, grp = 0, sp = 0, tgrp = 0, tn = 0;
 	uint32_t nbox = 0, ntri = 0, nsph = 0, nstep = 0, nlr = 0, nun = 0;
-	while (node != RTX_NONE) {
+	for (;;) {
+		const u64 walking = ballot(node != RTX_NONE);
+		const u64 holding = ballot(tgrp != 0);
+		if (!(walking | holding))
+			break;
+		if (!walking || popc64(holding) >= RTX_W8_DEFER || ballot(tn == RTX_W8_TQ)) {
+			/* a round of deferred transparent-leaf tests */
+			if (COUNT)
+				nlr++;
+			if (tgrp) {
+				const char *pr = (const char *)(Q.w8 + (tgrp >> 8) + (__builtin_ctz(tgrp) ^ K));
+				tgrp &= tgrp - 1;
+				if (!(tgrp & 0xFFu))
+					tgrp = tn ? tq[--tn * WAVE] : 0u;
+				shadow_prim<COUNT>(ldg4(pr, 0), ldg4(pr, 16), ldg4(pr, 32), mats, o, d, tl, emit_obj, li, ntri, nsph);
+			}
+			continue;
+		}
+		if (node == RTX_NONE)
+			continue;
 		uint32_t w[16];
 		const uint32_t un = uni(node);
 		if (RTX_W_SUNI && !ballot(node != un)) {
-			/* every live lane is at one node: read it through the scalar cache */
+			/* every walking lane is at one node: read it through the scalar cache */
 			const auto *U = (const __attribute__((address_space(4))) u4v *)(Q.w8 + (size_t)un);
 #pragma unroll
 			for (int k = 0; k < 4; k++) {
@@ -576,11 +607,12 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 		f3 s, b;
 		w8_frame(w, invq, oi, s, b);
 		const uint32_t hm = w8_hits<OCT, K>(w, s, b, tl);
-		const uint32_t base = w[2] >> 8, io = perm_xor<K>(w[2] & 0xFFu);
-		uint32_t lm = hm & ~io, im = hm & io;
+		const uint32_t base = w[2] >> 8, io = perm_xor<K>(w[2] & 0xFFu), to = perm_xor<K>((w[3] >> 8) & 0xFFu);
+		uint32_t lm = hm & ~io & ~to, im = hm & io;
+		const uint32_t dm = hm & to;
 		if (COUNT) {
 			nstep++;
-			nbox += popc64(w[3]);
+			nbox += popc64(w[3] & 0xFFu);
 			nun += ballot(node != uni(node)) ? 0u : 1u;
 			uint32_t r = 0;
 			for (uint32_t m = lm;; m &= m - 1) {
@@ -591,7 +623,7 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 			nlr += r;
 		}
 		bool blocked = false;
-		while (lm) {
+		while (lm) { /* opaque leaves: at once, an opaque hit ends the ray */
 			const uint32_t p = __builtin_ctz(lm);
 			lm &= lm - 1;
 			const char *pr = (const char *)(Q.w8 + base + (p ^ K));
@@ -602,7 +634,16 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 		}
 		if (blocked) {
 			tl = -1.f;
-			break;
+			node = RTX_NONE;
+			tgrp = 0;
+			continue;
+		}
+		if (dm) { /* transparent leaves: deferred */
+			const uint32_t g = (base << 8) | dm;
+			if (tgrp)
+				tq[tn++ * WAVE] = g;
+			else
+				tgrp = g;
 		}
 		if (im) {
 			node = base + (__builtin_ctz(im) ^ K);
@@ -658,8 +699,9 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
  * lane shares it.  Returns the lane's blocked flag; li carries the transmittance product. */
 template <bool COUNT, int WALK>
 __device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restrict__ recs, const DMaterial *__restrict__ mats,
-					     const DPlane *__restrict__ planes, uint32_t num_planes, bool have_tree, bool act,
-					     f3 o, f3 d, float dist, uint32_t emit_obj, f3 &li, ShadowCount &sc)
+					     const DPlane *__restrict__ planes, uint32_t num_planes, const DEmitter *__restrict__ emitters,
+					     uint32_t test_emitters, bool have_tree, bool act, f3 o, f3 d, float dist,
+					     uint32_t emit_obj, f3 &li, ShadowCount &sc)
 {
 	float tl = act ? dist : -1.f;
 	for (uint32_t i = 0; i < num_planes; i++) { /* plane records are wave-uniform: s_load */
@@ -671,6 +713,27 @@ __device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restri
 				li = mul3v(li, mk3(pl->kt[0], pl->kt[1], pl->kt[2]));
 		} else if (h) {
 			tl = -1.f;
+		}
+	}
+	/* the emitters other than the one sampled, when the 8-wide tree leaves them out
+	 * (rtx_device.h DW8): tested like the planes, records wave-uniform (s_load) */
+	for (uint32_t i = 0; i < test_emitters; i++) {
+		const auto *e = cptr(emitters) + i;
+		if (e->obj == emit_obj || !(tl >= 0.f))
+			continue;
+		bool h;
+		if (e->type == RTX_SPHERE) {
+			float t = 0.f;
+			h = hit_sphere(mk3(e->p0[0], e->p0[1], e->p0[2]), e->radius, o, d, e->eps, t) && t < tl;
+		} else {
+			h = any_tri(mk3(e->p0[0], e->p0[1], e->p0[2]), mk3(e->e1[0], e->e1[1], e->e1[2]),
+				    mk3(e->e2[0], e->e2[1], e->e2[2]), o, d, e->eps, tl);
+		}
+		if (h) {
+			if (e->transparent)
+				li = mul3v(li, mk3(e->kt[0], e->kt[1], e->kt[2]));
+			else
+				tl = -1.f;
 		}
 	}
 	if (COUNT)
@@ -719,9 +782,10 @@ struct KShadow {
 	const DQNode *qnodes; /* threaded quantised BVH */
 	const DQNode *wnodes; /* 4-wide quantised BVH (WALK_W4 instances) */
 	const char *wtris;    /* its leaves' 48-byte triangle records */
-	const DW8 *w8;        /* 8-wide compressed BVH (WALK_W8 instances) */
+	const DW8 *w8;        /* 8-wide compressed BVH (WALK_W8 instances; qo / qs / qsi are then its frame) */
 	uint32_t *w8spill;    /* lane-stack spill area, [entry][grid lane] */
 	uint32_t w8lstk;      /* lane-stack entries in LDS */
+	uint32_t test_emitters; /* emitters shadow_query tests linearly (the 8-wide tree leaves them out), else 0 */
 	float qo[3], qs[3], qsi[3];
 	const uint32_t *top; /* its top levels (rtx_device.h RTX_QTOP_CUT), copied to LDS per workgroup */
 	uint32_t ntop, nq;
@@ -876,8 +940,9 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	Q.spill = WALK == WALK_W8 ? unip(ks.w8spill) + blockIdx.x * blockDim.x + threadIdx.x : nullptr;
 	Q.lstk = uni(ks.w8lstk);
 	Q.stk = stk;
+	Q.tq = stk + RTX_W8_STACK * WAVE;
 	const bool blocked = shadow_query<COUNT, WALK>(Q, unip(ks.recs), unip(ks.mats), unip(ks.planes), uni(ks.num_planes),
-						 have_tree, act, p, ldir, ldist, E.obj, li, sc);
+						 emitters, uni(ks.test_emitters), have_tree, act, p, ldir, ldist, E.obj, li, sc);
 	reread_barrier();
 	f3 contribution = mk3(0.f, 0.f, 0.f);
 	if (act && !blocked)
@@ -898,7 +963,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 	__shared__ uint4 top_q[TOP ? RTX_TOP_MAX : 1];    /* the top records (rtx_device.h RTX_QTOP_CUT) */
 	__shared__ uint32_t top_e[TOP ? RTX_TOP_MAX : 1]; /* cut records: the DQNode index after the subtree */
 	/* the wide walks' lane stacks */
-	__shared__ uint32_t wstk[RTX_SH_NW][WALK == WALK_W4 ? RTX_W_STACK : WALK == WALK_W8 ? RTX_W8_STACK : 1][WAVE];
+	__shared__ uint32_t wstk[RTX_SH_NW][WALK == WALK_W4 ? RTX_W_STACK : WALK == WALK_W8 ? RTX_W8_STACK + RTX_W8_TQ : 1][WAVE];
 	__shared__ KShadow ks_w[RTX_SH_NW];
 	/* one wave's tables in one struct, so every lane addresses them from one base register */
 	struct WaveTables {
@@ -1335,6 +1400,15 @@ extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const
 	ka.w8 = S->w8;
 	ka.w8spill = S->w8spill;
 	ka.w8lstk = S->w8lstk;
+	ka.test_emitters = 0;
+	if (walk == WALK_W8) { /* the 8-wide tree's own frame; the emitters it leaves out are tested linearly */
+		for (int a = 0; a < 3; a++) {
+			ka.qo[a] = S->w8qo[a];
+			ka.qs[a] = S->w8qs[a];
+			ka.qsi[a] = 1.f / S->w8qs[a];
+		}
+		ka.test_emitters = S->w8noemit ? S->num_emitters : 0u;
+	}
 	if (walk == WALK_W8)
 		return launch_walk<WALK_W8>(ka, nw, cus, count, stream);
 	if (walk == WALK_W4)

@@ -1,12 +1,22 @@
 /*
  * The 8-wide compressed shadow BVH (rtx_device.h DW8), collapsed on the host from the BVH2 that
  * replaces the reference's tree (accel.c:266-315; any BVH answers is_light_blocked the same,
- * accel.c:360-387).  Every wide node opens its BVH2 subtree's top, the child of largest surface
- * area first, until it has eight children (the usual SAH-driven collapse); a leaf of several
- * primitives opens into one slot per primitive.  Child boxes are quantised to 8 bits in the
- * node's own frame on the 16-bit grid of the threaded BVH, rounded outward; slots follow the
- * children's centroid octant about the node centre, so the walk's slot order c ^ (~OCT & 7) is
- * front to back for a ray of direction octant OCT.
+ * accel.c:360-387).
+ *
+ * Which BVH2 nodes become wide nodes is decided by a surface-area cost optimisation over the
+ * BVH2 (the dynamic programme of Ylitie, Karras and Laine's compressed wide BVH): C(n, j) is
+ * the least expected cost of the subtree n spread over at most j slots of its wide parent,
+ *   C(prim, j)  = A(prim) * c_prim                                  (a leaf slot)
+ *   C(n, 1)     = A(n) * c_node + D(n, 8)                           (n becomes a wide node)
+ *   C(n, j > 1) = min(C(n, j - 1), D(n, j)),  D(n, j) = min_k C(l, k) + C(r, j - k)
+ * with A the box's surface area.  A leaf of several primitives enters the programme as a
+ * balanced binary tree of its primitives (boxes from the host records).  Primitives of the
+ * objects in skip_objs (the emitters) are left out when the host has the records, and the
+ * boxes are refitted bottom-up; the tree gets its own 16-bit frame over what remains.  Child
+ * boxes are
+ * quantised to 8 bits in the node's own frame on the 16-bit grid of the threaded BVH, rounded
+ * outward; slots follow the children's centroid octant about the node centre, so the walk's
+ * slot order c ^ (~OCT & 7) is front to back for a ray of direction octant OCT.
  */
 #include <float.h>
 #include <string.h>
@@ -20,49 +30,47 @@
 
 namespace {
 
-struct Kid {
-	uint32_t ref;  /* BVH2 device ref of a subtree (RTX_NONE: a single primitive) */
-	uint32_t prim; /* record-order primitive index when ref == RTX_NONE */
+/* expected-cost weights of a node visit (one 64-byte fetch, eight box tests) and of a primitive
+ * test, per unit of surface area */
+constexpr float C_NODE = 1.0f;
+constexpr float C_PRIM = 0.3f;
+
+struct TNode {
 	float lo[3], hi[3];
+	int32_t kid[2];  /* tree indices, -1 for a primitive */
+	uint32_t prim;   /* primitive index (record order) when kid[0] < 0 */
+};
+
+struct Slot {
+	int32_t t;   /* tree index */
+	bool node;   /* becomes a wide node (else a primitive's leaf slot) */
 };
 
 struct Builder {
 	const std::vector<DNode> &inner;
 	uint32_t nnodes;
-	const DPrim *prims; /* host primitive records (leaves of several primitives only), or null */
-	const QFrame &F;
+	const DPrim *prims;
+	const std::vector<uint32_t> &skip_objs;
+	QFrame F;
 	std::vector<DW8> &out;
 	std::vector<uint32_t> &leafmap;
+	std::vector<TNode> tree;
+	std::vector<float> cost;   /* [t * 9 + j], j = 1..8 */
+	std::vector<int8_t> pick;  /* [t * 9 + j]: 0 = C(t, j - 1), k > 0 = split k / j - k, -1 = wide node (j = 1) */
 	bool ok = true;
 
-	static bool is_leaf(uint32_t ref) { return (ref & RTX_REF_LEAF) != 0; }
-	uint32_t leaf_first(uint32_t ref) const { return (ref & RTX_REF_OFF) / (uint32_t)sizeof(DNode) - nnodes; }
-	static uint32_t leaf_count(uint32_t ref) { return (ref & RTX_REF_CNT) + 1; }
-
-	/* a child ref with its box as a kid: single-primitive leaves become primitive kids */
-	Kid kid(uint32_t ref, const float lo[3], const float hi[3]) const
+	static float area(const float lo[3], const float hi[3])
 	{
-		Kid k;
-		k.ref = ref;
-		k.prim = RTX_NONE;
-		memcpy(k.lo, lo, 12);
-		memcpy(k.hi, hi, 12);
-		if (is_leaf(ref) && leaf_count(ref) == 1) {
-			k.prim = leaf_first(ref);
-			k.ref = RTX_NONE;
-		}
-		return k;
+		const float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+		return dx * dy + dy * dz + dz * dx;
 	}
 
 	/* a primitive's box from its record, padded like the leaf boxes of rtx_build_scene */
-	Kid prim_kid(uint32_t i) const
+	void prim_box(uint32_t i, float lo[3], float hi[3]) const
 	{
 		const DPrim &p = prims[i];
 		uint32_t meta;
 		memcpy(&meta, &p.c[3], 4);
-		Kid k;
-		k.ref = RTX_NONE;
-		k.prim = i;
 		float l[3], h[3];
 		for (int a = 0; a < 3; a++) {
 			if ((meta >> 24) == RTX_SPHERE) {
@@ -76,78 +84,189 @@ struct Builder {
 		}
 		const float ext = std::max(h[0] - l[0], std::max(h[1] - l[1], h[2] - l[2]));
 		for (int a = 0; a < 3; a++) {
-			k.lo[a] = l[a] - (std::fabs(l[a]) + ext) * 4e-6f - 1e-30f;
-			k.hi[a] = h[a] + (std::fabs(h[a]) + ext) * 4e-6f + 1e-30f;
+			lo[a] = l[a] - (std::fabs(l[a]) + ext) * 4e-6f - 1e-30f;
+			hi[a] = h[a] + (std::fabs(h[a]) + ext) * 4e-6f + 1e-30f;
 		}
-		return k;
 	}
 
-	static float half_area(const Kid &k)
+	bool skipped(uint32_t prim) const
 	{
-		const float dx = k.hi[0] - k.lo[0], dy = k.hi[1] - k.lo[1], dz = k.hi[2] - k.lo[2];
-		return dx * dy + dy * dz + dz * dx;
+		if (!prims || skip_objs.empty())
+			return false;
+		uint32_t obj;
+		memcpy(&obj, &prims[prim].b[3], 4);
+		return std::find(skip_objs.begin(), skip_objs.end(), obj) != skip_objs.end();
 	}
 
-	/* how many slots opening k adds (0: not openable) */
-	uint32_t grows(const Kid &k) const
+	/* an inner tree node over children a and b (either may be -1: nothing left), box = union */
+	int32_t join(int32_t a, int32_t b)
 	{
-		if (k.ref == RTX_NONE)
-			return 0;
-		if (!is_leaf(k.ref))
-			return 1;
-		return prims ? leaf_count(k.ref) - 1 : 0;
+		if (a < 0 || b < 0)
+			return a < 0 ? b : a;
+		TNode t;
+		for (int k = 0; k < 3; k++) {
+			t.lo[k] = std::min(tree[a].lo[k], tree[b].lo[k]);
+			t.hi[k] = std::max(tree[a].hi[k], tree[b].hi[k]);
+		}
+		t.kid[0] = a;
+		t.kid[1] = b;
+		t.prim = RTX_NONE;
+		tree.push_back(t);
+		return (int32_t)tree.size() - 1;
 	}
 
-	/* the children of the wide node made from the subtree `seed`: open the largest openable kid
-	 * while it fits into eight slots */
-	void open_kids(const Kid &seed, Kid kids[8], uint32_t &n) const
+	int32_t leaf(uint32_t prim, const float lo[3], const float hi[3])
 	{
-		kids[0] = seed;
-		n = 1;
-		for (;;) {
-			int best = -1;
-			float ba = -1.f;
-			for (uint32_t i = 0; i < n; i++) {
-				const uint32_t g = grows(kids[i]);
-				if (g && n + g <= 8 && half_area(kids[i]) > ba) {
-					ba = half_area(kids[i]);
-					best = (int)i;
+		if (skipped(prim))
+			return -1;
+		TNode t;
+		memcpy(t.lo, lo, 12);
+		memcpy(t.hi, hi, 12);
+		t.kid[0] = t.kid[1] = -1;
+		t.prim = prim;
+		tree.push_back(t);
+		return (int32_t)tree.size() - 1;
+	}
+
+	/* primitives [first, first + cnt) of a BVH2 leaf as a balanced subtree of single primitives */
+	int32_t add_prims(uint32_t first, uint32_t cnt)
+	{
+		if (cnt == 1) {
+			float lo[3], hi[3];
+			prim_box(first, lo, hi);
+			return leaf(first, lo, hi);
+		}
+		const uint32_t h = cnt / 2;
+		const int32_t a = add_prims(first, h);
+		return join(a, add_prims(first + h, cnt - h));
+	}
+
+	/* the BVH2 subtree at device ref `ref` (box lo/hi in its parent) into `tree`, children
+	 * before their parent; -1 when nothing of it is left */
+	int32_t add(uint32_t ref, const float lo[3], const float hi[3])
+	{
+		if (ref & RTX_REF_LEAF) {
+			const uint32_t first = (ref & RTX_REF_OFF) / (uint32_t)sizeof(DNode) - nnodes, cnt = (ref & RTX_REF_CNT) + 1;
+			if (cnt == 1)
+				return leaf(first, lo, hi);
+			if (!prims) {
+				ok = false;
+				return -1;
+			}
+			return add_prims(first, cnt);
+		}
+		const DNode &d = inner[(ref & RTX_REF_OFF) / (uint32_t)sizeof(DNode)];
+		const float l0[3] = { d.lo0x, d.lo0y, d.lo0z }, h0[3] = { d.hi0x, d.hi0y, d.hi0z };
+		const float l1[3] = { d.lo1x, d.lo1y, d.lo1z }, h1[3] = { d.hi1x, d.hi1y, d.hi1z };
+		const int32_t a = add(d.ref0, l0, h0);
+		return join(a, add(d.ref1, l1, h1));
+	}
+
+	/* the cost programme over all tree nodes; children always precede their parent */
+	void solve()
+	{
+		const size_t n = tree.size();
+		cost.assign(n * 9, FLT_MAX);
+		pick.assign(n * 9, 0);
+		for (size_t t = 0; t < n; t++) {
+			const TNode &x = tree[t];
+			const float A = area(x.lo, x.hi);
+			float *C = &cost[t * 9];
+			int8_t *P = &pick[t * 9];
+			if (x.kid[0] < 0) {
+				for (int j = 1; j <= 8; j++)
+					C[j] = A * C_PRIM;
+				continue;
+			}
+			const float *L = &cost[(size_t)x.kid[0] * 9], *R = &cost[(size_t)x.kid[1] * 9];
+			float D[9];
+			int8_t K[9];
+			for (int j = 2; j <= 8; j++) {
+				D[j] = FLT_MAX;
+				K[j] = 1;
+				for (int k = 1; k < j; k++) {
+					const float v = L[k] + R[j - k];
+					if (v < D[j]) {
+						D[j] = v;
+						K[j] = (int8_t)k;
+					}
 				}
 			}
-			if (best < 0)
-				break;
-			const Kid k = kids[best];
-			if (!is_leaf(k.ref)) {
-				const DNode &d = inner[(k.ref & RTX_REF_OFF) / (uint32_t)sizeof(DNode)];
-				const float l0[3] = { d.lo0x, d.lo0y, d.lo0z }, h0[3] = { d.hi0x, d.hi0y, d.hi0z };
-				const float l1[3] = { d.lo1x, d.lo1y, d.lo1z }, h1[3] = { d.hi1x, d.hi1y, d.hi1z };
-				kids[best] = kid(d.ref0, l0, h0);
-				kids[n++] = kid(d.ref1, l1, h1);
-			} else {
-				const uint32_t first = leaf_first(k.ref), cnt = leaf_count(k.ref);
-				kids[best] = prim_kid(first);
-				for (uint32_t j = 1; j < cnt; j++)
-					kids[n++] = prim_kid(first + j);
+			C[1] = A * C_NODE + D[8];
+			P[1] = -1;
+			for (int j = 2; j <= 8; j++) {
+				if (D[j] < C[j - 1]) {
+					C[j] = D[j];
+					P[j] = K[j];
+				} else {
+					C[j] = C[j - 1];
+					P[j] = 0;
+				}
 			}
 		}
 	}
 
-	/* slot of each kid: greedy assignment of the best (kid, slot) pairs, where slot s's score is
-	 * how far the kid's centroid lies towards octant s of the node centre (extent-normalised) */
-	static void assign_slots(const Kid *kids, uint32_t n, int slot_of[8])
+	/* the slots subtree t fills when given j of them */
+	void slots(int32_t t, int j, std::vector<Slot> &s) const
 	{
+		const TNode &x = tree[t];
+		if (x.kid[0] < 0) {
+			s.push_back(Slot{ t, false });
+			return;
+		}
+		for (;;) {
+			const int8_t p = pick[(size_t)t * 9 + j];
+			if (p < 0) {
+				s.push_back(Slot{ t, true });
+				return;
+			}
+			if (p == 0) {
+				j--;
+				continue;
+			}
+			slots(x.kid[0], p, s);
+			slots(x.kid[1], j - p, s);
+			return;
+		}
+	}
+
+	/* the children of the wide node made from tree node t: its eight slots distributed */
+	void children(int32_t t, std::vector<Slot> &s) const
+	{
+		s.clear();
+		const TNode &x = tree[t];
+		if (x.kid[0] < 0) { /* a single primitive as the root */
+			s.push_back(Slot{ t, false });
+			return;
+		}
+		/* D(t, 8): the best split of eight slots over its two subtrees */
+		const float *L = &cost[(size_t)x.kid[0] * 9], *R = &cost[(size_t)x.kid[1] * 9];
+		int best = 1;
+		for (int k = 2; k < 8; k++)
+			if (L[k] + R[8 - k] < L[best] + R[8 - best])
+				best = k;
+		slots(x.kid[0], best, s);
+		slots(x.kid[1], 8 - best, s);
+	}
+
+	/* slot of each child: greedy assignment of the best (child, slot) pairs, where slot s's score
+	 * is how far the child's centroid lies towards octant s of the node centre (extent-normalised) */
+	void assign_slots(const std::vector<Slot> &kids, int slot_of[8]) const
+	{
+		const uint32_t n = (uint32_t)kids.size();
 		float lo[3] = { FLT_MAX, FLT_MAX, FLT_MAX }, hi[3] = { -FLT_MAX, -FLT_MAX, -FLT_MAX };
 		for (uint32_t i = 0; i < n; i++)
 			for (int a = 0; a < 3; a++) {
-				lo[a] = std::min(lo[a], kids[i].lo[a]);
-				hi[a] = std::max(hi[a], kids[i].hi[a]);
+				lo[a] = std::min(lo[a], tree[kids[i].t].lo[a]);
+				hi[a] = std::max(hi[a], tree[kids[i].t].hi[a]);
 			}
 		float score[8][8];
 		for (uint32_t i = 0; i < n; i++) {
+			const TNode &k = tree[kids[i].t];
 			float off[3];
 			for (int a = 0; a < 3; a++) {
 				const float ext = std::max(hi[a] - lo[a], 1e-30f);
-				off[a] = (0.5f * (kids[i].lo[a] + kids[i].hi[a]) - 0.5f * (lo[a] + hi[a])) / ext;
+				off[a] = (0.5f * (k.lo[a] + k.hi[a]) - 0.5f * (lo[a] + hi[a])) / ext;
 			}
 			for (int s = 0; s < 8; s++)
 				score[i][s] = ((s & 1) ? off[0] : -off[0]) + ((s & 2) ? off[1] : -off[1]) + ((s & 4) ? off[2] : -off[2]);
@@ -172,29 +291,31 @@ struct Builder {
 		}
 	}
 
-	/* node entry `me` from its children; returns the depth of its subtree (1 = leaves only) */
-	uint32_t emit(uint32_t me, const Kid *kids, uint32_t n)
+	/* node entry `me` for tree node t; returns the depth of its subtree (1 = leaf slots only) */
+	uint32_t emit(uint32_t me, int32_t t)
 	{
 		if (out.size() + 8 > RTX_W8_MAX_ENTRIES) {
 			ok = false;
 			return 0;
 		}
+		std::vector<Slot> kids;
+		children(t, kids);
+		const uint32_t n = (uint32_t)kids.size();
 		const uint32_t base = (uint32_t)out.size();
 		out.resize(base + 8);
 		leafmap.resize(base + 8, RTX_NONE);
 		memset(&out[base], 0, 8 * sizeof(DW8));
 		int slot_of[8];
-		assign_slots(kids, n, slot_of);
+		assign_slots(kids, slot_of);
 		/* 16-bit grid boxes of the children, the node origin and per-axis steps */
-		uint32_t ql[8][3], qh[8][3], org[3], ex[3];
+		uint32_t q16[8][3], org[3], ex[3];
 		for (int a = 0; a < 3; a++) {
 			uint32_t mn = 0xFFFFu, mx = 0;
 			for (uint32_t i = 0; i < n; i++) {
-				const uint32_t q = rtx_quantise(kids[i].lo[a], kids[i].hi[a], F.qo[a], F.qs[a]);
-				ql[i][a] = q & 0xFFFFu;
-				qh[i][a] = q >> 16;
-				mn = std::min(mn, ql[i][a]);
-				mx = std::max(mx, qh[i][a]);
+				const TNode &k = tree[kids[i].t];
+				q16[i][a] = rtx_quantise(k.lo[a], k.hi[a], F.qo[a], F.qs[a]);
+				mn = std::min(mn, q16[i][a] & 0xFFFFu);
+				mx = std::max(mx, q16[i][a] >> 16);
 			}
 			org[a] = mn;
 			uint32_t e = 0;
@@ -205,42 +326,40 @@ struct Builder {
 		uint8_t lo8[3][8], hi8[3][8];
 		memset(lo8, 255, sizeof(lo8));
 		memset(hi8, 0, sizeof(hi8));
-		uint32_t imask = 0, vmask = 0;
+		uint32_t imask = 0, vmask = 0, tmask = 0;
 		for (uint32_t i = 0; i < n; i++) {
 			const int s = slot_of[i];
 			for (int a = 0; a < 3; a++) {
-				const uint32_t q8 = rtx_quantise8(ql[i][a] | (qh[i][a] << 16), org[a], ex[a]);
+				const uint32_t q8 = rtx_quantise8(q16[i][a], org[a], ex[a]);
 				lo8[a][s] = (uint8_t)(q8 & 0xFFu);
 				hi8[a][s] = (uint8_t)(q8 >> 8);
 			}
 			vmask |= 1u << s;
-			if (kids[i].ref != RTX_NONE)
+			if (kids[i].node) {
 				imask |= 1u << s;
-			else
-				leafmap[base + s] = kids[i].prim;
+			} else {
+				const uint32_t pr = tree[kids[i].t].prim;
+				leafmap[base + s] = pr;
+				uint32_t meta = 0; /* without host records no slot is marked (its test is not deferred) */
+				if (prims)
+					memcpy(&meta, &prims[pr].c[3], 4);
+				if (meta & RTX_META_TRANSPARENT)
+					tmask |= 1u << s;
+			}
 		}
 		DW8 &N = out[me];
 		N.w[0] = org[0] | (org[1] << 16);
 		N.w[1] = org[2] | (ex[0] << 16) | (ex[1] << 20) | (ex[2] << 24);
 		N.w[2] = (base << 8) | imask;
-		N.w[3] = vmask;
+		N.w[3] = vmask | (tmask << 8);
 		for (int a = 0; a < 3; a++) {
 			memcpy(&N.w[4 + 4 * a], lo8[a], 8);
 			memcpy(&N.w[6 + 4 * a], hi8[a], 8);
 		}
 		uint32_t dep = 1;
-		for (uint32_t i = 0; i < n && ok; i++) {
-			if (kids[i].ref == RTX_NONE)
-				continue;
-			Kid sub[8];
-			uint32_t m = 0;
-			open_kids(kids[i], sub, m);
-			if (m == 1 && sub[0].ref != RTX_NONE) { /* a leaf of more than eight primitives */
-				ok = false;
-				return 0;
-			}
-			dep = std::max(dep, 1 + emit(base + (uint32_t)slot_of[i], sub, m));
-		}
+		for (uint32_t i = 0; i < n && ok; i++)
+			if (kids[i].node)
+				dep = std::max(dep, 1 + emit(base + (uint32_t)slot_of[i], kids[i].t));
 		return dep;
 	}
 };
@@ -248,31 +367,44 @@ struct Builder {
 } // namespace
 
 /* Collapses the BVH2 (inner records `inner`, root `root_ref`, bounded objects' box lo/hi) into
- * the 8-wide entries `out` (frame F) and the map entry -> primitive index of the leaf slots.
- * prims: the host primitive records (needed only when a leaf holds several primitives).  Returns
- * the wide tree's depth, or 0 when it cannot be built (empty tree, more than 2^24 entries, a
- * leaf of more than eight primitives or of several without host records). */
+ * the 8-wide entries `out` and the map entry -> primitive index of the leaf slots, leaving out
+ * the primitives of the objects in skip_objs when the host records `prims` are given (skipped =
+ * true then).  F receives the tree's 16-bit frame.  Returns the wide tree's depth, or 0 when it
+ * cannot be built (empty tree, more than 2^24 entries, a leaf of several primitives without
+ * host records). */
 uint32_t rtx_wide8_build(const std::vector<DNode> &inner, uint32_t nnodes, const DPrim *prims, uint32_t root_ref,
-			 const float lo[3], const float hi[3], const QFrame &F, std::vector<DW8> &out,
-			 std::vector<uint32_t> &leafmap)
+			 const float lo[3], const float hi[3], const std::vector<uint32_t> &skip_objs, QFrame &F,
+			 bool &skipped, std::vector<DW8> &out, std::vector<uint32_t> &leafmap)
 {
 	out.clear();
 	leafmap.clear();
+	skipped = false;
 	if (root_ref == RTX_EMPTY_REF)
 		return 0;
-	Builder b{ inner, nnodes, prims, F, out, leafmap };
-	out.resize(2);
-	leafmap.assign(2, RTX_NONE);
-	memset(out.data(), 0, 2 * sizeof(DW8));
-	Kid kids[8];
-	uint32_t n = 0;
-	b.open_kids(b.kid(root_ref, lo, hi), kids, n);
-	if (n == 1 && kids[0].ref != RTX_NONE) {
+	Builder b{ inner, nnodes, prims, skip_objs, QFrame{}, out, leafmap };
+	b.tree.reserve(2 * (size_t)nnodes + 2);
+	const int32_t root = b.add(root_ref, lo, hi);
+	if (!b.ok || root < 0) {
 		out.clear();
 		leafmap.clear();
 		return 0;
 	}
-	const uint32_t dep = b.emit(0, kids, n);
+	skipped = prims && !skip_objs.empty();
+	/* the frame: the remaining primitives' box, 65533 steps per axis (as the threaded BVH's) */
+	const TNode &R = b.tree[root];
+	float ext_max = 0.f;
+	for (int a = 0; a < 3; a++)
+		ext_max = std::max(ext_max, R.hi[a] - R.lo[a]);
+	for (int a = 0; a < 3; a++) {
+		b.F.qo[a] = R.lo[a];
+		b.F.qs[a] = 65533.f / std::max(R.hi[a] - R.lo[a], std::max(ext_max, 1.f) * 1e-6f);
+	}
+	F = b.F;
+	b.solve();
+	out.resize(2);
+	leafmap.assign(2, RTX_NONE);
+	memset(out.data(), 0, 2 * sizeof(DW8));
+	const uint32_t dep = b.emit(0, root);
 	if (!b.ok) {
 		out.clear();
 		leafmap.clear();

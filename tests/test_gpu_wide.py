@@ -64,7 +64,7 @@ def test_gpu_walks_agree(renderer, name):
     assert ok, (name, info)
 
 
-@pytest.mark.parametrize("name", ["s5_path2", "s6_amb", "s3_path2"])
+@pytest.mark.parametrize("name", ["s5_path2", "s6_amb", "s4_path2_blinn"])
 def test_gpu_w8_lane_stack_spill(renderer, name):
     """Trees deeper than the LDS lane stack walk on with the deeper entries in HBM: with one LDS
     entry every wide node below the second level spills (the path the depth-cliff fallback of
