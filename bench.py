@@ -61,6 +61,9 @@ def parse():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--scene", default="scene5", choices=["scene5", "scene5_l8", "scene6", "scene3", "scene1"])
+    ap.add_argument("--launch", default="group", choices=["group", "torchrun"],
+                    help="--gpus N > 1 without torchrun: one process driving the C-ABI device group "
+                         "(default), or N torchrun ranks")
     ap.add_argument("--walk", default="auto", choices=["auto", "w8", "w4", "bvh2"],
                     help="shadow-walk BVH layout (rtx_set_option RTX_OPT_SHADOW_WALK; auto = the library default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -73,37 +76,45 @@ def parse():
     return ap.parse_args()
 
 
-def launch_ranks(a):
-    """`--gpus N` without a torchrun environment: start N ranks through torch.distributed.run as a
-    child process (nothing here has touched a GPU, so this is not an exec of a GPU process) and
-    return its exit code.  Under torchrun, WORLD_SIZE must equal --gpus.  Returns None when this
-    process is itself the (only) rank to run."""
-    import socket
-    import subprocess
+def launch_mode(a):
+    """How `--gpus N` runs.  Under torchrun (WORLD_SIZE set) this process is one rank of N: it
+    must equal --gpus.  Without torchrun: N = 1 renders on one device; N > 1 renders in THIS
+    process through the C-ABI device group (rtx_group_*: one host thread per device, the tile
+    shards gathered to the first device with RCCL send/recv), the path `engine --gpus N` ships;
+    `--launch torchrun` instead starts N ranks through torch.distributed.run as a child process
+    (before anything touches a GPU, so no exec of a GPU process).  Returns ("rank", None),
+    ("group", None) or ("exit", code)."""
     world = os.environ.get("WORLD_SIZE")
     if world is not None:
         if int(world) != a.gpus:
             print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}: refusing to report a different "
                   f"GPU count than asked", file=sys.stderr)
-            return 2
-        return None
+            return "exit", 2
+        return "rank", None
     if a.gpus < 1:
         print(f"bench.py: --gpus {a.gpus}: need at least one", file=sys.stderr)
-        return 2
+        return "exit", 2
     if a.gpus == 1:
-        return None
+        return "rank", None
+    if a.launch == "group":
+        return "group", None
+    import socket
+    import subprocess
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
-    return subprocess.run(cmd, env=env).returncode
+    return "exit", subprocess.run(cmd, env=env).returncode
 
 
-def dry_run(a):
-    """Rank bring-up without a GPU: every rank joins a gloo group; rank 0 prints the world size
-    the JSON line would carry."""
+def dry_run(a, mode):
+    """Launch bring-up without a GPU: every torchrun rank joins a gloo group and rank 0 prints the
+    world size the JSON line would carry; the device-group mode prints its plan."""
+    if mode == "group":
+        print(json.dumps({"dry_run": True, "n_gpus": a.gpus, "launch": "group", "processes": 1}), flush=True)
+        return
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -116,7 +127,8 @@ def dry_run(a):
     else:
         ranks = 1
     if rank == 0:
-        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_joined": ranks, "gpus_flag": a.gpus}), flush=True)
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_joined": ranks, "gpus_flag": a.gpus,
+                          "launch": "torchrun" if world > 1 else "single"}), flush=True)
 
 
 def scene_path(which):
@@ -372,14 +384,43 @@ def post_leg(r, d_rgb, d_z, w, h, dev, log, reps=5):
     return res
 
 
+CONFIGS = {("scene1", 512, 512): ("configs[0]", None), ("scene3", 1920, 1080): ("configs[1]", 16),
+           ("scene5", 1920, 1080): ("configs[2]", 64), ("scene6", 3840, 2160): ("configs[4]", 128)}
+
+
+def workload(a):
+    """the BASELINE.json config this run measures, by name (configs[3] is configs[2]'s scene at
+    -n 256 on 8 GPUs), or "custom" """
+    name, spp = CONFIGS.get((a.scene, a.width, a.height), (None, None))
+    if a.scene == "scene5" and (a.width, a.height, a.spp) == (1920, 1080, 256):
+        name, spp = "configs[3]", 256
+    label = f"{a.scene} {a.width}x{a.height}" + ("" if a.scene == "scene1" else f" -g path -n {a.spp}")
+    return f"{label} (BASELINE {name})" if name and (spp is None or spp == a.spp) else f"{label} (custom)"
+
+
+def data_label(a):
+    if a.scene.startswith("scene5"):
+        return ("synthetic: reference scenes/scene5.json with the SURVEY §8(d) deterministic dragon stand-in (level-%d "
+                "displaced icosphere; meshes/dragon.stl is missing from the reference)" % (8 if a.scene == "scene5_l8" else 7))
+    if a.scene == "scene6":
+        return ("synthetic: reference scenes/scene6.json with the SURVEY §8(d) deterministic Menger stand-in (level 4, "
+                "672,768 triangles; meshes/menger_sponge.stl is missing from the reference)")
+    return f"the reference's own scenes/{a.scene}.json (no mesh)"
+
+
+WALKS = {"auto": -1, "w8": 2, "w4": 1, "bvh2": 0}
+
+
 def main():
     a = parse()
-    rc = launch_ranks(a)
-    if rc is not None:
+    mode, rc = launch_mode(a)
+    if mode == "exit":
         sys.exit(rc)
     if a.dry_run:
-        dry_run(a)
+        dry_run(a, mode)
         return
+    if mode == "group":
+        return main_group(a)
     import numpy as np
     import torch
     import rtxpy
@@ -409,8 +450,7 @@ def main():
     params.tile_offset, params.tile_stride = rank, world
 
     r = rtxpy.Renderer(local)
-    r.set_option(abi.RTX_OPT_SHADOW_WALK, {"auto": abi.RTX_WALK_AUTO, "w8": abi.RTX_WALK_W8, "w4": abi.RTX_WALK_W4,
-                                           "bvh2": abi.RTX_WALK_BVH2}[a.walk])
+    r.set_option(abi.RTX_OPT_SHADOW_WALK, WALKS[a.walk])
     t0 = time.perf_counter()
     r.upload(scene)
     st = r.stats()
@@ -421,17 +461,28 @@ def main():
     npx = a.width * a.height
     d_rgb = torch.zeros((npx, 3), dtype=torch.float32, device=dev)
     d_z = torch.zeros((npx,), dtype=torch.float32, device=dev)
-    gat = Gatherer(a.width, a.height, rank, world, dev)
+    gat = Gatherer(a.width, a.height, rank, world, dev) if world > 1 else None
     stream = torch.cuda.current_stream(dev)
+    # the render window runs up to the framebuffer on the host (rank 0, pinned)
+    h_rgb = torch.empty((npx, 3), dtype=torch.float32, pin_memory=True) if rank == 0 else None
+    h_z = torch.empty((npx,), dtype=torch.float32, pin_memory=True) if rank == 0 else None
 
     def step():
         r.render_device(frame, params, d_rgb.data_ptr(), d_z.data_ptr(), stream.cuda_stream)
         s = r.stats()
-        out = gat.gather(d_rgb, d_z)
-        return s, out
+        if gat is not None:  # shards to rank 0 over RCCL, unpacked there
+            out = gat.gather(d_rgb, d_z)
+            src = out if rank == 0 else None
+        else:
+            src = (d_rgb, d_z)
+        if src is not None:
+            h_rgb.copy_(src[0], non_blocking=True)
+            h_z.copy_(src[1], non_blocking=True)
+        torch.cuda.synchronize(dev)
+        return s
 
     for i in range(a.warmup):
-        s, _ = step()
+        s = step()
         log(f"warmup {i}: {s.kernel_ms:.1f} ms, {s.closest_rays}+{s.shadow_rays} rays")
 
     if world > 1:
@@ -441,7 +492,7 @@ def main():
     rays = 0
     kms, sms = [], []
     for i in range(a.steps):
-        s, _ = step()
+        s = step()
         rays += s.closest_rays + s.shadow_rays
         kms.append(s.kernel_ms)
         sms.append(s.shadow_ms)
@@ -468,17 +519,35 @@ def main():
     if not a.no_count:
         roofline = shadow_roofline(r, frame, params, d_rgb, d_z, stream, shadow_ms, a, world)
 
+    faithful = None
+    if rank == 0 and world == 1 and not a.no_post:
+        # the reference-faithful i.i.d. light samples (RTX_RNG_COUNTER) beside the stratified default
+        p2 = rtxpy.default_params(**{f: getattr(params, f) for f, _ in abi.Params._fields_})
+        p2.rng = abi.RTX_RNG_COUNTER
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        r.render_device(frame, p2, d_rgb.data_ptr(), d_z.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        sc_ = r.stats()
+        dt = time.perf_counter() - t1
+        faithful = {"rng": "counter (i.i.d. light samples, the reference's sampling)", "frame_ms": round(dt * 1e3, 1),
+                    "shadow_ms": round(sc_.shadow_ms, 1),
+                    "mrays_per_s": round((sc_.closest_rays + sc_.shadow_rays) / dt / 1e6, 1)}
+        log(f"counter-RNG frame: {faithful}")
+
     build = None
     if rank == 0 and world == 1 and not a.no_post:
         # §8(f) #2: both BVH builders on the benchmark scene (build time, then one frame each)
         try:
-            build = {"sah_host_ms": round(st.build_ms, 1)}
+            build = {"sah_host_ms": round(st.build_ms, 1), "sah_nodes": int(st.bvh_nodes), "sah_depth": int(st.bvh_depth),
+                     "sah_wide_nodes": int(st.wide_nodes), "sah_wide_depth": int(st.wide_depth),
+                     "sah_shadow_walk": ["bvh2", "w4", "w8"][st.shadow_walk]}
             r.set_builder(abi.RTX_BUILD_LBVH_GPU)
             r.upload(scene)
             sl = r.stats()
             build.update({"lbvh_gpu_ms": round(sl.build_ms, 1), "lbvh_nodes": int(sl.bvh_nodes),
-                          "lbvh_depth": int(sl.bvh_depth), "sah_nodes": int(st.bvh_nodes),
-                          "sah_depth": int(st.bvh_depth)})
+                          "lbvh_depth": int(sl.bvh_depth), "lbvh_wide_nodes": int(sl.wide_nodes),
+                          "lbvh_wide_depth": int(sl.wide_depth), "lbvh_shadow_walk": ["bvh2", "w4", "w8"][sl.shadow_walk]})
             r.render_device(frame, params, d_rgb.data_ptr(), d_z.data_ptr(), stream.cuda_stream)
             build["lbvh_shadow_ms"] = round(r.stats().shadow_ms, 1)
             build["sah_shadow_ms"] = round(float(np.mean(sms)), 1)
@@ -512,16 +581,22 @@ def main():
         value = rays / elapsed / 1e6
         out = {"metric": METRIC, "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
                "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
-               "scaling": "strong", "vs_baseline": None, "dtype": "f32",
-               "data": "synthetic: reference scenes/%s.json with the SURVEY §8(d) deterministic stand-in mesh" % (
-                   a.scene.split("_")[0]),
-               "config": {"workload": f"{a.scene} {a.width}x{a.height} -g path -n {a.spp} (BASELINE configs[2])",
+               "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": data_label(a),
+               "config": {"workload": workload(a),
                           "scene": os.path.basename(path), "width": a.width, "height": a.height, "spp": a.spp,
                           "objects": int(scene.num_objects), "rays_per_frame_rank0": stats_closest + stats_shadow,
                           "closest_rays_rank0": stats_closest, "shadow_rays_rank0": stats_shadow,
-                          "parallelism": f"tiles{world}", "kernel_ms_rank0": round(kernel_ms, 3),
-                          "kernels_rank0": split, "shadow_occ": os.environ.get("RTX_SHADOW_OCC", "default")},
+                          "parallelism": f"tiles{world}", "launch": "torchrun" if world > 1 else "single",
+                          "kernel_ms_rank0": round(kernel_ms, 3), "kernels_rank0": split,
+                          "shadow_walk": ["bvh2", "w4", "w8"][st.shadow_walk],
+                          "step": "render into HBM, tile shards gathered to rank 0 over RCCL (N > 1), frame copied "
+                                  "to pinned host memory (SURVEY 8(d): render window up to the framebuffer on the host)",
+                          "rng": "counter, stratified light samples (library default)"},
                "roofline": roofline, "cpu_baseline": cpu}
+        if gat is not None:
+            out["config"]["gather_message_bytes_per_rank"] = gat.message_bytes
+        if faithful:
+            out["rng_counter_frame"] = faithful
         if cpu:
             out["config"]["gpu_over_cpu"] = round(value / cpu["value"], 1)
         if port:
@@ -534,6 +609,65 @@ def main():
     r.close()
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def main_group(a):
+    """--gpus N > 1 in one process: the C-ABI device group (rtx_group_*), the path engine --gpus N
+    ships.  A step is rtx_group_render: every device renders its tile shard on its own host
+    thread, devices 1..N-1 pack their shards and RCCL send/recv moves them to device 0, which
+    unpacks and copies the frame to (pinned) host memory."""
+    import numpy as np
+    import torch
+    import rtxpy
+    from rtxpy import abi
+
+    def log(msg):
+        print(f"[group] {msg}", file=sys.stderr, flush=True)
+
+    path = scene_path(a.scene)
+    scene = rtxpy.Scene.load(path, base_dir=os.path.join(ROOT, "tests", "golden"))
+    frame = scene.frame(a.width, a.height)
+    flags = flags_for(a.scene, a.spp)
+    params = rtxpy.params_from_args(flags, seed=1)
+    g = rtxpy.Group(list(range(a.gpus)))
+    n = g.size()
+    g.set_option(abi.RTX_OPT_SHADOW_WALK, WALKS[a.walk])
+    t0 = time.perf_counter()
+    g.upload(scene)
+    log(f"{n} devices, scene {os.path.basename(path)} uploaded in {time.perf_counter() - t0:.2f}s")
+    h_rgb = torch.empty((a.height, a.width, 3), dtype=torch.float32, pin_memory=True).numpy()
+    h_z = torch.empty((a.height, a.width), dtype=torch.float32, pin_memory=True).numpy()
+    for i in range(a.warmup):
+        g.render(frame, params, h_rgb, h_z)
+        s = g.stats()
+        log(f"warmup {i}: {s.kernel_ms:.1f} ms (slowest device), gather {s.gather_ms:.2f} ms")
+    t0 = time.perf_counter()
+    rays = 0
+    per_dev = []
+    for i in range(a.steps):
+        g.render(frame, params, h_rgb, h_z)
+        s = g.stats()
+        rays += s.closest_rays + s.shadow_rays
+        per_dev.append([g.device_stats(r).kernel_ms for r in range(n)])
+    elapsed = time.perf_counter() - t0
+    dev_ms = np.array(per_dev)
+    value = rays / elapsed / 1e6
+    out = {"metric": METRIC, "value": round(value, 2), "unit": "Mrays/s", "n_gpus": n, "steps": a.steps,
+           "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
+           "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": data_label(a),
+           "config": {"workload": workload(a), "scene": os.path.basename(path), "width": a.width, "height": a.height,
+                      "spp": a.spp, "objects": int(scene.num_objects), "parallelism": f"tiles{n}", "launch": "group",
+                      "rays_per_frame": s.closest_rays + s.shadow_rays,
+                      "step": "rtx_group_render: shards on every device, RCCL send/recv to device 0, unpack, copy to "
+                              "pinned host memory (SURVEY 8(d) window)"},
+           "group": {"rtx_group_size": n, "rccl_devices": n if n > 1 else 0,
+                     "device_kernel_ms_max": round(float(dev_ms.mean(0).max()), 3),
+                     "device_kernel_ms_min": round(float(dev_ms.mean(0).min()), 3),
+                     "gather_ms": round(s.gather_ms, 3),
+                     "gather_message_bytes_per_device": int(16 * 64 * -(-((a.width + 7) // 8) * ((a.height + 7) // 8) // n))},
+           "roofline": None, "cpu_baseline": None}
+    print(json.dumps(out), flush=True)
+    g.close()
 
 
 if __name__ == "__main__":

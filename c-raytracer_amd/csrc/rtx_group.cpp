@@ -320,6 +320,16 @@ extern "C" int rtx_group_get_stats(const rtx_group *g, rtx_stats *out)
 	return RTX_OK;
 }
 
+extern "C" int rtx_group_device_stats(const rtx_group *g, int r, rtx_stats *out)
+{
+	if (!g || !out)
+		return fail(RTX_ERR_ARG, "null argument");
+	if (r < 0 || r >= g->n)
+		return fail(RTX_ERR_ARG, "device %d of a group of %d", r, g->n);
+	*out = g->ctx[r]->stats;
+	return RTX_OK;
+}
+
 /* ---- tile records: host reference and device entry points (rtx_tiles.h) ---- */
 
 extern "C" size_t rtx_tile_pack_count(uint32_t w, uint32_t h, uint32_t off, uint32_t stride)

@@ -297,16 +297,30 @@ class Group:
     def upload(self, scene):
         _check(self.lib.rtx_group_upload_scene(self._g, C.byref(scene.desc)))
 
-    def render(self, frame, params):
+    def render(self, frame, params, rgb=None, z=None):
+        """the whole frame on the group's first device's host side; rgb / z: optional preallocated
+        float32 (H, W, 3) / (H, W) host arrays (pinned ones make the copy faster)"""
         w, h = frame.width, frame.height
-        rgb = np.zeros((h, w, 3), np.float32)
-        z = np.zeros((h, w), np.float32)
+        if rgb is None:
+            rgb = np.zeros((h, w, 3), np.float32)
+        if z is None:
+            z = np.zeros((h, w), np.float32)
+        assert rgb.dtype == np.float32 and rgb.flags.c_contiguous and rgb.size == w * h * 3
+        assert z.dtype == np.float32 and z.flags.c_contiguous and z.size == w * h
         _check(self.lib.rtx_group_render(self._g, C.byref(frame), C.byref(params), rgb.ctypes.data, z.ctypes.data))
         return rgb, z
+
+    def size(self):
+        return self.lib.rtx_group_size(self._g)
 
     def stats(self):
         s = Stats()
         _check(self.lib.rtx_group_get_stats(self._g, C.byref(s)))
+        return s
+
+    def device_stats(self, r):
+        s = Stats()
+        _check(self.lib.rtx_group_device_stats(self._g, r, C.byref(s)))
         return s
 
     def close(self):

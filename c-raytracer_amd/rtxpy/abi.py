@@ -102,7 +102,7 @@ KAT_NAMES = ["moller", "sphere", "plane", "slab", "noise", "texture", "sph_light
 RTX_SYMBOLS = ["rtx_params_default", "rtx_device_count", "rtx_open", "rtx_upload_scene", "rtx_render",
                "rtx_render_device", "rtx_get_stats", "rtx_close", "rtx_last_error", "rtx_kat", "rtx_postprocess",
                "rtx_postprocess_device", "rtx_set_builder", "rtx_set_option", "rtx_group_open", "rtx_group_size",
-               "rtx_group_set_builder", "rtx_group_set_option", "rtx_group_upload_scene", "rtx_group_render", "rtx_group_get_stats",
+               "rtx_group_set_builder", "rtx_group_set_option", "rtx_group_upload_scene", "rtx_group_render", "rtx_group_get_stats", "rtx_group_device_stats",
                "rtx_group_close", "rtx_tile_pack_count", "rtx_tile_pack_host", "rtx_tile_unpack_host",
                "rtx_tile_pack_device", "rtx_tile_unpack_device"]
 RTX_SCENE_SYMBOLS = ["rtx_scene_load", "rtx_scene_parse", "rtx_scene_desc_of", "rtx_scene_num_json_objects",
@@ -189,6 +189,8 @@ def declare_rtx(lib):
     lib.rtx_group_render.restype = C.c_int
     lib.rtx_group_get_stats.argtypes = [C.c_void_p, C.POINTER(Stats)]
     lib.rtx_group_get_stats.restype = C.c_int
+    lib.rtx_group_device_stats.argtypes = [C.c_void_p, C.c_int, C.POINTER(Stats)]
+    lib.rtx_group_device_stats.restype = C.c_int
     lib.rtx_group_close.argtypes = [C.c_void_p]
     lib.rtx_group_close.restype = None
     lib.rtx_tile_pack_count.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]

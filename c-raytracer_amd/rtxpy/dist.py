@@ -5,8 +5,9 @@ t with t % N == r (rtx_params.tile_offset / tile_stride).  Interleaving deals
 the expensive centre of the frame to every rank.  After rendering, each rank
 packs its tiles (rgb + z = 16 B per pixel) into one contiguous buffer and the
 buffers are all-gathered (RCCL over xGMI with the "nccl" backend on GPUs, gloo in
-the CPU tests); rank 0 unpacks.  The only collective is this exchange: pixels
-are independent, so there is no reduction.
+the CPU tests) to rank 0, which unpacks: one message of 16 B x max_tiles x 64 per rank
+(4.1 MB / N at 1080p).  The only collective is this exchange: pixels are independent, so
+there is no reduction.
 """
 import numpy as np
 import torch
@@ -60,6 +61,8 @@ class Gatherer:
         self.all_valid = self.all_idx >= 0
         self.packed = torch.empty((self.max_tiles * 64, 4), dtype=torch.float32, device=device)
         self.gathered = torch.empty((world * self.max_tiles * 64, 4), dtype=torch.float32, device=device)
+        self.parts = list(self.gathered.chunk(world)) if world > 1 else None
+        self.message_bytes = self.max_tiles * 64 * 16
 
     def pack(self, rgb_flat, z_flat):
         """rgb_flat: (W*H, 3), z_flat: (W*H,) tensors on self.device."""
@@ -69,12 +72,15 @@ class Gatherer:
         return self.packed
 
     def gather(self, rgb_flat, z_flat, group=None):
-        """All-gather every rank's tiles; returns full (W*H,3), (W*H,) on every rank."""
+        """Gather every rank's tiles to rank 0: returns the full (W*H,3), (W*H,) frame on rank 0,
+        None elsewhere."""
         packed = self.pack(rgb_flat, z_flat)
         if self.world == 1:
             self.gathered.copy_(packed)
         else:
-            torch.distributed.all_gather_into_tensor(self.gathered, packed, group=group)
+            torch.distributed.gather(packed, self.parts if self.rank == 0 else None, dst=0, group=group)
+            if self.rank != 0:
+                return None
         return self.unpack(self.gathered)
 
     def unpack(self, gathered):

@@ -288,6 +288,8 @@ int rtx_group_render(rtx_group *g, const rtx_frame *frame, const rtx_params *par
 /* ray and traversal counts summed over the devices, kernel times the slowest device's,
  * gather_ms the pack + RCCL + unpack time */
 int rtx_group_get_stats(const rtx_group *g, rtx_stats *out);
+/* the statistics of device r (0 <= r < rtx_group_size) for the last frame */
+int rtx_group_device_stats(const rtx_group *g, int r, rtx_stats *out);
 void rtx_group_close(rtx_group *g);
 
 /* The gather's tile records (rtx_tiles.h): shard `offset` of `stride` of a W x H frame packs

@@ -16,11 +16,39 @@ def run(args, env=None):
 
 
 def test_gpus_flag_launches_that_many_ranks():
-    p = run(["--gpus", "2", "--dry-run"])
+    p = run(["--gpus", "2", "--dry-run", "--launch", "torchrun"])
     assert p.returncode == 0, p.stderr[-2000:]
     line = [l for l in p.stdout.splitlines() if l.startswith("{")][-1]
     out = json.loads(line)
-    assert out["n_gpus"] == 2 and out["ranks_joined"] == 2
+    assert out["n_gpus"] == 2 and out["ranks_joined"] == 2 and out["launch"] == "torchrun"
+
+
+def test_gpus_flag_without_torchrun_drives_the_device_group():
+    """`--gpus N` run directly: one process drives rtx_group over N devices (the path
+    `engine --gpus N` ships), no child ranks are started."""
+    p = run(["--gpus", "4", "--dry-run"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert out == {"dry_run": True, "n_gpus": 4, "launch": "group", "processes": 1}
+
+
+def test_workload_labels_name_the_baseline_config():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    A = type("A", (), {})
+    for scene, w, h, spp, want in [("scene5", 1920, 1080, 64, "configs[2]"), ("scene3", 1920, 1080, 16, "configs[1]"),
+                                   ("scene6", 3840, 2160, 128, "configs[4]"), ("scene5", 1920, 1080, 256, "configs[3]"),
+                                   ("scene1", 512, 512, 64, "configs[0]"), ("scene5", 960, 540, 64, "custom")]:
+        a = A()
+        a.scene, a.width, a.height, a.spp = scene, w, h, spp
+        assert want in b.workload(a), (scene, b.workload(a))
+    a = A()
+    a.scene = "scene3"
+    assert "no mesh" in b.data_label(a)
+    a.scene = "scene6"
+    assert "Menger" in b.data_label(a)
 
 
 def test_gpus_flag_must_match_torchrun_world():

@@ -1,4 +1,4 @@
-"""Multi-rank tile sharding + framebuffer all-gather (rtxpy.dist, used by bench.py over RCCL),
+"""Multi-rank tile sharding + framebuffer gather to rank 0 (rtxpy.dist, used by bench.py over RCCL),
 exercised with the gloo backend on CPU at world_size 2 and 3.  Each rank renders its
 tiles with the CPU oracle (test infrastructure standing in for the GPU here); the
 gathered frame must be bit-identical to a single-rank render."""
@@ -34,10 +34,12 @@ def _worker(rank, world, port, out_dir):
     params.tile_offset, params.tile_stride = rank, world
     rgb, z, counts = oracle.render(scene, frame, params, threads=1)
     g = Gatherer(frame.width, frame.height, rank, world, torch.device("cpu"))
-    full_rgb, full_z = g.gather(torch.from_numpy(rgb.reshape(-1, 3)), torch.from_numpy(z.reshape(-1)))
+    out = g.gather(torch.from_numpy(rgb.reshape(-1, 3)), torch.from_numpy(z.reshape(-1)))
+    assert (out is None) == (rank != 0)  # gathered to rank 0 only
     c = torch.tensor(counts, dtype=torch.int64)
     torch.distributed.all_reduce(c)
     if rank == 0:
+        full_rgb, full_z = out
         np.savez(os.path.join(out_dir, "gathered.npz"), rgb=full_rgb.numpy(), z=full_z.numpy(), counts=c.numpy())
     torch.distributed.destroy_process_group()
 
