@@ -49,7 +49,8 @@ extern "C" hipError_t rtx_launch_kat(int kind, uint32_t n, const float *in, floa
 				     hipStream_t stream);
 extern "C" hipError_t rtx_launch_pack_tris(const DPrim *prims, uint32_t n, float4 *out, hipStream_t stream);
 extern "C" hipError_t rtx_launch_kat_shadow(int kind, uint32_t n, const float *in, float *out, hipStream_t stream);
-extern "C" hipError_t rtx_launch_w8_fill(const DPrim *prims, const uint32_t *leafmap, uint32_t n, DW8 *out, hipStream_t stream);
+extern "C" hipError_t rtx_launch_w8_fill(const DPrim *prims, const DMaterial *mats, const uint32_t *leafmap, uint32_t n, DW8 *out,
+					  hipStream_t stream);
 extern "C" hipError_t rtx_shadow_grid_lanes(uint32_t cus, uint32_t *lanes);
 
 static thread_local char g_err[512] = "";
@@ -697,8 +698,8 @@ int rtx_upload_built(rtx_ctx *c, const HostScene &hs)
 		uint32_t *d_map = nullptr;
 		if ((rc = upload(d_map, hs.w8leaf)))
 			return rc;
-		hipError_t e = rtx_launch_w8_fill((const DPrim *)(c->d_nodes + hs.nnodes), d_map, (uint32_t)hs.w8.size(), c->d_w8,
-						  c->stream);
+		hipError_t e = rtx_launch_w8_fill((const DPrim *)(c->d_nodes + hs.nnodes), c->d_mats, d_map, (uint32_t)hs.w8.size(),
+						  c->d_w8, c->stream);
 		if (e == hipSuccess)
 			e = hipStreamSynchronize(c->stream);
 		dfree(d_map);

@@ -131,8 +131,9 @@ typedef struct __attribute__((aligned(16))) DQNode {
  * Child c's box is [o + lo * 2^e, o + hi * 2^e] on the grid, outward-rounded from its 16-bit box
  * (rtx_quant.h), so it contains the float box.  An empty slot has lo = 255, hi = 0 on every axis
  * (never hit by the octant-specialised test; the generic test masks with vmask).  An inner
- * slot's entry is the child node; a leaf slot's entry is the primitive's 64-byte DPrim record
- * (one primitive per leaf slot).  A node's eight child entries are contiguous (unused ones are
+ * slot's entry is the child node; a leaf slot's entry is a copy of the primitive's 64-byte DPrim
+ * record (one primitive per leaf slot) with its material's kt in place of the normal (the
+ * shadow walk needs no normal; a transparent hit multiplies by it without a material fetch).  A node's eight child entries are contiguous (unused ones are
  * holes), so a lane's pending siblings are one 32-bit group base << 8 | slot mask.
  * Slots follow the children's centroid octant about the node centre (bit a: the + side of
  * axis a), so a ray of direction octant OCT meets them front to back roughly in the order

@@ -549,11 +549,59 @@ __device__ __forceinline__ uint32_t w8_hits(const uint32_t (&w)[16], f3 s, f3 b,
 #ifndef RTX_W8_DEFER
 #define RTX_W8_DEFER 32 /* lanes holding deferred leaf tests that trigger a round of them */
 #endif
+#ifndef RTX_W8_ORDER
+#define RTX_W8_ORDER 1 /* visit hit children in the octant's slot order (0: plain slot order) */
+#endif
+
+/* a deferred leaf test: the transparent primitive at entry pr (rtx_device.h DW8 leaf entry,
+ * whose 4th float4 holds its material's kt) against this lane's shadow ray; a hit multiplies
+ * the transmittance (accel.c:370-377) */
+template <bool COUNT>
+__device__ __forceinline__ void w8_defer_test(const char *pr, f3 o, f3 d, float tl, f3 &li, uint32_t &ntri, uint32_t &nsph)
+{
+	const float4 a = ldg4(pr, 0), b = ldg4(pr, 16), c = ldg4(pr, 32);
+	bool h;
+	if ((__float_as_uint(c.w) >> 24) == RTX_SPHERE) {
+		if (COUNT)
+			nsph++;
+		float t = 0.f;
+		h = hit_sphere(mk3(a.x, a.y, a.z), b.x, o, d, a.w, t) && t < tl;
+	} else {
+		if (COUNT)
+			ntri++;
+		h = any_tri(mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z), mk3(c.x, c.y, c.z), o, d, a.w, tl);
+	}
+	if (h) {
+		const float4 kt = ldg4(pr, 48);
+		li = mul3v(li, mk3(kt.x, kt.y, kt.z));
+	}
+}
+
+/* one 8-wide node visit's box tests: the hit mask in visit order and the node's masks */
+struct W8Visit {
+	uint32_t hm, base, io, to, nv;
+};
+template <int OCT, uint32_t K, bool UNI>
+__device__ __forceinline__ W8Visit w8_visit(const uint32_t (&w)[16], f3 invq, f3 oi, float tl)
+{
+	f3 s, b;
+	w8_frame(w, invq, oi, s, b);
+	W8Visit v;
+	v.hm = w8_hits<OCT, K>(w, s, b, tl);
+	v.base = w[2] >> 8;
+	v.io = perm_xor<K>(w[2] & 0xFFu);
+	v.to = perm_xor<K>((w[3] >> 8) & 0xFFu);
+	v.nv = w[3] & 0xFFu;
+	if (UNI) /* keeps the two instances apart (the scalar one reads SGPR operands, no copies) */
+		asm volatile("" ::: "memory");
+	return v;
+}
+
 template <bool COUNT, int OCT>
 __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__restrict__ mats, f3 o, f3 d, f3 inv,
 					     float &tl, uint32_t emit_obj, f3 &li, ShadowCount &sc)
 {
-	constexpr uint32_t K = OCT == 8 ? 0u : (~(uint32_t)OCT & 7u);
+	constexpr uint32_t K = (OCT == 8 || !RTX_W8_ORDER) ? 0u : (~(uint32_t)OCT & 7u);
 	const f3 invq = mk3(inv.x * Q.qsi.x, inv.y * Q.qsi.y, inv.z * Q.qsi.z);
 	const f3 oq = mk3((o.x - Q.qo.x) * Q.qs.x, (o.y - Q.qo.y) * Q.qs.y, (o.z - Q.qo.z) * Q.qs.z);
 	const f3 oi = mul3v(oq, invq);
@@ -574,45 +622,46 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 				tgrp &= tgrp - 1;
 				if (!(tgrp & 0xFFu))
 					tgrp = tn ? tq[--tn * WAVE] : 0u;
-				shadow_prim<COUNT>(ldg4(pr, 0), ldg4(pr, 16), ldg4(pr, 32), mats, o, d, tl, emit_obj, li, ntri, nsph);
+				w8_defer_test<COUNT>(pr, o, d, tl, li, ntri, nsph);
 			}
 			continue;
 		}
 		if (node == RTX_NONE)
 			continue;
-		uint32_t w[16];
+		W8Visit v;
 		const uint32_t un = uni(node);
 		if (RTX_W_SUNI && !ballot(node != un)) {
-			/* every walking lane is at one node: read it through the scalar cache */
+			/* every walking lane is at one node: read it through the scalar cache, test with SGPR operands */
+			uint32_t w[16];
 			const auto *U = (const __attribute__((address_space(4))) u4v *)(Q.w8 + (size_t)un);
 #pragma unroll
 			for (int k = 0; k < 4; k++) {
-				const u4v v = U[k];
-				w[4 * k] = v.x;
-				w[4 * k + 1] = v.y;
-				w[4 * k + 2] = v.z;
-				w[4 * k + 3] = v.w;
+				const u4v x = U[k];
+				w[4 * k] = x.x;
+				w[4 * k + 1] = x.y;
+				w[4 * k + 2] = x.z;
+				w[4 * k + 3] = x.w;
 			}
+			v = w8_visit<OCT, K, true>(w, invq, oi, tl);
 		} else {
+			uint32_t w[16];
 			const DW8 *N = Q.w8 + (size_t)node;
 #pragma unroll
 			for (int k = 0; k < 4; k++) {
-				const uint4 v = ldg4u((const uint32_t *)N + 4 * k);
-				w[4 * k] = v.x;
-				w[4 * k + 1] = v.y;
-				w[4 * k + 2] = v.z;
-				w[4 * k + 3] = v.w;
+				const uint4 x = ldg4u((const uint32_t *)N + 4 * k);
+				w[4 * k] = x.x;
+				w[4 * k + 1] = x.y;
+				w[4 * k + 2] = x.z;
+				w[4 * k + 3] = x.w;
 			}
+			v = w8_visit<OCT, K, false>(w, invq, oi, tl);
 		}
-		f3 s, b;
-		w8_frame(w, invq, oi, s, b);
-		const uint32_t hm = w8_hits<OCT, K>(w, s, b, tl);
-		const uint32_t base = w[2] >> 8, io = perm_xor<K>(w[2] & 0xFFu), to = perm_xor<K>((w[3] >> 8) & 0xFFu);
-		uint32_t lm = hm & ~io & ~to, im = hm & io;
-		const uint32_t dm = hm & to;
+		const uint32_t hm = v.hm, base = v.base;
+		uint32_t lm = hm & ~v.io & ~v.to, im = hm & v.io;
+		const uint32_t dm = hm & v.to;
 		if (COUNT) {
 			nstep++;
-			nbox += popc64(w[3] & 0xFFu);
+			nbox += popc64(v.nv);
 			nun += ballot(node != uni(node)) ? 0u : 1u;
 			uint32_t r = 0;
 			for (uint32_t m = lm;; m &= m - 1) {
@@ -1256,7 +1305,8 @@ __global__ void k_kat_shadow(int kind, uint32_t n, const float *__restrict__ in,
 
 /* the 8-wide BVH's leaf entries: the primitive records they stand for (leafmap[i] = primitive
  * index, RTX_NONE for node entries and holes) */
-__global__ void k_w8_fill(const DPrim *__restrict__ prims, const uint32_t *__restrict__ leafmap, uint32_t n, DW8 *__restrict__ out)
+__global__ void k_w8_fill(const DPrim *__restrict__ prims, const DMaterial *__restrict__ mats, const uint32_t *__restrict__ leafmap,
+			  uint32_t n, DW8 *__restrict__ out)
 {
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= 4 * n)
@@ -1264,14 +1314,20 @@ __global__ void k_w8_fill(const DPrim *__restrict__ prims, const uint32_t *__res
 	const uint32_t e = i >> 2, p = leafmap[e];
 	if (p == RTX_NONE)
 		return;
-	((float4 *)(out + e))[i & 3] = ldg4((const char *)(prims + p), 16 * (i & 3));
+	float4 v = ldg4((const char *)(prims + p), 16 * (i & 3));
+	if ((i & 3) == 3) { /* the shadow walk's copy carries the material's kt in place of the normal */
+		const DMaterial &m = mats[__float_as_uint(prims[p].c[3]) & RTX_META_MAT];
+		v = make_float4(m.kt[0], m.kt[1], m.kt[2], 0.f);
+	}
+	((float4 *)(out + e))[i & 3] = v;
 }
 
-extern "C" hipError_t rtx_launch_w8_fill(const DPrim *prims, const uint32_t *leafmap, uint32_t n, DW8 *out, hipStream_t stream)
+extern "C" hipError_t rtx_launch_w8_fill(const DPrim *prims, const DMaterial *mats, const uint32_t *leafmap, uint32_t n, DW8 *out,
+					  hipStream_t stream)
 {
 	if (!n)
 		return hipSuccess;
-	hipLaunchKernelGGL(k_w8_fill, dim3((4 * n + 255) / 256), dim3(256), 0, stream, prims, leafmap, n, out);
+	hipLaunchKernelGGL(k_w8_fill, dim3((4 * n + 255) / 256), dim3(256), 0, stream, prims, mats, leafmap, n, out);
 	return hipGetLastError();
 }
 
