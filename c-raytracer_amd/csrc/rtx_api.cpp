@@ -110,6 +110,7 @@ static void free_scene(rtx_ctx *c)
 	dfree(c->d_wnodes);
 	dfree(c->d_wtris);
 	dfree(c->d_w8);
+	dfree(c->d_w8s);
 	c->have_scene = false;
 }
 
@@ -694,6 +695,27 @@ int rtx_upload_built(rtx_ctx *c, const HostScene &hs)
 	}
 	if ((rc = upload(c->d_w8, hs.w8)))
 		return rc;
+	{ /* the scalar-path node copies (rtx_device.h DW8S) */
+		std::vector<DW8S> w8s(hs.w8.size());
+		memset(w8s.data(), 0, w8s.size() * sizeof(DW8S));
+		for (size_t i = 0; i < hs.w8.size(); i++) {
+			const DW8 &n = hs.w8[i];
+			if (!(n.w[3] & 0xFFu) || hs.w8leaf[i] != RTX_NONE)
+				continue;
+			DW8S &f = w8s[i];
+			memcpy(f.w, n.w, 16);
+			f.org[0] = (float)(n.w[0] & 0xFFFFu);
+			f.org[1] = (float)(n.w[0] >> 16);
+			f.org[2] = (float)(n.w[1] & 0xFFFFu);
+			for (int k = 0; k < 6; k++)
+				for (int ch = 0; ch < 8; ch++) {
+					const _Float16 h = (_Float16)((n.w[4 + 2 * k + (ch >> 2)] >> (8 * (ch & 3))) & 0xFFu);
+					memcpy(&f.q[k][ch], &h, 2); /* 0..255: exact in half precision */
+				}
+		}
+		if ((rc = upload(c->d_w8s, w8s)))
+			return rc;
+	}
 	if (!hs.w8.empty()) { /* the 8-wide tree's leaf entries: copies of their primitive records */
 		uint32_t *d_map = nullptr;
 		if ((rc = upload(d_map, hs.w8leaf)))
@@ -732,6 +754,7 @@ int rtx_upload_built(rtx_ctx *c, const HostScene &hs)
 	memcpy(S.w8qo, hs.w8f.qo, 12);
 	memcpy(S.w8qs, hs.w8f.qs, 12);
 	S.w8noemit = hs.w8noemit ? 1u : 0u;
+	S.w8s = hs.w8.empty() ? nullptr : c->d_w8s;
 	S.root_ref = hs.root_ref;
 	S.num_prims = hs.nb;
 	S.num_planes = (uint32_t)hs.planes.size();

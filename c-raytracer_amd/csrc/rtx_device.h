@@ -142,11 +142,27 @@ typedef struct __attribute__((aligned(16))) DQNode {
  * 16-bit frame (DScene.w8qo / w8qs) over its primitives; the emitters are left out of it when the
  * host has the primitive records (DScene.w8noemit): k_shadow tests them linearly, like planes,
  * so a shadow ray no longer walks down to the light it was cast to. */
+#ifndef RTX_W8_STACK
 #define RTX_W8_STACK 8     /* k_shadow lane-stack entries in LDS; deeper ones spill to HBM (DScene.w8spill) */
+#endif
 #define RTX_W8_MAX_ENTRIES (1u << 24)
 typedef struct __attribute__((aligned(64))) DW8 {
 	uint32_t w[16];
 } DW8;
+
+/* The scalar-path copy of an 8-wide node (DScene.w8s, indexed like the entries; only node
+ * entries are filled): when every walking lane of a wave is at one node, k_shadow reads it with
+ * two s_load_dwordx16 and takes the 8-bit plane offsets as ready half floats (SGPR operands of
+ * v_fma_mix_f32) instead of converting 48 bytes per lane.  The halves are the bytes' exact
+ * values, so both paths compute bit-identical box tests.
+ *   w = the node's w0..w3;  org = its origin as floats;  q[k][c] = byte c of plane k (lo_x, hi_x,
+ *   lo_y, hi_y, lo_z, hi_z) as an IEEE half */
+typedef struct __attribute__((aligned(128))) DW8S {
+	uint32_t w[4];
+	float org[3];
+	uint32_t pad;
+	uint16_t q[6][8];
+} DW8S;
 
 typedef struct DPlane {
 	float n[3];
@@ -201,6 +217,7 @@ typedef struct DScene {
 	const DW8 *w8;          /* 8-wide compressed BVH (num_w8 entries), null when not built */
 	uint32_t num_w8, w8depth;
 	float w8qo[3], w8qs[3]; /* its 16-bit frame */
+	const DW8S *w8s;        /* scalar-path copies of its nodes (num_w8 slots, node entries filled) */
 	uint32_t w8noemit;      /* the emitters are not in it (k_shadow tests them linearly) */
 	uint32_t *w8spill;      /* k_shadow lane-stack entries from RTX_W8_STACK on, [entry][grid lane] */
 	uint32_t w8spill_lanes; /* grid lanes the spill area was sized for (0: no spill area) */

@@ -58,6 +58,7 @@ struct rtx_ctx {
 	DQNode *d_wnodes = nullptr;
 	float4 *d_wtris = nullptr;
 	DW8 *d_w8 = nullptr;
+	DW8S *d_w8s = nullptr;
 	uint32_t *d_w8spill = nullptr; /* k_shadow lane-stack spill of deep 8-wide trees (DScene.w8spill) */
 	size_t w8spill_bytes = 0;
 	DScene scene{};

@@ -243,6 +243,7 @@ struct QBvh {
 	const DQNode *w;      /* the 4-wide BVH (rtx_device.h RTX_W_STACK), WALK_W4 */
 	const char *wt;       /* ... and its 48-byte leaf triangle records */
 	const DW8 *w8;        /* the 8-wide BVH (rtx_device.h DW8), WALK_W8 */
+	const DW8S *w8s;      /* ... its nodes' scalar-path copies */
 	uint32_t *spill;      /* this lane's stack entries from lstk on: entry k at spill[(k - lstk) * spill_stride] */
 	uint32_t spill_stride;
 	uint32_t lstk;        /* lane-stack entries in LDS (<= RTX_W8_STACK) */
@@ -482,13 +483,9 @@ template <uint32_t K> __device__ __forceinline__ uint32_t perm_xor(uint32_t m)
  * on the box rounded outward to the node's 8-bit frame (KAT: RTX_KAT_BOX_Q8).  OCT < 8: every
  * live lane's direction lies in octant OCT, entry planes known at compile time; an empty slot
  * (lo 255 > hi 0) is then never hit. */
-template <int OCT, int C>
-__device__ __forceinline__ bool w8_child(const uint32_t (&w)[16], f3 s, f3 b, float tl)
+template <int OCT>
+__device__ __forceinline__ bool w8_slab(float lx, float hx, float ly, float hy, float lz, float hz, float tl)
 {
-	constexpr int W = C >> 2, B = C & 3;
-	const float lx = fmaf(ubyte<B>(w[4 + W]), s.x, b.x), hx = fmaf(ubyte<B>(w[6 + W]), s.x, b.x);
-	const float ly = fmaf(ubyte<B>(w[8 + W]), s.y, b.y), hy = fmaf(ubyte<B>(w[10 + W]), s.y, b.y);
-	const float lz = fmaf(ubyte<B>(w[12 + W]), s.z, b.z), hz = fmaf(ubyte<B>(w[14 + W]), s.z, b.z);
 	if (OCT == 8) {
 		const float tn = fmaxf(fmaxf(fminf(lx, hx), fminf(ly, hy)), fmaxf(fminf(lz, hz), 0.f));
 		const float tf = fminf(fminf(fmaxf(lx, hx), fmaxf(ly, hy)), fminf(fmaxf(lz, hz), tl));
@@ -501,6 +498,27 @@ __device__ __forceinline__ bool w8_child(const uint32_t (&w)[16], f3 s, f3 b, fl
 	float tf = fminf(fminf(fx, fy), fz);
 	asm("v_min_f32 %0, %0, %1" : "+v"(tf) : "v"(tl));
 	return tn <= tf;
+}
+template <int OCT, int C>
+__device__ __forceinline__ bool w8_child(const uint32_t (&w)[16], f3 s, f3 b, float tl)
+{
+	constexpr int W = C >> 2, B = C & 3;
+	return w8_slab<OCT>(fmaf(ubyte<B>(w[4 + W]), s.x, b.x), fmaf(ubyte<B>(w[6 + W]), s.x, b.x),
+			    fmaf(ubyte<B>(w[8 + W]), s.y, b.y), fmaf(ubyte<B>(w[10 + W]), s.y, b.y),
+			    fmaf(ubyte<B>(w[12 + W]), s.z, b.z), fmaf(ubyte<B>(w[14 + W]), s.z, b.z), tl);
+}
+/* the same child test on the scalar-path copy (rtx_device.h DW8S): the plane offsets are ready
+ * floats, the same values the conversions above produce, so the results are bit-identical */
+template <int OCT, int C>
+__device__ __forceinline__ bool w8_child_s(const uint32_t (&q)[24], f3 s, f3 b, float tl)
+{
+	/* plane k's offset of child C: the half in word 4k + C/2, half C & 1 (v_fma_mix_f32 op_sel) */
+	auto h = [&](int k) -> float {
+		const uint32_t v = q[4 * k + (C >> 1)];
+		return (float)__builtin_bit_cast(_Float16, (uint16_t)((C & 1) ? (v >> 16) : (v & 0xFFFFu)));
+	};
+	return w8_slab<OCT>(fmaf(h(0), s.x, b.x), fmaf(h(1), s.x, b.x), fmaf(h(2), s.y, b.y), fmaf(h(3), s.y, b.y),
+			    fmaf(h(4), s.z, b.z), fmaf(h(5), s.z, b.z), tl);
 }
 
 /* the node frame of an 8-wide node: per-axis scale s = invq * 2^e and offset b = o * invq - oi */
@@ -529,6 +547,22 @@ __device__ __forceinline__ uint32_t w8_hits(const uint32_t (&w)[16], f3 s, f3 b,
 		hm &= w[3]; /* K = 0: slot order; the min/max form would turn an empty slot's box around */
 	return hm;
 }
+template <int OCT, uint32_t K>
+__device__ __forceinline__ uint32_t w8_hits_s(const uint32_t (&q)[24], uint32_t w3, f3 s, f3 b, float tl)
+{
+	uint32_t hm = 0;
+	hm |= w8_child_s<OCT, 0>(q, s, b, tl) ? 1u << (0 ^ K) : 0u;
+	hm |= w8_child_s<OCT, 1>(q, s, b, tl) ? 1u << (1 ^ K) : 0u;
+	hm |= w8_child_s<OCT, 2>(q, s, b, tl) ? 1u << (2 ^ K) : 0u;
+	hm |= w8_child_s<OCT, 3>(q, s, b, tl) ? 1u << (3 ^ K) : 0u;
+	hm |= w8_child_s<OCT, 4>(q, s, b, tl) ? 1u << (4 ^ K) : 0u;
+	hm |= w8_child_s<OCT, 5>(q, s, b, tl) ? 1u << (5 ^ K) : 0u;
+	hm |= w8_child_s<OCT, 6>(q, s, b, tl) ? 1u << (6 ^ K) : 0u;
+	hm |= w8_child_s<OCT, 7>(q, s, b, tl) ? 1u << (7 ^ K) : 0u;
+	if (OCT == 8)
+		hm &= w3;
+	return hm;
+}
 
 /* is_light_blocked's BVH part (accel.c:360-387) over the 8-wide BVH (rtx_device.h DW8): one
  * 64-byte node per step (four 16-byte loads, or one s_load_dwordx16 when every live lane is at
@@ -547,7 +581,7 @@ __device__ __forceinline__ uint32_t w8_hits(const uint32_t (&w)[16], f3 s, f3 b,
 #define RTX_W8_TQ 4 /* deferred leaf groups per lane in LDS (besides the one in a register) */
 #endif
 #ifndef RTX_W8_DEFER
-#define RTX_W8_DEFER 32 /* lanes holding deferred leaf tests that trigger a round of them */
+#define RTX_W8_DEFER 64 /* lanes holding deferred leaf tests that trigger a round of them (16 / 32 / 48 / 64: 613 / 601 / 598 / 594 ms) */
 #endif
 #ifndef RTX_W8_ORDER
 #define RTX_W8_ORDER 1 /* visit hit children in the octant's slot order (0: plain slot order) */
@@ -597,6 +631,34 @@ __device__ __forceinline__ W8Visit w8_visit(const uint32_t (&w)[16], f3 invq, f3
 	return v;
 }
 
+/* the same visit on the scalar-path copy (every walking lane at the node: SGPR operands) */
+template <int OCT, uint32_t K>
+__device__ __forceinline__ W8Visit w8_visit_s(const DW8S *n, f3 invq, f3 oi, float tl)
+{
+	typedef uint32_t u16v __attribute__((ext_vector_type(16)));
+	const auto *U = (const __attribute__((address_space(4))) u16v *)n;
+	const u16v p0 = U[0], p1 = U[1];
+	uint32_t q[24];
+#pragma unroll
+	for (int k = 0; k < 8; k++)
+		q[k] = p0[8 + k];
+#pragma unroll
+	for (int k = 0; k < 16; k++)
+		q[8 + k] = p1[k];
+	const uint32_t w1 = p0[1], w2 = p0[2], w3 = p0[3];
+	const float org0 = __uint_as_float(p0[4]), org1 = __uint_as_float(p0[5]), org2 = __uint_as_float(p0[6]);
+	const f3 s = mk3(ldexpf(invq.x, (int)((w1 >> 16) & 15u)), ldexpf(invq.y, (int)((w1 >> 20) & 15u)),
+			 ldexpf(invq.z, (int)((w1 >> 24) & 15u)));
+	const f3 b = mk3(fmaf(org0, invq.x, -oi.x), fmaf(org1, invq.y, -oi.y), fmaf(org2, invq.z, -oi.z));
+	W8Visit v;
+	v.hm = w8_hits_s<OCT, K>(q, w3, s, b, tl);
+	v.base = w2 >> 8;
+	v.io = perm_xor<K>(w2 & 0xFFu);
+	v.to = perm_xor<K>((w3 >> 8) & 0xFFu);
+	v.nv = w3 & 0xFFu;
+	return v;
+}
+
 template <bool COUNT, int OCT>
 __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__restrict__ mats, f3 o, f3 d, f3 inv,
 					     float &tl, uint32_t emit_obj, f3 &li, ShadowCount &sc)
@@ -631,18 +693,9 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 		W8Visit v;
 		const uint32_t un = uni(node);
 		if (RTX_W_SUNI && !ballot(node != un)) {
-			/* every walking lane is at one node: read it through the scalar cache, test with SGPR operands */
-			uint32_t w[16];
-			const auto *U = (const __attribute__((address_space(4))) u4v *)(Q.w8 + (size_t)un);
-#pragma unroll
-			for (int k = 0; k < 4; k++) {
-				const u4v x = U[k];
-				w[4 * k] = x.x;
-				w[4 * k + 1] = x.y;
-				w[4 * k + 2] = x.z;
-				w[4 * k + 3] = x.w;
-			}
-			v = w8_visit<OCT, K, true>(w, invq, oi, tl);
+			/* every walking lane is at one node: its scalar-path copy through the scalar cache,
+			 * the planes as SGPR float operands */
+			v = w8_visit_s<OCT, K>(Q.w8s + (size_t)un, invq, oi, tl);
 		} else {
 			uint32_t w[16];
 			const DW8 *N = Q.w8 + (size_t)node;
@@ -832,6 +885,7 @@ struct KShadow {
 	const DQNode *wnodes; /* 4-wide quantised BVH (WALK_W4 instances) */
 	const char *wtris;    /* its leaves' 48-byte triangle records */
 	const DW8 *w8;        /* 8-wide compressed BVH (WALK_W8 instances; qo / qs / qsi are then its frame) */
+	const DW8S *w8s;      /* its nodes' scalar-path copies */
 	uint32_t *w8spill;    /* lane-stack spill area, [entry][grid lane] */
 	uint32_t w8lstk;      /* lane-stack entries in LDS */
 	uint32_t test_emitters; /* emitters shadow_query tests linearly (the 8-wide tree leaves them out), else 0 */
@@ -985,6 +1039,7 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	Q.w = WALK == WALK_W4 ? unip(ks.wnodes) : nullptr;
 	Q.wt = WALK == WALK_W4 ? unip(ks.wtris) : nullptr;
 	Q.w8 = WALK == WALK_W8 ? unip(ks.w8) : nullptr;
+	Q.w8s = WALK == WALK_W8 ? unip(ks.w8s) : nullptr;
 	Q.spill_stride = gridDim.x * blockDim.x;
 	Q.spill = WALK == WALK_W8 ? unip(ks.w8spill) + blockIdx.x * blockDim.x + threadIdx.x : nullptr;
 	Q.lstk = uni(ks.w8lstk);
@@ -1454,6 +1509,7 @@ extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const
 	ka.wnodes = S->wnodes;
 	ka.wtris = (const char *)S->wtris;
 	ka.w8 = S->w8;
+	ka.w8s = S->w8s;
 	ka.w8spill = S->w8spill;
 	ka.w8lstk = S->w8lstk;
 	ka.test_emitters = 0;
