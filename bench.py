@@ -38,7 +38,7 @@ VALU_PEAK_GINST = 256 * 4 * 2.4e9 / 2 / 1e9
 # max/max3/min3/min, cmp), any_tri 39, a plane test 12, and per light sample 100 (counter RNG,
 # light point, direction, attenuation, Phong/Blinn incl. powf)
 USEFUL_VALU = {"box": 17, "tri": 39, "sphere": 25, "plane": 12, "sample": 100}
-SHADOW_SRCS = ["c-raytracer_amd/csrc/rtx_shadow.hip", "c-raytracer_amd/csrc/rtx_wave.h",
+SHADOW_SRCS = ["c-raytracer_amd/csrc/rtx_shadow.hip", "c-raytracer_amd/csrc/rtx_w8.h", "c-raytracer_amd/csrc/rtx_wave.h",
                "c-raytracer_amd/csrc/rtx_math.h", "c-raytracer_amd/csrc/rtx_device.h", "include/rtx_rng.h"]
 
 
@@ -66,6 +66,8 @@ def parse():
                          "(default), or N torchrun ranks")
     ap.add_argument("--walk", default="auto", choices=["auto", "w8", "w4", "bvh2"],
                     help="shadow-walk BVH layout (rtx_set_option RTX_OPT_SHADOW_WALK; auto = the library default)")
+    ap.add_argument("--trace-walk", default="auto", choices=["auto", "w8", "bvh2"],
+                    help="closest-hit BVH layout (rtx_set_option RTX_OPT_TRACE_WALK)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the traversal-counting pass (roofline)")
     ap.add_argument("--no-post", action="store_true", help="skip the postprocess (DoF + mist) side leg")
@@ -451,6 +453,7 @@ def main():
 
     r = rtxpy.Renderer(local)
     r.set_option(abi.RTX_OPT_SHADOW_WALK, WALKS[a.walk])
+    r.set_option(abi.RTX_OPT_TRACE_WALK, WALKS[a.trace_walk])
     t0 = time.perf_counter()
     r.upload(scene)
     st = r.stats()
@@ -589,6 +592,7 @@ def main():
                           "parallelism": f"tiles{world}", "launch": "torchrun" if world > 1 else "single",
                           "kernel_ms_rank0": round(kernel_ms, 3), "kernels_rank0": split,
                           "shadow_walk": ["bvh2", "w4", "w8"][st.shadow_walk],
+                          "trace_walk": ["bvh2", "w4", "w8"][s.trace_walk],
                           "step": "render into HBM, tile shards gathered to rank 0 over RCCL (N > 1), frame copied "
                                   "to pinned host memory (SURVEY 8(d): render window up to the framebuffer on the host)",
                           "rng": "counter, stratified light samples (library default)"},
@@ -632,6 +636,7 @@ def main_group(a):
     g = rtxpy.Group(list(range(a.gpus)))
     n = g.size()
     g.set_option(abi.RTX_OPT_SHADOW_WALK, WALKS[a.walk])
+    g.set_option(abi.RTX_OPT_TRACE_WALK, WALKS[a.trace_walk])
     t0 = time.perf_counter()
     g.upload(scene)
     log(f"{n} devices, scene {os.path.basename(path)} uploaded in {time.perf_counter() - t0:.2f}s")

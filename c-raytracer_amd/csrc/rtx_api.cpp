@@ -547,6 +547,7 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 		memcpy(e.e1, o.e1, 12);
 		memcpy(e.e2, o.e2, 12);
 		e.eps = o.epsilon;
+		e.prim = RTX_NONE;
 		e.transparent = (mats[o.material].flags & RTX_MF_TRANSPARENT) ? 1u : 0u;
 		memcpy(e.kt, mats[o.material].kt, 12);
 	}
@@ -628,6 +629,14 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 		}
 		if (nb)
 			memcpy(recs.data() + nnodes, prims.data(), nb * sizeof(DPrim));
+		/* the emitters' record indices (the 8-wide closest-hit walk tests them apart from the tree) */
+		{
+			std::vector<uint32_t> rec_of(sc->num_objects, RTX_NONE);
+			for (uint32_t k = 0; k < nb; k++)
+				rec_of[bounded[bvh.order[k]]] = k;
+			for (DEmitter &e : emit)
+				e.prim = rec_of[e.obj];
+		}
 		root_ref = dref(bvh.root_ref);
 		depth = bvh.depth;
 		inner.assign(recs.begin(), recs.begin() + nnodes);
@@ -871,6 +880,8 @@ int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, floa
 	c->scene.ostk = c->d_ostk;
 	c->scene.w8spill = nullptr;
 	c->scene.w8spill_lanes = 0;
+	c->scene.trace_w8 = (c->scene.w8 && c->opt_trace_walk != RTX_WALK_BVH2) ? 1u : 0u;
+	c->stats.trace_walk = c->scene.trace_w8 ? RTX_WALK_W8 : RTX_WALK_BVH2;
 	c->scene.w8lstk = c->opt_lstk;
 	if (c->scene.w8 && c->scene.w8depth > c->scene.w8lstk + 1) {
 		/* 8-wide trees deeper than the LDS lane stacks: the deeper entries of every lane of the
@@ -1147,6 +1158,11 @@ extern "C" int rtx_set_option(rtx_ctx *c, int option, int64_t value)
 		if (value < 1 || value > RTX_W8_STACK)
 			return fail(RTX_ERR_ARG, "shadow LDS stack %lld outside 1..%d", (long long)value, RTX_W8_STACK);
 		c->opt_lstk = (uint32_t)value;
+		return RTX_OK;
+	case RTX_OPT_TRACE_WALK:
+		if (value != RTX_WALK_AUTO && value != RTX_WALK_W8 && value != RTX_WALK_BVH2)
+			return fail(RTX_ERR_ARG, "closest-hit walk %lld is not AUTO, W8 or BVH2", (long long)value);
+		c->opt_trace_walk = (int)value;
 		return RTX_OK;
 	case RTX_OPT_SHADOW_GRAB:
 		if (value < 1 || value > (1 << 24))

@@ -133,7 +133,8 @@ typedef struct __attribute__((aligned(16))) DQNode {
  * (never hit by the octant-specialised test; the generic test masks with vmask).  An inner
  * slot's entry is the child node; a leaf slot's entry is a copy of the primitive's 64-byte DPrim
  * record (one primitive per leaf slot) with its material's kt in place of the normal (the
- * shadow walk needs no normal; a transparent hit multiplies by it without a material fetch).  A node's eight child entries are contiguous (unused ones are
+ * shadow walk needs no normal; a transparent hit multiplies by it without a material fetch)
+ * and the primitive's record index in the last word (the closest-hit walk's hit id).  A node's eight child entries are contiguous (unused ones are
  * holes), so a lane's pending siblings are one 32-bit group base << 8 | slot mask.
  * Slots follow the children's centroid octant about the node centre (bit a: the + side of
  * axis a), so a ray of direction octant OCT meets them front to back roughly in the order
@@ -196,6 +197,7 @@ typedef struct DEmitter {
 	float eps;          /* out of the 8-wide shadow tree (DScene.w8noemit) */
 	uint32_t transparent;
 	float kt[3];
+	uint32_t prim;      /* its primitive record index (closest hits of the 8-wide walk) */
 } DEmitter;
 
 #define RTX_MAX_EMITTERS 64
@@ -218,6 +220,7 @@ typedef struct DScene {
 	uint32_t num_w8, w8depth;
 	float w8qo[3], w8qs[3]; /* its 16-bit frame */
 	const DW8S *w8s;        /* scalar-path copies of its nodes (num_w8 slots, node entries filled) */
+	uint32_t trace_w8;      /* k_trace walks the 8-wide tree for closest hits (else the float BVH2) */
 	uint32_t w8noemit;      /* the emitters are not in it (k_shadow tests them linearly) */
 	uint32_t *w8spill;      /* k_shadow lane-stack entries from RTX_W8_STACK on, [entry][grid lane] */
 	uint32_t w8spill_lanes; /* grid lanes the spill area was sized for (0: no spill area) */

@@ -98,6 +98,7 @@ struct rtx_ctx {
 	uint32_t opt_slot = 0;
 	uint32_t opt_grab = 4096;
 	uint32_t opt_lstk = RTX_W8_STACK;
+	int opt_trace_walk = RTX_WALK_AUTO;
 };
 
 struct QFrame {

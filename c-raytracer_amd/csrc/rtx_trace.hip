@@ -27,6 +27,7 @@
 
 #include "rtx_kat.h"
 #include "rtx_wave.h"
+#include "rtx_w8.h"
 
 /* ------------------------------------------------------------------------ */
 /* closest hit: inside-object shortcut, planes, then BVH (render.c:118-147)  */
@@ -37,8 +38,8 @@ struct TraceCount {
 };
 
 template <bool COUNT>
-__device__ void trace_closest(const DScene &S, uint32_t *stk, bool act, f3 o, f3 d, uint32_t inside, float &t_out,
-			      uint32_t &hid_out, TraceCount &tc)
+__device__ void trace_closest_bvh2(const DScene &S, uint32_t *stk, bool act, f3 o, f3 d, uint32_t inside, float &t_out,
+				   uint32_t &hid_out, TraceCount &tc)
 {
 	float tbest = FLT_MAX;
 	uint32_t hid = RTX_NONE;
@@ -151,6 +152,189 @@ __device__ void trace_closest(const DScene &S, uint32_t *stk, bool act, f3 o, f3
 	}
 	t_out = tbest;
 	hid_out = hid;
+}
+
+/* Closest hit over the 8-wide compressed BVH (rtx_device.h DW8): the reference's
+ * bvh_get_closest_intersection (accel.c:322-353) with eight children per node.  Hit leaf
+ * slots are tested at once with the exact IEEE intersectors (the same t as the reference);
+ * hit inner children are taken in the octant's visit order (front to back, roughly), the
+ * first visited next, the rest kept as one group (base << 8 | mask) in a register and older
+ * groups on the lane's stack (LDS, deeper entries in HBM), and every node's boxes are tested
+ * against the current closest t.  The emitters the tree leaves out (DScene.w8noemit) are
+ * tested before the walk.  Strict < everywhere: the first hit found at the least t wins. */
+template <bool COUNT, int OCT>
+__device__ __forceinline__ void closest_walk8(const DScene &S, uint32_t *stk, uint32_t *ostk, size_t ostride, f3 o, f3 d,
+					      f3 inv, float &tbest, uint32_t &hid, TraceCount &tc)
+{
+	constexpr uint32_t K = (OCT == 8 || !RTX_W8_ORDER) ? 0u : (~(uint32_t)OCT & 7u);
+	const f3 qs = ld3(S.w8qs), qo = ld3(S.w8qo);
+	const f3 invq = mk3(inv.x / qs.x, inv.y / qs.y, inv.z / qs.z);
+	const f3 oq = mk3((o.x - qo.x) * qs.x, (o.y - qo.y) * qs.y, (o.z - qo.z) * qs.z);
+	const f3 oi = mul3v(oq, invq);
+	uint32_t node = 0, grp = 0, sp = 0;
+	while (node != RTX_NONE) {
+		W8Visit v;
+		const uint32_t un = uni(node);
+		if (!ballot(node != un)) {
+			v = w8_visit_s<OCT, K>(S.w8s + (size_t)un, invq, oi, tbest);
+		} else {
+			uint32_t w[16];
+			const DW8 *N = S.w8 + (size_t)node;
+#pragma unroll
+			for (int k = 0; k < 4; k++) {
+				const uint4 x = ldg4u((const uint32_t *)N + 4 * k);
+				w[4 * k] = x.x;
+				w[4 * k + 1] = x.y;
+				w[4 * k + 2] = x.z;
+				w[4 * k + 3] = x.w;
+			}
+			v = w8_visit<OCT, K, false>(w, invq, oi, tbest);
+		}
+		if (COUNT)
+			tc.nodes++;
+		uint32_t lm = v.hm & ~v.io, im = v.hm & v.io;
+		while (lm) {
+			const uint32_t p = __builtin_ctz(lm);
+			lm &= lm - 1;
+			const char *pr = (const char *)(S.w8 + v.base + (p ^ K));
+			const float4 a = ldg4(pr, 0), b = ldg4(pr, 16), c = ldg4(pr, 32);
+			float t = 0.f;
+			bool h;
+			if ((__float_as_uint(c.w) >> 24) == RTX_SPHERE) {
+				if (COUNT)
+					tc.sph++;
+				h = hit_sphere(mk3(a.x, a.y, a.z), b.x, o, d, a.w, t);
+			} else {
+				if (COUNT)
+					tc.tris++;
+				h = hit_triangle(mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z), mk3(c.x, c.y, c.z), o, d, a.w, t);
+			}
+			if (h && t < tbest) {
+				tbest = t;
+				hid = __float_as_uint(ldg4(pr, 48).w);
+			}
+		}
+		if (im) {
+			node = v.base + (__builtin_ctz(im) ^ K);
+			im &= im - 1;
+			if (im) {
+				if (grp) {
+					if (sp < RTX_TRACE_LSTK)
+						stk[sp * WAVE] = grp;
+					else
+						ostk[(sp - RTX_TRACE_LSTK) * ostride] = grp;
+					sp++;
+				}
+				grp = (v.base << 8) | im;
+			}
+		} else if (grp) {
+			node = (grp >> 8) + (__builtin_ctz(grp) ^ K);
+			grp &= grp - 1;
+			if (!(grp & 0xFFu)) {
+				grp = 0;
+				if (sp) {
+					sp--;
+					grp = sp < RTX_TRACE_LSTK ? stk[sp * WAVE] : ostk[(sp - RTX_TRACE_LSTK) * ostride];
+				}
+			}
+		} else {
+			node = RTX_NONE;
+		}
+	}
+}
+
+template <bool COUNT>
+__device__ void trace_closest_w8(const DScene &S, uint32_t *stk, bool act, f3 o, f3 d, uint32_t inside, float &t_out,
+				 uint32_t &hid_out, TraceCount &tc)
+{
+	float tbest = FLT_MAX;
+	uint32_t hid = RTX_NONE;
+	if (act && isnan3(d)) /* TIR / degenerate directions hit nothing */
+		act = false;
+	if (act && inside != RTX_NONE) {
+		float t;
+		bool h;
+		if (inside & RTX_PLANE_BIT) {
+			const DPlane &pl = S.planes[inside & ~RTX_PLANE_BIT];
+			h = hit_plane(ld3(pl.n), pl.d, o, d, pl.eps, t);
+		} else {
+			const DPrim &pr = S.prims[inside];
+			if ((__float_as_uint(pr.c[3]) >> 24) == RTX_SPHERE)
+				h = hit_sphere(mk3(pr.a[0], pr.a[1], pr.a[2]), pr.b[0], o, d, pr.a[3], t);
+			else
+				h = hit_triangle(mk3(pr.a[0], pr.a[1], pr.a[2]), mk3(pr.b[0], pr.b[1], pr.b[2]),
+						 mk3(pr.c[0], pr.c[1], pr.c[2]), o, d, pr.a[3], t);
+		}
+		if (h) {
+			tbest = t;
+			hid = inside;
+			act = false;
+		}
+	}
+	if (act) {
+		for (uint32_t i = 0; i < S.num_planes; i++) {
+			const DPlane &pl = S.planes[i];
+			float t;
+			if (COUNT)
+				tc.pln++;
+			if (hit_plane(ld3(pl.n), pl.d, o, d, pl.eps, t) && t < tbest) {
+				tbest = t;
+				hid = RTX_PLANE_BIT | i;
+			}
+		}
+		if (S.w8noemit)
+			for (uint32_t i = 0; i < S.num_emitters; i++) {
+				const DEmitter &e = S.emitters[i];
+				float t = 0.f;
+				bool h;
+				if (e.type == RTX_SPHERE)
+					h = hit_sphere(ld3(e.p0), e.radius, o, d, e.eps, t);
+				else
+					h = hit_triangle(ld3(e.p0), ld3(e.e1), ld3(e.e2), o, d, e.eps, t);
+				if (h && t < tbest) {
+					tbest = t;
+					hid = e.prim;
+				}
+			}
+	}
+	const u64 live = ballot(act);
+	if (live) {
+		const f3 inv = safe_inv_fast(d);
+		stk += lane_id();
+		uint32_t *ostk = S.ostk + (size_t)blockIdx.x * WAVE + lane_id();
+		const size_t ostride = (size_t)gridDim.x * WAVE;
+		const uint32_t oct = ((~__float_as_uint(inv.x)) >> 31) | (((~__float_as_uint(inv.y)) >> 31) << 1) |
+				     (((~__float_as_uint(inv.z)) >> 31) << 2);
+		const uint32_t lead = readlane(oct, (uint32_t)__ffsll((long long)live) - 1);
+		const uint32_t sel = ballot(act & (oct != lead)) ? 8u : lead;
+		if (act) {
+			switch (sel) {
+#define RTX_CWALK(K)                                                                    \
+	case K:                                                                             \
+		closest_walk8<COUNT, K>(S, stk, ostk, ostride, o, d, inv, tbest, hid, tc);      \
+		break;
+				RTX_CWALK(0) RTX_CWALK(1) RTX_CWALK(2) RTX_CWALK(3) RTX_CWALK(4) RTX_CWALK(5) RTX_CWALK(6)
+				RTX_CWALK(7)
+#undef RTX_CWALK
+			default:
+				closest_walk8<COUNT, 8>(S, stk, ostk, ostride, o, d, inv, tbest, hid, tc);
+				break;
+			}
+		}
+	}
+	t_out = tbest;
+	hid_out = hid;
+}
+
+/* the closest-hit walk of this scene: the 8-wide tree when built and chosen (DScene.trace_w8) */
+template <bool COUNT>
+__device__ __forceinline__ void trace_closest(const DScene &S, uint32_t *stk, bool act, f3 o, f3 d, uint32_t inside,
+					      float &t_out, uint32_t &hid_out, TraceCount &tc)
+{
+	if (S.trace_w8)
+		trace_closest_w8<COUNT>(S, stk, act, o, d, inside, t_out, hid_out, tc);
+	else
+		trace_closest_bvh2<COUNT>(S, stk, act, o, d, inside, t_out, hid_out, tc);
 }
 
 struct HitInfo {

@@ -1,0 +1,213 @@
+/*
+ * Device helpers shared by the walks of the 8-wide compressed BVH (rtx_device.h DW8 / DW8S):
+ * the shadow any-hit walk (rtx_shadow.hip shadow_walk8) and the closest-hit walk
+ * (rtx_trace.hip trace_closest_w8).  Both test a node's eight child boxes the same way
+ * (accel.c:112-158's slab test, conservative on the quantised boxes).
+ */
+#ifndef RTX_W8_H
+#define RTX_W8_H
+
+#include <hip/hip_runtime.h>
+
+#include "rtx_device.h"
+#include "rtx_math.h"
+
+/* ------------------------------------------------------------------------ */
+/* loads                                                                    */
+/* ------------------------------------------------------------------------ */
+/* per-lane loads through the global address space (global_load, not flat_load: the pointers
+ * come from LDS and the compiler cannot prove where they point) */
+template <typename T> __device__ __forceinline__ const __attribute__((address_space(1))) T *gptr(const T *p)
+{
+	return (const __attribute__((address_space(1))) T *)p;
+}
+template <typename T> __device__ __forceinline__ __attribute__((address_space(1))) T *gptrw(T *p)
+{
+	return (__attribute__((address_space(1))) T *)p;
+}
+/* wave-uniform reads of read-only scene tables (s_load) */
+template <typename T> __device__ __forceinline__ const __attribute__((address_space(4))) T *cptr(const T *p)
+{
+	return (const __attribute__((address_space(4))) T *)p;
+}
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ldg4(const void *p, uint32_t off)
+{
+	const f4v v = *(const __attribute__((address_space(1))) f4v *)((const char *)p + off);
+	return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint4 ldg4u(const void *p)
+{
+	const u4v v = *(const __attribute__((address_space(1))) u4v *)p;
+	return make_uint4(v.x, v.y, v.z, v.w);
+}
+/* LDS reads through generic pointers that point into LDS */
+__device__ __forceinline__ uint4 lds4u(const void *p)
+{
+	const u4v v = *(const __attribute__((address_space(3))) u4v *)p;
+	return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint32_t lds1u(const uint32_t *p)
+{
+	return *(const __attribute__((address_space(3))) uint32_t *)p;
+}
+__device__ __forceinline__ void lds1st(uint32_t *p, uint32_t v) { *(__attribute__((address_space(3))) uint32_t *)p = v; }
+/* a 32-bit LDS pointer (the lane stacks): one VGPR instead of a 64-bit generic pointer */
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+/* byte B of w as a float (v_cvt_f32_ubyteB) */
+template <int B> __device__ __forceinline__ float ubyte(uint32_t w) { return (float)((w >> (8 * B)) & 0xFFu); }
+
+/* the 8-bit mask m with bit i moved to bit i ^ K (K < 8 a compile-time constant) */
+template <uint32_t K> __device__ __forceinline__ uint32_t perm_xor(uint32_t m)
+{
+	if (K & 1u)
+		m = ((m & 0x55u) << 1) | ((m >> 1) & 0x55u);
+	if (K & 2u)
+		m = ((m & 0x33u) << 2) | ((m >> 2) & 0x33u);
+	if (K & 4u)
+		m = ((m & 0x0Fu) << 4) | ((m >> 4) & 0x0Fu);
+	return m;
+}
+
+/* The slab test (accel.c:112-158) of child C of an 8-wide node (rtx_device.h DW8) on the segment
+ * (0, tl): t = q8 * s + b per plane, with s = invq * 2^e and b = o * invq - oi the node frame's
+ * scale and offset of the walk's ray transform (box_hit_q), so the same conservative grid test
+ * on the box rounded outward to the node's 8-bit frame (KAT: RTX_KAT_BOX_Q8).  OCT < 8: every
+ * live lane's direction lies in octant OCT, entry planes known at compile time; an empty slot
+ * (lo 255 > hi 0) is then never hit. */
+template <int OCT>
+__device__ __forceinline__ bool w8_slab(float lx, float hx, float ly, float hy, float lz, float hz, float tl)
+{
+	if (OCT == 8) {
+		const float tn = fmaxf(fmaxf(fminf(lx, hx), fminf(ly, hy)), fmaxf(fminf(lz, hz), 0.f));
+		const float tf = fminf(fminf(fmaxf(lx, hx), fmaxf(ly, hy)), fminf(fmaxf(lz, hz), tl));
+		return tn <= tf;
+	}
+	const float nx = (OCT & 1) ? lx : hx, fx = (OCT & 1) ? hx : lx;
+	const float ny = (OCT & 2) ? ly : hy, fy = (OCT & 2) ? hy : ly;
+	const float nz = (OCT & 4) ? lz : hz, fz = (OCT & 4) ? hz : lz;
+	const float tn = fmaxf(fmaxf(nx, ny), fmaxf(nz, 0.f));
+	float tf = fminf(fminf(fx, fy), fz);
+	asm("v_min_f32 %0, %0, %1" : "+v"(tf) : "v"(tl));
+	return tn <= tf;
+}
+template <int OCT, int C>
+__device__ __forceinline__ bool w8_child(const uint32_t (&w)[16], f3 s, f3 b, float tl)
+{
+	constexpr int W = C >> 2, B = C & 3;
+	return w8_slab<OCT>(fmaf(ubyte<B>(w[4 + W]), s.x, b.x), fmaf(ubyte<B>(w[6 + W]), s.x, b.x),
+			    fmaf(ubyte<B>(w[8 + W]), s.y, b.y), fmaf(ubyte<B>(w[10 + W]), s.y, b.y),
+			    fmaf(ubyte<B>(w[12 + W]), s.z, b.z), fmaf(ubyte<B>(w[14 + W]), s.z, b.z), tl);
+}
+/* the same child test on the scalar-path copy (rtx_device.h DW8S): the plane offsets are ready
+ * floats, the same values the conversions above produce, so the results are bit-identical */
+template <int OCT, int C>
+__device__ __forceinline__ bool w8_child_s(const uint32_t (&q)[24], f3 s, f3 b, float tl)
+{
+	/* plane k's offset of child C: the half in word 4k + C/2, half C & 1 (v_fma_mix_f32 op_sel) */
+	auto h = [&](int k) -> float {
+		const uint32_t v = q[4 * k + (C >> 1)];
+		return (float)__builtin_bit_cast(_Float16, (uint16_t)((C & 1) ? (v >> 16) : (v & 0xFFFFu)));
+	};
+	return w8_slab<OCT>(fmaf(h(0), s.x, b.x), fmaf(h(1), s.x, b.x), fmaf(h(2), s.y, b.y), fmaf(h(3), s.y, b.y),
+			    fmaf(h(4), s.z, b.z), fmaf(h(5), s.z, b.z), tl);
+}
+
+/* the node frame of an 8-wide node: per-axis scale s = invq * 2^e and offset b = o * invq - oi */
+__device__ __forceinline__ void w8_frame(const uint32_t (&w)[16], f3 invq, f3 oi, f3 &s, f3 &b)
+{
+	s = mk3(ldexpf(invq.x, (int)((w[1] >> 16) & 15u)), ldexpf(invq.y, (int)((w[1] >> 20) & 15u)),
+		ldexpf(invq.z, (int)((w[1] >> 24) & 15u)));
+	b = mk3(fmaf((float)(w[0] & 0xFFFFu), invq.x, -oi.x), fmaf((float)(w[0] >> 16), invq.y, -oi.y),
+		fmaf((float)(w[1] & 0xFFFFu), invq.z, -oi.z));
+}
+
+/* hit mask of an 8-wide node's children in visit order: bit p for slot p ^ K */
+template <int OCT, uint32_t K>
+__device__ __forceinline__ uint32_t w8_hits(const uint32_t (&w)[16], f3 s, f3 b, float tl)
+{
+	uint32_t hm = 0;
+	hm |= w8_child<OCT, 0>(w, s, b, tl) ? 1u << (0 ^ K) : 0u;
+	hm |= w8_child<OCT, 1>(w, s, b, tl) ? 1u << (1 ^ K) : 0u;
+	hm |= w8_child<OCT, 2>(w, s, b, tl) ? 1u << (2 ^ K) : 0u;
+	hm |= w8_child<OCT, 3>(w, s, b, tl) ? 1u << (3 ^ K) : 0u;
+	hm |= w8_child<OCT, 4>(w, s, b, tl) ? 1u << (4 ^ K) : 0u;
+	hm |= w8_child<OCT, 5>(w, s, b, tl) ? 1u << (5 ^ K) : 0u;
+	hm |= w8_child<OCT, 6>(w, s, b, tl) ? 1u << (6 ^ K) : 0u;
+	hm |= w8_child<OCT, 7>(w, s, b, tl) ? 1u << (7 ^ K) : 0u;
+	if (OCT == 8)
+		hm &= w[3]; /* K = 0: slot order; the min/max form would turn an empty slot's box around */
+	return hm;
+}
+template <int OCT, uint32_t K>
+__device__ __forceinline__ uint32_t w8_hits_s(const uint32_t (&q)[24], uint32_t w3, f3 s, f3 b, float tl)
+{
+	uint32_t hm = 0;
+	hm |= w8_child_s<OCT, 0>(q, s, b, tl) ? 1u << (0 ^ K) : 0u;
+	hm |= w8_child_s<OCT, 1>(q, s, b, tl) ? 1u << (1 ^ K) : 0u;
+	hm |= w8_child_s<OCT, 2>(q, s, b, tl) ? 1u << (2 ^ K) : 0u;
+	hm |= w8_child_s<OCT, 3>(q, s, b, tl) ? 1u << (3 ^ K) : 0u;
+	hm |= w8_child_s<OCT, 4>(q, s, b, tl) ? 1u << (4 ^ K) : 0u;
+	hm |= w8_child_s<OCT, 5>(q, s, b, tl) ? 1u << (5 ^ K) : 0u;
+	hm |= w8_child_s<OCT, 6>(q, s, b, tl) ? 1u << (6 ^ K) : 0u;
+	hm |= w8_child_s<OCT, 7>(q, s, b, tl) ? 1u << (7 ^ K) : 0u;
+	if (OCT == 8)
+		hm &= w3;
+	return hm;
+}
+
+#ifndef RTX_W8_ORDER
+#define RTX_W8_ORDER 1 /* visit hit children in the octant's slot order (0: plain slot order) */
+#endif
+
+/* one 8-wide node visit's box tests: the hit mask in visit order and the node's masks */
+struct W8Visit {
+	uint32_t hm, base, io, to, nv;
+};
+template <int OCT, uint32_t K, bool UNI>
+__device__ __forceinline__ W8Visit w8_visit(const uint32_t (&w)[16], f3 invq, f3 oi, float tl)
+{
+	f3 s, b;
+	w8_frame(w, invq, oi, s, b);
+	W8Visit v;
+	v.hm = w8_hits<OCT, K>(w, s, b, tl);
+	v.base = w[2] >> 8;
+	v.io = perm_xor<K>(w[2] & 0xFFu);
+	v.to = perm_xor<K>((w[3] >> 8) & 0xFFu);
+	v.nv = w[3] & 0xFFu;
+	if (UNI) /* keeps the two instances apart (the scalar one reads SGPR operands, no copies) */
+		asm volatile("" ::: "memory");
+	return v;
+}
+
+/* the same visit on the scalar-path copy (every walking lane at the node: SGPR operands) */
+template <int OCT, uint32_t K>
+__device__ __forceinline__ W8Visit w8_visit_s(const DW8S *n, f3 invq, f3 oi, float tl)
+{
+	typedef uint32_t u16v __attribute__((ext_vector_type(16)));
+	const auto *U = (const __attribute__((address_space(4))) u16v *)n;
+	const u16v p0 = U[0], p1 = U[1];
+	uint32_t q[24];
+#pragma unroll
+	for (int k = 0; k < 8; k++)
+		q[k] = p0[8 + k];
+#pragma unroll
+	for (int k = 0; k < 16; k++)
+		q[8 + k] = p1[k];
+	const uint32_t w1 = p0[1], w2 = p0[2], w3 = p0[3];
+	const float org0 = __uint_as_float(p0[4]), org1 = __uint_as_float(p0[5]), org2 = __uint_as_float(p0[6]);
+	const f3 s = mk3(ldexpf(invq.x, (int)((w1 >> 16) & 15u)), ldexpf(invq.y, (int)((w1 >> 20) & 15u)),
+			 ldexpf(invq.z, (int)((w1 >> 24) & 15u)));
+	const f3 b = mk3(fmaf(org0, invq.x, -oi.x), fmaf(org1, invq.y, -oi.y), fmaf(org2, invq.z, -oi.z));
+	W8Visit v;
+	v.hm = w8_hits_s<OCT, K>(q, w3, s, b, tl);
+	v.base = w2 >> 8;
+	v.io = perm_xor<K>(w2 & 0xFFu);
+	v.to = perm_xor<K>((w3 >> 8) & 0xFFu);
+	v.nv = w3 & 0xFFu;
+	return v;
+}
+
+#endif

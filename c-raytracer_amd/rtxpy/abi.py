@@ -70,13 +70,14 @@ class Stats(C.Structure):
                 ("shadow_wave_steps", C.c_uint64), ("shadow_wave_walks", C.c_uint64),
                 ("wide_nodes", C.c_uint32), ("wide_depth", C.c_uint32), ("shadow_leaf_rounds", C.c_uint64),
                 ("gather_ms", C.c_double), ("devices", C.c_uint32), ("pad_", C.c_uint32),
-                ("shadow_uniform_steps", C.c_uint64), ("shadow_walk", C.c_uint32), ("wide_entries", C.c_uint32)]
+                ("shadow_uniform_steps", C.c_uint64), ("shadow_walk", C.c_uint32), ("wide_entries", C.c_uint32),
+                ("trace_walk", C.c_uint32), ("pad2_", C.c_uint32)]
 
 
 RTX_BUILD_SAH_HOST, RTX_BUILD_LBVH_GPU = 0, 1
 RTX_WALK_AUTO, RTX_WALK_BVH2, RTX_WALK_W4, RTX_WALK_W8 = -1, 0, 1, 2
 RTX_OPT_SHADOW_WALK, RTX_OPT_BVH_LEAF, RTX_OPT_SPSORT, RTX_OPT_SHADOW_SLOT, RTX_OPT_SHADOW_GRAB, \
-    RTX_OPT_SHADOW_LDS_STACK = 1, 2, 3, 4, 5, 6
+    RTX_OPT_SHADOW_LDS_STACK, RTX_OPT_TRACE_WALK = 1, 2, 3, 4, 5, 6, 7
 RTX_DOF_NONE, RTX_DOF_SCALE_BIAS, RTX_DOF_CAMERA = 0, 1, 2
 RTX_FALLOFF_QUAD, RTX_FALLOFF_LIN, RTX_FALLOFF_INV_QUAD = 0, 1, 2
 

@@ -215,6 +215,8 @@ typedef struct rtx_stats {
 	uint64_t shadow_uniform_steps;    /* only with count_traversal, wide walks: wave steps whose active lanes all fetched one node */
 	uint32_t shadow_walk;             /* the BVH k_shadow walks: RTX_WALK_W8 / RTX_WALK_W4 / RTX_WALK_BVH2 */
 	uint32_t wide_entries;            /* 8-wide walk: 64-byte entries (nodes, primitive records, holes) */
+	uint32_t trace_walk;              /* the BVH k_trace walks for closest hits: RTX_WALK_W8 / RTX_WALK_BVH2 */
+	uint32_t pad2_;
 } rtx_stats;
 
 typedef struct rtx_ctx rtx_ctx;
@@ -257,8 +259,10 @@ enum rtx_option {
 	RTX_OPT_SPSORT = 3,      /* 1: shade points in Morton order for k_shadow (default); 0: emission order */
 	RTX_OPT_SHADOW_SLOT = 4, /* k_shadow lanes per shade-point slot: 0 = automatic (default), else a power of two <= 64 */
 	RTX_OPT_SHADOW_GRAB = 5, /* lane slots per k_shadow work-queue grab, >= 1 (default 4096) */
-	RTX_OPT_SHADOW_LDS_STACK = 6 /* 8-wide walk: lane-stack entries kept in LDS, 1..8 (default 8); deeper
-	                              * ones spill to HBM (tests use 1 to exercise the spill on any tree) */
+	RTX_OPT_SHADOW_LDS_STACK = 6, /* 8-wide walk: lane-stack entries kept in LDS, 1..8 (default 8); deeper
+	                               * ones spill to HBM (tests use 1 to exercise the spill on any tree) */
+	RTX_OPT_TRACE_WALK = 7        /* closest hits (k_trace): RTX_WALK_AUTO (the 8-wide tree when built,
+	                               * default), RTX_WALK_W8 or RTX_WALK_BVH2 (the float BVH2) */
 };
 int rtx_set_option(rtx_ctx *ctx, int option, int64_t value);
 void rtx_close(rtx_ctx *ctx);

@@ -28,6 +28,8 @@ for s in $STEPS; do
     bench) run bench 900 python3 bench.py --verbose ;;
     benchq) run benchq 600 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --verbose ;;
     walks) for w in ${WALKS:-w8 w4}; do run walk_$w 600 python3 bench.py --walk $w --steps 2 --warmup 1 --no-cpu-baseline --no-post --verbose; done ;;
+    twalks) for w in ${TWALKS:-w8 bvh2}; do run twalk_$w 600 python3 bench.py --trace-walk $w --steps 2 --warmup 1 --no-cpu-baseline --no-post --no-count --verbose; done ;;
+    s6) for w in ${TWALKS:-w8}; do run s6_$w 900 python3 bench.py --scene scene6 --width 3840 --height 2160 --spp 128 --trace-walk $w --steps 1 --warmup 1 --no-cpu-baseline --no-post --verbose; done ;;
     occsweep) for o in ${OCCS:-1 6 7 8}; do RTX_SHADOW_OCC=$o run occ$o 600 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-count --no-post; done ;;
     benchr1) RTX_SH_R=1 run benchr1 600 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-post --verbose ;;
     variantsc) for v in ${VARS:-$(ls c-raytracer_amd/lib/var)}; do RTX_LIBRTX=$PWD/c-raytracer_amd/lib/var/$v/librtx.so run varc_$v 600 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-post --verbose; done ;;
