@@ -68,6 +68,8 @@ def parse():
                     help="shadow-walk BVH layout (rtx_set_option RTX_OPT_SHADOW_WALK; auto = the library default)")
     ap.add_argument("--trace-walk", default="auto", choices=["auto", "w8", "bvh2"],
                     help="closest-hit BVH layout (rtx_set_option RTX_OPT_TRACE_WALK)")
+    ap.add_argument("--shadow-slot", type=int, default=0,
+                    help="k_shadow lanes per shade-point slot (rtx_set_option RTX_OPT_SHADOW_SLOT; 0 = automatic)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the traversal-counting pass (roofline)")
     ap.add_argument("--no-post", action="store_true", help="skip the postprocess (DoF + mist) side leg")
@@ -454,6 +456,7 @@ def main():
     r = rtxpy.Renderer(local)
     r.set_option(abi.RTX_OPT_SHADOW_WALK, WALKS[a.walk])
     r.set_option(abi.RTX_OPT_TRACE_WALK, WALKS[a.trace_walk])
+    r.set_option(abi.RTX_OPT_SHADOW_SLOT, a.shadow_slot)
     t0 = time.perf_counter()
     r.upload(scene)
     st = r.stats()

@@ -204,6 +204,7 @@ struct QBvh {
 	uint32_t *spill;      /* this lane's stack entries from lstk on: entry k at spill[(k - lstk) * spill_stride] */
 	uint32_t spill_stride;
 	uint32_t lstk;        /* lane-stack entries in LDS (<= RTX_W8_STACK) */
+	uint32_t known;       /* WALK_W8: leaf slots marked transparent / opaque, no emitter in the tree */
 	lds_u32 *stk;         /* this lane's LDS stack of sibling groups: entry k at stk[k * WAVE] */
 	lds_u32 *tq;          /* WALK_W8: this lane's LDS queue of deferred leaf groups, entry k at tq[k * WAVE] */
 };
@@ -462,6 +463,23 @@ __device__ __forceinline__ void w8_defer_test(const char *pr, f3 o, f3 d, float 
 	}
 }
 
+/* an opaque leaf test: does the primitive at entry pr block this lane's shadow ray?  (no
+ * emitter or transparency cases: the 8-wide tree marks its leaves when built from host records) */
+template <bool COUNT>
+__device__ __forceinline__ bool w8_opaque_test(const char *pr, f3 o, f3 d, float tl, uint32_t &ntri, uint32_t &nsph)
+{
+	const float4 a = ldg4(pr, 0), b = ldg4(pr, 16), c = ldg4(pr, 32);
+	if ((__float_as_uint(c.w) >> 24) == RTX_SPHERE) {
+		if (COUNT)
+			nsph++;
+		float t = 0.f;
+		return hit_sphere(mk3(a.x, a.y, a.z), b.x, o, d, a.w, t) && t < tl;
+	}
+	if (COUNT)
+		ntri++;
+	return any_tri(mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z), mk3(c.x, c.y, c.z), o, d, a.w, tl);
+}
+
 template <bool COUNT, int OCT>
 __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__restrict__ mats, f3 o, f3 d, f3 inv,
 					     float &tl, uint32_t emit_obj, f3 &li, ShadowCount &sc)
@@ -528,13 +546,25 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 			nlr += r;
 		}
 		bool blocked = false;
-		while (lm) { /* opaque leaves: at once, an opaque hit ends the ray */
-			const uint32_t p = __builtin_ctz(lm);
-			lm &= lm - 1;
-			const char *pr = (const char *)(Q.w8 + base + (p ^ K));
-			if (shadow_prim<COUNT>(ldg4(pr, 0), ldg4(pr, 16), ldg4(pr, 32), mats, o, d, tl, emit_obj, li, ntri, nsph)) {
-				blocked = true;
-				break;
+		if (Q.known) {
+			/* the tree's leaf slots are marked (tmask) and hold no emitter: these are opaque */
+			while (lm) {
+				const uint32_t p = __builtin_ctz(lm);
+				lm &= lm - 1;
+				if (w8_opaque_test<COUNT>((const char *)(Q.w8 + base + (p ^ K)), o, d, tl, ntri, nsph)) {
+					blocked = true;
+					break;
+				}
+			}
+		} else {
+			while (lm) { /* unmarked leaves (a tree built without host records): the full test */
+				const uint32_t p = __builtin_ctz(lm);
+				lm &= lm - 1;
+				const char *pr = (const char *)(Q.w8 + base + (p ^ K));
+				if (shadow_prim<COUNT>(ldg4(pr, 0), ldg4(pr, 16), ldg4(pr, 32), mats, o, d, tl, emit_obj, li, ntri, nsph)) {
+					blocked = true;
+					break;
+				}
 			}
 		}
 		if (blocked) {
@@ -692,6 +722,7 @@ struct KShadow {
 	uint32_t *w8spill;    /* lane-stack spill area, [entry][grid lane] */
 	uint32_t w8lstk;      /* lane-stack entries in LDS */
 	uint32_t test_emitters; /* emitters shadow_query tests linearly (the 8-wide tree leaves them out), else 0 */
+	uint32_t w8known;       /* the 8-wide tree was built from host records (leaf slots marked, no emitters) */
 	float qo[3], qs[3], qsi[3];
 	const uint32_t *top; /* its top levels (rtx_device.h RTX_QTOP_CUT), copied to LDS per workgroup */
 	uint32_t ntop, nq;
@@ -846,6 +877,7 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	Q.spill_stride = gridDim.x * blockDim.x;
 	Q.spill = WALK == WALK_W8 ? unip(ks.w8spill) + blockIdx.x * blockDim.x + threadIdx.x : nullptr;
 	Q.lstk = uni(ks.w8lstk);
+	Q.known = uni(ks.w8known);
 	Q.stk = stk;
 	Q.tq = stk + RTX_W8_STACK * WAVE;
 	const bool blocked = shadow_query<COUNT, WALK>(Q, unip(ks.recs), unip(ks.mats), unip(ks.planes), uni(ks.num_planes),
@@ -1316,6 +1348,7 @@ extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const
 	ka.w8spill = S->w8spill;
 	ka.w8lstk = S->w8lstk;
 	ka.test_emitters = 0;
+	ka.w8known = 0;
 	if (walk == WALK_W8) { /* the 8-wide tree's own frame; the emitters it leaves out are tested linearly */
 		for (int a = 0; a < 3; a++) {
 			ka.qo[a] = S->w8qo[a];
@@ -1323,6 +1356,7 @@ extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const
 			ka.qsi[a] = 1.f / S->w8qs[a];
 		}
 		ka.test_emitters = S->w8noemit ? S->num_emitters : 0u;
+		ka.w8known = S->w8noemit;
 	}
 	if (walk == WALK_W8)
 		return launch_walk<WALK_W8>(ka, nw, cus, count, stream);

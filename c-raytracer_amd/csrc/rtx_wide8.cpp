@@ -32,8 +32,11 @@ namespace {
 
 /* expected-cost weights of a node visit (one 64-byte fetch, eight box tests) and of a primitive
  * test, per unit of surface area */
+#ifndef RTX_W8_C_PRIM
+#define RTX_W8_C_PRIM 0.3f
+#endif
 constexpr float C_NODE = 1.0f;
-constexpr float C_PRIM = 0.3f;
+constexpr float C_PRIM = RTX_W8_C_PRIM;
 
 struct TNode {
 	float lo[3], hi[3];

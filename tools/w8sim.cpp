@@ -218,7 +218,10 @@ int main(int argc, char **argv)
 	}
 	std::vector<DW8> w8;
 	std::vector<uint32_t> leafmap;
-	const uint32_t depth = rtx_wide8_build(inner, nnodes, prims.data(), dref(bvh.root_ref), blo, bhi, F, w8, leafmap);
+	std::vector<uint32_t> emit_objs(sc->emitters, sc->emitters + sc->num_emitters);
+	bool skipped = false;
+	const uint32_t depth = rtx_wide8_build(inner, nnodes, prims.data(), dref(bvh.root_ref), blo, bhi, emit_objs, F, skipped,
+					       w8, leafmap);
 	uint32_t nodes = 0, kids = 0, inner_kids = 0;
 	std::vector<uint32_t> hist(9, 0);
 	for (const DW8 &e : w8)
