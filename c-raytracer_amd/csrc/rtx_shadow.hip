@@ -480,6 +480,58 @@ __device__ __forceinline__ bool w8_opaque_test(const char *pr, f3 o, f3 d, float
 	return any_tri(mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z), mk3(c.x, c.y, c.z), o, d, a.w, tl);
 }
 
+/* One or more rounds of opaque leaf tests dealt over the wave (all 64 lanes active): the lanes'
+ * jobs (owner lane, entry) are numbered by an exclusive prefix sum, job j goes to lane j % 63 of
+ * round j / 63 through ds_permute (forward; lane 63 takes the writes of lanes without a job),
+ * each tester fetches its owner's ray with ds_bpermute and tests, and the owners of blocking
+ * jobs are collected from the blocked testers' ballot.  Returns this lane's blocked flag. */
+template <bool COUNT>
+__device__ __forceinline__ bool w8_opaque_round(const QBvh &Q, uint32_t lm, uint32_t base, uint32_t K, f3 o, f3 d, float tl,
+						uint32_t &ntri, uint32_t &nsph, uint32_t &nlr)
+{
+	uint32_t total;
+	const uint32_t pre = wave_excl_scan((uint32_t)__builtin_popcount(lm), &total);
+	u64 owners = 0;
+	const uint32_t me = lane_id();
+	for (uint32_t r0 = 0; r0 < total; r0 += WAVE - 1) {
+		if (COUNT)
+			nlr++;
+		/* deal this round's jobs */
+		uint32_t job = 0, m = lm, j = pre;
+		for (;;) {
+			const bool has = m != 0;
+			if (!ballot(has))
+				break;
+			const bool mine = has && j >= r0 && j < r0 + WAVE - 1;
+			const uint32_t val = mine ? (me << 24) | (base + (__builtin_ctz(m) ^ K)) : 0u;
+			const uint32_t dst = mine ? j - r0 : WAVE - 1;
+			job |= (uint32_t)__builtin_amdgcn_ds_permute((int)(dst * 4), (int)val);
+			if (has) {
+				m &= m - 1;
+				j++;
+			}
+		}
+		if (me == WAVE - 1)
+			job = 0;
+		/* test it against the owner's ray */
+		const uint32_t owner = job >> 24;
+		const int src = (int)(owner * 4);
+		const f3 oo = mk3(__int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(o.x))),
+				  __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(o.y))),
+				  __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(o.z))));
+		const f3 od = mk3(__int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(d.x))),
+				  __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(d.y))),
+				  __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(d.z))));
+		const float otl = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(tl)));
+		bool hit = false;
+		if (job)
+			hit = w8_opaque_test<COUNT>((const char *)(Q.w8 + (job & 0xFFFFFFu)), oo, od, otl, ntri, nsph);
+		for (u64 b = ballot(hit); b; b &= b - 1) /* the owners of blocking jobs (a few per round at most) */
+			owners |= 1ull << readlane(owner, (uint32_t)__ffsll((long long)b) - 1);
+	}
+	return (owners >> me) & 1ull;
+}
+
 template <bool COUNT, int OCT>
 __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__restrict__ mats, f3 o, f3 d, f3 inv,
 					     float &tl, uint32_t emit_obj, f3 &li, ShadowCount &sc)
@@ -509,54 +561,91 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 			}
 			continue;
 		}
-		if (node == RTX_NONE)
-			continue;
-		W8Visit v;
-		const uint32_t un = uni(node);
-		if (RTX_W_SUNI && !ballot(node != un)) {
-			/* every walking lane is at one node: its scalar-path copy through the scalar cache,
-			 * the planes as SGPR float operands */
-			v = w8_visit_s<OCT, K>(Q.w8s + (size_t)un, invq, oi, tl);
-		} else {
-			uint32_t w[16];
-			const DW8 *N = Q.w8 + (size_t)node;
+		uint32_t lm = 0, base = 0; /* this step's opaque leaf hits (visit order) and their block */
+		if (node != RTX_NONE) {
+			W8Visit v;
+			const uint32_t un = uni(node);
+			if (RTX_W_SUNI && !ballot(node != un)) {
+				/* every walking lane is at one node: its scalar-path copy through the scalar cache,
+				 * the planes as SGPR float operands */
+				v = w8_visit_s<OCT, K>(Q.w8s + (size_t)un, invq, oi, tl);
+			} else {
+				uint32_t w[16];
+				const DW8 *N = Q.w8 + (size_t)node;
 #pragma unroll
-			for (int k = 0; k < 4; k++) {
-				const uint4 x = ldg4u((const uint32_t *)N + 4 * k);
-				w[4 * k] = x.x;
-				w[4 * k + 1] = x.y;
-				w[4 * k + 2] = x.z;
-				w[4 * k + 3] = x.w;
+				for (int k = 0; k < 4; k++) {
+					const uint4 x = ldg4u((const uint32_t *)N + 4 * k);
+					w[4 * k] = x.x;
+					w[4 * k + 1] = x.y;
+					w[4 * k + 2] = x.z;
+					w[4 * k + 3] = x.w;
+				}
+				v = w8_visit<OCT, K, false>(w, invq, oi, tl);
 			}
-			v = w8_visit<OCT, K, false>(w, invq, oi, tl);
-		}
-		const uint32_t hm = v.hm, base = v.base;
-		uint32_t lm = hm & ~v.io & ~v.to, im = hm & v.io;
-		const uint32_t dm = hm & v.to;
-		if (COUNT) {
-			nstep++;
-			nbox += popc64(v.nv);
-			nun += ballot(node != uni(node)) ? 0u : 1u;
-			uint32_t r = 0;
-			for (uint32_t m = lm;; m &= m - 1) {
-				if (!ballot(m != 0))
-					break;
-				r++;
+			const uint32_t hm = v.hm;
+			base = v.base;
+			lm = hm & ~v.io & ~v.to;
+			uint32_t im = hm & v.io;
+			const uint32_t dm = hm & v.to;
+			if (COUNT) {
+				nstep++;
+				nbox += popc64(v.nv);
+				nun += ballot(node != uni(node)) ? 0u : 1u;
 			}
-			nlr += r;
+			if (dm) { /* transparent leaves: deferred */
+				const uint32_t g = (base << 8) | dm;
+				if (tgrp)
+					tq[tn++ * WAVE] = g;
+				else
+					tgrp = g;
+			}
+			/* the next node (a lane the opaque leaves below block drops it again) */
+			if (im) {
+				node = base + (__builtin_ctz(im) ^ K);
+				im &= im - 1;
+				if (im) {
+					if (grp) {
+						if (sp < Q.lstk)
+							stk[sp * WAVE] = grp;
+						else
+							gptrw(Q.spill)[(size_t)(sp - Q.lstk) * Q.spill_stride] = grp;
+						sp++;
+					}
+					grp = (base << 8) | im;
+				}
+			} else if (grp) {
+				node = (grp >> 8) + (__builtin_ctz(grp) ^ K);
+				grp &= grp - 1;
+				if (!(grp & 0xFFu)) {
+					grp = 0;
+					if (sp) {
+						sp--;
+						grp = sp < Q.lstk ? stk[sp * WAVE] : gptr(Q.spill)[(size_t)(sp - Q.lstk) * Q.spill_stride];
+					}
+				}
+			} else {
+				node = RTX_NONE;
+			}
 		}
+		/* opaque leaves, at once (an opaque hit ends the ray) */
+		if (!ballot(lm != 0))
+			continue;
 		bool blocked = false;
 		if (Q.known) {
-			/* the tree's leaf slots are marked (tmask) and hold no emitter: these are opaque */
-			while (lm) {
-				const uint32_t p = __builtin_ctz(lm);
-				lm &= lm - 1;
-				if (w8_opaque_test<COUNT>((const char *)(Q.w8 + base + (p ^ K)), o, d, tl, ntri, nsph)) {
-					blocked = true;
-					break;
-				}
-			}
+			/* marked tree: every one is opaque.  The wave's tests are dealt over its lanes (a lane
+			 * tests a job against its owner's ray), so a step's few leaf hits take one round
+			 * instead of as many as the busiest lane holds */
+			blocked = w8_opaque_round<COUNT>(Q, lm, base, K, o, d, tl, ntri, nsph, nlr);
 		} else {
+			if (COUNT) {
+				uint32_t r = 0;
+				for (uint32_t m = lm;; m &= m - 1) {
+					if (!ballot(m != 0))
+						break;
+					r++;
+				}
+				nlr += r;
+			}
 			while (lm) { /* unmarked leaves (a tree built without host records): the full test */
 				const uint32_t p = __builtin_ctz(lm);
 				lm &= lm - 1;
@@ -571,40 +660,6 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 			tl = -1.f;
 			node = RTX_NONE;
 			tgrp = 0;
-			continue;
-		}
-		if (dm) { /* transparent leaves: deferred */
-			const uint32_t g = (base << 8) | dm;
-			if (tgrp)
-				tq[tn++ * WAVE] = g;
-			else
-				tgrp = g;
-		}
-		if (im) {
-			node = base + (__builtin_ctz(im) ^ K);
-			im &= im - 1;
-			if (im) {
-				if (grp) {
-					if (sp < Q.lstk)
-						stk[sp * WAVE] = grp;
-					else
-						gptrw(Q.spill)[(size_t)(sp - Q.lstk) * Q.spill_stride] = grp;
-					sp++;
-				}
-				grp = (base << 8) | im;
-			}
-		} else if (grp) {
-			node = (grp >> 8) + (__builtin_ctz(grp) ^ K);
-			grp &= grp - 1;
-			if (!(grp & 0xFFu)) {
-				grp = 0;
-				if (sp) {
-					sp--;
-					grp = sp < Q.lstk ? stk[sp * WAVE] : gptr(Q.spill)[(size_t)(sp - Q.lstk) * Q.spill_stride];
-				}
-			}
-		} else {
-			node = RTX_NONE;
 		}
 	}
 	if (COUNT) {
