@@ -931,9 +931,12 @@ __global__ void k_kat(int kind, uint32_t n, const float *__restrict__ in, float 
 /* ------------------------------------------------------------------------ */
 extern "C" size_t rtx_trace_lds_bytes(uint32_t stack_size)
 {
-	/* RTX_TRACE_LDS_PAD (measurement): extra bytes per wave, to read k_trace's occupancy slope */
+	size_t pad = 0;
+#if RTX_MEASURE
+	/* RTX_TRACE_LDS_PAD (measurement builds): extra bytes per wave, to read k_trace's occupancy slope */
 	const char *e = getenv("RTX_TRACE_LDS_PAD");
-	const size_t pad = e ? (size_t)atoi(e) : 0;
+	pad = e ? (size_t)atoi(e) : 0;
+#endif
 	const size_t lstk = stack_size < RTX_TRACE_LSTK ? stack_size : RTX_TRACE_LSTK;
 	return (size_t)WAVE * SPW * 4 + 80 * 4 + lstk * WAVE * 4 + pad;
 }

@@ -142,6 +142,7 @@ int main(int argc, char **argv)
 		return 1;
 	}
 	const int npts = argc > 3 ? atoi(argv[3]) : 4000;
+	const bool near = getenv("W8SIM_NEAR") != nullptr; /* visit the nearest hit inner child first */
 	const rtx_scene_desc *sc = rtx_scene_desc_of(scene);
 	std::vector<uint32_t> bounded;
 	for (uint32_t i = 0; i < sc->num_objects; i++)
@@ -227,9 +228,9 @@ int main(int argc, char **argv)
 	for (const DW8 &e : w8)
 		if (e.w[3]) {
 			nodes++;
-			kids += __builtin_popcount(e.w[3]);
+			kids += __builtin_popcount(e.w[3] & 0xFFu);
 			inner_kids += __builtin_popcount(e.w[2] & 0xFF);
-			hist[__builtin_popcount(e.w[3])]++;
+			hist[__builtin_popcount(e.w[3] & 0xFFu)]++;
 		}
 	printf("prims %u  bvh2 nodes %u depth %u  w8 entries %zu nodes %u depth %u  children/node %.2f (inner %.2f)  hist",
 	       nb, nnodes, bvh.depth, w8.size(), nodes, depth, (double)kids / nodes, (double)inner_kids / nodes);
@@ -361,10 +362,11 @@ int main(int argc, char **argv)
 						nv_imm++;
 					const DW8 &N = w8[node];
 					nv++;
-					S.boxes += __builtin_popcount(N.w[3]);
+					S.boxes += __builtin_popcount(N.w[3] & 0xFFu);
 					const double org[3] = { (double)(N.w[0] & 0xFFFF), (double)(N.w[0] >> 16), (double)(N.w[1] & 0xFFFF) };
 					const int ex[3] = { (int)((N.w[1] >> 16) & 15), (int)((N.w[1] >> 20) & 15), (int)((N.w[1] >> 24) & 15) };
-					uint32_t hm = 0;
+					uint32_t hm = 0, near_p = 8;
+					double near_t = 1e300;
 					for (int c = 0; c < 8; c++) {
 						if (!((N.w[3] >> c) & 1))
 							continue;
@@ -376,8 +378,13 @@ int main(int argc, char **argv)
 							tn = std::max(tn, std::min(t0, t1));
 							tf = std::min(tf, std::max(t0, t1));
 						}
-						if (tn <= tf)
+						if (tn <= tf) {
 							hm |= 1u << (c ^ K);
+							if (((N.w[2] >> c) & 1) && tn < near_t) {
+								near_t = tn;
+								near_p = c ^ K;
+							}
+						}
 					}
 					uint32_t io = 0;
 					for (int c = 0; c < 8; c++)
@@ -421,8 +428,9 @@ int main(int argc, char **argv)
 					}
 					leaves[l].push_back(nleaf);
 					if (im) {
-						node = base + (__builtin_ctz(im) ^ K);
-						im &= im - 1;
+						const uint32_t p0 = near ? near_p : (uint32_t)__builtin_ctz(im);
+						node = base + (p0 ^ K);
+						im &= ~(1u << p0);
 						if (im) {
 							if (grp)
 								stk.push_back(grp);
