@@ -548,14 +548,17 @@ def main():
             build = {"sah_host_ms": round(st.build_ms, 1), "sah_nodes": int(st.bvh_nodes), "sah_depth": int(st.bvh_depth),
                      "sah_wide_nodes": int(st.wide_nodes), "sah_wide_depth": int(st.wide_depth),
                      "sah_shadow_walk": ["bvh2", "w4", "w8"][st.shadow_walk]}
-            r.set_builder(abi.RTX_BUILD_LBVH_GPU)
-            r.upload(scene)
-            sl = r.stats()
-            build.update({"lbvh_gpu_ms": round(sl.build_ms, 1), "lbvh_nodes": int(sl.bvh_nodes),
-                          "lbvh_depth": int(sl.bvh_depth), "lbvh_wide_nodes": int(sl.wide_nodes),
-                          "lbvh_wide_depth": int(sl.wide_depth), "lbvh_shadow_walk": ["bvh2", "w4", "w8"][sl.shadow_walk]})
-            r.render_device(frame, params, d_rgb.data_ptr(), d_z.data_ptr(), stream.cuda_stream)
-            build["lbvh_shadow_ms"] = round(r.stats().shadow_ms, 1)
+            for tag, bid in (("lbvh", abi.RTX_BUILD_LBVH_GPU), ("ploc", abi.RTX_BUILD_PLOC_GPU)):
+                r.set_builder(bid)
+                r.upload(scene)
+                sl = r.stats()
+                build.update({f"{tag}_gpu_ms": round(sl.build_ms, 1), f"{tag}_nodes": int(sl.bvh_nodes),
+                              f"{tag}_depth": int(sl.bvh_depth), f"{tag}_wide_nodes": int(sl.wide_nodes),
+                              f"{tag}_wide_depth": int(sl.wide_depth),
+                              f"{tag}_shadow_walk": ["bvh2", "w4", "w8"][sl.shadow_walk]})
+                r.render_device(frame, params, d_rgb.data_ptr(), d_z.data_ptr(), stream.cuda_stream)
+                build[f"{tag}_shadow_ms"] = round(r.stats().shadow_ms, 1)
+                build[f"{tag}_trace_ms"] = round(r.stats().trace_ms, 1)
             build["sah_shadow_ms"] = round(float(np.mean(sms)), 1)
             r.set_builder(abi.RTX_BUILD_SAH_HOST)
             r.upload(scene)

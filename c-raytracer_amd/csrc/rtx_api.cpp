@@ -36,6 +36,15 @@ extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const
 extern "C" hipError_t rtx_launch_post(uint32_t w, uint32_t h, const rtx_post *pp, float *rgb, const float *z,
 				      int *rad, float4 *pv, unsigned *scratch, hipStream_t stream);
 extern "C" hipError_t rtx_spsort_temp_bytes(uint32_t n, size_t *bytes);
+extern "C" hipError_t rtx_ploc_build(uint32_t n, const float *d_lo, const float *d_hi, const DPrim *d_prims_in,
+				     const float blo[3], const float bhi[3], uint32_t max_leaf, DNode **recs_out,
+				     uint32_t *nnodes_out, uint32_t *root_out, uint32_t *depth_out, uint32_t *rounds_out,
+				     hipStream_t st);
+extern "C" hipError_t rtx_w8_collapse_device(const DNode *recs, uint32_t nnodes, uint32_t nb, const uint32_t *skip_obj,
+					     uint32_t num_objects, DW8 **w8_out, DW8S **w8s_out, uint32_t **leafmap_out,
+					     uint32_t *entries_out, uint32_t *depth_out, uint32_t *wide_out, float qo[3],
+					     float qs[3], hipStream_t st);
+extern "C" hipError_t rtx_launch_w8_scalar(uint32_t n, const DW8 *w8, const uint32_t *leafmap, DW8S *w8s, hipStream_t st);
 extern "C" hipError_t rtx_lbvh_build(uint32_t n, const float *d_lo, const float *d_hi, const DPrim *d_prims_in,
 				     const float blo[3], const float bhi[3], uint32_t max_leaf, DNode **recs_out,
 				     uint32_t *nnodes_out, uint32_t *root_out, uint32_t *depth_out, hipStream_t st);
@@ -555,9 +564,11 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 	const auto tb0 = std::chrono::steady_clock::now();
 	uint32_t nnodes = 0, root_ref = RTX_EMPTY_REF, depth = 0;
 	std::vector<DNode> inner; /* host copy of the inner-node records, for the threaded BVH */
+	std::vector<DPrim> prims_dl; /* device builders: the primitive records read back */
+	const DPrim *host_prims = nullptr; /* the primitive records in leaf order on the host */
 	int rc;
-	if (c->builder == RTX_BUILD_LBVH_GPU && nb) {
-		/* GPU linear BVH (rtx_build.hip): primitives uploaded in input order, records emitted on the device */
+	if ((c->builder == RTX_BUILD_LBVH_GPU || c->builder == RTX_BUILD_PLOC_GPU) && nb) {
+		/* GPU builders (rtx_build.hip): primitives uploaded in input order, records emitted on the device */
 		std::vector<DPrim> prims_in(nb);
 		uint32_t sph = 0;
 		for (uint32_t k = 0; k < nb; k++) {
@@ -574,8 +585,12 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 			dfree(d_in);
 			return rc;
 		}
-		hipError_t e = rtx_lbvh_build(nb, d_lo, d_hi, d_in, c->bound_lo, c->bound_hi, cfg.max_leaf, &recs, &nnodes,
-					      &root_ref, &depth, c->stream);
+		uint32_t rounds = 0;
+		hipError_t e = c->builder == RTX_BUILD_PLOC_GPU
+				       ? rtx_ploc_build(nb, d_lo, d_hi, d_in, c->bound_lo, c->bound_hi, cfg.max_leaf, &recs, &nnodes,
+							&root_ref, &depth, &rounds, c->stream)
+				       : rtx_lbvh_build(nb, d_lo, d_hi, d_in, c->bound_lo, c->bound_hi, cfg.max_leaf, &recs, &nnodes,
+							&root_ref, &depth, c->stream);
 		dfree(d_lo);
 		dfree(d_hi);
 		dfree(d_in);
@@ -591,10 +606,47 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 		inner.resize(nnodes);
 		if (nnodes)
 			HIP_TRY(hipMemcpy(inner.data(), recs, nnodes * sizeof(DNode), hipMemcpyDeviceToHost));
+		/* the 8-wide tree collapsed where the records are (single-primitive leaves, one device) */
+		if (!hs.want_host_recs && cfg.max_leaf == 1 && nnodes && (c->opt_walk == RTX_WALK_AUTO || c->opt_walk == RTX_WALK_W8)) {
+			std::vector<uint32_t> skip((sc->num_objects + 31) / 32 + 1, 0u);
+			for (uint32_t i = 0; i < sc->num_emitters; i++)
+				skip[sc->emitters[i] >> 5] |= 1u << (sc->emitters[i] & 31u);
+			uint32_t *d_skip = nullptr;
+			if ((rc = upload(d_skip, skip)))
+				return rc;
+			uint32_t ent = 0, dep = 0, wide = 0;
+			e = rtx_w8_collapse_device(recs, nnodes, nb, d_skip, sc->num_objects, &hs.dev_w8, &hs.dev_w8s, &hs.dev_w8leaf, &ent,
+						   &dep, &wide, hs.w8f.qo, hs.w8f.qs, c->stream);
+			dfree(d_skip);
+			if (e != hipSuccess)
+				return fail(RTX_ERR_HIP, "8-wide BVH collapse on the device failed: %s", hipGetErrorString(e));
+			if (dep) {
+				hs.w8_on_device = true;
+				hs.w8depth = dep;
+				hs.w8_entries = ent;
+				hs.w8_wide = wide;
+				hs.w8noemit = sc->num_emitters > 0;
+			}
+		}
 		if (hs.want_host_recs) { /* the other devices of a group get the records from the host */
 			hs.recs.resize((size_t)nnodes + nb);
 			HIP_TRY(hipMemcpy(hs.recs.data(), recs, hs.recs.size() * sizeof(DNode), hipMemcpyDeviceToHost));
+			host_prims = (const DPrim *)(hs.recs.data() + nnodes);
+		} else { /* the primitives in leaf order: the 8-wide tree marks its leaves from them */
+			prims_dl.resize(nb);
+			HIP_TRY(hipMemcpy(prims_dl.data(), recs + nnodes, (size_t)nb * sizeof(DPrim), hipMemcpyDeviceToHost));
+			host_prims = prims_dl.data();
 		}
+		/* the emitters' record indices (the 8-wide closest-hit walk tests them apart from the tree) */
+		std::vector<uint32_t> rec_of(sc->num_objects, RTX_NONE);
+		for (uint32_t k = 0; k < nb; k++) {
+			uint32_t obj;
+			memcpy(&obj, &host_prims[k].b[3], 4);
+			if (obj < sc->num_objects)
+				rec_of[obj] = k;
+		}
+		for (DEmitter &e : emit)
+			e.prim = rec_of[e.obj];
 	} else {
 		BvhOutput bvh;
 		bvh_build(BvhInput{ nb, lo.data(), hi.data() }, cfg, bvh);
@@ -641,6 +693,7 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 		depth = bvh.depth;
 		inner.assign(recs.begin(), recs.begin() + nnodes);
 		hs.recs = std::move(recs);
+		host_prims = (const DPrim *)(hs.recs.data() + nnodes);
 	}
 	std::vector<uint32_t> qdepth;
 	thread_bvh(inner, nb ? root_ref : RTX_EMPTY_REF, c->bound_lo, c->bound_hi, hs.qnodes, hs.qf, qdepth);
@@ -650,9 +703,11 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 	/* the shadow walk's BVH (RTX_OPT_SHADOW_WALK): the 8-wide compressed tree by default, which
 	 * walks any depth; the 4-wide tree (depth-limited by its LDS stacks) and the threaded BVH2 for
 	 * measurement, and the BVH2 when the 8-wide tree cannot be built (over 2^24 entries) */
-	if (c->opt_walk == RTX_WALK_AUTO || c->opt_walk == RTX_WALK_W8) {
+	if (hs.w8_on_device) {
+		/* collapsed on the device above */
+	} else if (c->opt_walk == RTX_WALK_AUTO || c->opt_walk == RTX_WALK_W8) {
 		/* with the host records the emitters are left out of the tree (k_shadow tests them linearly) */
-		const DPrim *hp = hs.recs.size() >= (size_t)nnodes + nb ? (const DPrim *)(hs.recs.data() + nnodes) : nullptr;
+		const DPrim *hp = nb ? host_prims : nullptr;
 		std::vector<uint32_t> emit_objs;
 		for (const DEmitter &e : emit)
 			emit_objs.push_back(e.obj);
@@ -665,7 +720,7 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 	}
 	if (hs.wnodes.empty())
 		hs.wdepth = 0;
-	if (hs.w8.empty())
+	if (hs.w8.empty() && !hs.w8_on_device)
 		hs.w8depth = 0;
 	hs.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count();
 	hs.mats = std::move(mats);
@@ -702,41 +757,34 @@ int rtx_upload_built(rtx_ctx *c, const HostScene &hs)
 		HIP_TRY(rtx_launch_pack_tris((const DPrim *)(c->d_nodes + hs.nnodes), hs.nb, c->d_wtris, c->stream));
 		HIP_TRY(hipStreamSynchronize(c->stream));
 	}
-	if ((rc = upload(c->d_w8, hs.w8)))
-		return rc;
-	{ /* the scalar-path node copies (rtx_device.h DW8S) */
-		std::vector<DW8S> w8s(hs.w8.size());
-		memset(w8s.data(), 0, w8s.size() * sizeof(DW8S));
-		for (size_t i = 0; i < hs.w8.size(); i++) {
-			const DW8 &n = hs.w8[i];
-			if (!(n.w[3] & 0xFFu) || hs.w8leaf[i] != RTX_NONE)
-				continue;
-			DW8S &f = w8s[i];
-			memcpy(f.w, n.w, 16);
-			f.org[0] = (float)(n.w[0] & 0xFFFFu);
-			f.org[1] = (float)(n.w[0] >> 16);
-			f.org[2] = (float)(n.w[1] & 0xFFFFu);
-			for (int k = 0; k < 6; k++)
-				for (int ch = 0; ch < 8; ch++) {
-					const _Float16 h = (_Float16)((n.w[4 + 2 * k + (ch >> 2)] >> (8 * (ch & 3))) & 0xFFu);
-					memcpy(&f.q[k][ch], &h, 2); /* 0..255: exact in half precision */
-				}
-		}
-		if ((rc = upload(c->d_w8s, w8s)))
+	const bool have_w8 = hs.w8_on_device || !hs.w8.empty();
+	const uint32_t num_w8 = hs.w8_on_device ? hs.w8_entries : (uint32_t)hs.w8.size();
+	uint32_t *d_map = nullptr; /* entry -> primitive index of the 8-wide tree's leaf entries */
+	if (hs.w8_on_device) { /* collapsed on this device: the buffers change hands */
+		dfree(c->d_w8);
+		dfree(c->d_w8s);
+		c->d_w8 = hs.dev_w8;
+		c->d_w8s = hs.dev_w8s;
+		d_map = hs.dev_w8leaf;
+	} else {
+		if ((rc = upload(c->d_w8, hs.w8)))
 			return rc;
-	}
-	if (!hs.w8.empty()) { /* the 8-wide tree's leaf entries: copies of their primitive records */
-		uint32_t *d_map = nullptr;
 		if ((rc = upload(d_map, hs.w8leaf)))
 			return rc;
-		hipError_t e = rtx_launch_w8_fill((const DPrim *)(c->d_nodes + hs.nnodes), c->d_mats, d_map, (uint32_t)hs.w8.size(),
-						  c->d_w8, c->stream);
+		dfree(c->d_w8s);
+		/* the scalar-path node copies (rtx_device.h DW8S) */
+		HIP_TRY(hipMalloc(&c->d_w8s, std::max<size_t>(num_w8, 1) * sizeof(DW8S)));
+		HIP_TRY(rtx_launch_w8_scalar(num_w8, c->d_w8, d_map, c->d_w8s, c->stream));
+	}
+	if (have_w8) { /* the 8-wide tree's leaf entries: copies of their primitive records */
+		hipError_t e = rtx_launch_w8_fill((const DPrim *)(c->d_nodes + hs.nnodes), c->d_mats, d_map, num_w8, c->d_w8, c->stream);
 		if (e == hipSuccess)
 			e = hipStreamSynchronize(c->stream);
 		dfree(d_map);
 		if (e != hipSuccess)
 			return fail(RTX_ERR_HIP, "8-wide BVH leaf fill failed: %s", hipGetErrorString(e));
 	}
+	dfree(d_map);
 	memcpy(c->bound_lo, hs.bound_lo, 12);
 	memcpy(c->bound_hi, hs.bound_hi, 12);
 	DScene &S = c->scene;
@@ -757,13 +805,13 @@ int rtx_upload_built(rtx_ctx *c, const HostScene &hs)
 	S.num_wnodes = (uint32_t)(hs.wnodes.size() / 4);
 	S.wtris = (const float *)c->d_wtris;
 	S.wdepth = hs.wdepth;
-	S.w8 = hs.w8.empty() ? nullptr : c->d_w8;
-	S.num_w8 = (uint32_t)hs.w8.size();
+	S.w8 = have_w8 ? c->d_w8 : nullptr;
+	S.num_w8 = num_w8;
 	S.w8depth = hs.w8depth;
 	memcpy(S.w8qo, hs.w8f.qo, 12);
 	memcpy(S.w8qs, hs.w8f.qs, 12);
 	S.w8noemit = hs.w8noemit ? 1u : 0u;
-	S.w8s = hs.w8.empty() ? nullptr : c->d_w8s;
+	S.w8s = have_w8 ? c->d_w8s : nullptr;
 	S.root_ref = hs.root_ref;
 	S.num_prims = hs.nb;
 	S.num_planes = (uint32_t)hs.planes.size();
@@ -781,9 +829,10 @@ int rtx_upload_built(rtx_ctx *c, const HostScene &hs)
 	c->stats.bvh_prims = hs.nb;
 	c->stats.shadow_walk = S.w8 ? RTX_WALK_W8 : S.wnodes ? RTX_WALK_W4 : RTX_WALK_BVH2;
 	if (S.w8) {
-		uint32_t inner_nodes = 0;
-		for (const DW8 &e : hs.w8)
-			inner_nodes += e.w[3] != 0;
+		uint32_t inner_nodes = hs.w8_wide;
+		if (!hs.w8_on_device)
+			for (const DW8 &e : hs.w8)
+				inner_nodes += e.w[3] != 0;
 		c->stats.wide_nodes = inner_nodes;
 		c->stats.wide_depth = S.w8depth;
 		c->stats.wide_entries = S.num_w8;
@@ -1123,7 +1172,7 @@ extern "C" int rtx_set_builder(rtx_ctx *c, int builder)
 {
 	if (!c)
 		return fail(RTX_ERR_ARG, "null argument");
-	if (builder != RTX_BUILD_SAH_HOST && builder != RTX_BUILD_LBVH_GPU)
+	if (builder != RTX_BUILD_SAH_HOST && builder != RTX_BUILD_LBVH_GPU && builder != RTX_BUILD_PLOC_GPU)
 		return fail(RTX_ERR_ARG, "unknown BVH builder %d", builder);
 	c->builder = builder;
 	return RTX_OK;

@@ -191,6 +191,36 @@ __device__ __forceinline__ uint32_t leaf_ref(uint32_t nnodes, uint32_t first, ui
 	return (nnodes + first) * (uint32_t)sizeof(DNode) | RTX_REF_LEAF | sph | (cnt - 1);
 }
 
+/* a BVH2 inner record from its children's boxes (lo xyz, hi xyz) and refs, with the per-octant
+ * child order of bvh_build.cpp (split axis = largest centroid separation) */
+__device__ DNode make_dnode(const float (&box)[2][6], const uint32_t (&ref)[2])
+{
+	DNode d;
+	float *f = &d.lo0x;
+	for (int c = 0; c < 2; c++)
+		for (int a = 0; a < 3; a++) {
+			f[6 * c + 2 * a] = box[c][a];
+			f[6 * c + 2 * a + 1] = box[c][3 + a];
+		}
+	d.ref0 = ref[0];
+	d.ref1 = ref[1];
+	int ax = 0;
+	float best = -1.f;
+	for (int a = 0; a < 3; a++) {
+		const float sep = fabsf((box[0][a] + box[0][3 + a]) - (box[1][a] + box[1][3 + a]));
+		if (sep > best) {
+			best = sep;
+			ax = a;
+		}
+	}
+	const bool lcg = (box[0][ax] + box[0][3 + ax]) > (box[1][ax] + box[1][3 + ax]);
+	d.order = 0;
+	for (uint32_t o = 0; o < 8; o++)
+		d.order |= ((((o >> ax) & 1u) != 0) != lcg) ? 1u << o : 0u;
+	d.pad = 0;
+	return d;
+}
+
 __global__ __launch_bounds__(256) void k_lb_emit(int n_int, int n, uint32_t nnodes, const uint32_t *__restrict__ keep,
 						  const uint32_t *__restrict__ idx, const uint32_t *__restrict__ child,
 						  const uint2 *__restrict__ range, const float *__restrict__ nbox,
@@ -218,31 +248,7 @@ __global__ __launch_bounds__(256) void k_lb_emit(int n_int, int n, uint32_t nnod
 						  : leaf_ref(nnodes, range[ch].x, range[ch].y - range[ch].x + 1, perm, prims_in);
 			}
 		}
-		DNode d;
-		float *f = &d.lo0x;
-		for (int c = 0; c < 2; c++)
-			for (int a = 0; a < 3; a++) {
-				f[6 * c + 2 * a] = box[c][a];
-				f[6 * c + 2 * a + 1] = box[c][3 + a];
-			}
-		d.ref0 = ref[0];
-		d.ref1 = ref[1];
-		/* child order per octant: split axis = largest centroid separation (bvh_build.cpp) */
-		int ax = 0;
-		float best = -1.f;
-		for (int a = 0; a < 3; a++) {
-			const float sep = fabsf((box[0][a] + box[0][3 + a]) - (box[1][a] + box[1][3 + a]));
-			if (sep > best) {
-				best = sep;
-				ax = a;
-			}
-		}
-		const bool lcg = (box[0][ax] + box[0][3 + ax]) > (box[1][ax] + box[1][3 + ax]);
-		d.order = 0;
-		for (uint32_t o = 0; o < 8; o++)
-			d.order |= ((((o >> ax) & 1u) != 0) != lcg) ? 1u << o : 0u;
-		d.pad = 0;
-		recs[idx[i]] = d;
+		recs[idx[i]] = make_dnode(box, ref);
 	}
 	if (i < n) /* primitives in leaf order after the nodes */
 		recs[nnodes + i] = *(const DNode *)&prims_in[perm[i]];
@@ -356,6 +362,356 @@ done:
 	(void)hipFree(nbox);
 	(void)hipFree(keep);
 	(void)hipFree(idx);
+	(void)hipFree(scal);
+	return e;
+}
+
+/* ------------------------------------------------------------------------ */
+/* PLOC: parallel locally-ordered clustering (Meister and Bittner 2018)      */
+/* ------------------------------------------------------------------------ */
+/* The clusters start as the primitives in Morton order.  Each round every cluster finds its
+ * nearest neighbour among the RTX_PLOC_R clusters either side (distance: surface area of the
+ * union box; ties to the lower pair index, so the order is total and the closest pair is always
+ * mutual), mutual pairs merge into a new inner node at the lower one's position and the list is
+ * compacted.  Tree node ids: 0..n-1 the primitives (sorted position), n.. the inner nodes in
+ * creation order.  The records are then laid out depth-first like the host builder's. */
+#ifndef RTX_PLOC_R
+#define RTX_PLOC_R 16 /* search radius (clusters either side) */
+#endif
+#define PLOC_T 256
+
+__device__ __forceinline__ float box_area6(const float *b)
+{
+	const float dx = b[3] - b[0], dy = b[4] - b[1], dz = b[5] - b[2];
+	return dx * dy + dy * dz + dz * dx;
+}
+
+/* leaf nodes: boxes in sorted order, counts; clusters = the leaves */
+__global__ __launch_bounds__(PLOC_T) void k_pl_init(uint32_t n, const uint32_t *__restrict__ perm, const float *__restrict__ lo,
+						    const float *__restrict__ hi, float *__restrict__ nb6, uint32_t *__restrict__ cnt,
+						    uint32_t *__restrict__ kcnt, uint32_t *__restrict__ cl, float *__restrict__ cb)
+{
+	const uint32_t q = blockIdx.x * PLOC_T + threadIdx.x;
+	if (q >= n)
+		return;
+	const uint32_t p = perm[q];
+	for (int a = 0; a < 3; a++) {
+		nb6[6 * q + a] = cb[6 * q + a] = lo[3 * p + a];
+		nb6[6 * q + 3 + a] = cb[6 * q + 3 + a] = hi[3 * p + a];
+	}
+	cnt[q] = 1;
+	kcnt[q] = 0;
+	cl[q] = q;
+}
+
+/* nearest neighbour of each cluster within the radius (boxes staged through LDS) */
+__global__ __launch_bounds__(PLOC_T) void k_pl_nn(uint32_t m, const float *__restrict__ cb, uint32_t *__restrict__ nn)
+{
+	__shared__ float sb[PLOC_T + 2 * RTX_PLOC_R][6];
+	const int b0 = (int)(blockIdx.x * PLOC_T) - RTX_PLOC_R;
+	for (int k = threadIdx.x; k < PLOC_T + 2 * RTX_PLOC_R; k += PLOC_T) {
+		const int j = b0 + k;
+		for (int a = 0; a < 6; a++)
+			sb[k][a] = (j >= 0 && j < (int)m) ? cb[6 * j + a] : 0.f;
+	}
+	__syncthreads();
+	const int i = (int)(blockIdx.x * PLOC_T + threadIdx.x);
+	if (i >= (int)m)
+		return;
+	const int li = i - b0;
+	float bd = FLT_MAX;
+	int bj = -1;
+	for (int o = -RTX_PLOC_R; o <= RTX_PLOC_R; o++) {
+		const int j = i + o;
+		if (o == 0 || j < 0 || j >= (int)m)
+			continue;
+		float u[6];
+		for (int a = 0; a < 3; a++) {
+			u[a] = fminf(sb[li][a], sb[li + o][a]);
+			u[3 + a] = fmaxf(sb[li][3 + a], sb[li + o][3 + a]);
+		}
+		const float d = box_area6(u);
+		/* pair order (d, lower index, higher index): for a fixed i the lower index decides ties
+		 * among j < i by j, and any j < i before any j > i */
+		if (d < bd || (d == bd && j < bj)) {
+			bd = d;
+			bj = j;
+		}
+	}
+	nn[i] = (uint32_t)bj;
+}
+
+/* merge / keep flags: merges count in the high word, surviving list entries in the low word */
+__global__ __launch_bounds__(PLOC_T) void k_pl_flags(uint32_t m, const uint32_t *__restrict__ nn, uint64_t *__restrict__ fl)
+{
+	const uint32_t i = blockIdx.x * PLOC_T + threadIdx.x;
+	if (i >= m)
+		return;
+	const uint32_t j = nn[i];
+	const bool mutual = j < m && nn[j] == i;
+	const bool merge = mutual && i < j, gone = mutual && i > j;
+	fl[i] = ((uint64_t)(merge ? 1u : 0u) << 32) | (gone ? 0u : 1u);
+}
+
+__global__ __launch_bounds__(PLOC_T) void k_pl_apply(uint32_t m, uint32_t n, uint32_t next_id, uint32_t max_leaf,
+						     const uint32_t *__restrict__ nn, const uint64_t *__restrict__ fl,
+						     const uint64_t *__restrict__ pre, const uint32_t *__restrict__ cl,
+						     const float *__restrict__ cb, uint32_t *__restrict__ cl2, float *__restrict__ cb2,
+						     float *__restrict__ nb6, uint2 *__restrict__ kids, uint32_t *__restrict__ par,
+						     uint32_t *__restrict__ cnt, uint32_t *__restrict__ kcnt)
+{
+	const uint32_t i = blockIdx.x * PLOC_T + threadIdx.x;
+	if (i >= m || !(fl[i] & 1u))
+		return;
+	const uint32_t pos = (uint32_t)pre[i];
+	if (!(fl[i] >> 32)) { /* unmerged: carried over */
+		cl2[pos] = cl[i];
+		for (int a = 0; a < 6; a++)
+			cb2[6 * pos + a] = cb[6 * i + a];
+		return;
+	}
+	const uint32_t j = nn[i], id = next_id + (uint32_t)(pre[i] >> 32);
+	const uint32_t a_ = cl[i], b_ = cl[j];
+	float u[6];
+	for (int a = 0; a < 3; a++) {
+		u[a] = fminf(cb[6 * i + a], cb[6 * j + a]);
+		u[3 + a] = fmaxf(cb[6 * i + 3 + a], cb[6 * j + 3 + a]);
+	}
+	for (int a = 0; a < 6; a++) {
+		nb6[6 * (size_t)id + a] = u[a];
+		cb2[6 * pos + a] = u[a];
+	}
+	cl2[pos] = id;
+	kids[id - n] = make_uint2(a_, b_);
+	par[a_] = id;
+	par[b_] = id;
+	const uint32_t c = cnt[a_] + cnt[b_];
+	cnt[id] = c;
+	kcnt[id] = (c > max_leaf ? 1u : 0u) + kcnt[a_] + kcnt[b_];
+}
+
+/* depth-first position of node v among the kept inner nodes (KEPT) or of its first primitive in
+ * leaf order (!KEPT): parent first, then the left subtree, then the right one */
+template <bool KEPT>
+__device__ __forceinline__ uint32_t pl_pos(uint32_t v, uint32_t root, const uint2 *__restrict__ kids,
+					   const uint32_t *__restrict__ par, const uint32_t *__restrict__ cnt,
+					   const uint32_t *__restrict__ kcnt, uint32_t n)
+{
+	uint32_t x = v, pos = 0;
+	for (int guard = 0; x != root && guard < (1 << 20); guard++) {
+		const uint32_t p = par[x];
+		const uint2 k = kids[p - n];
+		if (KEPT)
+			pos += 1;
+		if (x == k.y)
+			pos += KEPT ? kcnt[k.x] : cnt[k.x];
+		x = p;
+	}
+	return pos;
+}
+
+/* each primitive's position in leaf order (and the depth of kept nodes above it) */
+__global__ __launch_bounds__(PLOC_T) void k_pl_leafpos(uint32_t n, uint32_t root, uint32_t max_leaf,
+						       const uint32_t *__restrict__ perm, const uint2 *__restrict__ kids,
+						       const uint32_t *__restrict__ par, const uint32_t *__restrict__ cnt,
+						       const uint32_t *__restrict__ kcnt, uint32_t *__restrict__ posmap,
+						       unsigned *__restrict__ depth)
+{
+	const uint32_t q = blockIdx.x * PLOC_T + threadIdx.x;
+	if (q >= n)
+		return;
+	posmap[pl_pos<false>(q, root, kids, par, cnt, kcnt, n)] = perm[q];
+	unsigned dd = 0;
+	uint32_t x = q;
+	for (int guard = 0; x != root && guard < (1 << 20); guard++) {
+		x = par[x];
+		dd += (x == root || cnt[x] > max_leaf) ? 1u : 0u;
+	}
+	atomicMax(depth, dd);
+}
+
+__global__ __launch_bounds__(PLOC_T) void k_pl_emit(uint32_t n, uint32_t n_int, uint32_t root, uint32_t max_leaf, uint32_t nnodes,
+						    const uint2 *__restrict__ kids, const uint32_t *__restrict__ par,
+						    const uint32_t *__restrict__ cnt, const uint32_t *__restrict__ kcnt,
+						    const float *__restrict__ nb6, const uint32_t *__restrict__ posmap,
+						    const DPrim *__restrict__ prims_in, DNode *__restrict__ recs)
+{
+	const uint32_t i = blockIdx.x * PLOC_T + threadIdx.x;
+	if (i < n_int) {
+		const uint32_t v = n + i;
+		if (v == root || cnt[v] > max_leaf) {
+			const uint2 k = kids[i];
+			float box[2][6];
+			uint32_t ref[2];
+			for (int c = 0; c < 2; c++) {
+				const uint32_t ch = c ? k.y : k.x;
+				for (int a = 0; a < 6; a++)
+					box[c][a] = nb6[6 * (size_t)ch + a];
+				if (ch >= n && cnt[ch] > max_leaf) {
+					ref[c] = pl_pos<true>(ch, root, kids, par, cnt, kcnt, n) * (uint32_t)sizeof(DNode);
+				} else {
+					const uint32_t first = pl_pos<false>(ch, root, kids, par, cnt, kcnt, n), m = cnt[ch];
+					uint32_t sph = 0;
+					for (uint32_t q = first; q < first + m; q++)
+						if ((__float_as_uint(prims_in[posmap[q]].c[3]) >> 24) == RTX_SPHERE)
+							sph = RTX_REF_SPH;
+					ref[c] = (nnodes + first) * (uint32_t)sizeof(DNode) | RTX_REF_LEAF | sph | (m - 1);
+				}
+			}
+			recs[pl_pos<true>(v, root, kids, par, cnt, kcnt, n)] = make_dnode(box, ref);
+		}
+	}
+	if (i < n) /* primitives in leaf order after the nodes */
+		recs[nnodes + i] = *(const DNode *)&prims_in[posmap[i]];
+}
+
+/* The PLOC build: same contract as rtx_lbvh_build (records = inner nodes depth-first, then the
+ * primitives in leaf order; root record 0; n <= max_leaf leaves no inner node).  Each round
+ * reads back its list length (a few dozen rounds). */
+extern "C" hipError_t rtx_ploc_build(uint32_t n, const float *d_lo, const float *d_hi, const DPrim *d_prims_in,
+				     const float blo[3], const float bhi[3], uint32_t max_leaf, DNode **recs_out,
+				     uint32_t *nnodes_out, uint32_t *root_out, uint32_t *depth_out, uint32_t *rounds_out,
+				     hipStream_t st)
+{
+	hipError_t e = hipSuccess;
+	*recs_out = nullptr;
+	*nnodes_out = 0;
+	*depth_out = 0;
+	*rounds_out = 0;
+	void *temp = nullptr;
+	uint64_t *keys = nullptr, *fl = nullptr, *pre = nullptr, *tail = nullptr;
+	uint32_t *vals = nullptr, *cnt = nullptr, *kcnt = nullptr, *par = nullptr, *cl = nullptr, *cl2 = nullptr, *nn = nullptr,
+		 *posmap = nullptr;
+	float *nb6 = nullptr, *cb = nullptr, *cb2 = nullptr;
+	uint2 *kids = nullptr;
+	unsigned *scal = nullptr;
+	const size_t nt = 2 * (size_t)n; /* tree nodes (2n - 1) */
+#define TRY(x)                                  \
+	do {                                    \
+		if ((e = (x)) != hipSuccess)    \
+			goto done;              \
+	} while (0)
+	TRY(hipMalloc(&keys, 2 * (size_t)n * sizeof(uint64_t)));
+	TRY(hipMalloc(&vals, 2 * (size_t)n * sizeof(uint32_t)));
+	TRY(hipMalloc(&nb6, 6 * nt * sizeof(float)));
+	TRY(hipMalloc(&cnt, nt * sizeof(uint32_t)));
+	TRY(hipMalloc(&kcnt, nt * sizeof(uint32_t)));
+	TRY(hipMalloc(&par, nt * sizeof(uint32_t)));
+	TRY(hipMalloc(&kids, (size_t)n * sizeof(uint2)));
+	TRY(hipMalloc(&cl, (size_t)n * sizeof(uint32_t)));
+	TRY(hipMalloc(&cl2, (size_t)n * sizeof(uint32_t)));
+	TRY(hipMalloc(&cb, 6 * (size_t)n * sizeof(float)));
+	TRY(hipMalloc(&cb2, 6 * (size_t)n * sizeof(float)));
+	TRY(hipMalloc(&nn, (size_t)n * sizeof(uint32_t)));
+	TRY(hipMalloc(&fl, (size_t)n * sizeof(uint64_t)));
+	TRY(hipMalloc(&pre, (size_t)n * sizeof(uint64_t)));
+	TRY(hipMalloc(&posmap, (size_t)n * sizeof(uint32_t)));
+	TRY(hipHostMalloc(&tail, 2 * sizeof(uint64_t)));
+	TRY(hipMalloc(&scal, 4 * sizeof(unsigned)));
+	{
+		float s[3];
+		for (int a = 0; a < 3; a++) {
+			const float ext = bhi[a] - blo[a];
+			s[a] = ext > 0.f ? 2097151.f / ext : 0.f;
+		}
+		const dim3 gn((n + PLOC_T - 1) / PLOC_T);
+		hipLaunchKernelGGL(k_lb_morton, gn, dim3(256), 0, st, n, d_lo, d_hi, blo[0], blo[1], blo[2], s[0], s[1], s[2],
+				   keys, vals);
+		TRY(hipGetLastError());
+		hipcub::DoubleBuffer<uint64_t> kb(keys, keys + n);
+		hipcub::DoubleBuffer<uint32_t> vb(vals, vals + n);
+		size_t tb = 0, tb2 = 0;
+		TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kb, vb, (int)n, 0, 63, st));
+		TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, fl, pre, (int)n, st));
+		TRY(hipMalloc(&temp, tb > tb2 ? tb : tb2));
+		TRY(hipcub::DeviceRadixSort::SortPairs(temp, tb, kb, vb, (int)n, 0, 63, st));
+		const uint32_t *perm = vb.Current();
+		uint32_t nnodes = 0, root = 0, depth = 0;
+		hipLaunchKernelGGL(k_pl_init, gn, dim3(PLOC_T), 0, st, n, perm, d_lo, d_hi, nb6, cnt, kcnt, cl, cb);
+		TRY(hipGetLastError());
+		uint32_t m = n, next_id = n, rounds = 0;
+		while (m > 1) {
+			if (++rounds > 4096) { /* a round always merges the closest pair: cannot happen */
+				e = hipErrorUnknown;
+				goto done;
+			}
+			const dim3 gm((m + PLOC_T - 1) / PLOC_T);
+			hipLaunchKernelGGL(k_pl_nn, gm, dim3(PLOC_T), 0, st, m, cb, nn);
+			hipLaunchKernelGGL(k_pl_flags, gm, dim3(PLOC_T), 0, st, m, nn, fl);
+			TRY(hipGetLastError());
+			TRY(hipcub::DeviceScan::ExclusiveSum(temp, tb2, fl, pre, (int)m, st));
+			hipLaunchKernelGGL(k_pl_apply, gm, dim3(PLOC_T), 0, st, m, n, next_id, max_leaf, nn, fl, pre, cl, cb, cl2, cb2,
+					   nb6, kids, par, cnt, kcnt);
+			TRY(hipGetLastError());
+			TRY(hipMemcpyAsync(&tail[0], pre + (m - 1), 8, hipMemcpyDeviceToHost, st));
+			TRY(hipMemcpyAsync(&tail[1], fl + (m - 1), 8, hipMemcpyDeviceToHost, st));
+			TRY(hipStreamSynchronize(st));
+			const uint64_t tot = tail[0] + tail[1];
+			if (!(tot >> 32)) {
+				e = hipErrorUnknown;
+				goto done;
+			}
+			next_id += (uint32_t)(tot >> 32);
+			m = (uint32_t)tot;
+			uint32_t *tc = cl;
+			cl = cl2;
+			cl2 = tc;
+			float *tf = cb;
+			cb = cb2;
+			cb2 = tf;
+		}
+		*rounds_out = rounds;
+		if (n > max_leaf) {
+			root = next_id - 1; /* the last merge */
+			TRY(hipMemcpyAsync(&nnodes, kcnt + root, 4, hipMemcpyDeviceToHost, st));
+			TRY(hipStreamSynchronize(st));
+		} else {
+			nnodes = 0;
+		}
+		TRY(hipMemsetAsync(scal, 0, 4 * sizeof(unsigned), st));
+		if (n > 1) {
+			hipLaunchKernelGGL(k_pl_leafpos, gn, dim3(PLOC_T), 0, st, n, next_id - 1, max_leaf, perm, kids, par, cnt, kcnt,
+					   posmap, scal);
+		} else {
+			TRY(hipMemcpyAsync(posmap, perm, 4, hipMemcpyDeviceToDevice, st));
+		}
+		TRY(hipGetLastError());
+		DNode *recs = nullptr;
+		TRY(hipMalloc(&recs, ((size_t)nnodes + n) * sizeof(DNode)));
+		hipLaunchKernelGGL(k_pl_emit, gn, dim3(PLOC_T), 0, st, n, n > max_leaf ? n - 1 : 0u, next_id - 1, max_leaf, nnodes, kids, par, cnt, kcnt, nb6, posmap, d_prims_in, recs);
+		e = hipGetLastError();
+		if (e == hipSuccess)
+			e = hipMemcpyAsync(&depth, scal, 4, hipMemcpyDeviceToHost, st);
+		if (e == hipSuccess)
+			e = hipStreamSynchronize(st);
+		if (e != hipSuccess) {
+			(void)hipFree(recs);
+			goto done;
+		}
+		*recs_out = recs;
+		*nnodes_out = nnodes;
+		*root_out = n > max_leaf ? 0u : RTX_EMPTY_REF;
+		*depth_out = n > max_leaf ? depth : 0u;
+	}
+done:
+#undef TRY
+	(void)hipFree(temp);
+	(void)hipFree(keys);
+	(void)hipFree(vals);
+	(void)hipFree(nb6);
+	(void)hipFree(cnt);
+	(void)hipFree(kcnt);
+	(void)hipFree(par);
+	(void)hipFree(kids);
+	(void)hipFree(cl);
+	(void)hipFree(cl2);
+	(void)hipFree(cb);
+	(void)hipFree(cb2);
+	(void)hipFree(nn);
+	(void)hipFree(fl);
+	(void)hipFree(pre);
+	(void)hipFree(posmap);
+	(void)hipHostFree(tail);
 	(void)hipFree(scal);
 	return e;
 }

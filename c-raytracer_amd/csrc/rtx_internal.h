@@ -123,6 +123,12 @@ struct HostScene {
 	uint32_t w8depth = 0;
 	QFrame w8f{};                 /* its 16-bit frame */
 	bool w8noemit = false;        /* emitters left out of it */
+	/* collapsed on the device (rtx_wide8_dev.hip): the buffers, handed to the context on upload */
+	bool w8_on_device = false;
+	DW8 *dev_w8 = nullptr;
+	DW8S *dev_w8s = nullptr;
+	uint32_t *dev_w8leaf = nullptr;
+	uint32_t w8_entries = 0, w8_wide = 0;
 	std::vector<DPlane> planes;
 	std::vector<DMaterial> mats;
 	std::vector<DEmitter> emit;

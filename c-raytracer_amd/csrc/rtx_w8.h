@@ -141,19 +141,29 @@ __device__ __forceinline__ uint32_t w8_hits(const uint32_t (&w)[16], f3 s, f3 b,
 		hm &= w[3]; /* K = 0: slot order; the min/max form would turn an empty slot's box around */
 	return hm;
 }
+#ifndef RTX_W8_SKIP
+#define RTX_W8_SKIP 0 /* scalar path: branch over the empty slots (the slot mask is wave-uniform) */
+#endif
+template <int OCT, uint32_t K, int C>
+__device__ __forceinline__ uint32_t w8_hit_s(const uint32_t (&q)[24], uint32_t w3, f3 s, f3 b, float tl)
+{
+	if (RTX_W8_SKIP && !((w3 >> C) & 1u))
+		return 0u;
+	return w8_child_s<OCT, C>(q, s, b, tl) ? 1u << (C ^ K) : 0u;
+}
 template <int OCT, uint32_t K>
 __device__ __forceinline__ uint32_t w8_hits_s(const uint32_t (&q)[24], uint32_t w3, f3 s, f3 b, float tl)
 {
 	uint32_t hm = 0;
-	hm |= w8_child_s<OCT, 0>(q, s, b, tl) ? 1u << (0 ^ K) : 0u;
-	hm |= w8_child_s<OCT, 1>(q, s, b, tl) ? 1u << (1 ^ K) : 0u;
-	hm |= w8_child_s<OCT, 2>(q, s, b, tl) ? 1u << (2 ^ K) : 0u;
-	hm |= w8_child_s<OCT, 3>(q, s, b, tl) ? 1u << (3 ^ K) : 0u;
-	hm |= w8_child_s<OCT, 4>(q, s, b, tl) ? 1u << (4 ^ K) : 0u;
-	hm |= w8_child_s<OCT, 5>(q, s, b, tl) ? 1u << (5 ^ K) : 0u;
-	hm |= w8_child_s<OCT, 6>(q, s, b, tl) ? 1u << (6 ^ K) : 0u;
-	hm |= w8_child_s<OCT, 7>(q, s, b, tl) ? 1u << (7 ^ K) : 0u;
-	if (OCT == 8)
+	hm |= w8_hit_s<OCT, K, 0>(q, w3, s, b, tl);
+	hm |= w8_hit_s<OCT, K, 1>(q, w3, s, b, tl);
+	hm |= w8_hit_s<OCT, K, 2>(q, w3, s, b, tl);
+	hm |= w8_hit_s<OCT, K, 3>(q, w3, s, b, tl);
+	hm |= w8_hit_s<OCT, K, 4>(q, w3, s, b, tl);
+	hm |= w8_hit_s<OCT, K, 5>(q, w3, s, b, tl);
+	hm |= w8_hit_s<OCT, K, 6>(q, w3, s, b, tl);
+	hm |= w8_hit_s<OCT, K, 7>(q, w3, s, b, tl);
+	if (OCT == 8 && !RTX_W8_SKIP)
 		hm &= w3;
 	return hm;
 }

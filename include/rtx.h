@@ -224,7 +224,8 @@ typedef struct rtx_ctx rtx_ctx;
 /* BVH builders for rtx_upload_scene (replacing accel_init, accel.c:266-315) */
 enum {
 	RTX_BUILD_SAH_HOST = 0, /* binned SAH on the host (default: fewest node visits) */
-	RTX_BUILD_LBVH_GPU = 1  /* Morton-code linear BVH built on the device (rtx_build.hip) */
+	RTX_BUILD_LBVH_GPU = 1, /* Morton-code linear BVH built on the device (rtx_build.hip) */
+	RTX_BUILD_PLOC_GPU = 2  /* locally-ordered clustering (PLOC) on the device (rtx_build.hip) */
 };
 
 int rtx_device_count(int *count);

@@ -1,4 +1,5 @@
-"""GPU BVH builder (csrc/rtx_build.hip via rtx_set_builder(RTX_BUILD_LBVH_GPU)).
+"""GPU BVH builders (csrc/rtx_build.hip via rtx_set_builder(RTX_BUILD_LBVH_GPU /
+RTX_BUILD_PLOC_GPU)).
 
 Closest-hit answers do not depend on the tree (up to exact ties), so frames rendered over the
 GPU-built LBVH must match the reference goldens exactly as well as frames over the host SAH
@@ -31,13 +32,19 @@ def render(r, builder, scene, frame, params):
     return rgb, z, r.stats()
 
 
+GPU_BUILDERS = [abi.RTX_BUILD_LBVH_GPU, abi.RTX_BUILD_PLOC_GPU]
+
+
+@pytest.mark.parametrize("builder", GPU_BUILDERS, ids=["lbvh", "ploc"])
 @pytest.mark.parametrize("name", CONFIGS)
-def test_gpu_lbvh_frames_match(renderer, name):
+def test_gpu_builder_frames_match(renderer, name, builder):
     scene, frame, params, m = C.load_config(name)
     a, za, sa = render(renderer, abi.RTX_BUILD_SAH_HOST, scene, frame, params)
-    b, zb, sb = render(renderer, abi.RTX_BUILD_LBVH_GPU, scene, frame, params)
-    assert sb.builder == abi.RTX_BUILD_LBVH_GPU and sa.builder == abi.RTX_BUILD_SAH_HOST
+    b, zb, sb = render(renderer, builder, scene, frame, params)
+    assert sb.builder == builder and sa.builder == abi.RTX_BUILD_SAH_HOST
     assert sb.bvh_depth <= 63 and sb.build_ms > 0
+    # the 8-wide shadow tree collapsed on the device from the device-built records
+    assert sb.shadow_walk == abi.RTX_WALK_W8 and sb.wide_depth >= 1 and sb.wide_nodes >= 1
     assert np.array_equal(za, zb), name  # closest hits do not depend on the tree
     assert (sa.closest_rays, sa.shadow_rays) == (sb.closest_rays, sb.shadow_rays)
     ref_rgb, ref_z = C.golden_frame(name + "_o2")
@@ -46,17 +53,18 @@ def test_gpu_lbvh_frames_match(renderer, name):
     assert np.abs(a - b).max() <= 1e-5 * max(1.0, float(np.abs(a).max())), name
 
 
-def test_gpu_lbvh_deterministic_and_tiny_scenes(renderer):
+@pytest.mark.parametrize("builder", GPU_BUILDERS, ids=["lbvh", "ploc"])
+def test_gpu_builder_deterministic_and_tiny_scenes(renderer, builder):
     scene, frame, params, _ = C.load_config("s5_path2")
-    a, za, st = render(renderer, abi.RTX_BUILD_LBVH_GPU, scene, frame, params)
-    b, zb, _ = render(renderer, abi.RTX_BUILD_LBVH_GPU, scene, frame, params)
+    a, za, st = render(renderer, builder, scene, frame, params)
+    b, zb, _ = render(renderer, builder, scene, frame, params)
     assert np.array_equal(a, b) and np.array_equal(za, zb)
     assert st.bvh_nodes == st.bvh_prims - 1  # single-primitive leaves (the default): a full binary tree
     # scene1: 3 spheres + a light -> with leaves of up to 4 primitives, a single-leaf root
     renderer.set_option(abi.RTX_OPT_BVH_LEAF, 4)
     scene, frame, params, _ = C.load_config("s1_amb")
     try:
-        a, za, st = render(renderer, abi.RTX_BUILD_LBVH_GPU, scene, frame, params)
+        a, za, st = render(renderer, builder, scene, frame, params)
     finally:
         renderer.set_option(abi.RTX_OPT_BVH_LEAF, 1)
     assert st.bvh_nodes == 0
@@ -65,4 +73,21 @@ def test_gpu_lbvh_deterministic_and_tiny_scenes(renderer):
     assert ok, info
     with pytest.raises(rtxpy.RtxError):
         renderer.set_builder(7)
+    renderer.set_builder(abi.RTX_BUILD_SAH_HOST)
+
+
+@pytest.mark.parametrize("leaf", [2, 4])
+def test_gpu_ploc_multi_primitive_leaves(renderer, leaf):
+    """Leaves of up to `leaf` primitives: each subtree of at most that many primitives becomes one
+    leaf of a contiguous range (depth-first leaf order); the frame stays exact."""
+    scene, frame, params, _ = C.load_config("s3_path2")
+    renderer.set_option(abi.RTX_OPT_BVH_LEAF, leaf)
+    try:
+        b, zb, sb = render(renderer, abi.RTX_BUILD_PLOC_GPU, scene, frame, params)
+    finally:
+        renderer.set_option(abi.RTX_OPT_BVH_LEAF, 1)
+    assert sb.bvh_nodes < sb.bvh_prims - 1
+    ref_rgb, ref_z = C.golden_frame("s3_path2_o2")
+    ok, info = C.compare_const(b, zb, ref_rgb, ref_z)
+    assert ok, info
     renderer.set_builder(abi.RTX_BUILD_SAH_HOST)

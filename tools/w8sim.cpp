@@ -8,6 +8,7 @@
  * are stratified like RTX_RNG_STRAT.
  *   build: tools/w8sim.sh       run: tools/w8sim <scene.json> [base_dir] [points]
  */
+#include <chrono>
 #include <float.h>
 #include <math.h>
 #include <stdio.h>
@@ -173,7 +174,9 @@ int main(int argc, char **argv)
 	}
 	BvhConfig cfg;
 	BvhOutput bvh;
+	const auto t0 = std::chrono::steady_clock::now();
 	bvh_build(BvhInput{ nb, lo.data(), hi.data() }, cfg, bvh);
+	const auto t1 = std::chrono::steady_clock::now();
 	const uint32_t nnodes = (uint32_t)bvh.nodes.size();
 	std::vector<DPrim> prims(nb);
 	for (uint32_t k = 0; k < nb; k++) {
@@ -223,6 +226,9 @@ int main(int argc, char **argv)
 	bool skipped = false;
 	const uint32_t depth = rtx_wide8_build(inner, nnodes, prims.data(), dref(bvh.root_ref), blo, bhi, emit_objs, F, skipped,
 					       w8, leafmap);
+	const auto t2 = std::chrono::steady_clock::now();
+	printf("host SAH build %.1f ms, 8-wide collapse %.1f ms\n", std::chrono::duration<double, std::milli>(t1 - t0).count(),
+	       std::chrono::duration<double, std::milli>(t2 - t1).count());
 	uint32_t nodes = 0, kids = 0, inner_kids = 0;
 	std::vector<uint32_t> hist(9, 0);
 	for (const DW8 &e : w8)
