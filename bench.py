@@ -313,19 +313,23 @@ def shadow_roofline(r, frame, params, d_rgb, d_z, stream, shadow_ms, a, world):
     except (OSError, ValueError):
         rec = None
     if rec:
+        # the PMC passes average over k_shadow launches; a frame of several chunks launches it once
+        # per chunk, and the counts here (and dur) are the frame's
+        nl = max(1, int(c.chunks))
         out["pmc"] = {"source": rec.get("source"), "kernel_src_sha": rec.get("kernel_src_sha"),
-                      "matches_this_kernel": rec.get("kernel_src_sha") == shadow_src_sha()}
+                      "matches_this_kernel": rec.get("kernel_src_sha") == shadow_src_sha(), "launches_per_frame": nl}
         if "hbm_bytes_per_launch" in rec:
-            out["traffic"] = int(rec["hbm_bytes_per_launch"])
-            out["hbm"] = {"bytes_per_launch": int(rec["hbm_bytes_per_launch"]),
-                          "achieved": round(rec["hbm_bytes_per_launch"] / dur / 1e9, 1), "peak": HBM_PEAK_GBS,
-                          "unit": "GB/s", "frac": round(rec["hbm_bytes_per_launch"] / dur / 1e9 / HBM_PEAK_GBS, 4),
+            hbm = nl * rec["hbm_bytes_per_launch"]
+            out["traffic"] = int(hbm)
+            out["hbm"] = {"bytes_per_launch": int(hbm),
+                          "achieved": round(hbm / dur / 1e9, 1), "peak": HBM_PEAK_GBS,
+                          "unit": "GB/s", "frac": round(hbm / dur / 1e9 / HBM_PEAK_GBS, 4),
                           "source": "PMC 2*FETCH_SIZE + WRITE_SIZE (L2 -> fabric, gfx950 correction)"}
         if "sq_insts_valu" in rec:
-            issued = rec["sq_insts_valu"] / dur / 1e9
+            issued = nl * rec["sq_insts_valu"] / dur / 1e9
             out["issued"] = round(issued, 1)
             out["issued_frac"] = round(issued / VALU_PEAK_GINST, 4)
-            out["useful_over_issued"] = round(useful / rec["sq_insts_valu"], 4)
+            out["useful_over_issued"] = round(useful / (nl * rec["sq_insts_valu"]), 4)
         if "ta_busy_frac" in rec:
             out["vmem"] = {"ta_busy_frac": rec["ta_busy_frac"], "td_busy_frac": rec.get("td_busy_frac"),
                            "note": "PMC TA_TA_BUSY / TD_TD_BUSY per CU cycle: the vector-memory address / data "

@@ -29,9 +29,12 @@ struct BvhOutput {
 	uint32_t leaves = 0;
 };
 
+#ifndef RTX_BVH_BINS
+#define RTX_BVH_BINS 32
+#endif
 struct BvhConfig {
 	uint32_t max_leaf = 1; /* single-primitive leaves: fewest shadow-walk steps on the bench frame (1078 vs 1239 ms at 4) */
-	uint32_t bins = 32;
+	uint32_t bins = RTX_BVH_BINS;
 	uint32_t max_depth = 48;
 	float c_trav = 1.0f;
 	float c_isect = 1.0f;

@@ -711,7 +711,8 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 		std::vector<uint32_t> emit_objs;
 		for (const DEmitter &e : emit)
 			emit_objs.push_back(e.obj);
-		hs.w8depth = rtx_wide8_build(inner, nnodes, hp, nb ? root_ref : RTX_EMPTY_REF, c->bound_lo, c->bound_hi, emit_objs,
+		/* the walks need every leaf slot marked from its record: no records, no 8-wide tree */
+		hs.w8depth = rtx_wide8_build(inner, nnodes, hp, hp ? root_ref : RTX_EMPTY_REF, c->bound_lo, c->bound_hi, emit_objs,
 					     hs.w8f, hs.w8noemit, hs.w8, hs.w8leaf);
 	} else if (c->opt_walk == RTX_WALK_W4) {
 		hs.wdepth = wide_bvh(inner, nb ? root_ref : RTX_EMPTY_REF, c->bound_lo, c->bound_hi, hs.qf, hs.wnodes);

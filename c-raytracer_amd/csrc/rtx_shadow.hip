@@ -480,6 +480,26 @@ __device__ __forceinline__ bool w8_opaque_test(const char *pr, f3 o, f3 d, float
 	return any_tri(mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z), mk3(c.x, c.y, c.z), o, d, a.w, tl);
 }
 
+#ifndef RTX_W8_SLEAF
+#define RTX_W8_SLEAF 0 /* uniform steps: opaque leaf tests slot by slot, the entry through scalar loads */
+#endif
+/* the same test on a wave-uniform entry, read with one s_load_dwordx16 (SGPR operands) */
+template <bool COUNT>
+__device__ __forceinline__ bool w8_opaque_test_s(const DW8 *e, f3 o, f3 d, float tl, uint32_t &ntri, uint32_t &nsph)
+{
+	typedef float f16v __attribute__((ext_vector_type(16)));
+	const f16v v = *(const __attribute__((address_space(4))) f16v *)e;
+	if ((__float_as_uint(v[11]) >> 24) == RTX_SPHERE) {
+		if (COUNT)
+			nsph++;
+		float t = 0.f;
+		return hit_sphere(mk3(v[0], v[1], v[2]), v[4], o, d, v[3], t) && t < tl;
+	}
+	if (COUNT)
+		ntri++;
+	return any_tri(mk3(v[0], v[1], v[2]), mk3(v[4], v[5], v[6]), mk3(v[8], v[9], v[10]), o, d, v[3], tl);
+}
+
 template <bool COUNT, int OCT>
 __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__restrict__ mats, f3 o, f3 d, f3 inv,
 					     float &tl, uint32_t emit_obj, f3 &li, ShadowCount &sc)
@@ -510,6 +530,7 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 			continue;
 		}
 		uint32_t lm = 0, base = 0; /* this step's opaque leaf hits (visit order) and their block */
+		bool ustep = false;         /* every walking lane at one node (base wave-uniform) */
 		if (node != RTX_NONE) {
 			W8Visit v;
 			const uint32_t un = uni(node);
@@ -517,6 +538,7 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 				/* every walking lane is at one node: its scalar-path copy through the scalar cache,
 				 * the planes as SGPR float operands */
 				v = w8_visit_s<OCT, K>(Q.w8s + (size_t)un, invq, oi, tl);
+				ustep = true;
 			} else {
 				uint32_t w[16];
 				const DW8 *N = Q.w8 + (size_t)node;
@@ -579,9 +601,34 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 		if (!ballot(lm != 0))
 			continue;
 		bool blocked = false;
-		if (Q.known) {
-			/* (dealing the wave's tests over its lanes with ds_permute, one round for all, measured
-			 * slower on scene6: 2834 vs 2806 ms, every dealt job tested without the early break) */
+		if (RTX_W8_SLEAF && ballot(ustep)) {
+			/* marked tree, uniform step: the wave's hit slots in visit order, each slot's entry read
+			 * once through the scalar cache and tested by the lanes that hit it (no vector-memory
+			 * traffic; a blocked lane drops out) */
+			const uint32_t ub = readlane(base, (uint32_t)__ffsll((long long)ballot(ustep)) - 1); /* a walking lane's */
+			uint32_t om = 0;
+#pragma unroll
+			for (int q = 0; q < 8; q++)
+				om |= ballot((lm >> q) & 1u) ? 1u << q : 0u;
+			while (om) {
+				const uint32_t p = __builtin_ctz(om);
+				om &= om - 1;
+				if (COUNT)
+					nlr++;
+				if ((lm >> p) & 1u) {
+					if (w8_opaque_test_s<COUNT>(Q.w8 + ub + (p ^ K), o, d, tl, ntri, nsph)) {
+						blocked = true;
+						lm = 0;
+					}
+				}
+				if (!ballot((lm & om) != 0))
+					break;
+			}
+		} else {
+			/* the tree marks every leaf slot (built from the primitive records, emitters left out):
+			 * these are opaque, each lane tests its own.  (Dealing the wave's tests over its lanes
+			 * with ds_permute, one round for all, measured slower on scene6: 2834 vs 2806 ms, every
+			 * dealt job tested without the early break) */
 			if (COUNT) {
 				uint32_t r = 0;
 				for (uint32_t m = lm;; m &= m - 1) {
@@ -591,29 +638,10 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 				}
 				nlr += r;
 			}
-			while (lm) { /* marked tree: opaque leaves, each lane its own */
+			while (lm) {
 				const uint32_t p = __builtin_ctz(lm);
 				lm &= lm - 1;
 				if (w8_opaque_test<COUNT>((const char *)(Q.w8 + base + (p ^ K)), o, d, tl, ntri, nsph)) {
-					blocked = true;
-					break;
-				}
-			}
-		} else {
-			if (COUNT) {
-				uint32_t r = 0;
-				for (uint32_t m = lm;; m &= m - 1) {
-					if (!ballot(m != 0))
-						break;
-					r++;
-				}
-				nlr += r;
-			}
-			while (lm) { /* unmarked leaves (a tree built without host records): the full test */
-				const uint32_t p = __builtin_ctz(lm);
-				lm &= lm - 1;
-				const char *pr = (const char *)(Q.w8 + base + (p ^ K));
-				if (shadow_prim<COUNT>(ldg4(pr, 0), ldg4(pr, 16), ldg4(pr, 32), mats, o, d, tl, emit_obj, li, ntri, nsph)) {
 					blocked = true;
 					break;
 				}
