@@ -563,6 +563,9 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 
 	const auto tb0 = std::chrono::steady_clock::now();
 	uint32_t nnodes = 0, root_ref = RTX_EMPTY_REF, depth = 0;
+	/* RTX_WALK_AUTO: a scene whose threaded BVH2 fits the LDS top records is walked from LDS alone
+	 * (scene3, 3 spheres: 102 ms vs 114 ms over the 8-wide tree); larger ones over the 8-wide tree */
+	const bool small = (uint64_t)2 * nb <= RTX_TOP_MAX + 1;
 	std::vector<DNode> inner; /* host copy of the inner-node records, for the threaded BVH */
 	std::vector<DPrim> prims_dl; /* device builders: the primitive records read back */
 	const DPrim *host_prims = nullptr; /* the primitive records in leaf order on the host */
@@ -607,7 +610,7 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 		if (nnodes)
 			HIP_TRY(hipMemcpy(inner.data(), recs, nnodes * sizeof(DNode), hipMemcpyDeviceToHost));
 		/* the 8-wide tree collapsed where the records are (single-primitive leaves, one device) */
-		if (!hs.want_host_recs && cfg.max_leaf == 1 && nnodes && (c->opt_walk == RTX_WALK_AUTO || c->opt_walk == RTX_WALK_W8)) {
+		if (!hs.want_host_recs && cfg.max_leaf == 1 && nnodes && (c->opt_walk == RTX_WALK_W8 || (c->opt_walk == RTX_WALK_AUTO && !small))) {
 			std::vector<uint32_t> skip((sc->num_objects + 31) / 32 + 1, 0u);
 			for (uint32_t i = 0; i < sc->num_emitters; i++)
 				skip[sc->emitters[i] >> 5] |= 1u << (sc->emitters[i] & 31u);
@@ -705,7 +708,7 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 	 * measurement, and the BVH2 when the 8-wide tree cannot be built (over 2^24 entries) */
 	if (hs.w8_on_device) {
 		/* collapsed on the device above */
-	} else if (c->opt_walk == RTX_WALK_AUTO || c->opt_walk == RTX_WALK_W8) {
+	} else if (c->opt_walk == RTX_WALK_W8 || (c->opt_walk == RTX_WALK_AUTO && !small)) {
 		/* with the host records the emitters are left out of the tree (k_shadow tests them linearly) */
 		const DPrim *hp = nb ? host_prims : nullptr;
 		std::vector<uint32_t> emit_objs;

@@ -25,8 +25,17 @@ def renderer():
     r.close()
 
 
+@pytest.fixture(autouse=True)
+def _defaults(renderer):
+    yield
+    renderer.set_builder(abi.RTX_BUILD_SAH_HOST)
+    renderer.set_option(abi.RTX_OPT_SHADOW_WALK, abi.RTX_WALK_AUTO)
+    renderer.set_option(abi.RTX_OPT_BVH_LEAF, 1)
+
+
 def render(r, builder, scene, frame, params):
     r.set_builder(builder)
+    r.set_option(abi.RTX_OPT_SHADOW_WALK, abi.RTX_WALK_W8)  # the 8-wide tree on small scenes too
     r.upload(scene)
     rgb, z = r.render(frame, params)
     return rgb, z, r.stats()
@@ -90,4 +99,3 @@ def test_gpu_ploc_multi_primitive_leaves(renderer, leaf):
     ref_rgb, ref_z = C.golden_frame("s3_path2_o2")
     ok, info = C.compare_const(b, zb, ref_rgb, ref_z)
     assert ok, info
-    renderer.set_builder(abi.RTX_BUILD_SAH_HOST)

@@ -45,13 +45,19 @@ def render(r, scene, frame, params, walk=abi.RTX_WALK_AUTO):
     return rgb, z, r.stats()
 
 
+SMALL = {"s1_amb", "s3_path2", "st_amb", "st2_r2"}  # threaded BVH2 within the LDS top (<= 1024 primitives)
+
+
 @pytest.mark.parametrize("name", CONFIGS)
 def test_gpu_walks_agree(renderer, name):
     scene, frame, params, _ = C.load_config(name)
-    a, za, sa = render(renderer, scene, frame, params)
+    a, za, sa = render(renderer, scene, frame, params, abi.RTX_WALK_W8)
     assert sa.shadow_walk == abi.RTX_WALK_W8 and sa.wide_nodes > 0 and sa.wide_depth >= 1
     assert sa.wide_entries >= 8 * sa.wide_nodes
     ref_rgb, ref_z = C.golden_frame(name + "_o2")
+    # RTX_WALK_AUTO: the LDS-resident threaded BVH2 for small scenes, the 8-wide tree otherwise
+    _, _, sd = render(renderer, scene, frame, params)
+    assert sd.shadow_walk == (abi.RTX_WALK_BVH2 if name in SMALL else abi.RTX_WALK_W8), name
     for walk in (abi.RTX_WALK_W4, abi.RTX_WALK_BVH2):
         b, zb, sb = render(renderer, scene, frame, params, walk)
         assert sb.shadow_walk == walk

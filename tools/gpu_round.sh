@@ -32,6 +32,7 @@ for s in $STEPS; do
     s6w4) run s6_walkw4 900 python3 bench.py --scene scene6 --width 3840 --height 2160 --spp 128 --walk w4 --steps 1 --warmup 1 --no-cpu-baseline --no-post --verbose ;;
     s6var) for v in ${VARS:-$(ls c-raytracer_amd/lib/var)}; do RTX_LIBRTX=$PWD/c-raytracer_amd/lib/var/$v/librtx.so run s6var_$v 900 python3 bench.py --scene scene6 --width 3840 --height 2160 --spp 128 --steps 1 --warmup 1 --no-cpu-baseline --no-post --verbose; done ;;
     s6slot) for sl in ${SLOTS:-64 16}; do run s6slot_$sl 900 python3 bench.py --scene scene6 --width 3840 --height 2160 --spp 128 --shadow-slot $sl --steps 1 --warmup 1 --no-cpu-baseline --no-post --no-count --verbose; done ;;
+    s3) run s3 600 python3 bench.py --scene scene3 --width 1920 --height 1080 --spp 16 --steps 3 --warmup 1 --no-cpu-baseline --no-post --verbose ;;
     l8) run l8 900 python3 bench.py --scene scene5_l8 --steps 1 --warmup 1 --no-cpu-baseline --no-post --verbose ;;
     s6) for w in ${TWALKS:-w8}; do run s6_$w 900 python3 bench.py --scene scene6 --width 3840 --height 2160 --spp 128 --trace-walk $w --steps 1 --warmup 1 --no-cpu-baseline --no-post --verbose; done ;;
     occsweep) for o in ${OCCS:-1 6 7 8}; do RTX_SHADOW_OCC=$o run occ$o 600 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-count --no-post; done ;;
