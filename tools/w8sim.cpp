@@ -128,6 +128,10 @@ static bool closest(const Scene2 &S, const double o[3], const double d[3], doubl
 struct Stats {
 	double rays = 0, visits = 0, boxes = 0, tris = 0, wave_steps = 0, leaf_rounds = 0, packets = 0, blocked = 0;
 	double emit = 0;
+	/* divergent wave steps (walking lanes at more than one node): distinct 64-B node entries and
+	 * 128-B lines per step, and the line touches of the four per-lane loads vs a transposed fetch
+	 * (load k = the 16-B quarters of lanes 16k..16k+15's nodes, four lanes per node) */
+	double dsteps = 0, dnodes = 0, dlines = 0, touch_lane = 0, touch_tr = 0, walkers = 0;
 	double post_nodes[8] = {}, post_leaves[8] = {}; /* postponed leaf tests, threshold T = 8 * k lanes */
 };
 
@@ -319,7 +323,7 @@ int main(int argc, char **argv)
 		/* packets of 64 light samples */
 		for (uint32_t b0 = 0; b0 < nl; b0 += 64) {
 			std::vector<uint32_t> visits_lane, leaf_at; /* per-lane per-visit leaf hits */
-			std::vector<std::vector<uint32_t>> leaves(64);
+			std::vector<std::vector<uint32_t>> leaves(64), seq(64);
 			uint32_t block_at[64]; /* ordinal (in discovery order) of the lane's blocking leaf test, or ~0 */
 			uint32_t maxv = 0, imm_len[64] = {};
 			for (uint32_t l = 0; l < 64 && b0 + l < nl; l++) {
@@ -364,8 +368,10 @@ int main(int argc, char **argv)
 				bool blocked = false;
 				uint32_t nv_imm = 0; /* visits of the immediate-test walk (ends at the blocker's visit) */
 				while (node != RTX_NONE) {
-					if (!blocked)
+					if (!blocked) {
 						nv_imm++;
+						seq[l].push_back(node);
+					}
 					const DW8 &N = w8[node];
 					nv++;
 					S.boxes += __builtin_popcount(N.w[3] & 0xFFu);
@@ -497,6 +503,43 @@ int main(int argc, char **argv)
 			}
 			S.wave_steps += maxv;
 			for (uint32_t i = 0; i < maxv; i++) {
+				std::vector<uint32_t> at(64, ~0u);
+				uint32_t first = ~0u;
+				bool div = false;
+				for (int l = 0; l < 64; l++)
+					if (i < seq[l].size()) {
+						at[l] = seq[l][i];
+						if (first == ~0u)
+							first = at[l];
+						div |= at[l] != first;
+					}
+				if (!div)
+					continue;
+				S.dsteps++;
+				std::vector<uint32_t> nodes, lines;
+				for (int l = 0; l < 64; l++)
+					if (at[l] != ~0u) {
+						S.walkers++;
+						nodes.push_back(at[l]);
+						lines.push_back(at[l] >> 1);
+					}
+				auto uniq = [](std::vector<uint32_t> v) {
+					std::sort(v.begin(), v.end());
+					return (double)(std::unique(v.begin(), v.end()) - v.begin());
+				};
+				S.dnodes += uniq(nodes);
+				const double dl = uniq(lines);
+				S.dlines += dl;
+				S.touch_lane += 4 * dl;
+				for (int k = 0; k < 4; k++) {
+					std::vector<uint32_t> g;
+					for (int l = 16 * k; l < 16 * k + 16; l++)
+						if (at[l] != ~0u)
+							g.push_back(at[l] >> 1);
+					S.touch_tr += uniq(g);
+				}
+			}
+			for (uint32_t i = 0; i < maxv; i++) {
 				uint32_t m = 0;
 				for (int l = 0; l < 64; l++)
 					if (i < imm_len[l])
@@ -512,6 +555,10 @@ int main(int argc, char **argv)
 	printf("emitter leaf hits/ray %.3f\npostponed leaf tests (no emitter leaves), per packet: T  node steps  leaf rounds  "
 	       "cost(290/step + 99/round)\n",
 	       S.emit / S.rays);
+	printf("divergent steps/packet %.2f  walking lanes %.1f  distinct nodes %.2f  lines %.2f  line touches per step: "
+	       "per-lane loads %.1f  transposed %.1f\n",
+	       S.dsteps / S.packets, S.walkers / S.dsteps, S.dnodes / S.dsteps, S.dlines / S.dsteps, S.touch_lane / S.dsteps,
+	       S.touch_tr / S.dsteps);
 	for (int k = 0; k < 8; k++)
 		printf("  %2d  %6.2f  %6.2f  %7.0f\n", k ? 8 * k : 1, S.post_nodes[k] / S.packets, S.post_leaves[k] / S.packets,
 		       (290 * S.post_nodes[k] + 99 * S.post_leaves[k]) / S.packets);
