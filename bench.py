@@ -298,6 +298,11 @@ def shadow_roofline(r, frame, params, d_rgb, d_z, stream, shadow_ms, a, world):
            "plane_tests": int(c.shadow_plane_tests), "wave_steps": int(c.shadow_wave_steps),
            "wave_walks": int(c.shadow_wave_walks), "leaf_rounds": int(c.shadow_leaf_rounds),
            "uniform_steps": int(c.shadow_uniform_steps),
+           "k_trace": {"closest_rays": int(c.closest_rays),
+                       "node_visits": int(c.node_visits - c.shadow_node_visits),
+                       "prim_tests": int(c.tri_tests + c.sphere_tests - c.shadow_tri_tests - c.shadow_sphere_tests),
+                       "note": "closest-hit walk counts of the same counting render (8-wide node visits, "
+                               "primitive tests)"},
            "wide_nodes": int(c.wide_nodes), "wide_depth": int(c.wide_depth),
            "records": {"bytes_per_launch": int(algo_bytes), "lds_bytes_per_launch": 16 * lds_box,
                        "GBs": round(algo_bytes / dur / 1e9, 1),
@@ -547,24 +552,29 @@ def main():
 
     build = None
     if rank == 0 and world == 1 and not a.no_post:
-        # §8(f) #2: both BVH builders on the benchmark scene (build time, then one frame each)
+        # §8(f) #2: every BVH builder on the benchmark scene (build time, then one frame each)
         try:
-            build = {"sah_host_ms": round(st.build_ms, 1), "sah_nodes": int(st.bvh_nodes), "sah_depth": int(st.bvh_depth),
-                     "sah_wide_nodes": int(st.wide_nodes), "sah_wide_depth": int(st.wide_depth),
-                     "sah_shadow_walk": ["bvh2", "w4", "w8"][st.shadow_walk]}
-            for tag, bid in (("lbvh", abi.RTX_BUILD_LBVH_GPU), ("ploc", abi.RTX_BUILD_PLOC_GPU)):
+            names = {abi.RTX_BUILD_SAH_HOST: "sah_host", abi.RTX_BUILD_LBVH_GPU: "lbvh", abi.RTX_BUILD_PLOC_GPU: "ploc",
+                     abi.RTX_BUILD_SAH_GPU: "sah_gpu"}
+            d = names[int(st.builder)]
+            build = {"default": d, f"{d}_ms": round(st.build_ms, 1), f"{d}_nodes": int(st.bvh_nodes),
+                     f"{d}_depth": int(st.bvh_depth), f"{d}_wide_nodes": int(st.wide_nodes),
+                     f"{d}_wide_depth": int(st.wide_depth), f"{d}_shadow_walk": ["bvh2", "w4", "w8"][st.shadow_walk],
+                     f"{d}_shadow_ms": round(float(np.mean(sms)), 1)}
+            for bid, tag in names.items():
+                if bid == int(st.builder):
+                    continue
                 r.set_builder(bid)
                 r.upload(scene)
                 sl = r.stats()
-                build.update({f"{tag}_gpu_ms": round(sl.build_ms, 1), f"{tag}_nodes": int(sl.bvh_nodes),
+                build.update({f"{tag}_ms": round(sl.build_ms, 1), f"{tag}_nodes": int(sl.bvh_nodes),
                               f"{tag}_depth": int(sl.bvh_depth), f"{tag}_wide_nodes": int(sl.wide_nodes),
                               f"{tag}_wide_depth": int(sl.wide_depth),
                               f"{tag}_shadow_walk": ["bvh2", "w4", "w8"][sl.shadow_walk]})
                 r.render_device(frame, params, d_rgb.data_ptr(), d_z.data_ptr(), stream.cuda_stream)
                 build[f"{tag}_shadow_ms"] = round(r.stats().shadow_ms, 1)
                 build[f"{tag}_trace_ms"] = round(r.stats().trace_ms, 1)
-            build["sah_shadow_ms"] = round(float(np.mean(sms)), 1)
-            r.set_builder(abi.RTX_BUILD_SAH_HOST)
+            r.set_builder(int(st.builder))
             r.upload(scene)
             r.render_device(frame, params, d_rgb.data_ptr(), d_z.data_ptr(), stream.cuda_stream)
             log(f"builders: {build}")

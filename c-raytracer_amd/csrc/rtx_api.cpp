@@ -40,6 +40,10 @@ extern "C" hipError_t rtx_ploc_build(uint32_t n, const float *d_lo, const float 
 				     const float blo[3], const float bhi[3], uint32_t max_leaf, DNode **recs_out,
 				     uint32_t *nnodes_out, uint32_t *root_out, uint32_t *depth_out, uint32_t *rounds_out,
 				     hipStream_t st);
+extern "C" hipError_t rtx_sah_build(uint32_t n, const float *d_lo, const float *d_hi, const DPrim *d_prims_in,
+				    uint32_t max_leaf, uint32_t bins, uint32_t max_depth, float c_trav, float c_isect,
+				    DNode **recs_out, uint32_t *nnodes_out, uint32_t *root_out, uint32_t *depth_out,
+				    uint32_t *levels_out, hipStream_t st);
 extern "C" hipError_t rtx_w8_collapse_device(const DNode *recs, uint32_t nnodes, uint32_t nb, const uint32_t *skip_obj,
 					     uint32_t num_objects, DW8 **w8_out, DW8S **w8s_out, uint32_t **leafmap_out,
 					     uint32_t *entries_out, uint32_t *depth_out, uint32_t *wide_out, float qo[3],
@@ -570,7 +574,7 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 	std::vector<DPrim> prims_dl; /* device builders: the primitive records read back */
 	const DPrim *host_prims = nullptr; /* the primitive records in leaf order on the host */
 	int rc;
-	if ((c->builder == RTX_BUILD_LBVH_GPU || c->builder == RTX_BUILD_PLOC_GPU) && nb) {
+	if ((c->builder == RTX_BUILD_LBVH_GPU || c->builder == RTX_BUILD_PLOC_GPU || c->builder == RTX_BUILD_SAH_GPU) && nb) {
 		/* GPU builders (rtx_build.hip): primitives uploaded in input order, records emitted on the device */
 		std::vector<DPrim> prims_in(nb);
 		uint32_t sph = 0;
@@ -592,6 +596,9 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 		hipError_t e = c->builder == RTX_BUILD_PLOC_GPU
 				       ? rtx_ploc_build(nb, d_lo, d_hi, d_in, c->bound_lo, c->bound_hi, cfg.max_leaf, &recs, &nnodes,
 							&root_ref, &depth, &rounds, c->stream)
+			       : c->builder == RTX_BUILD_SAH_GPU
+				       ? rtx_sah_build(nb, d_lo, d_hi, d_in, cfg.max_leaf, cfg.bins, cfg.max_depth, cfg.c_trav, cfg.c_isect,
+						       &recs, &nnodes, &root_ref, &depth, &rounds, c->stream)
 				       : rtx_lbvh_build(nb, d_lo, d_hi, d_in, c->bound_lo, c->bound_hi, cfg.max_leaf, &recs, &nnodes,
 							&root_ref, &depth, c->stream);
 		dfree(d_lo);
@@ -1176,7 +1183,8 @@ extern "C" int rtx_set_builder(rtx_ctx *c, int builder)
 {
 	if (!c)
 		return fail(RTX_ERR_ARG, "null argument");
-	if (builder != RTX_BUILD_SAH_HOST && builder != RTX_BUILD_LBVH_GPU && builder != RTX_BUILD_PLOC_GPU)
+	if (builder != RTX_BUILD_SAH_HOST && builder != RTX_BUILD_LBVH_GPU && builder != RTX_BUILD_PLOC_GPU &&
+	    builder != RTX_BUILD_SAH_GPU)
 		return fail(RTX_ERR_ARG, "unknown BVH builder %d", builder);
 	c->builder = builder;
 	return RTX_OK;

@@ -715,3 +715,514 @@ done:
 	(void)hipFree(scal);
 	return e;
 }
+
+/* ------------------------------------------------------------------------ */
+/* Binned SAH on the device: bvh_build.cpp's algorithm, level by level       */
+/* ------------------------------------------------------------------------ */
+/* Every level holds the active nodes (two or more primitives), each a contiguous range of the
+ * position array.  Per level: node boxes and centroid bounds (atomic min / max on order-preserving
+ * integer encodings of the floats, exact), the SAH bins of every axis (same bin rule, same float
+ * arithmetic, so the same costs), one thread per node sweeping the bins in the host's order (axis
+ * 0..2, split 0..NB-2, strict <), then a stable partition of each range by an exclusive scan of the
+ * left flags.  Nodes the host would split at the centroid median (depth budget) or by index (all
+ * centroids equal) split at the middle of the range.  For single-primitive leaves (the default)
+ * the tree is the host builder's node for node: its records are byte-identical
+ * (tests/test_gpu_build.py).  The tree then goes through the PLOC builder's depth-first emission
+ * (ids 0..n-1 the final positions, n.. the inner nodes). */
+#define SB_T 256
+#define SB_NBMAX 64
+/* the host's float arithmetic exactly: no contraction into FMAs (this file is built without
+ * -ffp-contract=off) */
+#pragma clang fp contract(off)
+#define SB_ACC(NB) (12 + 3 * (NB) * 7) /* per node: box + centroid bounds, then per axis and bin 6 bounds + count */
+
+__device__ __forceinline__ uint32_t f2o(float f) /* order-preserving encoding */
+{
+	const uint32_t b = __float_as_uint(f);
+	return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float o2f(uint32_t o) { return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o); }
+
+/* the host's Box::area */
+__device__ __forceinline__ float sb_area(const float *lo, const float *hi)
+{
+	const float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+	if (dx < 0 || dy < 0 || dz < 0)
+		return 0.f;
+	return 2.f * (dx * dy + dy * dz + dz * dx);
+}
+
+struct SbNode {
+	uint32_t b, e, id, depth;
+};
+
+/* accumulators of M nodes: mins at +FLT_MAX, maxes at -FLT_MAX, counts 0 */
+__global__ __launch_bounds__(SB_T) void k_sb_reset(uint32_t M, uint32_t nb, uint32_t *__restrict__ acc)
+{
+	const uint32_t stride = SB_ACC(nb);
+	const size_t i = (size_t)blockIdx.x * SB_T + threadIdx.x;
+	if (i >= (size_t)M * stride)
+		return;
+	const uint32_t k = (uint32_t)(i % stride);
+	uint32_t v;
+	if (k < 12)
+		v = (k % 6) < 3 ? f2o(FLT_MAX) : f2o(-FLT_MAX);
+	else {
+		const uint32_t j = (k - 12) % 7;
+		v = j == 6 ? 0u : j < 3 ? f2o(FLT_MAX) : f2o(-FLT_MAX);
+	}
+	acc[i] = v;
+}
+
+/* node boxes and centroid bounds.  A wave whose positions all lie in one node reduces first. */
+__global__ __launch_bounds__(SB_T) void k_sb_bounds(uint32_t n, uint32_t nb, const uint32_t *__restrict__ seg,
+						     const uint32_t *__restrict__ pidx, const float *__restrict__ lo,
+						     const float *__restrict__ hi, uint32_t *__restrict__ acc)
+{
+	const uint32_t q = blockIdx.x * SB_T + threadIdx.x;
+	const uint32_t s = q < n ? seg[q] : RTX_NONE;
+	float v[12];
+	if (s != RTX_NONE) {
+		const uint32_t p = pidx[q];
+		for (int a = 0; a < 3; a++) {
+			v[a] = lo[3 * (size_t)p + a];
+			v[3 + a] = hi[3 * (size_t)p + a];
+			v[6 + a] = v[9 + a] = 0.5f * (v[a] + v[3 + a]);
+		}
+	} else {
+		for (int a = 0; a < 3; a++) {
+			v[a] = v[6 + a] = FLT_MAX;
+			v[3 + a] = v[9 + a] = -FLT_MAX;
+		}
+	}
+	const uint32_t s0 = __shfl(s, 0);
+	if (__all(s == s0)) {
+		if (s0 == RTX_NONE)
+			return;
+		for (int k = 0; k < 12; k++)
+			for (int m = 32; m > 0; m >>= 1) {
+				const float o = __shfl_xor(v[k], m);
+				v[k] = ((k % 6) < 3) ? fminf(v[k], o) : fmaxf(v[k], o);
+			}
+		if ((threadIdx.x & 63u) == 0) {
+			uint32_t *A = acc + (size_t)s0 * SB_ACC(nb);
+			for (int k = 0; k < 12; k++)
+				((k % 6) < 3) ? atomicMin(&A[k], f2o(v[k])) : atomicMax(&A[k], f2o(v[k]));
+		}
+		return;
+	}
+	if (s == RTX_NONE)
+		return;
+	uint32_t *A = acc + (size_t)s * SB_ACC(nb);
+	for (int k = 0; k < 12; k++)
+		((k % 6) < 3) ? atomicMin(&A[k], f2o(v[k])) : atomicMax(&A[k], f2o(v[k]));
+}
+
+/* the host's bin of a centroid coordinate */
+__device__ __forceinline__ int sb_bin(float c, float clo, float k, int nb)
+{
+	int bi = (int)((c - clo) * k);
+	return min(max(bi, 0), nb - 1);
+}
+
+__global__ __launch_bounds__(SB_T) void k_sb_bins(uint32_t n, uint32_t nb, const uint32_t *__restrict__ seg,
+						   const uint32_t *__restrict__ pidx, const float *__restrict__ lo,
+						   const float *__restrict__ hi, uint32_t *__restrict__ acc)
+{
+	const uint32_t q = blockIdx.x * SB_T + threadIdx.x;
+	if (q >= n)
+		return;
+	const uint32_t s = seg[q];
+	if (s == RTX_NONE)
+		return;
+	uint32_t *A = acc + (size_t)s * SB_ACC(nb);
+	const uint32_t p = pidx[q];
+	float b[6];
+	for (int a = 0; a < 3; a++) {
+		b[a] = lo[3 * (size_t)p + a];
+		b[3 + a] = hi[3 * (size_t)p + a];
+	}
+	for (int ax = 0; ax < 3; ax++) {
+		const float clo = o2f(A[6 + ax]), chi = o2f(A[9 + ax]), ext = chi - clo;
+		if (!(ext > 0.f))
+			continue;
+		const float k = (float)nb * (1.f - 1e-6f) / ext;
+		const int bi = sb_bin(0.5f * (b[ax] + b[3 + ax]), clo, k, (int)nb);
+		uint32_t *B = A + 12 + ((size_t)ax * nb + bi) * 7;
+		for (int a = 0; a < 3; a++) {
+			atomicMin(&B[a], f2o(b[a]));
+			atomicMax(&B[3 + a], f2o(b[3 + a]));
+		}
+		atomicAdd(&B[6], 1u);
+	}
+}
+
+/* the split of each node (bvh_build.cpp Builder::build): mode 0 = SAH (axis, bin), 1 = middle
+ * of the range; nleft; the node's box into the tree; children that stay active */
+__global__ __launch_bounds__(SB_T) void k_sb_split(uint32_t M, uint32_t nb, uint32_t max_leaf, uint32_t max_depth,
+						    float c_trav, float c_isect, const SbNode *__restrict__ act,
+						    const uint32_t *__restrict__ acc, uint4 *__restrict__ dec,
+						    uint32_t *__restrict__ nact, float *__restrict__ nb6, uint32_t *__restrict__ cnt)
+{
+	const uint32_t i = blockIdx.x * SB_T + threadIdx.x;
+	if (i >= M)
+		return;
+	const SbNode nd = act[i];
+	const uint32_t n = nd.e - nd.b;
+	const uint32_t *A = acc + (size_t)i * SB_ACC(nb);
+	float blo[3], bhi[3], clo[3], chi[3];
+	for (int a = 0; a < 3; a++) {
+		blo[a] = o2f(A[a]);
+		bhi[a] = o2f(A[3 + a]);
+		clo[a] = o2f(A[6 + a]);
+		chi[a] = o2f(A[9 + a]);
+		nb6[6 * (size_t)nd.id + a] = blo[a];
+		nb6[6 * (size_t)nd.id + 3 + a] = bhi[a];
+	}
+	cnt[nd.id] = n;
+	int need = 0;
+	while ((1u << need) < (n + max_leaf - 1) / max_leaf)
+		need++;
+	const bool force_median = (int)nd.depth + need + 1 >= (int)max_depth;
+	int best_axis = -1;
+	uint32_t best_split = 0, best_left = 0;
+	float best_cost = FLT_MAX;
+	if (!force_median) {
+		for (int ax = 0; ax < 3; ax++) {
+			const float ext = chi[ax] - clo[ax];
+			if (!(ext > 0.f))
+				continue;
+			const uint32_t *B = A + 12 + (size_t)ax * nb * 7;
+			float ra[SB_NBMAX];
+			uint32_t rc[SB_NBMAX];
+			float alo[3] = { FLT_MAX, FLT_MAX, FLT_MAX }, ahi[3] = { -FLT_MAX, -FLT_MAX, -FLT_MAX };
+			uint32_t c = 0;
+			for (int k = (int)nb - 1; k > 0; k--) {
+				for (int a = 0; a < 3; a++) {
+					alo[a] = fminf(alo[a], o2f(B[7 * k + a]));
+					ahi[a] = fmaxf(ahi[a], o2f(B[7 * k + 3 + a]));
+				}
+				c += B[7 * k + 6];
+				ra[k] = sb_area(alo, ahi);
+				rc[k] = c;
+			}
+			for (int a = 0; a < 3; a++) {
+				alo[a] = FLT_MAX;
+				ahi[a] = -FLT_MAX;
+			}
+			c = 0;
+			for (uint32_t k = 0; k + 1 < nb; k++) {
+				for (int a = 0; a < 3; a++) {
+					alo[a] = fminf(alo[a], o2f(B[7 * k + a]));
+					ahi[a] = fmaxf(ahi[a], o2f(B[7 * k + 3 + a]));
+				}
+				c += B[7 * k + 6];
+				if (!c || !rc[k + 1])
+					continue;
+				const float cost = sb_area(alo, ahi) * c + ra[k + 1] * rc[k + 1];
+				if (cost < best_cost) {
+					best_cost = cost;
+					best_axis = ax;
+					best_split = k;
+					best_left = c;
+				}
+			}
+		}
+	}
+	const float parea = sb_area(blo, bhi);
+	const float split_cost = best_axis >= 0 && parea > 0 ? c_trav + c_isect * best_cost / parea : FLT_MAX;
+	const float leaf_cost = c_isect * n;
+	uint32_t mode, nleft;
+	if (best_axis >= 0 && !force_median && !(n <= max_leaf && leaf_cost <= split_cost)) {
+		mode = 0;
+		nleft = best_left;
+	} else { /* depth budget, equal centroids, or a leaf the emission collapses: the middle */
+		mode = 1;
+		nleft = n / 2;
+	}
+	dec[i] = make_uint4(mode | ((uint32_t)(best_axis < 0 ? 0 : best_axis) << 1), best_split, nleft, 0u);
+	nact[i] = (nleft >= 2 ? 1u : 0u) + (n - nleft >= 2 ? 1u : 0u);
+}
+
+/* left flags of the positions (stable partition by scan) */
+__global__ __launch_bounds__(SB_T) void k_sb_flags(uint32_t n, uint32_t nb, const uint32_t *__restrict__ seg,
+						    const uint32_t *__restrict__ pidx, const float *__restrict__ lo,
+						    const float *__restrict__ hi, const SbNode *__restrict__ act,
+						    const uint4 *__restrict__ dec, const uint32_t *__restrict__ acc,
+						    uint32_t *__restrict__ flag)
+{
+	const uint32_t q = blockIdx.x * SB_T + threadIdx.x;
+	if (q >= n)
+		return;
+	const uint32_t s = seg[q];
+	uint32_t f = 0;
+	if (s != RTX_NONE) {
+		const uint4 d = dec[s];
+		if (d.x & 1u) {
+			f = q - act[s].b < d.z ? 1u : 0u;
+		} else {
+			const uint32_t ax = d.x >> 1, p = pidx[q];
+			const uint32_t *A = acc + (size_t)s * SB_ACC(nb);
+			const float clo = o2f(A[6 + ax]), ext = o2f(A[9 + ax]) - clo;
+			const float k = (float)nb * (1.f - 1e-6f) / ext;
+			const float c = 0.5f * (lo[3 * (size_t)p + ax] + hi[3 * (size_t)p + ax]);
+			f = (uint32_t)sb_bin(c, clo, k, (int)nb) <= d.y ? 1u : 0u;
+		}
+	}
+	flag[q] = f;
+}
+
+/* children: tree ids (a one-primitive child is its position), parents, next level's nodes */
+__global__ __launch_bounds__(SB_T) void k_sb_children(uint32_t M, uint32_t n, uint32_t id_base, const SbNode *__restrict__ act,
+						       const uint4 *__restrict__ dec, const uint32_t *__restrict__ off,
+						       SbNode *__restrict__ next, uint2 *__restrict__ kids, uint32_t *__restrict__ par)
+{
+	const uint32_t i = blockIdx.x * SB_T + threadIdx.x;
+	if (i >= M)
+		return;
+	const SbNode nd = act[i];
+	const uint32_t nl = dec[i].z;
+	uint32_t o = off[i], ch[2];
+	const uint32_t b[2] = { nd.b, nd.b + nl }, e[2] = { nd.b + nl, nd.e };
+	for (int c = 0; c < 2; c++) {
+		if (e[c] - b[c] >= 2) {
+			ch[c] = id_base + o;
+			SbNode x;
+			x.b = b[c];
+			x.e = e[c];
+			x.id = ch[c];
+			x.depth = nd.depth + 1;
+			next[o++] = x;
+		} else {
+			ch[c] = b[c];
+		}
+		par[ch[c]] = nd.id;
+	}
+	kids[nd.id - n] = make_uint2(ch[0], ch[1]);
+}
+
+/* stable partition; each position's node in the next level (RTX_NONE: a leaf) */
+__global__ __launch_bounds__(SB_T) void k_sb_scatter(uint32_t n, const uint32_t *__restrict__ seg, const uint32_t *__restrict__ pidx,
+						      const SbNode *__restrict__ act, const uint4 *__restrict__ dec,
+						      const uint32_t *__restrict__ flag, const uint32_t *__restrict__ scan,
+						      const uint32_t *__restrict__ off, uint32_t *__restrict__ pidx2,
+						      uint32_t *__restrict__ seg2)
+{
+	const uint32_t q = blockIdx.x * SB_T + threadIdx.x;
+	if (q >= n)
+		return;
+	const uint32_t s = seg[q];
+	if (s == RTX_NONE) {
+		pidx2[q] = pidx[q];
+		seg2[q] = RTX_NONE;
+		return;
+	}
+	const SbNode nd = act[s];
+	const uint32_t nl = dec[s].z, lrank = scan[q] - scan[nd.b];
+	const bool left = flag[q] != 0;
+	const uint32_t pos = left ? nd.b + lrank : nd.b + nl + (q - nd.b - lrank);
+	pidx2[pos] = pidx[q];
+	const uint32_t o = off[s];
+	uint32_t ns = RTX_NONE;
+	if (left) {
+		if (nl >= 2)
+			ns = o;
+	} else if (nd.e - nd.b - nl >= 2) {
+		ns = o + (nl >= 2 ? 1u : 0u);
+	}
+	seg2[pos] = ns;
+}
+
+/* leaves (positions): their boxes, counts */
+__global__ __launch_bounds__(SB_T) void k_sb_leaves(uint32_t n, const uint32_t *__restrict__ pidx, const float *__restrict__ lo,
+						     const float *__restrict__ hi, float *__restrict__ nb6, uint32_t *__restrict__ cnt,
+						     uint32_t *__restrict__ kcnt)
+{
+	const uint32_t q = blockIdx.x * SB_T + threadIdx.x;
+	if (q >= n)
+		return;
+	const uint32_t p = pidx[q];
+	for (int a = 0; a < 3; a++) {
+		nb6[6 * (size_t)q + a] = lo[3 * (size_t)p + a];
+		nb6[6 * (size_t)q + 3 + a] = hi[3 * (size_t)p + a];
+	}
+	cnt[q] = 1;
+	kcnt[q] = 0;
+}
+
+/* kept inner nodes per subtree, one level at a time from the deepest */
+__global__ __launch_bounds__(SB_T) void k_sb_kcnt(uint32_t M, uint32_t n, uint32_t max_leaf, uint32_t root,
+						   const SbNode *__restrict__ lev, const uint2 *__restrict__ kids,
+						   const uint32_t *__restrict__ cnt, uint32_t *__restrict__ kcnt)
+{
+	const uint32_t i = blockIdx.x * SB_T + threadIdx.x;
+	if (i >= M)
+		return;
+	const uint32_t v = lev[i].id;
+	const uint2 k = kids[v - n];
+	kcnt[v] = ((v == root || cnt[v] > max_leaf) ? 1u : 0u) + kcnt[k.x] + kcnt[k.y];
+}
+
+extern "C" hipError_t rtx_sah_build(uint32_t n, const float *d_lo, const float *d_hi, const DPrim *d_prims_in,
+				    uint32_t max_leaf, uint32_t bins, uint32_t max_depth, float c_trav, float c_isect,
+				    DNode **recs_out, uint32_t *nnodes_out, uint32_t *root_out, uint32_t *depth_out,
+				    uint32_t *levels_out, hipStream_t st)
+{
+	hipError_t e = hipSuccess;
+	*recs_out = nullptr;
+	*nnodes_out = 0;
+	*depth_out = 0;
+	*levels_out = 0;
+	if (bins < 2 || bins > SB_NBMAX)
+		return hipErrorInvalidValue;
+	void *temp = nullptr;
+	uint32_t *pidx = nullptr, *pidx2 = nullptr, *seg = nullptr, *seg2 = nullptr, *flag = nullptr, *scan = nullptr,
+		 *acc = nullptr, *nact = nullptr, *off = nullptr, *cnt = nullptr, *kcnt = nullptr, *par = nullptr, *posmap = nullptr;
+	SbNode *lev = nullptr; /* every level's nodes, one after the other (the inner nodes, n - 1 of them) */
+	uint4 *dec = nullptr;
+	uint2 *kids = nullptr;
+	float *nb6 = nullptr;
+	unsigned *scal = nullptr;
+	uint32_t *tail = nullptr;
+	const size_t nt = 2 * (size_t)n;
+	const uint32_t nb = bins;
+	std::vector<uint32_t> lev_off;
+	/* accumulators for at most this many nodes at a time */
+	const uint32_t chunk = 1u << 15;
+#define TRY(x)                                  \
+	do {                                    \
+		if ((e = (x)) != hipSuccess)    \
+			goto done;              \
+	} while (0)
+	TRY(hipMalloc(&pidx, (size_t)n * 4));
+	TRY(hipMalloc(&pidx2, (size_t)n * 4));
+	TRY(hipMalloc(&seg, (size_t)n * 4));
+	TRY(hipMalloc(&seg2, (size_t)n * 4));
+	TRY(hipMalloc(&flag, (size_t)n * 4));
+	TRY(hipMalloc(&scan, ((size_t)n + 1) * 4));
+	TRY(hipMalloc(&acc, (size_t)chunk * SB_ACC(nb) * 4));
+	TRY(hipMalloc(&nact, (size_t)n * 4));
+	TRY(hipMalloc(&off, ((size_t)n + 1) * 4));
+	TRY(hipMalloc(&dec, (size_t)n * sizeof(uint4)));
+	TRY(hipMalloc(&lev, (size_t)n * sizeof(SbNode)));
+	TRY(hipMalloc(&kids, (size_t)n * sizeof(uint2)));
+	TRY(hipMalloc(&par, nt * 4));
+	TRY(hipMalloc(&cnt, nt * 4));
+	TRY(hipMalloc(&kcnt, nt * 4));
+	TRY(hipMalloc(&nb6, 6 * nt * sizeof(float)));
+	TRY(hipMalloc(&posmap, (size_t)n * 4));
+	TRY(hipMalloc(&scal, 4 * sizeof(unsigned)));
+	TRY(hipHostMalloc(&tail, 4 * sizeof(uint32_t)));
+	{
+		const dim3 gn((n + SB_T - 1) / SB_T);
+		size_t tb = 0, tb2 = 0;
+		TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, flag, scan, (int)n + 1, st));
+		TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, nact, off, (int)n + 1, st));
+		TRY(hipMalloc(&temp, tb > tb2 ? tb : tb2));
+		/* positions = input order; one active node (the root, id n) over all of them */
+		{
+			std::vector<uint32_t> io(n);
+			for (uint32_t k = 0; k < n; k++)
+				io[k] = k;
+			TRY(hipMemcpyAsync(pidx, io.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
+			TRY(hipMemsetAsync(seg, 0, (size_t)n * 4, st));
+			SbNode r{ 0u, n, n, 1u };
+			TRY(hipMemcpyAsync(lev, &r, sizeof(r), hipMemcpyHostToDevice, st));
+			TRY(hipStreamSynchronize(st));
+		}
+		uint32_t nnodes = 0, root = RTX_EMPTY_REF, depth = 0;
+		if (n > max_leaf && n >= 2) {
+			uint32_t M = 1, base = 0, id_next = n + 1;
+			lev_off.push_back(0);
+			while (M) {
+				if (M > chunk || lev_off.size() > 4096) { /* a level wider than the accumulators: not expected at n < 2^31 */
+					e = hipErrorInvalidValue;
+					goto done;
+				}
+				SbNode *act = lev + base;
+				const size_t na = (size_t)M * SB_ACC(nb);
+				hipLaunchKernelGGL(k_sb_reset, dim3((uint32_t)((na + SB_T - 1) / SB_T)), dim3(SB_T), 0, st, M, nb, acc);
+				hipLaunchKernelGGL(k_sb_bounds, gn, dim3(SB_T), 0, st, n, nb, seg, pidx, d_lo, d_hi, acc);
+				hipLaunchKernelGGL(k_sb_bins, gn, dim3(SB_T), 0, st, n, nb, seg, pidx, d_lo, d_hi, acc);
+				const dim3 gm((M + SB_T - 1) / SB_T);
+				hipLaunchKernelGGL(k_sb_split, gm, dim3(SB_T), 0, st, M, nb, max_leaf, max_depth, c_trav, c_isect, act, acc, dec,
+						   nact, nb6, cnt);
+				TRY(hipGetLastError());
+				TRY(hipMemsetAsync(nact + M, 0, 4, st));
+				TRY(hipcub::DeviceScan::ExclusiveSum(temp, tb2, nact, off, (int)M + 1, st));
+				hipLaunchKernelGGL(k_sb_flags, gn, dim3(SB_T), 0, st, n, nb, seg, pidx, d_lo, d_hi, act, dec, acc, flag);
+				TRY(hipGetLastError());
+				TRY(hipcub::DeviceScan::ExclusiveSum(temp, tb, flag, scan, (int)n, st));
+				hipLaunchKernelGGL(k_sb_children, gm, dim3(SB_T), 0, st, M, n, id_next, act, dec, off, lev + base + M, kids, par);
+				hipLaunchKernelGGL(k_sb_scatter, gn, dim3(SB_T), 0, st, n, seg, pidx, act, dec, flag, scan, off, pidx2, seg2);
+				TRY(hipGetLastError());
+				TRY(hipMemcpyAsync(&tail[0], off + M, 4, hipMemcpyDeviceToHost, st));
+				TRY(hipStreamSynchronize(st));
+				std::swap(pidx, pidx2);
+				std::swap(seg, seg2);
+				base += M;
+				id_next += tail[0];
+				M = tail[0];
+				lev_off.push_back(base);
+			}
+			root = n;
+			nnodes = base; /* every inner node is kept at max_leaf 1; counted exactly below */
+			hipLaunchKernelGGL(k_sb_leaves, gn, dim3(SB_T), 0, st, n, pidx, d_lo, d_hi, nb6, cnt, kcnt);
+			for (size_t l = lev_off.size() - 1; l-- > 0;) {
+				const uint32_t m = lev_off[l + 1] - lev_off[l];
+				hipLaunchKernelGGL(k_sb_kcnt, dim3((m + SB_T - 1) / SB_T), dim3(SB_T), 0, st, m, n, max_leaf, root,
+						   lev + lev_off[l], kids, cnt, kcnt);
+			}
+			TRY(hipGetLastError());
+			TRY(hipMemcpyAsync(&nnodes, kcnt + root, 4, hipMemcpyDeviceToHost, st));
+			TRY(hipMemsetAsync(scal, 0, 4 * sizeof(unsigned), st));
+			hipLaunchKernelGGL(k_pl_leafpos, gn, dim3(PLOC_T), 0, st, n, root, max_leaf, pidx, kids, par, cnt, kcnt, posmap, scal);
+			TRY(hipGetLastError());
+			TRY(hipMemcpyAsync(&depth, scal, 4, hipMemcpyDeviceToHost, st));
+			TRY(hipStreamSynchronize(st));
+			depth += 1; /* the host builder's count: the leaves' level */
+		} else {
+			TRY(hipMemcpyAsync(posmap, pidx, (size_t)n * 4, hipMemcpyDeviceToDevice, st));
+		}
+		DNode *recs = nullptr;
+		TRY(hipMalloc(&recs, ((size_t)nnodes + n) * sizeof(DNode)));
+		/* k_pl_emit: inner ids n .. n + (n - 2), root n */
+		hipLaunchKernelGGL(k_pl_emit, gn, dim3(PLOC_T), 0, st, n, root != RTX_EMPTY_REF ? n - 1 : 0u, root, max_leaf, nnodes, kids,
+				   par, cnt, kcnt, nb6, posmap, d_prims_in, recs);
+		e = hipGetLastError();
+		if (e == hipSuccess)
+			e = hipStreamSynchronize(st);
+		if (e != hipSuccess) {
+			(void)hipFree(recs);
+			goto done;
+		}
+		*recs_out = recs;
+		*nnodes_out = nnodes;
+		*root_out = root != RTX_EMPTY_REF ? 0u : RTX_EMPTY_REF;
+		*depth_out = root != RTX_EMPTY_REF ? depth : 0u;
+		*levels_out = (uint32_t)(lev_off.empty() ? 0 : lev_off.size() - 1);
+	}
+done:
+#undef TRY
+	(void)hipFree(temp);
+	(void)hipFree(pidx);
+	(void)hipFree(pidx2);
+	(void)hipFree(seg);
+	(void)hipFree(seg2);
+	(void)hipFree(flag);
+	(void)hipFree(scan);
+	(void)hipFree(acc);
+	(void)hipFree(nact);
+	(void)hipFree(off);
+	(void)hipFree(dec);
+	(void)hipFree(lev);
+	(void)hipFree(kids);
+	(void)hipFree(par);
+	(void)hipFree(cnt);
+	(void)hipFree(kcnt);
+	(void)hipFree(nb6);
+	(void)hipFree(posmap);
+	(void)hipFree(scal);
+	(void)hipHostFree(tail);
+	return e;
+}

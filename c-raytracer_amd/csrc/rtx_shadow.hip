@@ -436,6 +436,9 @@ __device__ __forceinline__ void shadow_walk4(const QBvh &Q, const char *__restri
 #ifndef RTX_W8_TQ
 #define RTX_W8_TQ 4 /* deferred leaf groups per lane in LDS (besides the one in a register) */
 #endif
+#ifndef RTX_W8_OR
+#define RTX_W8_OR 0 /* > 0: a lane tests at most this many of a step's opaque leaf hits at once, the rest join its deferred groups */
+#endif
 #ifndef RTX_W8_DEFER
 #define RTX_W8_DEFER 64 /* lanes holding deferred leaf tests that trigger a round of them (16 / 32 / 48 / 64: 613 / 601 / 598 / 594 ms) */
 #endif
@@ -443,7 +446,7 @@ __device__ __forceinline__ void shadow_walk4(const QBvh &Q, const char *__restri
  * whose 4th float4 holds its material's kt) against this lane's shadow ray; a hit multiplies
  * the transmittance (accel.c:370-377) */
 template <bool COUNT>
-__device__ __forceinline__ void w8_defer_test(const char *pr, f3 o, f3 d, float tl, f3 &li, uint32_t &ntri, uint32_t &nsph)
+__device__ __forceinline__ bool w8_defer_test(const char *pr, f3 o, f3 d, float tl, f3 &li, uint32_t &ntri, uint32_t &nsph)
 {
 	const float4 a = ldg4(pr, 0), b = ldg4(pr, 16), c = ldg4(pr, 32);
 	bool h;
@@ -458,9 +461,12 @@ __device__ __forceinline__ void w8_defer_test(const char *pr, f3 o, f3 d, float 
 		h = any_tri(mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z), mk3(c.x, c.y, c.z), o, d, a.w, tl);
 	}
 	if (h) {
+		if (RTX_W8_OR && !(__float_as_uint(c.w) & RTX_META_TRANSPARENT))
+			return true; /* a deferred opaque leaf (RTX_W8_OR): the ray is blocked */
 		const float4 kt = ldg4(pr, 48);
 		li = mul3v(li, mk3(kt.x, kt.y, kt.z));
 	}
+	return false;
 }
 
 /* an opaque leaf test: does the primitive at entry pr block this lane's shadow ray?  (no
@@ -500,6 +506,90 @@ __device__ __forceinline__ bool w8_opaque_test_s(const DW8 *e, f3 o, f3 d, float
 	return any_tri(mk3(v[0], v[1], v[2]), mk3(v[4], v[5], v[6]), mk3(v[8], v[9], v[10]), o, d, v[3], tl);
 }
 
+#ifndef RTX_W8_VH
+#define RTX_W8_VH 0 /* measurement option: divergent steps read the half-float node copies (DW8S) per lane */
+#endif
+#ifndef RTX_W8_TR
+#define RTX_W8_TR 0 /* measurement option: divergent steps fetch nodes quad by quad (one line per 4-lane quad) */
+#endif
+/* A divergent step's node fetch, quad-coherent.  The texture path takes a wave's 16-byte loads
+ * four lanes (64 B) per cycle and a cycle more for every further line a quad touches, so four
+ * per-lane loads of 64 lanes' different nodes cost up to 4 x 64 cycles.  Here load k of quad q
+ * (lanes 4q..4q+3) reads the four quarters of ray 4q+k's node, one line per quad (4 x 16 cycles
+ * at most, only for walking rays), and a 4 x 4 transpose within each quad (two DPP butterfly
+ * stages) gives every lane its own node's 16 words.  Every lane of the wave takes part (the
+ * DPP moves read the quad's other lanes); lanes whose ray is not walking get garbage. */
+template <int K> __device__ __forceinline__ uint32_t quad_bcast(uint32_t v)
+{
+	return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, K * 0x55, 0xF, 0xF, false); /* quad_perm [K,K,K,K] */
+}
+/* this lane's entries of a per-wave [entry][lane] LDS array, from the wave's base address
+ * (SGPR): the lane offset is recomputed at every access (volatile), so no VGPR holds it across
+ * the walk (the 64-VGPR budget spilled the lane pointer to scratch) */
+struct LaneLds {
+	uint32_t base; /* LDS byte address of entry 0, lane 0 */
+	__device__ __forceinline__ lds_u32 &operator[](uint32_t k) const
+	{
+		uint32_t l4;
+		asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\tv_lshlrev_b32 %0, 2, %0" : "=v"(l4));
+		return *(lds_u32 *)(base + l4 + 4u * k);
+	}
+};
+template <int M> __device__ __forceinline__ uint32_t quad_xor(uint32_t v)
+{
+	return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, M == 1 ? 0xB1 : 0x4E, 0xF, 0xF, true); /* quad_perm [1,0,3,2] / [2,3,0,1] */
+}
+template <int K> __device__ __forceinline__ void w8_quad_load(const DW8 *__restrict__ w8, uint32_t node, uint32_t q16,
+							       uint32_t (&b)[4])
+{
+	const uint32_t nk = quad_bcast<K>(node); /* ray 4q+K's node */
+	uint4 x = make_uint4(0u, 0u, 0u, 0u);
+	if (nk != RTX_NONE) /* ray 4q+K walks; 32-bit byte offset from the tree's base */
+		x = ldg4u((const char *)w8 + (nk * (uint32_t)sizeof(DW8) + q16));
+	b[0] = x.x;
+	b[1] = x.y;
+	b[2] = x.z;
+	b[3] = x.w;
+}
+__device__ __forceinline__ void w8_fetch_quads(const DW8 *__restrict__ w8, uint32_t node, uint32_t (&w)[16])
+{
+	/* 16 x (lane & 3), recomputed here (volatile: kept out of the register budget between steps) */
+	uint32_t q16;
+	asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\tv_and_b32 %0, 3, %0\n\tv_lshlrev_b32 %0, 4, %0"
+		     : "=v"(q16));
+	const uint32_t i = q16 >> 4;
+	uint32_t B[4][4];
+	w8_quad_load<0>(w8, node, q16, B[0]);
+	w8_quad_load<1>(w8, node, q16, B[1]);
+	w8_quad_load<2>(w8, node, q16, B[2]);
+	w8_quad_load<3>(w8, node, q16, B[3]);
+	/* lane i holds quarter i of rays k = 0..3; lane j wants quarters 0..3 of ray j */
+	const bool odd = i & 1u, hi = i & 2u;
+#pragma unroll
+	for (int e = 0; e < 4; e += 2)
+#pragma unroll
+		for (int d = 0; d < 4; d++) {
+			const uint32_t pe = quad_xor<1>(B[e + 1][d]), po = quad_xor<1>(B[e][d]);
+			const uint32_t ne = odd ? pe : B[e][d], no = odd ? B[e + 1][d] : po;
+			B[e][d] = ne;
+			B[e + 1][d] = no;
+		}
+#pragma unroll
+	for (int e = 0; e < 2; e++)
+#pragma unroll
+		for (int d = 0; d < 4; d++) {
+			const uint32_t pl = quad_xor<2>(B[e + 2][d]), ph = quad_xor<2>(B[e][d]);
+			const uint32_t nl = hi ? pl : B[e][d], nh = hi ? B[e + 2][d] : ph;
+			B[e][d] = nl;
+			B[e + 2][d] = nh;
+		}
+#pragma unroll
+	for (int k = 0; k < 4; k++)
+#pragma unroll
+		for (int d = 0; d < 4; d++)
+			w[4 * k + d] = B[k][d];
+}
+
 template <bool COUNT, int OCT>
 __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__restrict__ mats, f3 o, f3 d, f3 inv,
 					     float &tl, uint32_t emit_obj, f3 &li, ShadowCount &sc)
@@ -508,7 +598,11 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 	const f3 invq = mk3(inv.x * Q.qsi.x, inv.y * Q.qsi.y, inv.z * Q.qsi.z);
 	const f3 oq = mk3((o.x - Q.qo.x) * Q.qs.x, (o.y - Q.qo.y) * Q.qs.y, (o.z - Q.qo.z) * Q.qs.z);
 	const f3 oi = mul3v(oq, invq);
+#if RTX_W8_TR
+	const LaneLds stk{ uni((uint32_t)(uintptr_t)Q.stk - 4u * lane_id()) }, tq{ uni((uint32_t)(uintptr_t)Q.tq - 4u * lane_id()) };
+#else
 	lds_u32 *stk = Q.stk, *tq = Q.tq;
+#endif
 	uint32_t node = tl >= 0.f ? 0u : RTX_NONE, grp = 0, sp = 0, tgrp = 0, tn = 0;
 	uint32_t nbox = 0, ntri = 0, nsph = 0, nstep = 0, nlr = 0, nun = 0;
 	for (;;) {
@@ -525,20 +619,41 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 				tgrp &= tgrp - 1;
 				if (!(tgrp & 0xFFu))
 					tgrp = tn ? tq[--tn * WAVE] : 0u;
-				w8_defer_test<COUNT>(pr, o, d, tl, li, ntri, nsph);
+				if (w8_defer_test<COUNT>(pr, o, d, tl, li, ntri, nsph)) {
+					tl = -1.f;
+					node = RTX_NONE;
+					tgrp = 0;
+					tn = 0;
+				}
 			}
 			continue;
 		}
 		uint32_t lm = 0, base = 0; /* this step's opaque leaf hits (visit order) and their block */
 		bool ustep = false;         /* every walking lane at one node (base wave-uniform) */
+		W8Visit v;
+		bool vdone = false;
+		if (RTX_W8_TR) {
+			/* a divergent step: the nodes fetched quad by quad and tested by every lane (the
+			 * transpose reads all lanes of a quad; lanes that are not walking test garbage and
+			 * ignore it) */
+			const uint32_t un = readlane(node, (uint32_t)__ffsll((long long)walking) - 1);
+			if (ballot(node != RTX_NONE && node != un)) {
+				uint32_t w[16];
+				w8_fetch_quads(Q.w8, node, w);
+				v = w8_visit<OCT, K, false>(w, invq, oi, tl);
+				vdone = true;
+			}
+		}
 		if (node != RTX_NONE) {
-			W8Visit v;
 			const uint32_t un = uni(node);
-			if (RTX_W_SUNI && !ballot(node != un)) {
+			if (vdone) {
+			} else if (RTX_W8_TR || (RTX_W_SUNI && !ballot(node != un))) {
 				/* every walking lane is at one node: its scalar-path copy through the scalar cache,
 				 * the planes as SGPR float operands */
 				v = w8_visit_s<OCT, K>(Q.w8s + (size_t)un, invq, oi, tl);
 				ustep = true;
+			} else if (RTX_W8_VH) {
+				v = w8_visit_v<OCT, K>(Q.w8s + (size_t)node, invq, oi, tl);
 			} else {
 				uint32_t w[16];
 				const DW8 *N = Q.w8 + (size_t)node;
@@ -557,13 +672,21 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 			lm = hm & ~v.io & ~v.to;
 			uint32_t im = hm & v.io;
 			const uint32_t dm = hm & v.to;
+			uint32_t dmo = dm;
 			if (COUNT) {
 				nstep++;
 				nbox += popc64(v.nv);
 				nun += ballot(node != uni(node)) ? 0u : 1u;
 			}
-			if (dm) { /* transparent leaves: deferred */
-				const uint32_t g = (base << 8) | dm;
+			if (RTX_W8_OR) { /* opaque leaf hits beyond the first RTX_W8_OR: deferred with the transparent ones */
+				uint32_t keep = lm;
+				for (int r = 0; r < RTX_W8_OR; r++)
+					keep &= keep - 1;
+				dmo = dm | keep;
+				lm &= ~keep;
+			}
+			if (dmo) { /* transparent leaves: deferred */
+				const uint32_t g = (base << 8) | dmo;
 				if (tgrp)
 					tq[tn++ * WAVE] = g;
 				else
@@ -647,10 +770,11 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 				}
 			}
 		}
-		if (blocked) {
+		if (blocked) { /* the queue too: a full queue left behind would keep the wave in deferred rounds */
 			tl = -1.f;
 			node = RTX_NONE;
 			tgrp = 0;
+			tn = 0;
 		}
 	}
 	if (COUNT) {

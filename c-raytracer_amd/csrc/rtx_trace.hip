@@ -162,6 +162,15 @@ __device__ void trace_closest_bvh2(const DScene &S, uint32_t *stk, bool act, f3 
  * groups on the lane's stack (LDS, deeper entries in HBM), and every node's boxes are tested
  * against the current closest t.  The emitters the tree leaves out (DScene.w8noemit) are
  * tested before the walk.  Strict < everywhere: the first hit found at the least t wins. */
+#ifndef RTX_TRACE_NEAR
+#define RTX_TRACE_NEAR 0 /* closest hits: visit the nearest hit inner child first */
+#endif
+#ifndef RTX_TRACE_CULL
+#define RTX_TRACE_CULL 0 /* closest hits: drop kept sibling groups that start beyond the closest hit */
+#endif
+#ifndef RTX_TRACE_EMPTYCOUNT
+#define RTX_TRACE_EMPTYCOUNT 0 /* measurement builds: count only the visits that hit no child */
+#endif
 template <bool COUNT, int OCT>
 __device__ __forceinline__ void closest_walk8(const DScene &S, uint32_t *stk, uint32_t *ostk, size_t ostride, f3 o, f3 d,
 					      f3 inv, float &tbest, uint32_t &hid, TraceCount &tc)
@@ -172,11 +181,22 @@ __device__ __forceinline__ void closest_walk8(const DScene &S, uint32_t *stk, ui
 	const f3 oq = mk3((o.x - qo.x) * qs.x, (o.y - qo.y) * qs.y, (o.z - qo.z) * qs.z);
 	const f3 oi = mul3v(oq, invq);
 	uint32_t node = 0, grp = 0, sp = 0;
+	float gt = -INFINITY; /* RTX_TRACE_CULL: least entry distance of the group in grp (-inf: unknown) */
+	constexpr bool T = RTX_TRACE_NEAR || RTX_TRACE_CULL;
 	while (node != RTX_NONE) {
 		W8Visit v;
+		uint32_t nearp = 8;
+		float tin = INFINITY;
 		const uint32_t un = uni(node);
 		if (!ballot(node != un)) {
-			v = w8_visit_s<OCT, K>(S.w8s + (size_t)un, invq, oi, tbest);
+			if (T) {
+				const W8VisitT r = w8_visit_st<OCT, K>(S.w8s + (size_t)un, invq, oi, tbest);
+				v = r.v;
+				nearp = r.near;
+				tin = r.tin;
+			} else {
+				v = w8_visit_s<OCT, K>(S.w8s + (size_t)un, invq, oi, tbest);
+			}
 		} else {
 			uint32_t w[16];
 			const DW8 *N = S.w8 + (size_t)node;
@@ -188,9 +208,16 @@ __device__ __forceinline__ void closest_walk8(const DScene &S, uint32_t *stk, ui
 				w[4 * k + 2] = x.z;
 				w[4 * k + 3] = x.w;
 			}
-			v = w8_visit<OCT, K, false>(w, invq, oi, tbest);
+			if (T) {
+				const W8VisitT r = w8_visit_t<OCT, K>(w, invq, oi, tbest);
+				v = r.v;
+				nearp = r.near;
+				tin = r.tin;
+			} else {
+				v = w8_visit<OCT, K, false>(w, invq, oi, tbest);
+			}
 		}
-		if (COUNT)
+		if (COUNT && (!RTX_TRACE_EMPTYCOUNT || !v.hm))
 			tc.nodes++;
 		uint32_t lm = v.hm & ~v.io, im = v.hm & v.io;
 		while (lm) {
@@ -214,9 +241,12 @@ __device__ __forceinline__ void closest_walk8(const DScene &S, uint32_t *stk, ui
 				hid = __float_as_uint(ldg4(pr, 48).w);
 			}
 		}
+		if (RTX_TRACE_CULL && tin > tbest) /* every hit inner child starts beyond the closest hit */
+			im = 0;
 		if (im) {
-			node = v.base + (__builtin_ctz(im) ^ K);
-			im &= im - 1;
+			const uint32_t p0 = (RTX_TRACE_NEAR && nearp < 8) ? nearp : (uint32_t)__builtin_ctz(im);
+			node = v.base + (p0 ^ K);
+			im &= ~(1u << p0);
 			if (im) {
 				if (grp) {
 					if (sp < RTX_TRACE_LSTK)
@@ -226,19 +256,31 @@ __device__ __forceinline__ void closest_walk8(const DScene &S, uint32_t *stk, ui
 					sp++;
 				}
 				grp = (v.base << 8) | im;
+				gt = tin;
 			}
-		} else if (grp) {
-			node = (grp >> 8) + (__builtin_ctz(grp) ^ K);
-			grp &= grp - 1;
-			if (!(grp & 0xFFu)) {
+		} else {
+			if (RTX_TRACE_CULL && grp && gt > tbest) { /* the kept group starts beyond the closest hit */
 				grp = 0;
 				if (sp) {
 					sp--;
 					grp = sp < RTX_TRACE_LSTK ? stk[sp * WAVE] : ostk[(sp - RTX_TRACE_LSTK) * ostride];
 				}
+				gt = -INFINITY;
 			}
-		} else {
-			node = RTX_NONE;
+			if (grp) {
+				node = (grp >> 8) + (__builtin_ctz(grp) ^ K);
+				grp &= grp - 1;
+				if (!(grp & 0xFFu)) {
+					grp = 0;
+					if (sp) {
+						sp--;
+						grp = sp < RTX_TRACE_LSTK ? stk[sp * WAVE] : ostk[(sp - RTX_TRACE_LSTK) * ostride];
+					}
+					gt = -INFINITY;
+				}
+			} else {
+				node = RTX_NONE;
+			}
 		}
 	}
 }

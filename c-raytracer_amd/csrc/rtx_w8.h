@@ -78,6 +78,24 @@ template <uint32_t K> __device__ __forceinline__ uint32_t perm_xor(uint32_t m)
  * live lane's direction lies in octant OCT, entry planes known at compile time; an empty slot
  * (lo 255 > hi 0) is then never hit. */
 template <int OCT>
+__device__ __forceinline__ bool w8_slab_tn(float lx, float hx, float ly, float hy, float lz, float hz, float tl, float &tn_out)
+{
+	if (OCT == 8) {
+		const float tn = fmaxf(fmaxf(fminf(lx, hx), fminf(ly, hy)), fmaxf(fminf(lz, hz), 0.f));
+		const float tf = fminf(fminf(fmaxf(lx, hx), fmaxf(ly, hy)), fminf(fmaxf(lz, hz), tl));
+		tn_out = tn;
+		return tn <= tf;
+	}
+	const float nx = (OCT & 1) ? lx : hx, fx = (OCT & 1) ? hx : lx;
+	const float ny = (OCT & 2) ? ly : hy, fy = (OCT & 2) ? hy : ly;
+	const float nz = (OCT & 4) ? lz : hz, fz = (OCT & 4) ? hz : lz;
+	const float tn = fmaxf(fmaxf(nx, ny), fmaxf(nz, 0.f));
+	float tf = fminf(fminf(fx, fy), fz);
+	asm("v_min_f32 %0, %0, %1" : "+v"(tf) : "v"(tl));
+	tn_out = tn;
+	return tn <= tf;
+}
+template <int OCT>
 __device__ __forceinline__ bool w8_slab(float lx, float hx, float ly, float hy, float lz, float hz, float tl)
 {
 	if (OCT == 8) {
@@ -93,10 +111,23 @@ __device__ __forceinline__ bool w8_slab(float lx, float hx, float ly, float hy, 
 	asm("v_min_f32 %0, %0, %1" : "+v"(tf) : "v"(tl));
 	return tn <= tf;
 }
+#ifndef RTX_W8_PK
+#define RTX_W8_PK 0 /* measurement option: an axis's two planes in one v_pk_fma_f32 (the same fused results) */
+#endif
+typedef float f2v __attribute__((ext_vector_type(2)));
 template <int OCT, int C>
 __device__ __forceinline__ bool w8_child(const uint32_t (&w)[16], f3 s, f3 b, float tl)
 {
 	constexpr int W = C >> 2, B = C & 3;
+	if (RTX_W8_PK) {
+		const f2v x = __builtin_elementwise_fma((f2v){ ubyte<B>(w[4 + W]), ubyte<B>(w[6 + W]) }, (f2v){ s.x, s.x },
+							(f2v){ b.x, b.x });
+		const f2v y = __builtin_elementwise_fma((f2v){ ubyte<B>(w[8 + W]), ubyte<B>(w[10 + W]) }, (f2v){ s.y, s.y },
+							(f2v){ b.y, b.y });
+		const f2v z = __builtin_elementwise_fma((f2v){ ubyte<B>(w[12 + W]), ubyte<B>(w[14 + W]) }, (f2v){ s.z, s.z },
+							(f2v){ b.z, b.z });
+		return w8_slab<OCT>(x.x, x.y, y.x, y.y, z.x, z.y, tl);
+	}
 	return w8_slab<OCT>(fmaf(ubyte<B>(w[4 + W]), s.x, b.x), fmaf(ubyte<B>(w[6 + W]), s.x, b.x),
 			    fmaf(ubyte<B>(w[8 + W]), s.y, b.y), fmaf(ubyte<B>(w[10 + W]), s.y, b.y),
 			    fmaf(ubyte<B>(w[12 + W]), s.z, b.z), fmaf(ubyte<B>(w[14 + W]), s.z, b.z), tl);
@@ -218,6 +249,138 @@ __device__ __forceinline__ W8Visit w8_visit_s(const DW8S *n, f3 invq, f3 oi, flo
 	v.to = perm_xor<K>((w3 >> 8) & 0xFFu);
 	v.nv = w3 & 0xFFu;
 	return v;
+}
+
+/* the same visit on the scalar-path copy read per lane (measurement option RTX_W8_VH: eight
+ * 16-byte loads instead of four, v_fma_mix_f32 on the halves instead of byte conversions) */
+template <int OCT, uint32_t K>
+__device__ __forceinline__ W8Visit w8_visit_v(const DW8S *n, f3 invq, f3 oi, float tl)
+{
+	uint32_t q[24], h[8];
+	{
+		const uint4 a = ldg4u((const uint32_t *)n), b = ldg4u((const uint32_t *)n + 4);
+		h[0] = a.x;
+		h[1] = a.y;
+		h[2] = a.z;
+		h[3] = a.w;
+		h[4] = b.x;
+		h[5] = b.y;
+		h[6] = b.z;
+		h[7] = b.w;
+	}
+#pragma unroll
+	for (int k = 0; k < 6; k++) {
+		const uint4 x = ldg4u((const uint32_t *)n + 8 + 4 * k);
+		q[4 * k] = x.x;
+		q[4 * k + 1] = x.y;
+		q[4 * k + 2] = x.z;
+		q[4 * k + 3] = x.w;
+	}
+	const uint32_t w1 = h[1], w2 = h[2], w3 = h[3];
+	const f3 s = mk3(ldexpf(invq.x, (int)((w1 >> 16) & 15u)), ldexpf(invq.y, (int)((w1 >> 20) & 15u)),
+			 ldexpf(invq.z, (int)((w1 >> 24) & 15u)));
+	const f3 b = mk3(fmaf(__uint_as_float(h[4]), invq.x, -oi.x), fmaf(__uint_as_float(h[5]), invq.y, -oi.y),
+			 fmaf(__uint_as_float(h[6]), invq.z, -oi.z));
+	W8Visit v;
+	v.hm = w8_hits_s<OCT, K>(q, w3, s, b, tl);
+	v.base = w2 >> 8;
+	v.io = perm_xor<K>(w2 & 0xFFu);
+	v.to = perm_xor<K>((w3 >> 8) & 0xFFu);
+	v.nv = w3 & 0xFFu;
+	return v;
+}
+
+/* closest-hit visits (k_trace) with entry distances: besides the hit mask, the nearest hit inner
+ * child (slot in visit order, or 8 for none) and the least entry distance of the hit inner
+ * children (a lower bound for every sibling kept for later: RTX_TRACE_CULL drops a kept group
+ * whose bound the closest hit so far has passed) */
+struct W8VisitT {
+	W8Visit v;
+	uint32_t near;
+	float tin;
+};
+template <int OCT, uint32_t K, int C, bool SC>
+__device__ __forceinline__ void w8_child_t(const uint32_t *w, f3 s, f3 b, float tl, uint32_t io, uint32_t &hm, uint32_t &near,
+					   float &tin)
+{
+	float l[6];
+	if (SC) {
+#pragma unroll
+		for (int k = 0; k < 6; k++) {
+			const uint32_t x = w[4 * k + (C >> 1)];
+			l[k] = (float)__builtin_bit_cast(_Float16, (uint16_t)((C & 1) ? (x >> 16) : (x & 0xFFFFu)));
+		}
+	} else {
+		constexpr int W = C >> 2, B = C & 3;
+#pragma unroll
+		for (int k = 0; k < 6; k++)
+			l[k] = ubyte<B>(w[4 + 2 * k + W]);
+	}
+	float tn;
+	const bool h = w8_slab_tn<OCT>(fmaf(l[0], s.x, b.x), fmaf(l[1], s.x, b.x), fmaf(l[2], s.y, b.y), fmaf(l[3], s.y, b.y),
+				       fmaf(l[4], s.z, b.z), fmaf(l[5], s.z, b.z), tl, tn) &&
+		       (OCT != 8 || ((io >> 8) >> C) & 1u);
+	hm |= h ? 1u << (C ^ K) : 0u;
+	const bool in = h && ((io >> C) & 1u);
+	near = (in && tn < tin) ? (uint32_t)(C ^ K) : near;
+	tin = (in && tn < tin) ? tn : tin;
+}
+template <int OCT, uint32_t K, bool SC>
+__device__ __forceinline__ void w8_hits_t(const uint32_t *w, f3 s, f3 b, float tl, uint32_t io, W8VisitT &r)
+{
+	uint32_t hm = 0, near = 8;
+	float tin = INFINITY;
+	w8_child_t<OCT, K, 0, SC>(w, s, b, tl, io, hm, near, tin);
+	w8_child_t<OCT, K, 1, SC>(w, s, b, tl, io, hm, near, tin);
+	w8_child_t<OCT, K, 2, SC>(w, s, b, tl, io, hm, near, tin);
+	w8_child_t<OCT, K, 3, SC>(w, s, b, tl, io, hm, near, tin);
+	w8_child_t<OCT, K, 4, SC>(w, s, b, tl, io, hm, near, tin);
+	w8_child_t<OCT, K, 5, SC>(w, s, b, tl, io, hm, near, tin);
+	w8_child_t<OCT, K, 6, SC>(w, s, b, tl, io, hm, near, tin);
+	w8_child_t<OCT, K, 7, SC>(w, s, b, tl, io, hm, near, tin);
+	r.v.hm = hm;
+	r.near = near;
+	r.tin = tin;
+}
+/* io argument: inner-child mask (bits 0-7, slot order) | slot mask << 8 (generic octant only) */
+template <int OCT, uint32_t K>
+__device__ __forceinline__ W8VisitT w8_visit_t(const uint32_t (&w)[16], f3 invq, f3 oi, float tl)
+{
+	f3 s, b;
+	w8_frame(w, invq, oi, s, b);
+	W8VisitT r;
+	w8_hits_t<OCT, K, false>(w, s, b, tl, (w[2] & 0xFFu) | ((w[3] & 0xFFu) << 8), r);
+	r.v.base = w[2] >> 8;
+	r.v.io = perm_xor<K>(w[2] & 0xFFu);
+	r.v.to = perm_xor<K>((w[3] >> 8) & 0xFFu);
+	r.v.nv = w[3] & 0xFFu;
+	return r;
+}
+template <int OCT, uint32_t K>
+__device__ __forceinline__ W8VisitT w8_visit_st(const DW8S *n, f3 invq, f3 oi, float tl)
+{
+	typedef uint32_t u16v __attribute__((ext_vector_type(16)));
+	const auto *U = (const __attribute__((address_space(4))) u16v *)n;
+	const u16v p0 = U[0], p1 = U[1];
+	uint32_t q[24];
+#pragma unroll
+	for (int k = 0; k < 8; k++)
+		q[k] = p0[8 + k];
+#pragma unroll
+	for (int k = 0; k < 16; k++)
+		q[8 + k] = p1[k];
+	const uint32_t w1 = p0[1], w2 = p0[2], w3 = p0[3];
+	const f3 s = mk3(ldexpf(invq.x, (int)((w1 >> 16) & 15u)), ldexpf(invq.y, (int)((w1 >> 20) & 15u)),
+			 ldexpf(invq.z, (int)((w1 >> 24) & 15u)));
+	const f3 b = mk3(fmaf(__uint_as_float(p0[4]), invq.x, -oi.x), fmaf(__uint_as_float(p0[5]), invq.y, -oi.y),
+			 fmaf(__uint_as_float(p0[6]), invq.z, -oi.z));
+	W8VisitT r;
+	w8_hits_t<OCT, K, true>(q, s, b, tl, (w2 & 0xFFu) | ((w3 & 0xFFu) << 8), r);
+	r.v.base = w2 >> 8;
+	r.v.io = perm_xor<K>(w2 & 0xFFu);
+	r.v.to = perm_xor<K>((w3 >> 8) & 0xFFu);
+	r.v.nv = w3 & 0xFFu;
+	return r;
 }
 
 #endif

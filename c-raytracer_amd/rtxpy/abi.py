@@ -74,7 +74,7 @@ class Stats(C.Structure):
                 ("trace_walk", C.c_uint32), ("pad2_", C.c_uint32)]
 
 
-RTX_BUILD_SAH_HOST, RTX_BUILD_LBVH_GPU, RTX_BUILD_PLOC_GPU = 0, 1, 2
+RTX_BUILD_SAH_HOST, RTX_BUILD_LBVH_GPU, RTX_BUILD_PLOC_GPU, RTX_BUILD_SAH_GPU = 0, 1, 2, 3
 RTX_WALK_AUTO, RTX_WALK_BVH2, RTX_WALK_W4, RTX_WALK_W8 = -1, 0, 1, 2
 RTX_OPT_SHADOW_WALK, RTX_OPT_BVH_LEAF, RTX_OPT_SPSORT, RTX_OPT_SHADOW_SLOT, RTX_OPT_SHADOW_GRAB, \
     RTX_OPT_SHADOW_LDS_STACK, RTX_OPT_TRACE_WALK = 1, 2, 3, 4, 5, 6, 7

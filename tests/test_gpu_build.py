@@ -1,5 +1,5 @@
 """GPU BVH builders (csrc/rtx_build.hip via rtx_set_builder(RTX_BUILD_LBVH_GPU /
-RTX_BUILD_PLOC_GPU)).
+RTX_BUILD_PLOC_GPU / RTX_BUILD_SAH_GPU)).
 
 Closest-hit answers do not depend on the tree (up to exact ties), so frames rendered over the
 GPU-built LBVH must match the reference goldens exactly as well as frames over the host SAH
@@ -41,10 +41,11 @@ def render(r, builder, scene, frame, params):
     return rgb, z, r.stats()
 
 
-GPU_BUILDERS = [abi.RTX_BUILD_LBVH_GPU, abi.RTX_BUILD_PLOC_GPU]
+GPU_BUILDERS = [abi.RTX_BUILD_LBVH_GPU, abi.RTX_BUILD_PLOC_GPU, abi.RTX_BUILD_SAH_GPU]
+IDS = ["lbvh", "ploc", "sahgpu"]
 
 
-@pytest.mark.parametrize("builder", GPU_BUILDERS, ids=["lbvh", "ploc"])
+@pytest.mark.parametrize("builder", GPU_BUILDERS, ids=IDS)
 @pytest.mark.parametrize("name", CONFIGS)
 def test_gpu_builder_frames_match(renderer, name, builder):
     scene, frame, params, m = C.load_config(name)
@@ -62,7 +63,7 @@ def test_gpu_builder_frames_match(renderer, name, builder):
     assert np.abs(a - b).max() <= 1e-5 * max(1.0, float(np.abs(a).max())), name
 
 
-@pytest.mark.parametrize("builder", GPU_BUILDERS, ids=["lbvh", "ploc"])
+@pytest.mark.parametrize("builder", GPU_BUILDERS, ids=IDS)
 def test_gpu_builder_deterministic_and_tiny_scenes(renderer, builder):
     scene, frame, params, _ = C.load_config("s5_path2")
     a, za, st = render(renderer, builder, scene, frame, params)
@@ -99,3 +100,27 @@ def test_gpu_ploc_multi_primitive_leaves(renderer, leaf):
     ref_rgb, ref_z = C.golden_frame("s3_path2_o2")
     ok, info = C.compare_const(b, zb, ref_rgb, ref_z)
     assert ok, info
+
+
+@pytest.mark.parametrize("name", ["s5_path2", "s6_amb", "s3_path2", "st_amb"])
+def test_gpu_sah_device_builds_the_host_tree(renderer, name):
+    """RTX_BUILD_SAH_GPU runs bvh_build.cpp's binned SAH on the device (same bins, same float
+    costs, same split order): with single-primitive leaves it builds the host's tree node for node,
+    so the 8-wide collapse, every traversal count and every pixel are the same as over the host
+    build (the dragon and Menger stand-ins included)."""
+    scene, frame, params, _ = C.load_config(name)
+    params.count_traversal = 1
+    out = {}
+    for b in (abi.RTX_BUILD_SAH_HOST, abi.RTX_BUILD_SAH_GPU):
+        renderer.set_builder(b)
+        renderer.upload(scene)
+        rgb, z = renderer.render(frame, params)
+        out[b] = (rgb, z, renderer.stats())
+    a, za, sa = out[abi.RTX_BUILD_SAH_HOST]
+    b, zb, sb = out[abi.RTX_BUILD_SAH_GPU]
+    assert sb.builder == abi.RTX_BUILD_SAH_GPU
+    for f in ("bvh_nodes", "bvh_prims", "bvh_depth", "wide_nodes", "wide_depth", "shadow_walk", "closest_rays",
+              "shadow_rays", "node_visits", "tri_tests", "sphere_tests", "shadow_box_tests", "shadow_wave_steps",
+              "shadow_leaf_rounds", "shadow_uniform_steps"):
+        assert getattr(sa, f) == getattr(sb, f), (name, f, getattr(sa, f), getattr(sb, f))
+    assert np.array_equal(a, b) and np.array_equal(za, zb), name

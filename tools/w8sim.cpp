@@ -131,7 +131,7 @@ struct Stats {
 	/* divergent wave steps (walking lanes at more than one node): distinct 64-B node entries and
 	 * 128-B lines per step, and the line touches of the four per-lane loads vs a transposed fetch
 	 * (load k = the 16-B quarters of lanes 16k..16k+15's nodes, four lanes per node) */
-	double dsteps = 0, dnodes = 0, dlines = 0, touch_lane = 0, touch_tr = 0, walkers = 0;
+	double dsteps = 0, dnodes = 0, dlines = 0, touch_lane = 0, touch_tr = 0, walkers = 0, quad_lane = 0, quad_tr = 0;
 	double post_nodes[8] = {}, post_leaves[8] = {}; /* postponed leaf tests, threshold T = 8 * k lanes */
 };
 
@@ -531,6 +531,18 @@ int main(int argc, char **argv)
 				const double dl = uniq(lines);
 				S.dlines += dl;
 				S.touch_lane += 4 * dl;
+				/* address-path cycles if the texture unit takes 4 lanes (64 B) per cycle and one more
+				 * cycle per further distinct line in a quad: per-lane loads (x4 instructions) vs
+				 * transposed (each quad = one ray's node) */
+				for (int q = 0; q < 16; q++) {
+					std::vector<uint32_t> g;
+					for (int l = 4 * q; l < 4 * q + 4; l++)
+						if (at[l] != ~0u)
+							g.push_back(at[l] >> 1);
+					if (!g.empty())
+						S.quad_lane += 4 * uniq(g);
+				}
+				S.quad_tr += nodes.size();
 				for (int k = 0; k < 4; k++) {
 					std::vector<uint32_t> g;
 					for (int l = 16 * k; l < 16 * k + 16; l++)
@@ -556,9 +568,9 @@ int main(int argc, char **argv)
 	       "cost(290/step + 99/round)\n",
 	       S.emit / S.rays);
 	printf("divergent steps/packet %.2f  walking lanes %.1f  distinct nodes %.2f  lines %.2f  line touches per step: "
-	       "per-lane loads %.1f  transposed %.1f\n",
+	       "per-lane loads %.1f  transposed %.1f  quad cycles: per-lane %.1f  transposed %.1f\n",
 	       S.dsteps / S.packets, S.walkers / S.dsteps, S.dnodes / S.dsteps, S.dlines / S.dsteps, S.touch_lane / S.dsteps,
-	       S.touch_tr / S.dsteps);
+	       S.touch_tr / S.dsteps, S.quad_lane / S.dsteps, S.quad_tr / S.dsteps);
 	for (int k = 0; k < 8; k++)
 		printf("  %2d  %6.2f  %6.2f  %7.0f\n", k ? 8 * k : 1, S.post_nodes[k] / S.packets, S.post_leaves[k] / S.packets,
 		       (290 * S.post_nodes[k] + 99 * S.post_leaves[k]) / S.packets);
