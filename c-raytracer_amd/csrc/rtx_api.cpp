@@ -125,6 +125,8 @@ static void free_scene(rtx_ctx *c)
 	dfree(c->d_w8);
 	dfree(c->d_w8s);
 	c->have_scene = false;
+	c->sp_tile_seen = 0.0;
+	c->sp_tile_key = 0;
 }
 
 extern "C" void rtx_close(rtx_ctx *c)
@@ -756,6 +758,8 @@ int rtx_upload_built(rtx_ctx *c, const HostScene &hs)
 	/* a failure below leaves the context without a scene (RTX_ERR_STATE on render), never with a
 	 * mix of old and new buffers */
 	c->have_scene = false;
+	c->sp_tile_seen = 0.0; /* the next render sizes its chunks from the static bound */
+	c->sp_tile_key = 0;
 	HIP_TRY(hipSetDevice(c->device));
 	if (!(hs.recs_on_device && c->d_nodes) && (rc = upload(c->d_nodes, hs.recs)))
 		return rc;
@@ -916,7 +920,13 @@ int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, floa
 	/* shade points per tile: 64 px x (primary + GI samples) + secondary-ray allowance */
 	const uint64_t gi_n = P.gi == RTX_GI_PATH ? (uint64_t)P.samples : 0u;
 	uint64_t staging_cap = 64ull * (1 + gi_n) + 64ull * 4 * std::min<uint32_t>(mb, 16u) * (gi_n ? 2 : 1) + 64;
-	const uint64_t avg_tile = 64ull * (1 + gi_n) * 5 / 4 + 64;
+	uint64_t avg_tile = 64ull * (1 + gi_n) * 5 / 4 + 64;
+	/* a render of the same scene and settings before: its shade points per tile (x 1.25, + 64)
+	 * instead of the bound above; an overflow still halves the chunk and retries */
+	const uint64_t sp_key = ((uint64_t)P.gi << 56) ^ ((uint64_t)P.samples << 32) ^ ((uint64_t)P.max_bounces << 16) ^
+				((uint64_t)P.reflection << 8) ^ (uint64_t)P.tile_stride;
+	if (c->sp_tile_key == sp_key && c->sp_tile_seen > 0.0)
+		avg_tile = std::min<uint64_t>(avg_tile, (uint64_t)(c->sp_tile_seen * 1.25) + 64);
 	size_t free_b = 0, total_b = 0;
 	HIP_TRY(hipMemGetInfo(&free_b, &total_b));
 	/* shade points of a chunk: up to a third of free HBM (96 GB cap; 288 GB per MI355X) */
@@ -1050,6 +1060,10 @@ int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, floa
 	}
 	HIP_TRY(hipEventRecord(c->ev1, stream));
 	HIP_TRY(hipStreamSynchronize(stream));
+	if (P.ntiles) {
+		c->sp_tile_seen = (double)shade_points / P.ntiles;
+		c->sp_tile_key = sp_key;
+	}
 	const unsigned long long *ctr = tot;
 	rtx_stats &st = c->stats;
 	st.closest_rays = ctr[RTX_C_CLOSEST];

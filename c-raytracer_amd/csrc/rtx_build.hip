@@ -775,12 +775,13 @@ __global__ __launch_bounds__(SB_T) void k_sb_reset(uint32_t M, uint32_t nb, uint
 }
 
 /* node boxes and centroid bounds.  A wave whose positions all lie in one node reduces first. */
-__global__ __launch_bounds__(SB_T) void k_sb_bounds(uint32_t n, uint32_t nb, const uint32_t *__restrict__ seg,
-						     const uint32_t *__restrict__ pidx, const float *__restrict__ lo,
-						     const float *__restrict__ hi, uint32_t *__restrict__ acc)
+__global__ __launch_bounds__(SB_T) void k_sb_bounds(uint32_t n, uint32_t nb, uint32_t s0b, uint32_t sn,
+						     const uint32_t *__restrict__ seg, const uint32_t *__restrict__ pidx,
+						     const float *__restrict__ lo, const float *__restrict__ hi, uint32_t *__restrict__ acc)
 {
 	const uint32_t q = blockIdx.x * SB_T + threadIdx.x;
-	const uint32_t s = q < n ? seg[q] : RTX_NONE;
+	uint32_t s = q < n ? seg[q] : RTX_NONE;
+	s = (s != RTX_NONE && s - s0b < sn) ? s - s0b : RTX_NONE; /* this batch's nodes only */
 	float v[12];
 	if (s != RTX_NONE) {
 		const uint32_t p = pidx[q];
@@ -825,16 +826,17 @@ __device__ __forceinline__ int sb_bin(float c, float clo, float k, int nb)
 	return min(max(bi, 0), nb - 1);
 }
 
-__global__ __launch_bounds__(SB_T) void k_sb_bins(uint32_t n, uint32_t nb, const uint32_t *__restrict__ seg,
-						   const uint32_t *__restrict__ pidx, const float *__restrict__ lo,
-						   const float *__restrict__ hi, uint32_t *__restrict__ acc)
+__global__ __launch_bounds__(SB_T) void k_sb_bins(uint32_t n, uint32_t nb, uint32_t s0b, uint32_t sn,
+						   const uint32_t *__restrict__ seg, const uint32_t *__restrict__ pidx,
+						   const float *__restrict__ lo, const float *__restrict__ hi, uint32_t *__restrict__ acc)
 {
 	const uint32_t q = blockIdx.x * SB_T + threadIdx.x;
 	if (q >= n)
 		return;
-	const uint32_t s = seg[q];
-	if (s == RTX_NONE)
+	uint32_t s = seg[q];
+	if (s == RTX_NONE || s - s0b >= sn)
 		return;
+	s -= s0b;
 	uint32_t *A = acc + (size_t)s * SB_ACC(nb);
 	const uint32_t p = pidx[q];
 	float b[6];
@@ -859,15 +861,15 @@ __global__ __launch_bounds__(SB_T) void k_sb_bins(uint32_t n, uint32_t nb, const
 
 /* the split of each node (bvh_build.cpp Builder::build): mode 0 = SAH (axis, bin), 1 = middle
  * of the range; nleft; the node's box into the tree; children that stay active */
-__global__ __launch_bounds__(SB_T) void k_sb_split(uint32_t M, uint32_t nb, uint32_t max_leaf, uint32_t max_depth,
+__global__ __launch_bounds__(SB_T) void k_sb_split(uint32_t sn, uint32_t s0b, uint32_t nb, uint32_t max_leaf, uint32_t max_depth,
 						    float c_trav, float c_isect, const SbNode *__restrict__ act,
 						    const uint32_t *__restrict__ acc, uint4 *__restrict__ dec,
 						    uint32_t *__restrict__ nact, float *__restrict__ nb6, uint32_t *__restrict__ cnt)
 {
-	const uint32_t i = blockIdx.x * SB_T + threadIdx.x;
-	if (i >= M)
+	const uint32_t i = blockIdx.x * SB_T + threadIdx.x; /* node s0b + i; accumulators i */
+	if (i >= sn)
 		return;
-	const SbNode nd = act[i];
+	const SbNode nd = act[s0b + i];
 	const uint32_t n = nd.e - nd.b;
 	const uint32_t *A = acc + (size_t)i * SB_ACC(nb);
 	float blo[3], bhi[3], clo[3], chi[3];
@@ -940,29 +942,31 @@ __global__ __launch_bounds__(SB_T) void k_sb_split(uint32_t M, uint32_t nb, uint
 		mode = 1;
 		nleft = n / 2;
 	}
-	dec[i] = make_uint4(mode | ((uint32_t)(best_axis < 0 ? 0 : best_axis) << 1), best_split, nleft, 0u);
-	nact[i] = (nleft >= 2 ? 1u : 0u) + (n - nleft >= 2 ? 1u : 0u);
+	dec[s0b + i] = make_uint4(mode | ((uint32_t)(best_axis < 0 ? 0 : best_axis) << 1), best_split, nleft, 0u);
+	nact[s0b + i] = (nleft >= 2 ? 1u : 0u) + (n - nleft >= 2 ? 1u : 0u);
 }
 
 /* left flags of the positions (stable partition by scan) */
-__global__ __launch_bounds__(SB_T) void k_sb_flags(uint32_t n, uint32_t nb, const uint32_t *__restrict__ seg,
-						    const uint32_t *__restrict__ pidx, const float *__restrict__ lo,
-						    const float *__restrict__ hi, const SbNode *__restrict__ act,
-						    const uint4 *__restrict__ dec, const uint32_t *__restrict__ acc,
-						    uint32_t *__restrict__ flag)
+__global__ __launch_bounds__(SB_T) void k_sb_flags(uint32_t n, uint32_t nb, uint32_t s0b, uint32_t sn,
+						    const uint32_t *__restrict__ seg, const uint32_t *__restrict__ pidx,
+						    const float *__restrict__ lo, const float *__restrict__ hi,
+						    const SbNode *__restrict__ act, const uint4 *__restrict__ dec,
+						    const uint32_t *__restrict__ acc, uint32_t *__restrict__ flag)
 {
 	const uint32_t q = blockIdx.x * SB_T + threadIdx.x;
 	if (q >= n)
 		return;
 	const uint32_t s = seg[q];
+	if (s == RTX_NONE || s - s0b >= sn) /* not this batch's (flags start at 0) */
+		return;
 	uint32_t f = 0;
-	if (s != RTX_NONE) {
+	{
 		const uint4 d = dec[s];
 		if (d.x & 1u) {
 			f = q - act[s].b < d.z ? 1u : 0u;
 		} else {
 			const uint32_t ax = d.x >> 1, p = pidx[q];
-			const uint32_t *A = acc + (size_t)s * SB_ACC(nb);
+			const uint32_t *A = acc + (size_t)(s - s0b) * SB_ACC(nb);
 			const float clo = o2f(A[6 + ax]), ext = o2f(A[9 + ax]) - clo;
 			const float k = (float)nb * (1.f - 1e-6f) / ext;
 			const float c = 0.5f * (lo[3 * (size_t)p + ax] + hi[3 * (size_t)p + ax]);
@@ -1088,7 +1092,7 @@ extern "C" hipError_t rtx_sah_build(uint32_t n, const float *d_lo, const float *
 	const uint32_t nb = bins;
 	std::vector<uint32_t> lev_off;
 	/* accumulators for at most this many nodes at a time */
-	const uint32_t chunk = 1u << 15;
+	const uint32_t chunk = 1u << 16;
 #define TRY(x)                                  \
 	do {                                    \
 		if ((e = (x)) != hipSuccess)    \
@@ -1135,23 +1139,28 @@ extern "C" hipError_t rtx_sah_build(uint32_t n, const float *d_lo, const float *
 			uint32_t M = 1, base = 0, id_next = n + 1;
 			lev_off.push_back(0);
 			while (M) {
-				if (M > chunk || lev_off.size() > 4096) { /* a level wider than the accumulators: not expected at n < 2^31 */
-					e = hipErrorInvalidValue;
+				if (lev_off.size() > 4096) { /* a level always splits every node: cannot happen */
+					e = hipErrorUnknown;
 					goto done;
 				}
 				SbNode *act = lev + base;
-				const size_t na = (size_t)M * SB_ACC(nb);
-				hipLaunchKernelGGL(k_sb_reset, dim3((uint32_t)((na + SB_T - 1) / SB_T)), dim3(SB_T), 0, st, M, nb, acc);
-				hipLaunchKernelGGL(k_sb_bounds, gn, dim3(SB_T), 0, st, n, nb, seg, pidx, d_lo, d_hi, acc);
-				hipLaunchKernelGGL(k_sb_bins, gn, dim3(SB_T), 0, st, n, nb, seg, pidx, d_lo, d_hi, acc);
+				TRY(hipMemsetAsync(flag, 0, (size_t)n * 4, st));
+				/* the level's nodes in batches of at most `chunk` (the accumulators) */
+				for (uint32_t s0b = 0; s0b < M; s0b += chunk) {
+					const uint32_t sn = std::min(chunk, M - s0b);
+					const size_t na = (size_t)sn * SB_ACC(nb);
+					hipLaunchKernelGGL(k_sb_reset, dim3((uint32_t)((na + SB_T - 1) / SB_T)), dim3(SB_T), 0, st, sn, nb, acc);
+					hipLaunchKernelGGL(k_sb_bounds, gn, dim3(SB_T), 0, st, n, nb, s0b, sn, seg, pidx, d_lo, d_hi, acc);
+					hipLaunchKernelGGL(k_sb_bins, gn, dim3(SB_T), 0, st, n, nb, s0b, sn, seg, pidx, d_lo, d_hi, acc);
+					hipLaunchKernelGGL(k_sb_split, dim3((sn + SB_T - 1) / SB_T), dim3(SB_T), 0, st, sn, s0b, nb, max_leaf,
+							   max_depth, c_trav, c_isect, act, acc, dec, nact, nb6, cnt);
+					hipLaunchKernelGGL(k_sb_flags, gn, dim3(SB_T), 0, st, n, nb, s0b, sn, seg, pidx, d_lo, d_hi, act, dec, acc,
+							   flag);
+					TRY(hipGetLastError());
+				}
 				const dim3 gm((M + SB_T - 1) / SB_T);
-				hipLaunchKernelGGL(k_sb_split, gm, dim3(SB_T), 0, st, M, nb, max_leaf, max_depth, c_trav, c_isect, act, acc, dec,
-						   nact, nb6, cnt);
-				TRY(hipGetLastError());
 				TRY(hipMemsetAsync(nact + M, 0, 4, st));
 				TRY(hipcub::DeviceScan::ExclusiveSum(temp, tb2, nact, off, (int)M + 1, st));
-				hipLaunchKernelGGL(k_sb_flags, gn, dim3(SB_T), 0, st, n, nb, seg, pidx, d_lo, d_hi, act, dec, acc, flag);
-				TRY(hipGetLastError());
 				TRY(hipcub::DeviceScan::ExclusiveSum(temp, tb, flag, scan, (int)n, st));
 				hipLaunchKernelGGL(k_sb_children, gm, dim3(SB_T), 0, st, M, n, id_next, act, dec, off, lev + base + M, kids, par);
 				hipLaunchKernelGGL(k_sb_scatter, gn, dim3(SB_T), 0, st, n, seg, pidx, act, dec, flag, scan, off, pidx2, seg2);

@@ -44,7 +44,7 @@ template <class T> static inline int upload(T *&dst, const std::vector<T> &v)
 
 struct rtx_ctx {
 	int device = 0;
-	int builder = RTX_BUILD_SAH_HOST;
+	int builder = RTX_BUILD_SAH_GPU; /* the host's SAH tree, built on the device (57 vs 296 ms on the dragon) */
 	hipStream_t stream = nullptr;
 	hipEvent_t ev0 = nullptr, ev1 = nullptr;
 	int cus = 0;
@@ -76,6 +76,10 @@ struct rtx_ctx {
 	size_t contrib_bytes = 0;
 	uint2 *d_tile_rec = nullptr;
 	size_t tile_rec_bytes = 0;
+	/* shade points per tile seen by the last render of this scene with the same GI / bounce
+	 * settings: sizes the next render's chunks (the static estimate is 5x too high on scene6) */
+	double sp_tile_seen = 0.0;
+	uint64_t sp_tile_key = 0;
 	uint32_t *d_sortbuf = nullptr; /* keys0 | keys1 | vals0 | vals1 (shade-point sort) */
 	size_t sortbuf_bytes = 0;
 	void *d_sorttmp = nullptr;

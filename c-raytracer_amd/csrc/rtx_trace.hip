@@ -163,7 +163,7 @@ __device__ void trace_closest_bvh2(const DScene &S, uint32_t *stk, bool act, f3 
  * against the current closest t.  The emitters the tree leaves out (DScene.w8noemit) are
  * tested before the walk.  Strict < everywhere: the first hit found at the least t wins. */
 #ifndef RTX_TRACE_NEAR
-#define RTX_TRACE_NEAR 0 /* closest hits: visit the nearest hit inner child first */
+#define RTX_TRACE_NEAR 1 /* closest hits: visit the nearest hit inner child first (scene6 k_trace 605 -> 417 ms) */
 #endif
 #ifndef RTX_TRACE_CULL
 #define RTX_TRACE_CULL 0 /* closest hits: drop kept sibling groups that start beyond the closest hit */

@@ -213,7 +213,8 @@ class Renderer:
         self.device = device
 
     def set_builder(self, builder):
-        """rtx_set_builder: abi.RTX_BUILD_SAH_HOST (default), abi.RTX_BUILD_LBVH_GPU or abi.RTX_BUILD_PLOC_GPU."""
+        """rtx_set_builder: abi.RTX_BUILD_SAH_GPU (default), abi.RTX_BUILD_SAH_HOST, abi.RTX_BUILD_LBVH_GPU or
+        abi.RTX_BUILD_PLOC_GPU."""
         _check(self.lib.rtx_set_builder(self._ctx, builder))
 
     def set_option(self, option, value):

@@ -28,7 +28,7 @@ def renderer():
 @pytest.fixture(autouse=True)
 def _defaults(renderer):
     yield
-    renderer.set_builder(abi.RTX_BUILD_SAH_HOST)
+    renderer.set_builder(abi.RTX_BUILD_SAH_GPU)
     renderer.set_option(abi.RTX_OPT_SHADOW_WALK, abi.RTX_WALK_AUTO)
     renderer.set_option(abi.RTX_OPT_BVH_LEAF, 1)
 
@@ -83,7 +83,7 @@ def test_gpu_builder_deterministic_and_tiny_scenes(renderer, builder):
     assert ok, info
     with pytest.raises(rtxpy.RtxError):
         renderer.set_builder(7)
-    renderer.set_builder(abi.RTX_BUILD_SAH_HOST)
+    renderer.set_builder(abi.RTX_BUILD_SAH_GPU)
 
 
 @pytest.mark.parametrize("leaf", [2, 4])
@@ -106,8 +106,8 @@ def test_gpu_ploc_multi_primitive_leaves(renderer, leaf):
 def test_gpu_sah_device_builds_the_host_tree(renderer, name):
     """RTX_BUILD_SAH_GPU runs bvh_build.cpp's binned SAH on the device (same bins, same float
     costs, same split order): with single-primitive leaves it builds the host's tree node for node,
-    so the 8-wide collapse, every traversal count and every pixel are the same as over the host
-    build (the dragon and Menger stand-ins included)."""
+    so the 8-wide collapse, every per-ray traversal count and every pixel are the same as over the
+    host build (the dragon and Menger stand-ins included)."""
     scene, frame, params, _ = C.load_config(name)
     params.count_traversal = 1
     out = {}
@@ -120,7 +120,8 @@ def test_gpu_sah_device_builds_the_host_tree(renderer, name):
     b, zb, sb = out[abi.RTX_BUILD_SAH_GPU]
     assert sb.builder == abi.RTX_BUILD_SAH_GPU
     for f in ("bvh_nodes", "bvh_prims", "bvh_depth", "wide_nodes", "wide_depth", "shadow_walk", "closest_rays",
-              "shadow_rays", "node_visits", "tri_tests", "sphere_tests", "shadow_box_tests", "shadow_wave_steps",
-              "shadow_leaf_rounds", "shadow_uniform_steps"):
+              "shadow_rays", "node_visits", "tri_tests", "sphere_tests", "shadow_box_tests"):
+        # per-ray work sums; wave-level counts (steps, leaf rounds) depend on which shade points share
+        # a wave, i.e. on k_trace's emission order, which varies between runs
         assert getattr(sa, f) == getattr(sb, f), (name, f, getattr(sa, f), getattr(sb, f))
     assert np.array_equal(a, b) and np.array_equal(za, zb), name

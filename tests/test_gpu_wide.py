@@ -32,7 +32,7 @@ def renderer():
 @pytest.fixture(autouse=True)
 def _defaults(renderer):
     yield
-    renderer.set_builder(abi.RTX_BUILD_SAH_HOST)
+    renderer.set_builder(abi.RTX_BUILD_SAH_GPU)
     renderer.set_option(abi.RTX_OPT_SHADOW_WALK, abi.RTX_WALK_AUTO)
     renderer.set_option(abi.RTX_OPT_BVH_LEAF, 1)
     renderer.set_option(abi.RTX_OPT_SHADOW_LDS_STACK, 8)
