@@ -408,6 +408,8 @@ def workload(a):
     if a.scene == "scene5" and (a.width, a.height, a.spp) == (1920, 1080, 256):
         name, spp = "configs[3]", 256
     label = f"{a.scene} {a.width}x{a.height}" + ("" if a.scene == "scene1" else f" -g path -n {a.spp}")
+    if a.scene == "scene5_l8" and (a.width, a.height, a.spp) == (1920, 1080, 64):
+        return f"{label} (SURVEY 8(d) level-8 dragon bracket of BASELINE configs[2])"
     return f"{label} (BASELINE {name})" if name and (spp is None or spp == a.spp) else f"{label} (custom)"
 
 
