@@ -318,23 +318,24 @@ def shadow_roofline(r, frame, params, d_rgb, d_z, stream, shadow_ms, a, world):
     except (OSError, ValueError):
         rec = None
     if rec:
-        # the PMC passes average over k_shadow launches; a frame of several chunks launches it once
-        # per chunk, and the counts here (and dur) are the frame's
+        # the counts here (and dur) are the frame's: the PMC summary's per-frame sums (a frame of
+        # several chunks launches k_shadow once per chunk), else launches x the per-launch mean
         nl = max(1, int(c.chunks))
         out["pmc"] = {"source": rec.get("source"), "kernel_src_sha": rec.get("kernel_src_sha"),
                       "matches_this_kernel": rec.get("kernel_src_sha") == shadow_src_sha(), "launches_per_frame": nl}
         if "hbm_bytes_per_launch" in rec:
-            hbm = nl * rec["hbm_bytes_per_launch"]
+            hbm = rec.get("hbm_bytes_per_frame", nl * rec["hbm_bytes_per_launch"])
             out["traffic"] = int(hbm)
             out["hbm"] = {"bytes_per_launch": int(hbm),
                           "achieved": round(hbm / dur / 1e9, 1), "peak": HBM_PEAK_GBS,
                           "unit": "GB/s", "frac": round(hbm / dur / 1e9 / HBM_PEAK_GBS, 4),
                           "source": "PMC 2*FETCH_SIZE + WRITE_SIZE (L2 -> fabric, gfx950 correction)"}
         if "sq_insts_valu" in rec:
-            issued = nl * rec["sq_insts_valu"] / dur / 1e9
+            valu = rec.get("sq_insts_valu_frame", nl * rec["sq_insts_valu"])  # per frame when recorded
+            issued = valu / dur / 1e9
             out["issued"] = round(issued, 1)
             out["issued_frac"] = round(issued / VALU_PEAK_GINST, 4)
-            out["useful_over_issued"] = round(useful / (nl * rec["sq_insts_valu"]), 4)
+            out["useful_over_issued"] = round(useful / valu, 4)
         if "ta_busy_frac" in rec:
             out["vmem"] = {"ta_busy_frac": rec["ta_busy_frac"], "td_busy_frac": rec.get("td_busy_frac"),
                            "note": "PMC TA_TA_BUSY / TD_TD_BUSY per CU cycle: the vector-memory address / data "
