@@ -95,23 +95,9 @@ __device__ __forceinline__ bool w8_slab_tn(float lx, float hx, float ly, float h
 	tn_out = tn;
 	return tn <= tf;
 }
-/* U (the shadow walk, RTX_W8_UNIT): t is measured in units of the segment length (the ray
- * transform scaled by 1 / tl), and the segment (0, 1) is applied by the clamp output modifier of
- * v_max3 / v_min3: hit iff clamp(tn) < clamp(tf).  Strict, because a clamped box beyond either
- * end compares equal; a box a blocking primitive lies in overlaps the segment over a positive
- * length (leaf boxes are padded before the outward 8-bit rounding), so no hit is lost. */
-template <int OCT, bool U = false>
+template <int OCT>
 __device__ __forceinline__ bool w8_slab(float lx, float hx, float ly, float hy, float lz, float hz, float tl)
 {
-	if (U && OCT != 8) {
-		const float nx = (OCT & 1) ? lx : hx, fx = (OCT & 1) ? hx : lx;
-		const float ny = (OCT & 2) ? ly : hy, fy = (OCT & 2) ? hy : ly;
-		const float nz = (OCT & 4) ? lz : hz, fz = (OCT & 4) ? hz : lz;
-		float tn, tf;
-		asm("v_max3_f32 %0, %1, %2, %3 clamp" : "=v"(tn) : "v"(nx), "v"(ny), "v"(nz));
-		asm("v_min3_f32 %0, %1, %2, %3 clamp" : "=v"(tf) : "v"(fx), "v"(fy), "v"(fz));
-		return tn < tf;
-	}
 	if (OCT == 8) {
 		const float tn = fmaxf(fmaxf(fminf(lx, hx), fminf(ly, hy)), fmaxf(fminf(lz, hz), 0.f));
 		const float tf = fminf(fminf(fmaxf(lx, hx), fmaxf(ly, hy)), fminf(fmaxf(lz, hz), tl));
@@ -129,7 +115,7 @@ __device__ __forceinline__ bool w8_slab(float lx, float hx, float ly, float hy, 
 #define RTX_W8_PK 0 /* measurement option: an axis's two planes in one v_pk_fma_f32 (the same fused results) */
 #endif
 typedef float f2v __attribute__((ext_vector_type(2)));
-template <int OCT, int C, bool U = false>
+template <int OCT, int C>
 __device__ __forceinline__ bool w8_child(const uint32_t (&w)[16], f3 s, f3 b, float tl)
 {
 	constexpr int W = C >> 2, B = C & 3;
@@ -140,15 +126,15 @@ __device__ __forceinline__ bool w8_child(const uint32_t (&w)[16], f3 s, f3 b, fl
 							(f2v){ b.y, b.y });
 		const f2v z = __builtin_elementwise_fma((f2v){ ubyte<B>(w[12 + W]), ubyte<B>(w[14 + W]) }, (f2v){ s.z, s.z },
 							(f2v){ b.z, b.z });
-		return w8_slab<OCT, U>(x.x, x.y, y.x, y.y, z.x, z.y, tl);
+		return w8_slab<OCT>(x.x, x.y, y.x, y.y, z.x, z.y, tl);
 	}
-	return w8_slab<OCT, U>(fmaf(ubyte<B>(w[4 + W]), s.x, b.x), fmaf(ubyte<B>(w[6 + W]), s.x, b.x),
+	return w8_slab<OCT>(fmaf(ubyte<B>(w[4 + W]), s.x, b.x), fmaf(ubyte<B>(w[6 + W]), s.x, b.x),
 			    fmaf(ubyte<B>(w[8 + W]), s.y, b.y), fmaf(ubyte<B>(w[10 + W]), s.y, b.y),
 			    fmaf(ubyte<B>(w[12 + W]), s.z, b.z), fmaf(ubyte<B>(w[14 + W]), s.z, b.z), tl);
 }
 /* the same child test on the scalar-path copy (rtx_device.h DW8S): the plane offsets are ready
  * floats, the same values the conversions above produce, so the results are bit-identical */
-template <int OCT, int C, bool U = false>
+template <int OCT, int C>
 __device__ __forceinline__ bool w8_child_s(const uint32_t (&q)[24], f3 s, f3 b, float tl)
 {
 	/* plane k's offset of child C: the half in word 4k + C/2, half C & 1 (v_fma_mix_f32 op_sel) */
@@ -156,7 +142,7 @@ __device__ __forceinline__ bool w8_child_s(const uint32_t (&q)[24], f3 s, f3 b, 
 		const uint32_t v = q[4 * k + (C >> 1)];
 		return (float)__builtin_bit_cast(_Float16, (uint16_t)((C & 1) ? (v >> 16) : (v & 0xFFFFu)));
 	};
-	return w8_slab<OCT, U>(fmaf(h(0), s.x, b.x), fmaf(h(1), s.x, b.x), fmaf(h(2), s.y, b.y), fmaf(h(3), s.y, b.y),
+	return w8_slab<OCT>(fmaf(h(0), s.x, b.x), fmaf(h(1), s.x, b.x), fmaf(h(2), s.y, b.y), fmaf(h(3), s.y, b.y),
 			    fmaf(h(4), s.z, b.z), fmaf(h(5), s.z, b.z), tl);
 }
 
@@ -170,18 +156,18 @@ __device__ __forceinline__ void w8_frame(const uint32_t (&w)[16], f3 invq, f3 oi
 }
 
 /* hit mask of an 8-wide node's children in visit order: bit p for slot p ^ K */
-template <int OCT, uint32_t K, bool U = false>
+template <int OCT, uint32_t K>
 __device__ __forceinline__ uint32_t w8_hits(const uint32_t (&w)[16], f3 s, f3 b, float tl)
 {
 	uint32_t hm = 0;
-	hm |= w8_child<OCT, 0, U>(w, s, b, tl) ? 1u << (0 ^ K) : 0u;
-	hm |= w8_child<OCT, 1, U>(w, s, b, tl) ? 1u << (1 ^ K) : 0u;
-	hm |= w8_child<OCT, 2, U>(w, s, b, tl) ? 1u << (2 ^ K) : 0u;
-	hm |= w8_child<OCT, 3, U>(w, s, b, tl) ? 1u << (3 ^ K) : 0u;
-	hm |= w8_child<OCT, 4, U>(w, s, b, tl) ? 1u << (4 ^ K) : 0u;
-	hm |= w8_child<OCT, 5, U>(w, s, b, tl) ? 1u << (5 ^ K) : 0u;
-	hm |= w8_child<OCT, 6, U>(w, s, b, tl) ? 1u << (6 ^ K) : 0u;
-	hm |= w8_child<OCT, 7, U>(w, s, b, tl) ? 1u << (7 ^ K) : 0u;
+	hm |= w8_child<OCT, 0>(w, s, b, tl) ? 1u << (0 ^ K) : 0u;
+	hm |= w8_child<OCT, 1>(w, s, b, tl) ? 1u << (1 ^ K) : 0u;
+	hm |= w8_child<OCT, 2>(w, s, b, tl) ? 1u << (2 ^ K) : 0u;
+	hm |= w8_child<OCT, 3>(w, s, b, tl) ? 1u << (3 ^ K) : 0u;
+	hm |= w8_child<OCT, 4>(w, s, b, tl) ? 1u << (4 ^ K) : 0u;
+	hm |= w8_child<OCT, 5>(w, s, b, tl) ? 1u << (5 ^ K) : 0u;
+	hm |= w8_child<OCT, 6>(w, s, b, tl) ? 1u << (6 ^ K) : 0u;
+	hm |= w8_child<OCT, 7>(w, s, b, tl) ? 1u << (7 ^ K) : 0u;
 	if (OCT == 8)
 		hm &= w[3]; /* K = 0: slot order; the min/max form would turn an empty slot's box around */
 	return hm;
@@ -189,25 +175,25 @@ __device__ __forceinline__ uint32_t w8_hits(const uint32_t (&w)[16], f3 s, f3 b,
 #ifndef RTX_W8_SKIP
 #define RTX_W8_SKIP 0 /* scalar path: branch over the empty slots (the slot mask is wave-uniform) */
 #endif
-template <int OCT, uint32_t K, int C, bool U = false>
+template <int OCT, uint32_t K, int C>
 __device__ __forceinline__ uint32_t w8_hit_s(const uint32_t (&q)[24], uint32_t w3, f3 s, f3 b, float tl)
 {
 	if (RTX_W8_SKIP && !((w3 >> C) & 1u))
 		return 0u;
-	return w8_child_s<OCT, C, U>(q, s, b, tl) ? 1u << (C ^ K) : 0u;
+	return w8_child_s<OCT, C>(q, s, b, tl) ? 1u << (C ^ K) : 0u;
 }
-template <int OCT, uint32_t K, bool U = false>
+template <int OCT, uint32_t K>
 __device__ __forceinline__ uint32_t w8_hits_s(const uint32_t (&q)[24], uint32_t w3, f3 s, f3 b, float tl)
 {
 	uint32_t hm = 0;
-	hm |= w8_hit_s<OCT, K, 0, U>(q, w3, s, b, tl);
-	hm |= w8_hit_s<OCT, K, 1, U>(q, w3, s, b, tl);
-	hm |= w8_hit_s<OCT, K, 2, U>(q, w3, s, b, tl);
-	hm |= w8_hit_s<OCT, K, 3, U>(q, w3, s, b, tl);
-	hm |= w8_hit_s<OCT, K, 4, U>(q, w3, s, b, tl);
-	hm |= w8_hit_s<OCT, K, 5, U>(q, w3, s, b, tl);
-	hm |= w8_hit_s<OCT, K, 6, U>(q, w3, s, b, tl);
-	hm |= w8_hit_s<OCT, K, 7, U>(q, w3, s, b, tl);
+	hm |= w8_hit_s<OCT, K, 0>(q, w3, s, b, tl);
+	hm |= w8_hit_s<OCT, K, 1>(q, w3, s, b, tl);
+	hm |= w8_hit_s<OCT, K, 2>(q, w3, s, b, tl);
+	hm |= w8_hit_s<OCT, K, 3>(q, w3, s, b, tl);
+	hm |= w8_hit_s<OCT, K, 4>(q, w3, s, b, tl);
+	hm |= w8_hit_s<OCT, K, 5>(q, w3, s, b, tl);
+	hm |= w8_hit_s<OCT, K, 6>(q, w3, s, b, tl);
+	hm |= w8_hit_s<OCT, K, 7>(q, w3, s, b, tl);
 	if (OCT == 8 && !RTX_W8_SKIP)
 		hm &= w3;
 	return hm;
@@ -221,13 +207,13 @@ __device__ __forceinline__ uint32_t w8_hits_s(const uint32_t (&q)[24], uint32_t 
 struct W8Visit {
 	uint32_t hm, base, io, to, nv;
 };
-template <int OCT, uint32_t K, bool UNI, bool U = false>
+template <int OCT, uint32_t K, bool UNI>
 __device__ __forceinline__ W8Visit w8_visit(const uint32_t (&w)[16], f3 invq, f3 oi, float tl)
 {
 	f3 s, b;
 	w8_frame(w, invq, oi, s, b);
 	W8Visit v;
-	v.hm = w8_hits<OCT, K, U>(w, s, b, tl);
+	v.hm = w8_hits<OCT, K>(w, s, b, tl);
 	v.base = w[2] >> 8;
 	v.io = perm_xor<K>(w[2] & 0xFFu);
 	v.to = perm_xor<K>((w[3] >> 8) & 0xFFu);
@@ -238,7 +224,7 @@ __device__ __forceinline__ W8Visit w8_visit(const uint32_t (&w)[16], f3 invq, f3
 }
 
 /* the same visit on the scalar-path copy (every walking lane at the node: SGPR operands) */
-template <int OCT, uint32_t K, bool U = false>
+template <int OCT, uint32_t K>
 __device__ __forceinline__ W8Visit w8_visit_s(const DW8S *n, f3 invq, f3 oi, float tl)
 {
 	typedef uint32_t u16v __attribute__((ext_vector_type(16)));
@@ -257,7 +243,7 @@ __device__ __forceinline__ W8Visit w8_visit_s(const DW8S *n, f3 invq, f3 oi, flo
 			 ldexpf(invq.z, (int)((w1 >> 24) & 15u)));
 	const f3 b = mk3(fmaf(org0, invq.x, -oi.x), fmaf(org1, invq.y, -oi.y), fmaf(org2, invq.z, -oi.z));
 	W8Visit v;
-	v.hm = w8_hits_s<OCT, K, U>(q, w3, s, b, tl);
+	v.hm = w8_hits_s<OCT, K>(q, w3, s, b, tl);
 	v.base = w2 >> 8;
 	v.io = perm_xor<K>(w2 & 0xFFu);
 	v.to = perm_xor<K>((w3 >> 8) & 0xFFu);
