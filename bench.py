@@ -70,6 +70,8 @@ def parse():
                     help="closest-hit BVH layout (rtx_set_option RTX_OPT_TRACE_WALK)")
     ap.add_argument("--shadow-slot", type=int, default=0,
                     help="k_shadow lanes per shade-point slot (rtx_set_option RTX_OPT_SHADOW_SLOT; 0 = automatic)")
+    ap.add_argument("--shadow-grab", type=int, default=0,
+                    help="k_shadow lane slots per work-queue grab (RTX_OPT_SHADOW_GRAB; 0 = library default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the traversal-counting pass (roofline)")
     ap.add_argument("--no-post", action="store_true", help="skip the postprocess (DoF + mist) side leg")
@@ -469,6 +471,8 @@ def main():
     r.set_option(abi.RTX_OPT_SHADOW_WALK, WALKS[a.walk])
     r.set_option(abi.RTX_OPT_TRACE_WALK, WALKS[a.trace_walk])
     r.set_option(abi.RTX_OPT_SHADOW_SLOT, a.shadow_slot)
+    if a.shadow_grab:
+        r.set_option(abi.RTX_OPT_SHADOW_GRAB, a.shadow_grab)
     t0 = time.perf_counter()
     r.upload(scene)
     st = r.stats()
@@ -660,6 +664,9 @@ def main_group(a):
     n = g.size()
     g.set_option(abi.RTX_OPT_SHADOW_WALK, WALKS[a.walk])
     g.set_option(abi.RTX_OPT_TRACE_WALK, WALKS[a.trace_walk])
+    g.set_option(abi.RTX_OPT_SHADOW_SLOT, a.shadow_slot)
+    if a.shadow_grab:
+        g.set_option(abi.RTX_OPT_SHADOW_GRAB, a.shadow_grab)
     t0 = time.perf_counter()
     g.upload(scene)
     log(f"{n} devices, scene {os.path.basename(path)} uploaded in {time.perf_counter() - t0:.2f}s")

@@ -221,7 +221,10 @@ __device__ __forceinline__ uint32_t w8_hits_s(const uint32_t (&q)[24], uint32_t 
 }
 
 #ifndef RTX_W8_ORDER
-#define RTX_W8_ORDER 1 /* visit hit children in the octant's slot order (0: plain slot order) */
+#define RTX_W8_ORDER 1 /* closest hits (k_trace): visit hit children in the octant's slot order (0: plain slot order) */
+#endif
+#ifndef RTX_W8_SORDER
+#define RTX_W8_SORDER 0 /* any-hit (k_shadow): the octant's slot order; plain slot order saves the mask permutes */
 #endif
 
 /* one 8-wide node visit's box tests: the hit mask in visit order and the node's masks */
@@ -325,6 +328,8 @@ template <int OCT, uint32_t K, int C, bool SC>
 __device__ __forceinline__ void w8_child_t(const uint32_t *w, f3 s, f3 b, float tl, uint32_t io, uint32_t &hm, uint32_t &near,
 					   float &tin)
 {
+	if (SC && RTX_W8_SKIP && !(((io >> 8) >> C) & 1u)) /* an empty slot (wave-uniform on the scalar path) */
+		return;
 	float l[6];
 	if (SC) {
 #pragma unroll
