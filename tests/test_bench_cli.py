@@ -40,7 +40,8 @@ def test_workload_labels_name_the_baseline_config():
     A = type("A", (), {})
     for scene, w, h, spp, want in [("scene5", 1920, 1080, 64, "configs[2]"), ("scene3", 1920, 1080, 16, "configs[1]"),
                                    ("scene6", 3840, 2160, 128, "configs[4]"), ("scene5", 1920, 1080, 256, "configs[3]"),
-                                   ("scene1", 512, 512, 64, "configs[0]"), ("scene5", 960, 540, 64, "custom")]:
+                                   ("scene1", 512, 512, 64, "configs[0]"), ("scene5", 960, 540, 64, "custom"),
+                                   ("scene5_l8", 1920, 1080, 64, "level-8 dragon bracket")]:
         a = A()
         a.scene, a.width, a.height, a.spp = scene, w, h, spp
         assert want in b.workload(a), (scene, b.workload(a))
@@ -54,3 +55,27 @@ def test_workload_labels_name_the_baseline_config():
 def test_gpus_flag_must_match_torchrun_world():
     p = run(["--gpus", "2", "--dry-run"], {"WORLD_SIZE": "3", "RANK": "0"})
     assert p.returncode == 2 and "WORLD_SIZE=3" in p.stderr
+
+
+def test_pmc_summary_sums_a_chunked_frame(tmp_path, monkeypatch):
+    """tools/pmc_summary.py: a frame rendered in two chunks launches k_shadow twice with unequal
+    work; the per-frame counts the bench's roofline uses are the sum over the launches, not
+    twice the mean of one (both agree only for equal chunks)."""
+    import importlib.util
+    import csv
+    spec = importlib.util.spec_from_file_location("pmc_summary", os.path.join(ROOT, "tools", "pmc_summary.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    d = tmp_path / "pmc"
+    d.mkdir()
+    with open(d / "run_counter_collection.csv", "w", newline="") as fh:
+        w = csv.DictWriter(fh, fieldnames=["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
+        w.writeheader()
+        for disp, v in ((1, 1631.0), (2, 701.0)):
+            w.writerow({"Dispatch_Id": disp, "Kernel_Name": "void k_shadow<false, 8, 2>(KShadow)",
+                        "Counter_Name": "SQ_INSTS_VALU", "Counter_Value": v})
+        w.writerow({"Dispatch_Id": 3, "Kernel_Name": "k_trace", "Counter_Name": "SQ_INSTS_VALU", "Counter_Value": 5.0})
+    mean, n = m.per_launch(str(d), "k_shadow")
+    assert n == 2 and mean["SQ_INSTS_VALU"] == 1166.0
+    assert m.per_frame(str(d), "k_shadow", 1)["SQ_INSTS_VALU"] == 2332.0
+    assert m.per_frame(str(d), "k_shadow", 2)["SQ_INSTS_VALU"] == 1166.0
