@@ -64,10 +64,12 @@ def parse():
     ap.add_argument("--launch", default="group", choices=["group", "torchrun"],
                     help="--gpus N > 1 without torchrun: one process driving the C-ABI device group "
                          "(default), or N torchrun ranks")
-    ap.add_argument("--walk", default="auto", choices=["auto", "w8", "w4", "bvh2"],
+    ap.add_argument("--walk", default="auto", choices=["auto", "w8", "bvh2"],
                     help="shadow-walk BVH layout (rtx_set_option RTX_OPT_SHADOW_WALK; auto = the library default)")
     ap.add_argument("--trace-walk", default="auto", choices=["auto", "w8", "bvh2"],
                     help="closest-hit BVH layout (rtx_set_option RTX_OPT_TRACE_WALK)")
+    ap.add_argument("--frame", default="auto", choices=["auto", "world"],
+                    help="the frame the BVHs are built in (rtx_set_option RTX_OPT_TREE_FRAME; auto = the library default)")
     ap.add_argument("--shadow-slot", type=int, default=0,
                     help="k_shadow lanes per shade-point slot (rtx_set_option RTX_OPT_SHADOW_SLOT; 0 = automatic)")
     ap.add_argument("--shadow-grab", type=int, default=0,
@@ -426,7 +428,13 @@ def data_label(a):
     return f"the reference's own scenes/{a.scene}.json (no mesh)"
 
 
-WALKS = {"auto": -1, "w8": 2, "w4": 1, "bvh2": 0}
+WALKS = {"auto": -1, "w8": 2, "bvh2": 0}
+FRAMES = {"auto": 0, "world": 1}
+
+
+def walk_name(w):
+    from rtxpy import abi
+    return abi.WALK_NAMES.get(int(w), str(w))
 
 
 def main():
@@ -471,13 +479,15 @@ def main():
     r.set_option(abi.RTX_OPT_SHADOW_WALK, WALKS[a.walk])
     r.set_option(abi.RTX_OPT_TRACE_WALK, WALKS[a.trace_walk])
     r.set_option(abi.RTX_OPT_SHADOW_SLOT, a.shadow_slot)
+    r.set_option(abi.RTX_OPT_TREE_FRAME, FRAMES[a.frame])
     if a.shadow_grab:
         r.set_option(abi.RTX_OPT_SHADOW_GRAB, a.shadow_grab)
     t0 = time.perf_counter()
     r.upload(scene)
     st = r.stats()
     log(f"scene {os.path.basename(path)}: {scene.num_objects} objects, BVH {st.bvh_nodes} nodes depth {st.bvh_depth}, "
-        f"shadow walk {['bvh2', 'w4', 'w8'][st.shadow_walk]}: {st.wide_nodes} wide nodes depth {st.wide_depth} "
+        f"shadow walk {walk_name(st.shadow_walk)}: {st.wide_nodes} wide nodes depth {st.wide_depth}, "
+        f"tree frame {'rotated' if st.tree_rotated else 'world'} (leaf-box cost x{st.frame_cost:.3f}) "
         f"({time.perf_counter() - t0:.2f}s build+upload)")
 
     npx = a.width * a.height
@@ -566,7 +576,7 @@ def main():
             d = names[int(st.builder)]
             build = {"default": d, f"{d}_ms": round(st.build_ms, 1), f"{d}_nodes": int(st.bvh_nodes),
                      f"{d}_depth": int(st.bvh_depth), f"{d}_wide_nodes": int(st.wide_nodes),
-                     f"{d}_wide_depth": int(st.wide_depth), f"{d}_shadow_walk": ["bvh2", "w4", "w8"][st.shadow_walk],
+                     f"{d}_wide_depth": int(st.wide_depth), f"{d}_shadow_walk": walk_name(st.shadow_walk),
                      f"{d}_shadow_ms": round(float(np.mean(sms)), 1)}
             for bid, tag in names.items():
                 if bid == int(st.builder):
@@ -577,7 +587,7 @@ def main():
                 build.update({f"{tag}_ms": round(sl.build_ms, 1), f"{tag}_nodes": int(sl.bvh_nodes),
                               f"{tag}_depth": int(sl.bvh_depth), f"{tag}_wide_nodes": int(sl.wide_nodes),
                               f"{tag}_wide_depth": int(sl.wide_depth),
-                              f"{tag}_shadow_walk": ["bvh2", "w4", "w8"][sl.shadow_walk]})
+                              f"{tag}_shadow_walk": walk_name(sl.shadow_walk)})
                 r.render_device(frame, params, d_rgb.data_ptr(), d_z.data_ptr(), stream.cuda_stream)
                 build[f"{tag}_shadow_ms"] = round(r.stats().shadow_ms, 1)
                 build[f"{tag}_trace_ms"] = round(r.stats().trace_ms, 1)
@@ -618,8 +628,10 @@ def main():
                           "closest_rays_rank0": stats_closest, "shadow_rays_rank0": stats_shadow,
                           "parallelism": f"tiles{world}", "launch": "torchrun" if world > 1 else "single",
                           "kernel_ms_rank0": round(kernel_ms, 3), "kernels_rank0": split,
-                          "shadow_walk": ["bvh2", "w4", "w8"][st.shadow_walk],
-                          "trace_walk": ["bvh2", "w4", "w8"][s.trace_walk],
+                          "shadow_walk": walk_name(st.shadow_walk),
+                          "trace_walk": walk_name(s.trace_walk),
+                          "tree_frame": {"rotated": bool(st.tree_rotated), "leaf_box_cost_vs_world": round(st.frame_cost, 4),
+                                         "choose_ms": round(st.frame_ms, 1)},
                           "step": "render into HBM, tile shards gathered to rank 0 over RCCL (N > 1), frame copied "
                                   "to pinned host memory (SURVEY 8(d): render window up to the framebuffer on the host)",
                           "rng": "counter, stratified light samples (library default)"},
@@ -665,6 +677,7 @@ def main_group(a):
     g.set_option(abi.RTX_OPT_SHADOW_WALK, WALKS[a.walk])
     g.set_option(abi.RTX_OPT_TRACE_WALK, WALKS[a.trace_walk])
     g.set_option(abi.RTX_OPT_SHADOW_SLOT, a.shadow_slot)
+    g.set_option(abi.RTX_OPT_TREE_FRAME, FRAMES[a.frame])
     if a.shadow_grab:
         g.set_option(abi.RTX_OPT_SHADOW_GRAB, a.shadow_grab)
     t0 = time.perf_counter()

@@ -18,6 +18,7 @@
 #include "bvh_build.h"
 #include "rtx.h"
 #include "rtx_device.h"
+#include "rtx_frame.h"
 #include "rtx_kat.h"
 #include "rtx_quant.h"
 #include "rtx_internal.h"
@@ -60,7 +61,8 @@ extern "C" hipError_t rtx_launch_accum(const DFrame *F, const DParams *P, const 
 				       hipStream_t stream);
 extern "C" hipError_t rtx_launch_kat(int kind, uint32_t n, const float *in, float *out, int u32mode,
 				     hipStream_t stream);
-extern "C" hipError_t rtx_launch_pack_tris(const DPrim *prims, uint32_t n, float4 *out, hipStream_t stream);
+extern "C" hipError_t rtx_launch_find_prims(const DPrim *prims, uint32_t n, const uint32_t *objs, uint32_t nobj, uint32_t *out,
+					     hipStream_t stream);
 extern "C" hipError_t rtx_launch_kat_shadow(int kind, uint32_t n, const float *in, float *out, hipStream_t stream);
 extern "C" hipError_t rtx_launch_w8_fill(const DPrim *prims, const DMaterial *mats, const uint32_t *leafmap, uint32_t n, DW8 *out,
 					  hipStream_t stream);
@@ -120,13 +122,11 @@ static void free_scene(rtx_ctx *c)
 	dfree(c->d_emitters);
 	dfree(c->d_qnodes);
 	dfree(c->d_top);
-	dfree(c->d_wnodes);
-	dfree(c->d_wtris);
 	dfree(c->d_w8);
 	dfree(c->d_w8s);
 	c->have_scene = false;
 	c->sp_tile_seen = 0.0;
-	c->sp_tile_key = 0;
+	c->sp_tile_key = SpKey{};
 }
 
 extern "C" void rtx_close(rtx_ctx *c)
@@ -308,109 +308,6 @@ static uint32_t thread_top(const std::vector<DQNode> &q, const std::vector<uint3
 	return nt;
 }
 
-/* The 4-wide shadow-walk BVH (rtx_device.h RTX_W_STACK): each wide node collapses its BVH2
- * node's subtree top, repeatedly opening the inner child of largest surface area until it has
- * four children (the usual SAH-driven collapse).  Inner children come first in a node's slots
- * and are allocated as consecutive nodes, depth first.  Returns the wide tree's depth. */
-struct WKid {
-	uint32_t ref;
-	float lo[3], hi[3];
-};
-
-static float half_area(const WKid &k)
-{
-	const float dx = k.hi[0] - k.lo[0], dy = k.hi[1] - k.lo[1], dz = k.hi[2] - k.lo[2];
-	return dx * dy + dy * dz + dz * dx;
-}
-
-static void wide_kids(const std::vector<DNode> &recs, uint32_t ref, WKid kids[4], uint32_t &n)
-{
-	auto open = [&](uint32_t r, WKid &a, WKid &b) {
-		const DNode &d = recs[(r & RTX_REF_OFF) / (uint32_t)sizeof(DNode)];
-		a = WKid{ d.ref0, { d.lo0x, d.lo0y, d.lo0z }, { d.hi0x, d.hi0y, d.hi0z } };
-		b = WKid{ d.ref1, { d.lo1x, d.lo1y, d.lo1z }, { d.hi1x, d.hi1y, d.hi1z } };
-	};
-	open(ref, kids[0], kids[1]);
-	n = 2;
-	while (n < 4) {
-		int best = -1;
-		float ba = -1.f;
-		for (uint32_t i = 0; i < n; i++)
-			if (!(kids[i].ref & RTX_REF_LEAF) && half_area(kids[i]) > ba) {
-				ba = half_area(kids[i]);
-				best = (int)i;
-			}
-		if (best < 0)
-			break;
-		const uint32_t r = kids[best].ref;
-		open(r, kids[best], kids[n]);
-		n++;
-	}
-	/* inner children first (stable), so slot c's child node is slot 0's + c */
-	std::stable_partition(kids, kids + n, [](const WKid &k) { return !(k.ref & RTX_REF_LEAF); });
-}
-
-/* a device leaf ref (record byte offset | flags) as the wide walk's leaf ref: primitive index
- * << 6 | flags, the index into the compact 48-byte triangle records (DScene.wtris) */
-static uint32_t wide_leaf_ref(uint32_t ref, uint32_t nnodes)
-{
-	return ((((ref & RTX_REF_OFF) / (uint32_t)sizeof(DNode)) - nnodes) << 6) | (ref & ~RTX_REF_OFF);
-}
-
-static uint32_t wide_emit(const std::vector<DNode> &recs, const QFrame &F, uint32_t ref, uint32_t me,
-			  std::vector<DQNode> &out)
-{
-	WKid kids[4];
-	uint32_t n = 0;
-	wide_kids(recs, ref, kids, n);
-	uint32_t ninner = 0;
-	while (ninner < n && !(kids[ninner].ref & RTX_REF_LEAF))
-		ninner++;
-	const uint32_t base = (uint32_t)(out.size() / 4);
-	out.resize(out.size() + 4 * (size_t)ninner);
-	for (uint32_t c = 0; c < 4; c++) {
-		DQNode &t = out[4 * (size_t)me + c];
-		if (c >= n) {
-			t.x = t.y = t.z = RTX_W_EMPTY_BOX;
-			t.link = RTX_EMPTY_REF;
-			continue;
-		}
-		t.x = rtx_quantise(kids[c].lo[0], kids[c].hi[0], F.qo[0], F.qs[0]);
-		t.y = rtx_quantise(kids[c].lo[1], kids[c].hi[1], F.qo[1], F.qs[1]);
-		t.z = rtx_quantise(kids[c].lo[2], kids[c].hi[2], F.qo[2], F.qs[2]);
-		t.link = c < ninner ? (base + c) << 6 : wide_leaf_ref(kids[c].ref, (uint32_t)recs.size());
-	}
-	uint32_t dep = 1;
-	for (uint32_t c = 0; c < ninner; c++)
-		dep = std::max(dep, 1 + wide_emit(recs, F, kids[c].ref, base + c, out));
-	return dep;
-}
-
-static uint32_t wide_bvh(const std::vector<DNode> &inner, uint32_t root_ref, const float lo[3], const float hi[3],
-			 const QFrame &F, std::vector<DQNode> &out)
-{
-	out.clear();
-	if (root_ref == RTX_EMPTY_REF)
-		return 0;
-	out.resize(4);
-	if (root_ref & RTX_REF_LEAF) { /* a single leaf: one node, one slot with the scene box */
-		for (uint32_t c = 0; c < 4; c++) {
-			out[c].x = out[c].y = out[c].z = RTX_W_EMPTY_BOX;
-			out[c].link = RTX_EMPTY_REF;
-		}
-		out[0].x = rtx_quantise(lo[0], hi[0], F.qo[0], F.qs[0]);
-		out[0].y = rtx_quantise(lo[1], hi[1], F.qo[1], F.qs[1]);
-		out[0].z = rtx_quantise(lo[2], hi[2], F.qo[2], F.qs[2]);
-		out[0].link = wide_leaf_ref(root_ref, (uint32_t)inner.size());
-		return 1;
-	}
-	return wide_emit(inner, F, root_ref, 0, out);
-}
-
-
-static inline float pad_lo(float x, float ext) { return x - (std::fabs(x) + ext) * 2e-6f - 1e-30f; }
-static inline float pad_hi(float x, float ext) { return x + (std::fabs(x) + ext) * 2e-6f + 1e-30f; }
-
 int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 {
 	if (!sc->num_materials || !sc->materials)
@@ -476,29 +373,12 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 	}
 
 	/* leaf boxes (sphere_get_corners / triangle_get_corners), padded so the traversal's
-	 * FMA slab test is conservative */
+	 * FMA slab test is conservative: in world space for the bounded objects' box (the
+	 * shade-point sort's frame), then in the trees' frame (rtx_frame.cpp) for the builders */
 	const uint32_t nb = (uint32_t)bounded.size();
 	std::vector<float> lo(3 * (size_t)nb), hi(3 * (size_t)nb);
-	for (uint32_t k = 0; k < nb; k++) {
-		const rtx_object &o = sc->objects[bounded[k]];
-		float l[3], h[3];
-		if (o.type == RTX_SPHERE) {
-			for (int a = 0; a < 3; a++) {
-				l[a] = o.p0[a] - o.radius;
-				h[a] = o.p0[a] + o.radius;
-			}
-		} else {
-			for (int a = 0; a < 3; a++) {
-				l[a] = std::min(o.p0[a], std::min(o.p1[a], o.p2[a]));
-				h[a] = std::max(o.p0[a], std::max(o.p1[a], o.p2[a]));
-			}
-		}
-		float ext = std::max(h[0] - l[0], std::max(h[1] - l[1], h[2] - l[2]));
-		for (int a = 0; a < 3; a++) {
-			lo[3 * (size_t)k + a] = pad_lo(l[a], ext);
-			hi[3 * (size_t)k + a] = pad_hi(h[a], ext);
-		}
-	}
+	for (uint32_t k = 0; k < nb; k++)
+		rtx_world_box(sc->objects[bounded[k]], &lo[3 * (size_t)k], &hi[3 * (size_t)k]);
 	for (int a = 0; a < 3; a++) {
 		c->bound_lo[a] = FLT_MAX;
 		c->bound_hi[a] = -FLT_MAX;
@@ -508,6 +388,30 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 			c->bound_lo[a] = std::min(c->bound_lo[a], lo[3 * (size_t)k + a]);
 			c->bound_hi[a] = std::max(c->bound_hi[a], hi[3 * (size_t)k + a]);
 		}
+	const auto tf0 = std::chrono::steady_clock::now();
+	DTreeFrame &tf = hs.tf;
+	hs.frame_ratio = c->opt_frame == RTX_FRAME_AUTO ? rtx_frame_choose(sc, bounded, c->bound_lo, c->bound_hi, tf) : 1.0;
+	if (c->opt_frame != RTX_FRAME_AUTO)
+		rtx_frame_choose(sc, {}, c->bound_lo, c->bound_hi, tf); /* the identity */
+	float tlo[3], thi[3]; /* the bounded objects' box in the trees' frame */
+	memcpy(tlo, c->bound_lo, 12);
+	memcpy(thi, c->bound_hi, 12);
+	if (tf.rotated) {
+		const double pad = rtx_frame_pad(rtx_frame_radius(sc, bounded, tf));
+		for (int a = 0; a < 3; a++) {
+			tlo[a] = FLT_MAX;
+			thi[a] = -FLT_MAX;
+		}
+		for (uint32_t k = 0; k < nb; k++) {
+			float *l = &lo[3 * (size_t)k], *h = &hi[3 * (size_t)k];
+			rtx_frame_box(sc->objects[bounded[k]], tf, pad, l, h);
+			for (int a = 0; a < 3; a++) {
+				tlo[a] = std::min(tlo[a], l[a]);
+				thi[a] = std::max(thi[a], h[a]);
+			}
+		}
+	}
+	hs.frame_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf0).count();
 	BvhConfig cfg;
 	cfg.max_leaf = c->opt_leaf; /* RTX_OPT_BVH_LEAF (default 1) */
 
@@ -572,9 +476,11 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 	/* RTX_WALK_AUTO: a scene whose threaded BVH2 fits the LDS top records is walked from LDS alone
 	 * (scene3, 3 spheres: 102 ms vs 114 ms over the 8-wide tree); larger ones over the 8-wide tree */
 	const bool small = (uint64_t)2 * nb <= RTX_TOP_MAX + 1;
-	std::vector<DNode> inner; /* host copy of the inner-node records, for the threaded BVH */
-	std::vector<DPrim> prims_dl; /* device builders: the primitive records read back */
+	const bool want_w8 = nb && (c->opt_walk == RTX_WALK_W8 || (c->opt_walk == RTX_WALK_AUTO && !small));
+	std::vector<DNode> inner; /* host copy of the inner-node records (threaded BVH2, host collapse) */
+	std::vector<DPrim> prims_dl; /* device builders: the primitive records read back (host collapse) */
 	const DPrim *host_prims = nullptr; /* the primitive records in leaf order on the host */
+	hs.device = c->device;
 	int rc;
 	if ((c->builder == RTX_BUILD_LBVH_GPU || c->builder == RTX_BUILD_PLOC_GPU || c->builder == RTX_BUILD_SAH_GPU) && nb) {
 		/* GPU builders (rtx_build.hip): primitives uploaded in input order, records emitted on the device */
@@ -596,12 +502,12 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 		}
 		uint32_t rounds = 0;
 		hipError_t e = c->builder == RTX_BUILD_PLOC_GPU
-				       ? rtx_ploc_build(nb, d_lo, d_hi, d_in, c->bound_lo, c->bound_hi, cfg.max_leaf, &recs, &nnodes,
+				       ? rtx_ploc_build(nb, d_lo, d_hi, d_in, tlo, thi, cfg.max_leaf, &recs, &nnodes,
 							&root_ref, &depth, &rounds, c->stream)
 			       : c->builder == RTX_BUILD_SAH_GPU
 				       ? rtx_sah_build(nb, d_lo, d_hi, d_in, cfg.max_leaf, cfg.bins, cfg.max_depth, cfg.c_trav, cfg.c_isect,
 						       &recs, &nnodes, &root_ref, &depth, &rounds, c->stream)
-				       : rtx_lbvh_build(nb, d_lo, d_hi, d_in, c->bound_lo, c->bound_hi, cfg.max_leaf, &recs, &nnodes,
+				       : rtx_lbvh_build(nb, d_lo, d_hi, d_in, tlo, thi, cfg.max_leaf, &recs, &nnodes,
 							&root_ref, &depth, c->stream);
 		dfree(d_lo);
 		dfree(d_hi);
@@ -615,11 +521,8 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 		if (((uint64_t)nnodes + nb) * sizeof(DNode) > 0xFFFFFFC0ull)
 			return fail(RTX_ERR_SCENE, "scene too large: %u BVH nodes + %u primitives exceed 4 GB of records", nnodes,
 				    nb);
-		inner.resize(nnodes);
-		if (nnodes)
-			HIP_TRY(hipMemcpy(inner.data(), recs, nnodes * sizeof(DNode), hipMemcpyDeviceToHost));
-		/* the 8-wide tree collapsed where the records are (single-primitive leaves, one device) */
-		if (!hs.want_host_recs && cfg.max_leaf == 1 && nnodes && (c->opt_walk == RTX_WALK_W8 || (c->opt_walk == RTX_WALK_AUTO && !small))) {
+		/* the 8-wide tree collapsed where the records are (single-primitive leaves) */
+		if (want_w8 && cfg.max_leaf == 1 && nnodes) {
 			std::vector<uint32_t> skip((sc->num_objects + 31) / 32 + 1, 0u);
 			for (uint32_t i = 0; i < sc->num_emitters; i++)
 				skip[sc->emitters[i] >> 5] |= 1u << (sc->emitters[i] & 31u);
@@ -640,25 +543,38 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 				hs.w8noemit = sc->num_emitters > 0;
 			}
 		}
-		if (hs.want_host_recs) { /* the other devices of a group get the records from the host */
-			hs.recs.resize((size_t)nnodes + nb);
-			HIP_TRY(hipMemcpy(hs.recs.data(), recs, hs.recs.size() * sizeof(DNode), hipMemcpyDeviceToHost));
-			host_prims = (const DPrim *)(hs.recs.data() + nnodes);
-		} else { /* the primitives in leaf order: the 8-wide tree marks its leaves from them */
+		/* the host needs the records only for the host collapse or the threaded BVH2 */
+		if (!hs.w8_on_device) {
+			inner.resize(nnodes);
+			if (nnodes)
+				HIP_TRY(hipMemcpy(inner.data(), recs, nnodes * sizeof(DNode), hipMemcpyDeviceToHost));
 			prims_dl.resize(nb);
 			HIP_TRY(hipMemcpy(prims_dl.data(), recs + nnodes, (size_t)nb * sizeof(DPrim), hipMemcpyDeviceToHost));
 			host_prims = prims_dl.data();
 		}
-		/* the emitters' record indices (the 8-wide closest-hit walk tests them apart from the tree) */
-		std::vector<uint32_t> rec_of(sc->num_objects, RTX_NONE);
-		for (uint32_t k = 0; k < nb; k++) {
-			uint32_t obj;
-			memcpy(&obj, &host_prims[k].b[3], 4);
-			if (obj < sc->num_objects)
-				rec_of[obj] = k;
+		/* the emitters' record indices (the 8-wide closest-hit walk tests them apart from the tree),
+		 * found on the device */
+		if (!emit.empty()) {
+			std::vector<uint32_t> objs(emit.size()), at(emit.size(), RTX_NONE);
+			for (size_t i = 0; i < emit.size(); i++)
+				objs[i] = emit[i].obj;
+			uint32_t *d_objs = nullptr, *d_at = nullptr;
+			if ((rc = upload(d_objs, objs)) || (rc = upload(d_at, at))) {
+				dfree(d_objs);
+				return rc;
+			}
+			e = rtx_launch_find_prims((const DPrim *)(recs + nnodes), nb, d_objs, (uint32_t)objs.size(), d_at, c->stream);
+			if (e == hipSuccess)
+				e = hipMemcpyAsync(at.data(), d_at, at.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream);
+			if (e == hipSuccess)
+				e = hipStreamSynchronize(c->stream);
+			dfree(d_objs);
+			dfree(d_at);
+			if (e != hipSuccess)
+				return fail(RTX_ERR_HIP, "emitter record lookup failed: %s", hipGetErrorString(e));
+			for (size_t i = 0; i < emit.size(); i++)
+				emit[i].prim = at[i];
 		}
-		for (DEmitter &e : emit)
-			e.prim = rec_of[e.obj];
 	} else {
 		BvhOutput bvh;
 		bvh_build(BvhInput{ nb, lo.data(), hi.data() }, cfg, bvh);
@@ -707,34 +623,27 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 		hs.recs = std::move(recs);
 		host_prims = (const DPrim *)(hs.recs.data() + nnodes);
 	}
-	std::vector<uint32_t> qdepth;
-	thread_bvh(inner, nb ? root_ref : RTX_EMPTY_REF, c->bound_lo, c->bound_hi, hs.qnodes, hs.qf, qdepth);
-	if (hs.qnodes.size() >= (1u << 26))
-		return fail(RTX_ERR_SCENE, "scene too large: %zu threaded BVH nodes (max 2^26)", hs.qnodes.size());
-	hs.ntop = thread_top(hs.qnodes, qdepth, hs.qtop);
 	/* the shadow walk's BVH (RTX_OPT_SHADOW_WALK): the 8-wide compressed tree by default, which
-	 * walks any depth; the 4-wide tree (depth-limited by its LDS stacks) and the threaded BVH2 for
-	 * measurement, and the BVH2 when the 8-wide tree cannot be built (over 2^24 entries) */
-	if (hs.w8_on_device) {
-		/* collapsed on the device above */
-	} else if (c->opt_walk == RTX_WALK_W8 || (c->opt_walk == RTX_WALK_AUTO && !small)) {
+	 * walks any depth (collapsed on the device above, else here from the host records); the
+	 * threaded BVH2 for small scenes (its top levels in LDS), for measurement, and when the 8-wide
+	 * tree cannot be built (over 2^24 entries) */
+	if (!hs.w8_on_device && want_w8) {
 		/* with the host records the emitters are left out of the tree (k_shadow tests them linearly) */
-		const DPrim *hp = nb ? host_prims : nullptr;
 		std::vector<uint32_t> emit_objs;
 		for (const DEmitter &e : emit)
 			emit_objs.push_back(e.obj);
-		/* the walks need every leaf slot marked from its record: no records, no 8-wide tree */
-		hs.w8depth = rtx_wide8_build(inner, nnodes, hp, hp ? root_ref : RTX_EMPTY_REF, c->bound_lo, c->bound_hi, emit_objs,
-					     hs.w8f, hs.w8noemit, hs.w8, hs.w8leaf);
-	} else if (c->opt_walk == RTX_WALK_W4) {
-		hs.wdepth = wide_bvh(inner, nb ? root_ref : RTX_EMPTY_REF, c->bound_lo, c->bound_hi, hs.qf, hs.wnodes);
-		if (hs.wdepth > RTX_W_STACK + 1 || hs.wnodes.size() / 4 >= (1u << 26)) /* the lane stacks would overflow */
-			hs.wnodes.clear();
+		hs.w8depth = rtx_wide8_build(inner, nnodes, host_prims, root_ref, tlo, thi, emit_objs, hs.w8f, hs.w8noemit, hs.w8,
+					     hs.w8leaf);
 	}
-	if (hs.wnodes.empty())
-		hs.wdepth = 0;
 	if (hs.w8.empty() && !hs.w8_on_device)
 		hs.w8depth = 0;
+	if (!hs.w8depth) {
+		std::vector<uint32_t> qdepth;
+		thread_bvh(inner, nb ? root_ref : RTX_EMPTY_REF, tlo, thi, hs.qnodes, hs.qf, qdepth);
+		if (hs.qnodes.size() >= (1u << 26))
+			return fail(RTX_ERR_SCENE, "scene too large: %zu threaded BVH nodes (max 2^26)", hs.qnodes.size());
+		hs.ntop = thread_top(hs.qnodes, qdepth, hs.qtop);
+	}
 	hs.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count();
 	hs.mats = std::move(mats);
 	hs.planes = std::move(planes);
@@ -751,36 +660,36 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 }
 
 /* the built scene onto c's device (c->d_nodes already holds the records when the device
- * builder ran on c) */
-int rtx_upload_built(rtx_ctx *c, const HostScene &hs)
+ * builder ran on c, or a group copied them to it); device buffers in hs (the 8-wide tree
+ * collapsed on the device) change hands to c */
+int rtx_upload_built(rtx_ctx *c, HostScene &hs)
 {
 	int rc;
 	/* a failure below leaves the context without a scene (RTX_ERR_STATE on render), never with a
 	 * mix of old and new buffers */
 	c->have_scene = false;
 	c->sp_tile_seen = 0.0; /* the next render sizes its chunks from the static bound */
-	c->sp_tile_key = 0;
+	c->sp_tile_key = SpKey{};
 	HIP_TRY(hipSetDevice(c->device));
 	if (!(hs.recs_on_device && c->d_nodes) && (rc = upload(c->d_nodes, hs.recs)))
 		return rc;
-	if ((rc = upload(c->d_qnodes, hs.qnodes)) || (rc = upload(c->d_top, hs.qtop)) || (rc = upload(c->d_wnodes, hs.wnodes)) ||
-	    (rc = upload(c->d_planes, hs.planes)) || (rc = upload(c->d_mats, hs.mats)) || (rc = upload(c->d_emitters, hs.emit)))
+	if ((rc = upload(c->d_qnodes, hs.qnodes)) || (rc = upload(c->d_top, hs.qtop)) || (rc = upload(c->d_planes, hs.planes)) ||
+	    (rc = upload(c->d_mats, hs.mats)) || (rc = upload(c->d_emitters, hs.emit)))
 		return rc;
-	dfree(c->d_wtris);
-	if (!hs.wnodes.empty() && hs.nb) { /* the wide walk's compact triangle records, from the primitives */
-		HIP_TRY(hipMalloc(&c->d_wtris, (size_t)hs.nb * 3 * sizeof(float4)));
-		HIP_TRY(rtx_launch_pack_tris((const DPrim *)(c->d_nodes + hs.nnodes), hs.nb, c->d_wtris, c->stream));
-		HIP_TRY(hipStreamSynchronize(c->stream));
-	}
 	const bool have_w8 = hs.w8_on_device || !hs.w8.empty();
 	const uint32_t num_w8 = hs.w8_on_device ? hs.w8_entries : (uint32_t)hs.w8.size();
 	uint32_t *d_map = nullptr; /* entry -> primitive index of the 8-wide tree's leaf entries */
 	if (hs.w8_on_device) { /* collapsed on this device: the buffers change hands */
+		if (hs.device != c->device)
+			return fail(RTX_ERR_STATE, "8-wide tree built on device %d uploaded to device %d", hs.device, c->device);
 		dfree(c->d_w8);
 		dfree(c->d_w8s);
 		c->d_w8 = hs.dev_w8;
 		c->d_w8s = hs.dev_w8s;
 		d_map = hs.dev_w8leaf;
+		hs.dev_w8 = nullptr;
+		hs.dev_w8s = nullptr;
+		hs.dev_w8leaf = nullptr;
 	} else {
 		if ((rc = upload(c->d_w8, hs.w8)))
 			return rc;
@@ -788,8 +697,13 @@ int rtx_upload_built(rtx_ctx *c, const HostScene &hs)
 			return rc;
 		dfree(c->d_w8s);
 		/* the scalar-path node copies (rtx_device.h DW8S) */
-		HIP_TRY(hipMalloc(&c->d_w8s, std::max<size_t>(num_w8, 1) * sizeof(DW8S)));
-		HIP_TRY(rtx_launch_w8_scalar(num_w8, c->d_w8, d_map, c->d_w8s, c->stream));
+		hipError_t e = hipMalloc(&c->d_w8s, std::max<size_t>(num_w8, 1) * sizeof(DW8S));
+		if (e == hipSuccess)
+			e = rtx_launch_w8_scalar(num_w8, c->d_w8, d_map, c->d_w8s, c->stream);
+		if (e != hipSuccess) {
+			dfree(d_map);
+			return fail(RTX_ERR_HIP, "8-wide BVH scalar copies failed: %s", hipGetErrorString(e));
+		}
 	}
 	if (have_w8) { /* the 8-wide tree's leaf entries: copies of their primitive records */
 		hipError_t e = rtx_launch_w8_fill((const DPrim *)(c->d_nodes + hs.nnodes), c->d_mats, d_map, num_w8, c->d_w8, c->stream);
@@ -816,10 +730,6 @@ int rtx_upload_built(rtx_ctx *c, const HostScene &hs)
 	memcpy(S.qs, hs.qf.qs, 12);
 	S.top = hs.ntop ? c->d_top : nullptr;
 	S.num_top = hs.ntop;
-	S.wnodes = hs.wnodes.empty() ? nullptr : c->d_wnodes;
-	S.num_wnodes = (uint32_t)(hs.wnodes.size() / 4);
-	S.wtris = (const float *)c->d_wtris;
-	S.wdepth = hs.wdepth;
 	S.w8 = have_w8 ? c->d_w8 : nullptr;
 	S.num_w8 = num_w8;
 	S.w8depth = hs.w8depth;
@@ -832,6 +742,7 @@ int rtx_upload_built(rtx_ctx *c, const HostScene &hs)
 	S.num_planes = (uint32_t)hs.planes.size();
 	S.num_emitters = hs.num_emitters;
 	S.stack_size = std::max<uint32_t>(hs.depth + 1, 4);
+	S.tf = hs.tf;
 	c->total_lights = 0;
 	for (const DEmitter &e : hs.emit)
 		c->total_lights += e.num_lights;
@@ -842,7 +753,10 @@ int rtx_upload_built(rtx_ctx *c, const HostScene &hs)
 	c->stats.bvh_depth = hs.depth;
 	c->stats.builder = (uint32_t)hs.builder;
 	c->stats.bvh_prims = hs.nb;
-	c->stats.shadow_walk = S.w8 ? RTX_WALK_W8 : S.wnodes ? RTX_WALK_W4 : RTX_WALK_BVH2;
+	c->stats.shadow_walk = S.w8 ? RTX_WALK_W8 : RTX_WALK_BVH2;
+	c->stats.tree_rotated = hs.tf.rotated;
+	c->stats.frame_cost = hs.frame_ratio;
+	c->stats.frame_ms = hs.frame_ms;
 	if (S.w8) {
 		uint32_t inner_nodes = hs.w8_wide;
 		if (!hs.w8_on_device)
@@ -852,8 +766,8 @@ int rtx_upload_built(rtx_ctx *c, const HostScene &hs)
 		c->stats.wide_depth = S.w8depth;
 		c->stats.wide_entries = S.num_w8;
 	} else {
-		c->stats.wide_nodes = S.num_wnodes;
-		c->stats.wide_depth = S.wdepth;
+		c->stats.wide_nodes = 0;
+		c->stats.wide_depth = 0;
 		c->stats.wide_entries = 0;
 	}
 	return RTX_OK;
@@ -923,15 +837,31 @@ int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, floa
 	uint64_t avg_tile = 64ull * (1 + gi_n) * 5 / 4 + 64;
 	/* a render of the same scene and settings before: its shade points per tile (x 1.25, + 64)
 	 * instead of the bound above; an overflow still halves the chunk and retries */
-	const uint64_t sp_key = ((uint64_t)P.gi << 56) ^ ((uint64_t)P.samples << 32) ^ ((uint64_t)P.max_bounces << 16) ^
-				((uint64_t)P.reflection << 8) ^ (uint64_t)P.tile_stride;
+	/* every setting the shade points per tile depend on: the scene (reset by an upload), the
+	 * frame and camera, the ray-tree and GI settings and the shard */
+	SpKey sp_key{};
+	sp_key.v[0] = (uint32_t)P.gi;
+	sp_key.v[1] = P.samples;
+	sp_key.v[2] = P.max_bounces;
+	sp_key.v[3] = (uint32_t)P.reflection;
+	sp_key.v[4] = P.tile_offset;
+	sp_key.v[5] = P.tile_stride;
+	sp_key.v[6] = F.width;
+	sp_key.v[7] = F.height;
+	memcpy(&sp_key.v[8], &P.min_intensity_sqr, 4);
+	memcpy(&sp_key.v[9], F.corner, 12);
+	memcpy(&sp_key.v[12], F.step_x, 12);
+	memcpy(&sp_key.v[15], F.step_y, 12);
+	memcpy(&sp_key.v[18], F.origin, 12);
+	sp_key.set = 1;
 	if (c->sp_tile_key == sp_key && c->sp_tile_seen > 0.0)
 		avg_tile = std::min<uint64_t>(avg_tile, (uint64_t)(c->sp_tile_seen * 1.25) + 64);
 	size_t free_b = 0, total_b = 0;
 	HIP_TRY(hipMemGetInfo(&free_b, &total_b));
 	/* shade points of a chunk: up to a third of free HBM (96 GB cap; 288 GB per MI355X) */
 	const uint64_t budget = std::min<uint64_t>(96ull << 30, free_b / 3);
-	uint32_t chunk_tiles = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(P.ntiles, budget / (avg_tile * 112)));
+	const uint32_t chunk_cap = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(P.ntiles, budget / (avg_tile * 112)));
+	uint32_t chunk_tiles = chunk_cap;
 
 	auto grow = [](auto *&ptr, size_t &have, size_t need) -> hipError_t {
 		if (need <= have)
@@ -1057,6 +987,7 @@ int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, floa
 		t_accum += cc;
 		chunks++;
 		begin = end;
+		chunk_tiles = std::min<uint32_t>(chunk_cap, 2 * chunk_tiles); /* grows back after an overflow halved it */
 	}
 	HIP_TRY(hipEventRecord(c->ev1, stream));
 	HIP_TRY(hipStreamSynchronize(stream));
@@ -1210,8 +1141,8 @@ extern "C" int rtx_set_option(rtx_ctx *c, int option, int64_t value)
 		return fail(RTX_ERR_ARG, "null argument");
 	switch (option) {
 	case RTX_OPT_SHADOW_WALK:
-		if (value < RTX_WALK_AUTO || value > RTX_WALK_W8)
-			return fail(RTX_ERR_ARG, "unknown shadow walk %lld", (long long)value);
+		if (value != RTX_WALK_AUTO && value != RTX_WALK_BVH2 && value != RTX_WALK_W8)
+			return fail(RTX_ERR_ARG, "shadow walk %lld is not AUTO, BVH2 or W8", (long long)value);
 		c->opt_walk = (int)value;
 		return RTX_OK;
 	case RTX_OPT_BVH_LEAF:
@@ -1238,6 +1169,11 @@ extern "C" int rtx_set_option(rtx_ctx *c, int option, int64_t value)
 		if (value != RTX_WALK_AUTO && value != RTX_WALK_W8 && value != RTX_WALK_BVH2)
 			return fail(RTX_ERR_ARG, "closest-hit walk %lld is not AUTO, W8 or BVH2", (long long)value);
 		c->opt_trace_walk = (int)value;
+		return RTX_OK;
+	case RTX_OPT_TREE_FRAME:
+		if (value != RTX_FRAME_AUTO && value != RTX_FRAME_WORLD)
+			return fail(RTX_ERR_ARG, "tree frame %lld is not AUTO or WORLD", (long long)value);
+		c->opt_frame = (int)value;
 		return RTX_OK;
 	case RTX_OPT_SHADOW_GRAB:
 		if (value < 1 || value > (1 << 24))

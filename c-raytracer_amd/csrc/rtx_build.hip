@@ -1091,8 +1091,9 @@ extern "C" hipError_t rtx_sah_build(uint32_t n, const float *d_lo, const float *
 	const size_t nt = 2 * (size_t)n;
 	const uint32_t nb = bins;
 	std::vector<uint32_t> lev_off;
-	/* accumulators for at most this many nodes at a time */
-	const uint32_t chunk = 1u << 16;
+	/* accumulators for at most this many nodes at a time: a level holds nodes of two or more
+	 * primitives, so never more than n / 2 of them (3 spheres: one node, not 65,536 x 2.8 KB) */
+	const uint32_t chunk = std::min<uint32_t>(1u << 16, std::max<uint32_t>(1u, n / 2));
 #define TRY(x)                                  \
 	do {                                    \
 		if ((e = (x)) != hipSuccess)    \
@@ -1234,4 +1235,28 @@ done:
 	(void)hipFree(scal);
 	(void)hipHostFree(tail);
 	return e;
+}
+
+/* the record index of each of nobj objects (the emitters) among n primitive records: out[j] = k
+ * where record k's object id (DPrim b[3]) is objs[j]; out left RTX_NONE for an object without
+ * a record.  One thread per record; each object has at most one record, so no races. */
+__global__ void k_find_prims(const DPrim *__restrict__ prims, uint32_t n, const uint32_t *__restrict__ objs, uint32_t nobj,
+			     uint32_t *__restrict__ out)
+{
+	const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+	if (k >= n)
+		return;
+	const uint32_t obj = __float_as_uint(prims[k].b[3]);
+	for (uint32_t j = 0; j < nobj; j++)
+		if (objs[j] == obj)
+			out[j] = k;
+}
+
+extern "C" hipError_t rtx_launch_find_prims(const DPrim *prims, uint32_t n, const uint32_t *objs, uint32_t nobj, uint32_t *out,
+					     hipStream_t stream)
+{
+	if (!n || !nobj)
+		return hipSuccess;
+	hipLaunchKernelGGL(k_find_prims, dim3((n + 255) / 256), dim3(256), 0, stream, prims, n, objs, nobj, out);
+	return hipGetLastError();
 }

@@ -103,20 +103,21 @@ typedef struct __attribute__((aligned(16))) DQNode {
 #define RTX_SH_NW 16 /* waves per k_shadow workgroup (they share the top copy) */
 #endif
 
-/* 4-wide copy of the BVH for the shadow walk (rtx_shadow.hip shadow_walk4): node i is four
- * 16-byte child slots (DQNode records 4i .. 4i+3, one 64-byte line), each {x, y, z, ref} with the
- * child's box quantised as in DQNode.  The slots hold the inner children first (ref = child node
- * index << 6; a node's inner children are consecutive nodes, so slot c's child is slot 0's + c),
- * then the leaves (ref = primitive index << 6 | RTX_REF_LEAF | RTX_REF_SPH | count-1, indexing
- * the compact 48-byte records DScene.wtris), then empty slots (ref =
- * RTX_EMPTY_REF, quantised box lo > hi on every axis, never hit).  Node 0 is the root.  A lane
- * keeps its pending siblings as groups (first child << 4 | slot mask), one per tree level, in
- * an LDS stack of RTX_W_STACK entries: the uploader builds the wide tree only when its depth
- * fits (num_wnodes = 0 otherwise, and k_shadow walks the threaded BVH2). */
-#ifndef RTX_W_STACK
-#define RTX_W_STACK 12
-#endif
-#define RTX_W_EMPTY_BOX 0x0000FFFFu
+/* The trees' frame.  Every BVH of a scene (the BVH2 records, the threaded copy, the 8-wide tree)
+ * is built over leaf boxes taken in one frame x' = R (x - c): R's rows are the frame's axes in
+ * world coordinates, c the centre of the bounded objects' world box.  The uploader picks R from
+ * the triangles (rtx_frame.cpp: the frame of least total leaf-box surface area among the identity
+ * and the frames of the largest triangles, e.g. a rotated mesh's own axes, where its faces have
+ * flat boxes), so R need not be the identity.  A walk transforms its ray once (origin and
+ * direction; the parameter t is unchanged, the map is linear) and tests boxes in that frame;
+ * primitives are always tested in world space with the reference's arithmetic.  Leaf boxes are
+ * padded for the transform's rounding (rtx_frame.cpp), so the culling stays conservative.
+ * rotated = 0: R = I, c = 0, and the walks skip the transform (the world-space trees). */
+typedef struct DTreeFrame {
+	float r[3][3];
+	float c[3];
+	uint32_t rotated;
+} DTreeFrame;
 
 /* 8-wide compressed BVH for the shadow walk (rtx_shadow.hip shadow_walk8), in the style of
  * Ylitie et al.'s compressed wide BVH: an array of 64-byte entries (one 64-byte half line, four
@@ -210,12 +211,9 @@ typedef struct DScene {
 	const DEmitter *emitters;
 	const DQNode *qnodes;   /* threaded quantised BVH (num_qnodes records), null when the BVH is empty */
 	uint32_t num_qnodes;
-	float qo[3], qs[3];     /* its quantisation frame: q = (x - qo) * qs */
+	float qo[3], qs[3];     /* its quantisation frame: q = (x' - qo) * qs, x' in the trees' frame tf */
 	const uint32_t *top;    /* its top levels (num_top records + num_top words, see RTX_QTOP_CUT) */
 	uint32_t num_top;
-	const DQNode *wnodes;   /* 4-wide BVH (4 records per node, same frame), null when not built */
-	const float *wtris;     /* its leaves' primitives as 48-byte records (the first 48 B of each DPrim) */
-	uint32_t num_wnodes, wdepth;
 	const DW8 *w8;          /* 8-wide compressed BVH (num_w8 entries), null when not built */
 	uint32_t num_w8, w8depth;
 	float w8qo[3], w8qs[3]; /* its 16-bit frame */
@@ -233,6 +231,7 @@ typedef struct DScene {
 	uint32_t stack_size;   /* per-lane closest-hit stack entries (>= BVH depth) */
 	float ambient[3];
 	uint32_t *ostk;        /* k_trace: lane-stack entries from RTX_TRACE_LSTK on, [entry][grid lane] in HBM */
+	DTreeFrame tf;         /* the frame every tree's boxes are in (identity unless rotated) */
 } DScene;
 
 /* k_trace keeps the first RTX_TRACE_LSTK entries of a lane's closest-hit stack in LDS and the
@@ -295,8 +294,8 @@ enum {
 	RTX_C_SPLANES,
 	RTX_C_SSTEPS,       /* ... walk-loop iterations of the waves */
 	RTX_C_SWALKS,       /* ... wave walks (64 shadow rays each) */
-	RTX_C_SLEAFR,       /* ... 4-wide walk: wave iterations of the leaf loop (rounds of primitive fetches) */
-	RTX_C_SUNIF,        /* ... 4-wide walk: wave steps whose active lanes all fetched the same node */
+	RTX_C_SLEAFR,       /* ... 8-wide walk: wave iterations of the leaf loops (rounds of primitive fetches) */
+	RTX_C_SUNIF,        /* ... 8-wide walk: wave steps whose active lanes were all at one node */
 	RTX_C_N
 };
 

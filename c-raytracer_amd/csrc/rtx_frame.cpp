@@ -1,0 +1,285 @@
+/*
+ * The trees' frame (rtx_device.h DTreeFrame) and the leaf boxes taken in it.
+ *
+ * The reference bounds every object by its world-space box (sphere_get_corners /
+ * triangle_get_corners, object.c:277-282, 375-388) and its BVH is built over those boxes
+ * (accel.c:266-315).  A mesh loaded with a rotation (scene.c mesh_load -> object.c:548-562) has
+ * axis-aligned faces only in its own frame: in world space a face's box is a slab of volume
+ * around a tilted square, and the boxes of neighbouring faces overlap, so a ray meets many
+ * boxes whose triangles it misses.  The BVHs here may instead be built over the boxes of the
+ * objects in a rotated frame x' = R (x - c); a walk then transforms its ray once and tests the
+ * same boxes it would test in world space, only tighter.  Which primitives are tested changes
+ * (fewer), their tests do not: every primitive whose box a ray meets is still tested with the
+ * reference's arithmetic in world space, and a primitive the ray hits always has its box met
+ * (the boxes are conservative, below), so closest hits (up to exact ties) and any-hit answers
+ * are the world-space trees' (tests/test_gpu_frame.py: bit-identical frames).
+ *
+ * The frame: among the identity and the frames of the scene's largest triangles (axes: the
+ * triangle's shortest edge, the normal, and their cross product), the one of least total
+ * surface area of the triangles' boxes over a fixed sample, if it saves at least a quarter of
+ * the identity's (a rotated Menger sponge: 0.3; the dragon stand-in keeps the identity).
+ *
+ * Conservativeness: a walk computes x' and d' in float with fused multiply-adds from the float
+ * R and c the device holds, within about 3 * 2^-24 (|x - c| + |t d|) of the exact image of the
+ * ray point at parameter t.  Every leaf box is computed exactly (double) from the same float R
+ * and c, rounded outward, and padded by RTX_FRAME_PAD times the scene's radius about c on top
+ * of the world trees' own relative padding and one 16-bit quantisation step: ample for rays that
+ * start within a few scene radii of c (shade points, the camera of any reference scene).
+ */
+#include <float.h>
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "rtx_frame.h"
+
+#define RTX_FRAME_PAD 4e-6     /* leaf-box padding for the ray transform, times the scene radius */
+#define RTX_FRAME_SAMPLE 16384 /* triangles the cost is summed over (every k-th) */
+#define RTX_FRAME_CANDS 16     /* largest sampled triangles whose frames are tried */
+#define RTX_FRAME_GAIN 0.75    /* a rotated frame must cost at most this fraction of the identity's */
+
+static double half_area(const double lo[3], const double hi[3])
+{
+	const double x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
+	return x * y + y * z + z * x;
+}
+
+/* sum of the sampled triangles' box half-areas in the frame with rows r */
+static double frame_cost(const rtx_scene_desc *sc, const std::vector<uint32_t> &tris, const double r[3][3])
+{
+	double cost = 0;
+	for (uint32_t oi : tris) {
+		const rtx_object &o = sc->objects[oi];
+		const float *p[3] = { o.p0, o.p1, o.p2 };
+		double lo[3] = { DBL_MAX, DBL_MAX, DBL_MAX }, hi[3] = { -DBL_MAX, -DBL_MAX, -DBL_MAX };
+		for (int k = 0; k < 3; k++)
+			for (int i = 0; i < 3; i++) {
+				const double y = r[i][0] * p[k][0] + r[i][1] * p[k][1] + r[i][2] * p[k][2];
+				lo[i] = std::min(lo[i], y);
+				hi[i] = std::max(hi[i], y);
+			}
+		cost += half_area(lo, hi);
+	}
+	return cost;
+}
+
+static bool unit(double v[3])
+{
+	const double l = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+	if (!(l > 0) || !std::isfinite(l))
+		return false;
+	for (int i = 0; i < 3; i++)
+		v[i] /= l;
+	return true;
+}
+
+/* the frame of triangle o: rows u (its shortest edge), v = n x u, n (its normal) */
+static bool tri_frame(const rtx_object &o, double r[3][3])
+{
+	double e[3][3];
+	for (int i = 0; i < 3; i++) {
+		e[0][i] = (double)o.p1[i] - o.p0[i];
+		e[1][i] = (double)o.p2[i] - o.p0[i];
+		e[2][i] = (double)o.p2[i] - o.p1[i];
+	}
+	double n[3] = { e[0][1] * e[1][2] - e[0][2] * e[1][1], e[0][2] * e[1][0] - e[0][0] * e[1][2],
+			e[0][0] * e[1][1] - e[0][1] * e[1][0] };
+	if (!unit(n))
+		return false;
+	int s = 0;
+	double best = DBL_MAX;
+	for (int k = 0; k < 3; k++) {
+		const double l = e[k][0] * e[k][0] + e[k][1] * e[k][1] + e[k][2] * e[k][2];
+		if (l < best) {
+			best = l;
+			s = k;
+		}
+	}
+	double u[3];
+	const double un = e[s][0] * n[0] + e[s][1] * n[1] + e[s][2] * n[2];
+	for (int i = 0; i < 3; i++)
+		u[i] = e[s][i] - un * n[i];
+	if (!unit(u))
+		return false;
+	const double v[3] = { n[1] * u[2] - n[2] * u[1], n[2] * u[0] - n[0] * u[2], n[0] * u[1] - n[1] * u[0] };
+	for (int i = 0; i < 3; i++) {
+		r[0][i] = u[i];
+		r[1][i] = v[i];
+		r[2][i] = n[i];
+	}
+	return true;
+}
+
+double rtx_frame_choose(const rtx_scene_desc *sc, const std::vector<uint32_t> &bounded, const float world_lo[3],
+			const float world_hi[3], DTreeFrame &F)
+{
+	memset(&F, 0, sizeof(F));
+	for (int i = 0; i < 3; i++)
+		F.r[i][i] = 1.f;
+	std::vector<uint32_t> tris;
+	for (uint32_t oi : bounded)
+		if (sc->objects[oi].type == RTX_TRIANGLE)
+			tris.push_back(oi);
+	if (tris.size() < 16)
+		return 1.0;
+	const size_t stride = (tris.size() + RTX_FRAME_SAMPLE - 1) / RTX_FRAME_SAMPLE;
+	std::vector<uint32_t> sample;
+	for (size_t k = 0; k < tris.size(); k += stride)
+		sample.push_back(tris[k]);
+	/* candidates: the frames of the largest sampled triangles (ties: lower object index) */
+	std::vector<std::pair<double, uint32_t>> by_area;
+	for (uint32_t oi : sample) {
+		const rtx_object &o = sc->objects[oi];
+		const double c[3] = { (double)o.e1[1] * o.e2[2] - (double)o.e1[2] * o.e2[1],
+				      (double)o.e1[2] * o.e2[0] - (double)o.e1[0] * o.e2[2],
+				      (double)o.e1[0] * o.e2[1] - (double)o.e1[1] * o.e2[0] };
+		by_area.push_back({ -(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]), oi });
+	}
+	std::sort(by_area.begin(), by_area.end());
+	const double id[3][3] = { { 1, 0, 0 }, { 0, 1, 0 }, { 0, 0, 1 } };
+	const double c_id = frame_cost(sc, sample, id);
+	double c_best = c_id, r_best[3][3];
+	memcpy(r_best, id, sizeof(id));
+	for (size_t k = 0; k < by_area.size() && k < RTX_FRAME_CANDS; k++) {
+		double r[3][3];
+		if (!tri_frame(sc->objects[by_area[k].second], r))
+			continue;
+		/* the frame as the device holds it (float rows) */
+		for (int i = 0; i < 3; i++)
+			for (int j = 0; j < 3; j++)
+				r[i][j] = (double)(float)r[i][j];
+		const double cost = frame_cost(sc, sample, r);
+		if (cost < c_best) {
+			c_best = cost;
+			memcpy(r_best, r, sizeof(r));
+		}
+	}
+	if (!(c_id > 0) || !(c_best <= RTX_FRAME_GAIN * c_id))
+		return 1.0;
+	for (int i = 0; i < 3; i++) {
+		F.c[i] = 0.5f * world_lo[i] + 0.5f * world_hi[i];
+		for (int j = 0; j < 3; j++)
+			F.r[i][j] = (float)r_best[i][j];
+	}
+	F.rotated = 1;
+	return c_best / c_id;
+}
+
+/* the largest float <= x / >= x */
+static float down(double x)
+{
+	float f = (float)x;
+	if ((double)f > x)
+		f = nextafterf(f, -FLT_MAX);
+	return f;
+}
+static float up(double x)
+{
+	float f = (float)x;
+	if ((double)f < x)
+		f = nextafterf(f, FLT_MAX);
+	return f;
+}
+
+double rtx_frame_radius(const rtx_scene_desc *sc, const std::vector<uint32_t> &bounded, const DTreeFrame &F)
+{
+	double rad = 0;
+	for (uint32_t oi : bounded) {
+		const rtx_object &o = sc->objects[oi];
+		const int n = o.type == RTX_SPHERE ? 1 : 3;
+		const float *p[3] = { o.p0, o.p1, o.p2 };
+		for (int k = 0; k < n; k++)
+			for (int i = 0; i < 3; i++)
+				rad = std::max(rad, fabs((double)p[k][i] - F.c[i]) + (o.type == RTX_SPHERE ? (double)o.radius : 0.0));
+	}
+	return rad;
+}
+
+void rtx_frame_box(const rtx_object &o, const DTreeFrame &F, double pad, float lo[3], float hi[3])
+{
+	double l[3], h[3];
+	if (o.type == RTX_SPHERE) {
+		for (int i = 0; i < 3; i++) {
+			double y = 0, rn = 0;
+			for (int j = 0; j < 3; j++) {
+				y += (double)F.r[i][j] * ((double)o.p0[j] - F.c[j]);
+				rn += (double)F.r[i][j] * F.r[i][j];
+			}
+			l[i] = y - o.radius * sqrt(rn);
+			h[i] = y + o.radius * sqrt(rn);
+		}
+	} else {
+		const float *p[3] = { o.p0, o.p1, o.p2 };
+		for (int i = 0; i < 3; i++) {
+			l[i] = DBL_MAX;
+			h[i] = -DBL_MAX;
+			for (int k = 0; k < 3; k++) {
+				double y = 0;
+				for (int j = 0; j < 3; j++)
+					y += (double)F.r[i][j] * ((double)p[k][j] - F.c[j]);
+				l[i] = std::min(l[i], y);
+				h[i] = std::max(h[i], y);
+			}
+		}
+	}
+	/* the world trees' relative padding (rtx_world_box) and the transform's */
+	for (int i = 0; i < 3; i++) {
+		const double ext = std::max(h[0] - l[0], std::max(h[1] - l[1], h[2] - l[2]));
+		lo[i] = down(l[i] - (fabs(l[i]) + ext) * 2e-6 - pad);
+		hi[i] = up(h[i] + (fabs(h[i]) + ext) * 2e-6 + pad);
+	}
+}
+
+double rtx_frame_pad(double radius) { return RTX_FRAME_PAD * radius; }
+
+void rtx_world_box(const rtx_object &o, float lo[3], float hi[3])
+{
+	float l[3], h[3];
+	for (int a = 0; a < 3; a++) {
+		if (o.type == RTX_SPHERE) {
+			l[a] = o.p0[a] - o.radius;
+			h[a] = o.p0[a] + o.radius;
+		} else {
+			l[a] = std::min(o.p0[a], std::min(o.p1[a], o.p2[a]));
+			h[a] = std::max(o.p0[a], std::max(o.p1[a], o.p2[a]));
+		}
+	}
+	/* padded so the traversal's FMA slab test is conservative */
+	const float ext = std::max(h[0] - l[0], std::max(h[1] - l[1], h[2] - l[2]));
+	for (int a = 0; a < 3; a++) {
+		lo[a] = l[a] - (std::fabs(l[a]) + ext) * 2e-6f - 1e-30f;
+		hi[a] = h[a] + (std::fabs(h[a]) + ext) * 2e-6f + 1e-30f;
+	}
+}
+
+extern "C" int rtx_tree_frame(const rtx_scene_desc *sc, int *rotated, float rot[9], float center[3], double *cost_ratio)
+{
+	if (!sc || !rotated || !rot || !center)
+		return rtx_fail(RTX_ERR_ARG, "null argument");
+	if (sc->num_objects && !sc->objects)
+		return rtx_fail(RTX_ERR_ARG, "objects pointer is null");
+	std::vector<uint32_t> bounded;
+	float lo[3] = { FLT_MAX, FLT_MAX, FLT_MAX }, hi[3] = { -FLT_MAX, -FLT_MAX, -FLT_MAX };
+	for (uint32_t i = 0; i < sc->num_objects; i++) {
+		const rtx_object &o = sc->objects[i];
+		if (o.type != RTX_SPHERE && o.type != RTX_TRIANGLE)
+			continue;
+		bounded.push_back(i);
+		float l[3], h[3];
+		rtx_world_box(o, l, h);
+		for (int a = 0; a < 3; a++) {
+			lo[a] = std::min(lo[a], l[a]);
+			hi[a] = std::max(hi[a], h[a]);
+		}
+	}
+	DTreeFrame F;
+	const double ratio = rtx_frame_choose(sc, bounded, lo, hi, F);
+	memcpy(rot, F.r, 36);
+	memcpy(center, F.c, 12);
+	if (cost_ratio)
+		*cost_ratio = ratio;
+	*rotated = F.rotated ? 1 : 0;
+	return RTX_OK;
+}

@@ -1,0 +1,30 @@
+/*
+ * The trees' frame (rtx_device.h DTreeFrame, rtx_frame.cpp): choosing it for a scene and the
+ * leaf boxes in it.  Library-internal (librtx); the public diagnostic is rtx_tree_frame (rtx.h).
+ */
+#ifndef RTX_FRAME_H
+#define RTX_FRAME_H
+
+#include <vector>
+
+#include "rtx.h"
+#include "rtx_device.h"
+
+int rtx_fail(int code, const char *fmt, ...);
+
+/* object o's world box (sphere_get_corners / triangle_get_corners, object.c:277-282, 375-388),
+ * padded for the walks' FMA slab test */
+void rtx_world_box(const rtx_object &o, float lo[3], float hi[3]);
+/* the frame for the bounded objects `bounded` of sc (world box lo / hi): F, and its sampled
+ * leaf-box cost relative to the identity's (1.0: the identity, F.rotated = 0) */
+double rtx_frame_choose(const rtx_scene_desc *sc, const std::vector<uint32_t> &bounded, const float world_lo[3],
+			const float world_hi[3], DTreeFrame &F);
+/* the largest |x - c| component over the bounded objects (spheres: + radius) */
+double rtx_frame_radius(const rtx_scene_desc *sc, const std::vector<uint32_t> &bounded, const DTreeFrame &F);
+/* the transform's leaf-box padding for a scene of that radius */
+double rtx_frame_pad(double radius);
+/* object o's box in frame F (F.rotated), rounded outward and padded by pad plus the relative
+ * padding of rtx_world_box */
+void rtx_frame_box(const rtx_object &o, const DTreeFrame &F, double pad, float lo[3], float hi[3]);
+
+#endif

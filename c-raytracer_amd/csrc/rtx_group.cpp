@@ -3,8 +3,9 @@
  * one process.  Replaces the reference's parallel point, the OpenMP row loop of render()
  * (render.c:349-352), with a tile deal over devices:
  *
- *   upload   the scene is flattened and its BVHs built ONCE on the host (rtx_build_scene,
- *            the work of accel_init, accel.c:266-315), then uploaded to every device
+ *   upload   the scene is flattened and its BVHs built ONCE, on device 0 (rtx_build_scene,
+ *            the work of accel_init, accel.c:266-315: device SAH build + 8-wide collapse); the
+ *            other devices get peer copies of the device-built records and tree over xGMI
  *   render   device r renders tiles t = r (mod n) on its own host thread (rtx_render_common
  *            with tile_offset r, tile_stride n), into its own HBM framebuffer
  *   gather   devices r > 0 pack their shard into 16-byte {r, g, b, z} tile records
@@ -141,24 +142,74 @@ extern "C" int rtx_group_set_option(rtx_group *g, int option, int64_t value)
 	return RTX_OK;
 }
 
+/* a device buffer of `bytes` on device dst, copied from src on device sd (xGMI peer copy) */
+template <class T> static int peer_copy(T *&out, int dst, const T *src, int sd, size_t bytes)
+{
+	out = nullptr;
+	if (!src || !bytes)
+		return RTX_OK;
+	HIP_TRY(hipSetDevice(dst));
+	HIP_TRY(hipMalloc(&out, bytes));
+	hipError_t e = hipMemcpyPeer(out, dst, src, sd, bytes);
+	if (e != hipSuccess) {
+		dfree(out);
+		return fail(RTX_ERR_HIP, "peer copy of %zu bytes from device %d to %d failed: %s", bytes, sd, dst, hipGetErrorString(e));
+	}
+	return RTX_OK;
+}
+
 extern "C" int rtx_group_upload_scene(rtx_group *g, const rtx_scene_desc *sc)
 {
 	if (!g || !sc)
 		return fail(RTX_ERR_ARG, "null argument");
+	/* built once, on device 0 (the device builder and the 8-wide collapse, as rtx_upload_scene);
+	 * the other devices get device-to-device copies of what the build left in HBM, and the host
+	 * parts (materials, planes, emitters, any host-built tree) from the host */
 	HostScene hs;
-	hs.want_host_recs = g->n > 1;
-	int rc = rtx_build_scene(g->ctx[0], sc, hs);
+	rtx_ctx *c0 = g->ctx[0];
+	int rc = rtx_build_scene(c0, sc, hs);
 	if (rc)
 		return rc;
-	const bool built_on_device = hs.recs_on_device;
-	for (int r = 0; r < g->n; r++) {
-		/* only the building device (ctx[0]) holds device-built records; the others take the
-		 * host copy (hs.want_host_recs) */
-		hs.recs_on_device = built_on_device && r == 0;
-		if ((rc = rtx_upload_built(g->ctx[r], hs)))
+	const bool recs_dev = hs.recs_on_device;
+	const size_t rec_bytes = ((size_t)hs.nnodes + hs.nb) * sizeof(DNode);
+	DW8 *w8 = hs.dev_w8;
+	DW8S *w8s = hs.dev_w8s;
+	uint32_t *leaf = hs.dev_w8leaf;
+	const size_t ent = hs.w8_on_device ? hs.w8_entries : 0;
+	for (int r = 1; r < g->n; r++) {
+		rtx_ctx *c = g->ctx[r];
+		HIP_TRY(hipSetDevice(c->device));
+		dfree(c->d_nodes);
+		c->have_scene = false;
+		if (recs_dev && (rc = peer_copy(c->d_nodes, c->device, c0->d_nodes, c0->device, rec_bytes)))
 			return rc;
+		hs.dev_w8 = nullptr;
+		hs.dev_w8s = nullptr;
+		hs.dev_w8leaf = nullptr;
+		hs.device = c->device;
+		if (!(rc = peer_copy(hs.dev_w8, c->device, w8, c0->device, ent * sizeof(DW8))) &&
+		    !(rc = peer_copy(hs.dev_w8s, c->device, w8s, c0->device, ent * sizeof(DW8S))) &&
+		    !(rc = peer_copy(hs.dev_w8leaf, c->device, leaf, c0->device, ent * sizeof(uint32_t)))) {
+			hs.recs_on_device = recs_dev;
+			rc = rtx_upload_built(c, hs); /* takes the copies */
+		}
+		if (rc) { /* copies a failure left behind */
+			(void)hipSetDevice(c->device);
+			dfree(hs.dev_w8);
+			dfree(hs.dev_w8s);
+			dfree(hs.dev_w8leaf);
+			break;
+		}
 	}
-	return RTX_OK;
+	/* device 0 last: it takes the original buffers (hs frees whatever a failure left) */
+	hs.dev_w8 = w8;
+	hs.dev_w8s = w8s;
+	hs.dev_w8leaf = leaf;
+	hs.device = c0->device;
+	if (rc)
+		return rc;
+	hs.recs_on_device = recs_dev;
+	return rtx_upload_built(c0, hs);
 }
 
 static int grow_recs(float4 *&p, size_t &have, size_t need)

@@ -42,6 +42,13 @@ template <class T> static inline int upload(T *&dst, const std::vector<T> &v)
 	return RTX_OK;
 }
 
+/* the settings a render's shade points per tile depend on (rtx_ctx.sp_tile_key) */
+struct SpKey {
+	uint32_t v[21] = {};
+	uint32_t set = 0;
+	bool operator==(const SpKey &o) const { return set && o.set && std::equal(v, v + 21, o.v); }
+};
+
 struct rtx_ctx {
 	int device = 0;
 	int builder = RTX_BUILD_SAH_GPU; /* the host's SAH tree, built on the device (57 vs 296 ms on the dragon) */
@@ -55,8 +62,6 @@ struct rtx_ctx {
 	DEmitter *d_emitters = nullptr;
 	DQNode *d_qnodes = nullptr;
 	uint32_t *d_top = nullptr;
-	DQNode *d_wnodes = nullptr;
-	float4 *d_wtris = nullptr;
 	DW8 *d_w8 = nullptr;
 	DW8S *d_w8s = nullptr;
 	uint32_t *d_w8spill = nullptr; /* k_shadow lane-stack spill of deep 8-wide trees (DScene.w8spill) */
@@ -79,7 +84,7 @@ struct rtx_ctx {
 	/* shade points per tile seen by the last render of this scene with the same GI / bounce
 	 * settings: sizes the next render's chunks (the static estimate is 5x too high on scene6) */
 	double sp_tile_seen = 0.0;
-	uint64_t sp_tile_key = 0;
+	SpKey sp_tile_key{};
 	uint32_t *d_sortbuf = nullptr; /* keys0 | keys1 | vals0 | vals1 (shade-point sort) */
 	size_t sortbuf_bytes = 0;
 	void *d_sorttmp = nullptr;
@@ -103,16 +108,18 @@ struct rtx_ctx {
 	uint32_t opt_grab = 4096;
 	uint32_t opt_lstk = RTX_W8_STACK;
 	int opt_trace_walk = RTX_WALK_AUTO;
+	int opt_frame = RTX_FRAME_AUTO;
 };
 
 struct QFrame {
 	float qo[3], qs[3];
 };
 
-/* a scene flattened and its BVHs built on the host, ready to upload to one or more devices */
+/* a scene flattened and its BVHs built (on the host, or on the building context's device), ready
+ * to upload to one or more devices.  Device buffers it still owns are freed with it. */
 struct HostScene {
 	int builder = RTX_BUILD_SAH_HOST;
-	bool want_host_recs = false;  /* device builder: copy the records back for other devices */
+	int device = 0;               /* the building context's device */
 	bool recs_on_device = false;  /* device builder: the building context holds the records */
 	std::vector<DNode> recs;      /* inner nodes then primitives (64-byte records) */
 	uint32_t nnodes = 0, nb = 0, root_ref = RTX_EMPTY_REF, depth = 0;
@@ -120,14 +127,13 @@ struct HostScene {
 	QFrame qf{};
 	std::vector<uint32_t> qtop;
 	uint32_t ntop = 0;
-	std::vector<DQNode> wnodes;   /* 4-wide BVH */
-	uint32_t wdepth = 0;
 	std::vector<DW8> w8;          /* 8-wide BVH entries (leaf entries filled on the device) */
 	std::vector<uint32_t> w8leaf; /* entry -> primitive index (RTX_NONE: node or hole) */
 	uint32_t w8depth = 0;
 	QFrame w8f{};                 /* its 16-bit frame */
 	bool w8noemit = false;        /* emitters left out of it */
-	/* collapsed on the device (rtx_wide8_dev.hip): the buffers, handed to the context on upload */
+	/* collapsed on the device (rtx_wide8_dev.hip): the buffers, handed to the context on upload
+	 * (rtx_upload_built clears these pointers when it takes them) */
 	bool w8_on_device = false;
 	DW8 *dev_w8 = nullptr;
 	DW8S *dev_w8s = nullptr;
@@ -138,12 +144,27 @@ struct HostScene {
 	std::vector<DEmitter> emit;
 	float bound_lo[3] = { 0, 0, 0 }, bound_hi[3] = { 0, 0, 0 }, ambient[3] = { 0, 0, 0 };
 	uint32_t num_emitters = 0;
+	DTreeFrame tf{};              /* the frame every tree's boxes are in (rtx_frame.cpp) */
+	double frame_ratio = 1.0;     /* its sampled leaf-box cost over the identity's */
+	double frame_ms = 0;          /* choosing it and the leaf boxes in it */
 	double build_ms = 0;
+	HostScene() = default;
+	HostScene(const HostScene &) = delete;
+	HostScene &operator=(const HostScene &) = delete;
+	~HostScene()
+	{
+		if (dev_w8 || dev_w8s || dev_w8leaf) {
+			(void)hipSetDevice(device);
+			dfree(dev_w8);
+			dfree(dev_w8s);
+			dfree(dev_w8leaf);
+		}
+	}
 };
 
 /* flatten sc and build its BVHs (on c's device for the device builder), then upload to c */
 int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs);
-int rtx_upload_built(rtx_ctx *c, const HostScene &hs);
+int rtx_upload_built(rtx_ctx *c, HostScene &hs);
 /* rtx_wide8.cpp: the 8-wide shadow BVH collapsed from the BVH2 (0 = not built) */
 uint32_t rtx_wide8_build(const std::vector<DNode> &inner, uint32_t nnodes, const DPrim *prims, uint32_t root_ref,
 			 const float lo[3], const float hi[3], const std::vector<uint32_t> &skip_objs, QFrame &F,

@@ -156,6 +156,18 @@ __device__ __forceinline__ f3 safe_inv_fast(f3 d)
 		   fabsf(d.z) > 1e-30f ? __builtin_amdgcn_rcpf(d.z) : copysignf(1e30f, d.z));
 }
 
+/* a point / direction in the trees' frame (rtx_device.h DTreeFrame): x' = R (x - c), d' = R d.
+ * Culling only: the leaf boxes are padded for this rounding (rtx_frame.cpp) */
+__device__ __forceinline__ f3 tf_dir(const float (&r)[3][3], f3 d)
+{
+	return mk3(fmaf(r[0][0], d.x, fmaf(r[0][1], d.y, r[0][2] * d.z)), fmaf(r[1][0], d.x, fmaf(r[1][1], d.y, r[1][2] * d.z)),
+		   fmaf(r[2][0], d.x, fmaf(r[2][1], d.y, r[2][2] * d.z)));
+}
+__device__ __forceinline__ f3 tf_point(const float (&r)[3][3], const float (&c)[3], f3 x)
+{
+	return tf_dir(r, mk3(x.x - c[0], x.y - c[1], x.z - c[2]));
+}
+
 /* slab test on the traversal path: hit iff [max(tnear,0), min(tfar,tlim)] non-empty */
 __device__ __forceinline__ bool slab(float lox, float hix, float loy, float hiy, float loz, float hiz, f3 oi, f3 inv,
 				     float tlim, float &tnear)

@@ -7,12 +7,14 @@
  * unbound planes, walks the BVH for any opaque blocker (multiplying the
  * transmittance of transparent ones), then evaluates Phong / Blinn.
  *
- * The walk: every lane walks its own shadow ray over the 4-wide quantised BVH
- * (rtx_device.h RTX_W_STACK, shadow_walk4): one 64-byte node per step, four box
- * tests per memory round trip, pending siblings as (first child, slot mask)
- * groups in a register and an LDS stack.  Scenes whose wide tree is too deep
- * for the stack walk the threaded BVH2 instead (shadow_walk: one 16-byte
- * record per step, no stack, the top levels in LDS).
+ * The walk: every lane walks its own shadow ray over the 8-wide compressed BVH
+ * (rtx_device.h DW8, shadow_walk8): one 64-byte node per step, eight box tests
+ * per memory round trip, pending siblings as (base, slot mask) groups in a
+ * register, an LDS lane stack and HBM below it (any depth).  Small scenes (the
+ * whole threaded BVH2 fits the LDS top copy) walk the threaded BVH2 instead
+ * (shadow_walk: one 16-byte record per step, no stack, read from LDS).  Both
+ * walks test boxes in the tree's frame (DScene.tf: the rotation the uploader
+ * chose for the leaf boxes) and primitives in world space.
  *
  * Scheduling: persistent workgroups; each wave takes `per_wave` shade points at
  * a time from a global queue in Morton order of their position (rtx_sort.hip),
@@ -34,12 +36,6 @@
 #endif
 #ifndef RTX_SH_OCT
 #define RTX_SH_OCT 1 /* walks specialised on a wave-uniform direction octant */
-#endif
-#ifndef RTX_W_SUNI
-#define RTX_W_SUNI 1 /* wide walk: a node all live lanes share is read with scalar loads */
-#endif
-#ifndef RTX_W_NEAR
-#define RTX_W_NEAR 1 /* wide walk: visit the nearest hit inner child first (blockers found sooner) */
 #endif
 #ifndef RTX_SH_FASTPOW
 #define RTX_SH_FASTPOW 1 /* specular powf from v_log_f32 / v_exp_f32 (sh_pow) */
@@ -190,27 +186,24 @@ __device__ __forceinline__ bool shadow_leaf(uint32_t L, const char *__restrict__
 	return false;
 }
 
-/* the quantised threaded BVH and its frame (rtx_device.h DQNode) */
+/* the trees of the shadow walks and their 16-bit frame (rtx_device.h DQNode, DW8) */
 struct QBvh {
 	const DQNode *q;
 	f3 qo, qs, qsi; /* qsi = 1 / qs (IEEE, per component) */
 	const uint4 *top;     /* the workgroup's LDS copy of the top records */
 	const uint32_t *tend; /* ... and of the cut records' range ends */
-	uint32_t nt, nq;      /* top records, DQNode records */
-	const DQNode *w;      /* the 4-wide BVH (rtx_device.h RTX_W_STACK), WALK_W4 */
-	const char *wt;       /* ... and its 48-byte leaf triangle records */
+	uint32_t nt;          /* top records */
 	const DW8 *w8;        /* the 8-wide BVH (rtx_device.h DW8), WALK_W8 */
 	const DW8S *w8s;      /* ... its nodes' scalar-path copies */
 	uint32_t *spill;      /* this lane's stack entries from lstk on: entry k at spill[(k - lstk) * spill_stride] */
 	uint32_t spill_stride;
 	uint32_t lstk;        /* lane-stack entries in LDS (<= RTX_W8_STACK) */
-	uint32_t known;       /* WALK_W8: leaf slots marked transparent / opaque, no emitter in the tree */
 	lds_u32 *stk;         /* this lane's LDS stack of sibling groups: entry k at stk[k * WAVE] */
 	lds_u32 *tq;          /* WALK_W8: this lane's LDS queue of deferred leaf groups, entry k at tq[k * WAVE] */
 };
 
 /* the shadow walks k_shadow instantiates */
-enum { WALK_BVH2 = 0, WALK_W4 = 1, WALK_W8 = 2 };
+enum { WALK_BVH2 = 0, WALK_W8 = 2 }; /* the RTX_WALK_* values */
 
 /* is_light_blocked's BVH part (accel.c:360-387) for this lane's ray.  The walk starts in the
  * workgroup's LDS copy of the tree's top levels: a cut record whose box is hit hands the lane
@@ -219,10 +212,10 @@ enum { WALK_BVH2 = 0, WALK_W4 = 1, WALK_W8 = 2 };
  * On an opaque hit tl becomes -1. */
 template <bool COUNT, int OCT>
 __device__ __forceinline__ void shadow_walk(const QBvh &Q, const char *__restrict__ recs, const DMaterial *__restrict__ mats,
-					    f3 o, f3 d, f3 inv, float &tl, uint32_t emit_obj, f3 &li, ShadowCount &sc)
+					    f3 o, f3 d, f3 ob, f3 inv, float &tl, uint32_t emit_obj, f3 &li, ShadowCount &sc)
 {
 	const f3 invq = mk3(inv.x * Q.qsi.x, inv.y * Q.qsi.y, inv.z * Q.qsi.z);
-	const f3 oq = mk3((o.x - Q.qo.x) * Q.qs.x, (o.y - Q.qo.y) * Q.qs.y, (o.z - Q.qo.z) * Q.qs.z);
+	const f3 oq = mk3((ob.x - Q.qo.x) * Q.qs.x, (ob.y - Q.qo.y) * Q.qs.y, (ob.z - Q.qo.z) * Q.qs.z);
 	const f3 oi = mul3v(oq, invq);
 	const uint32_t nt = Q.nt;
 	uint32_t t = tl >= 0.f ? 0u : nt, g = 0, ge = 0;
@@ -283,143 +276,6 @@ __device__ __forceinline__ void shadow_walk(const QBvh &Q, const char *__restric
 	}
 }
 
-/* is_light_blocked's BVH part (accel.c:360-387) over the 4-wide BVH (rtx_device.h
- * RTX_W_STACK): one 64-byte node per step (four 16-byte loads issued together, one memory
- * latency for four box tests).  Hit leaves are tested at once, in slot order; of the hit inner
- * children the first is visited next and the rest are kept as one group (first child << 4 |
- * slot mask) in a register, the older groups in the lane's LDS stack.  Any-hit needs no visit
- * order.  tl < 0 on entry: inactive lane.  On an opaque hit tl becomes -1. */
-template <bool COUNT, int OCT>
-__device__ __forceinline__ void shadow_walk4(const QBvh &Q, const char *__restrict__ recs, const DMaterial *__restrict__ mats,
-					     f3 o, f3 d, f3 inv, float &tl, uint32_t emit_obj, f3 &li, ShadowCount &sc)
-{
-	const f3 invq = mk3(inv.x * Q.qsi.x, inv.y * Q.qsi.y, inv.z * Q.qsi.z);
-	const f3 oq = mk3((o.x - Q.qo.x) * Q.qs.x, (o.y - Q.qo.y) * Q.qs.y, (o.z - Q.qo.z) * Q.qs.z);
-	const f3 oi = mul3v(oq, invq);
-	lds_u32 *stk = Q.stk;
-	uint32_t node = tl >= 0.f ? 0u : RTX_NONE, grp = 0, sp = 0;
-	uint32_t nbox = 0, ntri = 0, nsph = 0, nstep = 0, nlr = 0, nun = 0;
-	while (node != RTX_NONE) {
-		uint4 s0, s1, s2, s3;
-		const uint32_t un = uni(node);
-		if (RTX_W_SUNI && !ballot(node != un)) {
-			/* every live lane is at one node: read it through the scalar cache (no vector-memory
-			 * address / data cycles, which the divergent steps keep busy) */
-			const auto *U = (const __attribute__((address_space(4))) u4v *)(Q.w + 4 * (size_t)un);
-			const u4v a = U[0], b = U[1], c = U[2], e = U[3];
-			s0 = make_uint4(a.x, a.y, a.z, a.w);
-			s1 = make_uint4(b.x, b.y, b.z, b.w);
-			s2 = make_uint4(c.x, c.y, c.z, c.w);
-			s3 = make_uint4(e.x, e.y, e.z, e.w);
-		} else {
-			const DQNode *N = Q.w + 4 * (size_t)node;
-			s0 = ldg4u(N);
-			s1 = ldg4u(N + 1);
-			s2 = ldg4u(N + 2);
-			s3 = ldg4u(N + 3);
-		}
-		float n0, n1, n2, n3; /* entry distances: the nearest hit inner child is visited next */
-		bool h0 = box_hit_q<OCT>(s0, oi, invq, tl, n0), h1 = box_hit_q<OCT>(s1, oi, invq, tl, n1);
-		bool h2 = box_hit_q<OCT>(s2, oi, invq, tl, n2), h3 = box_hit_q<OCT>(s3, oi, invq, tl, n3);
-		if (OCT == 8) { /* the min/max slab form would turn an empty slot's inverted box around */
-			h1 = h1 && s1.w != RTX_EMPTY_REF;
-			h2 = h2 && s2.w != RTX_EMPTY_REF;
-			h3 = h3 && s3.w != RTX_EMPTY_REF;
-		}
-		if (COUNT) {
-			nstep++;
-			nbox += 1u + (s1.w != RTX_EMPTY_REF) + (s2.w != RTX_EMPTY_REF) + (s3.w != RTX_EMPTY_REF);
-			nun += ballot(node != uni(node)) ? 0u : 1u;
-		}
-		const uint32_t hm = (uint32_t)h0 | ((uint32_t)h1 << 1) | ((uint32_t)h2 << 2) | ((uint32_t)h3 << 3);
-		const uint32_t lf = ((s0.w & RTX_REF_LEAF) | ((s1.w & RTX_REF_LEAF) << 1) | ((s2.w & RTX_REF_LEAF) << 2) |
-				     ((s3.w & RTX_REF_LEAF) << 3)) >> 5;
-		uint32_t lm = hm & lf, im = hm & ~lf;
-		bool blocked = false;
-		if (COUNT) {
-			uint32_t r = 0;
-			for (uint32_t m = lm;; m &= m - 1) { /* rounds = the wave's largest leaf-hit count */
-				if (!ballot(m != 0))
-					break;
-				r++;
-			}
-			nlr += r;
-		}
-		while (lm) {
-			const uint32_t c = __builtin_ctz(lm);
-			lm &= lm - 1;
-			const uint32_t L = c == 0 ? s0.w : c == 1 ? s1.w : c == 2 ? s2.w : s3.w;
-			if (shadow_leaf<COUNT, 48>(L, Q.wt + (size_t)(L >> 6) * 48, mats, o, d, tl, emit_obj, li, ntri, nsph)) {
-				blocked = true;
-				break;
-			}
-		}
-		if (blocked) {
-			tl = -1.f;
-			break;
-		}
-		if (im) {
-			uint32_t c = __builtin_ctz(im);
-			if (RTX_W_NEAR) { /* inner children occupy the first slots */
-				float best = c == 0 ? n0 : c == 1 ? n1 : c == 2 ? n2 : n3;
-				if ((im & 2u) && n1 < best) {
-					best = n1;
-					c = 1;
-				}
-				if ((im & 4u) && n2 < best) {
-					best = n2;
-					c = 2;
-				}
-				if ((im & 8u) && n3 < best)
-					c = 3;
-			}
-			const uint32_t base = s0.w >> 6;
-			im &= ~(1u << c);
-			node = base + c;
-			if (im) {
-				if (grp) {
-					stk[sp * WAVE] = grp;
-					sp++;
-				}
-				grp = (base << 4) | im;
-			}
-		} else if (grp) {
-			const uint32_t c = __builtin_ctz(grp & 15u);
-			node = (grp >> 4) + c;
-			grp &= ~(1u << c);
-			if (!(grp & 15u)) {
-				grp = 0;
-				if (sp) {
-					sp--;
-					grp = stk[sp * WAVE];
-				}
-			}
-		} else {
-			node = RTX_NONE;
-		}
-	}
-	if (COUNT) {
-		uint32_t a = nbox, b = ntri, c = nsph;
-#pragma unroll
-		for (int s = 32; s > 0; s >>= 1) {
-			a += __shfl_xor(a, s, WAVE);
-			b += __shfl_xor(b, s, WAVE);
-			c += __shfl_xor(c, s, WAVE);
-			nstep = max(nstep, (uint32_t)__shfl_xor(nstep, s, WAVE));
-			nun = max(nun, (uint32_t)__shfl_xor(nun, s, WAVE));
-			nlr = max(nlr, (uint32_t)__shfl_xor(nlr, s, WAVE));
-		}
-		sc.boxes += uni(a);
-		sc.gboxes += uni(a);
-		sc.lrounds += uni(nlr);
-		sc.unif += uni(nun);
-		sc.tris += uni(b);
-		sc.sph += uni(c);
-		sc.steps += uni(nstep);
-		sc.walks++;
-	}
-}
-
 /* is_light_blocked's BVH part (accel.c:360-387) over the 8-wide BVH (rtx_device.h DW8): one
  * 64-byte node per step (four 16-byte loads, or one s_load_dwordx16 when every live lane is at
  * the node), eight box tests.  Hit children are taken in the octant's visit order (slot p ^ K):
@@ -436,9 +292,6 @@ __device__ __forceinline__ void shadow_walk4(const QBvh &Q, const char *__restri
 #ifndef RTX_W8_TQ
 #define RTX_W8_TQ 4 /* deferred leaf groups per lane in LDS (besides the one in a register) */
 #endif
-#ifndef RTX_W8_OR
-#define RTX_W8_OR 0 /* > 0: a lane tests at most this many of a step's opaque leaf hits at once, the rest join its deferred groups */
-#endif
 #ifndef RTX_W8_DEFER
 #define RTX_W8_DEFER 64 /* lanes holding deferred leaf tests that trigger a round of them (16 / 32 / 48 / 64: 613 / 601 / 598 / 594 ms) */
 #endif
@@ -446,7 +299,7 @@ __device__ __forceinline__ void shadow_walk4(const QBvh &Q, const char *__restri
  * whose 4th float4 holds its material's kt) against this lane's shadow ray; a hit multiplies
  * the transmittance (accel.c:370-377) */
 template <bool COUNT>
-__device__ __forceinline__ bool w8_defer_test(const char *pr, f3 o, f3 d, float tl, f3 &li, uint32_t &ntri, uint32_t &nsph)
+__device__ __forceinline__ void w8_defer_test(const char *pr, f3 o, f3 d, float tl, f3 &li, uint32_t &ntri, uint32_t &nsph)
 {
 	const float4 a = ldg4(pr, 0), b = ldg4(pr, 16), c = ldg4(pr, 32);
 	bool h;
@@ -461,12 +314,9 @@ __device__ __forceinline__ bool w8_defer_test(const char *pr, f3 o, f3 d, float 
 		h = any_tri(mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z), mk3(c.x, c.y, c.z), o, d, a.w, tl);
 	}
 	if (h) {
-		if (RTX_W8_OR && !(__float_as_uint(c.w) & RTX_META_TRANSPARENT))
-			return true; /* a deferred opaque leaf (RTX_W8_OR): the ray is blocked */
 		const float4 kt = ldg4(pr, 48);
 		li = mul3v(li, mk3(kt.x, kt.y, kt.z));
 	}
-	return false;
 }
 
 /* an opaque leaf test: does the primitive at entry pr block this lane's shadow ray?  (no
@@ -486,123 +336,17 @@ __device__ __forceinline__ bool w8_opaque_test(const char *pr, f3 o, f3 d, float
 	return any_tri(mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z), mk3(c.x, c.y, c.z), o, d, a.w, tl);
 }
 
-#ifndef RTX_W8_SLEAF
-#define RTX_W8_SLEAF 0 /* uniform steps: opaque leaf tests slot by slot, the entry through scalar loads */
-#endif
-/* the same test on a wave-uniform entry, read with one s_load_dwordx16 (SGPR operands) */
-template <bool COUNT>
-__device__ __forceinline__ bool w8_opaque_test_s(const DW8 *e, f3 o, f3 d, float tl, uint32_t &ntri, uint32_t &nsph)
-{
-	typedef float f16v __attribute__((ext_vector_type(16)));
-	const f16v v = *(const __attribute__((address_space(4))) f16v *)e;
-	if ((__float_as_uint(v[11]) >> 24) == RTX_SPHERE) {
-		if (COUNT)
-			nsph++;
-		float t = 0.f;
-		return hit_sphere(mk3(v[0], v[1], v[2]), v[4], o, d, v[3], t) && t < tl;
-	}
-	if (COUNT)
-		ntri++;
-	return any_tri(mk3(v[0], v[1], v[2]), mk3(v[4], v[5], v[6]), mk3(v[8], v[9], v[10]), o, d, v[3], tl);
-}
-
-#ifndef RTX_W8_VH
-#define RTX_W8_VH 0 /* measurement option: divergent steps read the half-float node copies (DW8S) per lane */
-#endif
-#ifndef RTX_W8_TR
-#define RTX_W8_TR 0 /* measurement option: divergent steps fetch nodes quad by quad (one line per 4-lane quad) */
-#endif
-/* A divergent step's node fetch, quad-coherent.  The texture path takes a wave's 16-byte loads
- * four lanes (64 B) per cycle and a cycle more for every further line a quad touches, so four
- * per-lane loads of 64 lanes' different nodes cost up to 4 x 64 cycles.  Here load k of quad q
- * (lanes 4q..4q+3) reads the four quarters of ray 4q+k's node, one line per quad (4 x 16 cycles
- * at most, only for walking rays), and a 4 x 4 transpose within each quad (two DPP butterfly
- * stages) gives every lane its own node's 16 words.  Every lane of the wave takes part (the
- * DPP moves read the quad's other lanes); lanes whose ray is not walking get garbage. */
-template <int K> __device__ __forceinline__ uint32_t quad_bcast(uint32_t v)
-{
-	return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, K * 0x55, 0xF, 0xF, false); /* quad_perm [K,K,K,K] */
-}
-/* this lane's entries of a per-wave [entry][lane] LDS array, from the wave's base address
- * (SGPR): the lane offset is recomputed at every access (volatile), so no VGPR holds it across
- * the walk (the 64-VGPR budget spilled the lane pointer to scratch) */
-struct LaneLds {
-	uint32_t base; /* LDS byte address of entry 0, lane 0 */
-	__device__ __forceinline__ lds_u32 &operator[](uint32_t k) const
-	{
-		uint32_t l4;
-		asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\tv_lshlrev_b32 %0, 2, %0" : "=v"(l4));
-		return *(lds_u32 *)(base + l4 + 4u * k);
-	}
-};
-template <int M> __device__ __forceinline__ uint32_t quad_xor(uint32_t v)
-{
-	return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, M == 1 ? 0xB1 : 0x4E, 0xF, 0xF, true); /* quad_perm [1,0,3,2] / [2,3,0,1] */
-}
-template <int K> __device__ __forceinline__ void w8_quad_load(const DW8 *__restrict__ w8, uint32_t node, uint32_t q16,
-							       uint32_t (&b)[4])
-{
-	const uint32_t nk = quad_bcast<K>(node); /* ray 4q+K's node */
-	uint4 x = make_uint4(0u, 0u, 0u, 0u);
-	if (nk != RTX_NONE) /* ray 4q+K walks; 32-bit byte offset from the tree's base */
-		x = ldg4u((const char *)w8 + (nk * (uint32_t)sizeof(DW8) + q16));
-	b[0] = x.x;
-	b[1] = x.y;
-	b[2] = x.z;
-	b[3] = x.w;
-}
-__device__ __forceinline__ void w8_fetch_quads(const DW8 *__restrict__ w8, uint32_t node, uint32_t (&w)[16])
-{
-	/* 16 x (lane & 3), recomputed here (volatile: kept out of the register budget between steps) */
-	uint32_t q16;
-	asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\tv_and_b32 %0, 3, %0\n\tv_lshlrev_b32 %0, 4, %0"
-		     : "=v"(q16));
-	const uint32_t i = q16 >> 4;
-	uint32_t B[4][4];
-	w8_quad_load<0>(w8, node, q16, B[0]);
-	w8_quad_load<1>(w8, node, q16, B[1]);
-	w8_quad_load<2>(w8, node, q16, B[2]);
-	w8_quad_load<3>(w8, node, q16, B[3]);
-	/* lane i holds quarter i of rays k = 0..3; lane j wants quarters 0..3 of ray j */
-	const bool odd = i & 1u, hi = i & 2u;
-#pragma unroll
-	for (int e = 0; e < 4; e += 2)
-#pragma unroll
-		for (int d = 0; d < 4; d++) {
-			const uint32_t pe = quad_xor<1>(B[e + 1][d]), po = quad_xor<1>(B[e][d]);
-			const uint32_t ne = odd ? pe : B[e][d], no = odd ? B[e + 1][d] : po;
-			B[e][d] = ne;
-			B[e + 1][d] = no;
-		}
-#pragma unroll
-	for (int e = 0; e < 2; e++)
-#pragma unroll
-		for (int d = 0; d < 4; d++) {
-			const uint32_t pl = quad_xor<2>(B[e + 2][d]), ph = quad_xor<2>(B[e][d]);
-			const uint32_t nl = hi ? pl : B[e][d], nh = hi ? B[e + 2][d] : ph;
-			B[e][d] = nl;
-			B[e + 2][d] = nh;
-		}
-#pragma unroll
-	for (int k = 0; k < 4; k++)
-#pragma unroll
-		for (int d = 0; d < 4; d++)
-			w[4 * k + d] = B[k][d];
-}
-
 template <bool COUNT, int OCT>
-__device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__restrict__ mats, f3 o, f3 d, f3 inv,
+__device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__restrict__ mats, f3 o, f3 d, f3 ob, f3 inv,
 					     float &tl, uint32_t emit_obj, f3 &li, ShadowCount &sc)
 {
 	constexpr uint32_t K = (OCT == 8 || !RTX_W8_SORDER) ? 0u : (~(uint32_t)OCT & 7u);
+	/* the ray in the tree's 16-bit frame: ob / inv are its origin and inverse direction in the
+	 * tree's rotated frame (shadow_query), o / d the world ray the primitives are tested with */
 	const f3 invq = mk3(inv.x * Q.qsi.x, inv.y * Q.qsi.y, inv.z * Q.qsi.z);
-	const f3 oq = mk3((o.x - Q.qo.x) * Q.qs.x, (o.y - Q.qo.y) * Q.qs.y, (o.z - Q.qo.z) * Q.qs.z);
+	const f3 oq = mk3((ob.x - Q.qo.x) * Q.qs.x, (ob.y - Q.qo.y) * Q.qs.y, (ob.z - Q.qo.z) * Q.qs.z);
 	const f3 oi = mul3v(oq, invq);
-#if RTX_W8_TR
-	const LaneLds stk{ uni((uint32_t)(uintptr_t)Q.stk - 4u * lane_id()) }, tq{ uni((uint32_t)(uintptr_t)Q.tq - 4u * lane_id()) };
-#else
 	lds_u32 *stk = Q.stk, *tq = Q.tq;
-#endif
 	uint32_t node = tl >= 0.f ? 0u : RTX_NONE, grp = 0, sp = 0, tgrp = 0, tn = 0;
 	uint32_t nbox = 0, ntri = 0, nsph = 0, nstep = 0, nlr = 0, nun = 0;
 	for (;;) {
@@ -619,41 +363,18 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 				tgrp &= tgrp - 1;
 				if (!(tgrp & 0xFFu))
 					tgrp = tn ? tq[--tn * WAVE] : 0u;
-				if (w8_defer_test<COUNT>(pr, o, d, tl, li, ntri, nsph)) {
-					tl = -1.f;
-					node = RTX_NONE;
-					tgrp = 0;
-					tn = 0;
-				}
+				w8_defer_test<COUNT>(pr, o, d, tl, li, ntri, nsph);
 			}
 			continue;
 		}
 		uint32_t lm = 0, base = 0; /* this step's opaque leaf hits (visit order) and their block */
-		bool ustep = false;         /* every walking lane at one node (base wave-uniform) */
-		W8Visit v;
-		bool vdone = false;
-		if (RTX_W8_TR) {
-			/* a divergent step: the nodes fetched quad by quad and tested by every lane (the
-			 * transpose reads all lanes of a quad; lanes that are not walking test garbage and
-			 * ignore it) */
-			const uint32_t un = readlane(node, (uint32_t)__ffsll((long long)walking) - 1);
-			if (ballot(node != RTX_NONE && node != un)) {
-				uint32_t w[16];
-				w8_fetch_quads(Q.w8, node, w);
-				v = w8_visit<OCT, K, false>(w, invq, oi, tl);
-				vdone = true;
-			}
-		}
 		if (node != RTX_NONE) {
 			const uint32_t un = uni(node);
-			if (vdone) {
-			} else if (RTX_W8_TR || (RTX_W_SUNI && !ballot(node != un))) {
+			W8Visit v;
+			if (!ballot(node != un)) {
 				/* every walking lane is at one node: its scalar-path copy through the scalar cache,
-				 * the planes as SGPR float operands */
+				 * the planes as SGPR float operands (no vector-memory address / data cycles) */
 				v = w8_visit_s<OCT, K>(Q.w8s + (size_t)un, invq, oi, tl);
-				ustep = true;
-			} else if (RTX_W8_VH) {
-				v = w8_visit_v<OCT, K>(Q.w8s + (size_t)node, invq, oi, tl);
 			} else {
 				uint32_t w[16];
 				const DW8 *N = Q.w8 + (size_t)node;
@@ -672,21 +393,13 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 			lm = hm & ~v.io & ~v.to;
 			uint32_t im = hm & v.io;
 			const uint32_t dm = hm & v.to;
-			uint32_t dmo = dm;
 			if (COUNT) {
 				nstep++;
 				nbox += popc64(v.nv);
 				nun += ballot(node != uni(node)) ? 0u : 1u;
 			}
-			if (RTX_W8_OR) { /* opaque leaf hits beyond the first RTX_W8_OR: deferred with the transparent ones */
-				uint32_t keep = lm;
-				for (int r = 0; r < RTX_W8_OR; r++)
-					keep &= keep - 1;
-				dmo = dm | keep;
-				lm &= ~keep;
-			}
-			if (dmo) { /* transparent leaves: deferred */
-				const uint32_t g = (base << 8) | dmo;
+			if (dm) { /* transparent leaves: deferred */
+				const uint32_t g = (base << 8) | dm;
 				if (tgrp)
 					tq[tn++ * WAVE] = g;
 				else
@@ -720,54 +433,28 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 				node = RTX_NONE;
 			}
 		}
-		/* opaque leaves, at once (an opaque hit ends the ray) */
+		/* opaque leaves, at once (an opaque hit ends the ray): the tree marks every leaf slot (built
+		 * from the primitive records, emitters left out), each lane tests its own.  (Dealing the
+		 * wave's tests over its lanes with ds_permute, one round for all, measured slower on scene6:
+		 * 2834 vs 2806 ms, every dealt job tested without the early break) */
 		if (!ballot(lm != 0))
 			continue;
+		if (COUNT) {
+			uint32_t r = 0;
+			for (uint32_t m = lm;; m &= m - 1) {
+				if (!ballot(m != 0))
+					break;
+				r++;
+			}
+			nlr += r;
+		}
 		bool blocked = false;
-		if (RTX_W8_SLEAF && ballot(ustep)) {
-			/* marked tree, uniform step: the wave's hit slots in visit order, each slot's entry read
-			 * once through the scalar cache and tested by the lanes that hit it (no vector-memory
-			 * traffic; a blocked lane drops out) */
-			const uint32_t ub = readlane(base, (uint32_t)__ffsll((long long)ballot(ustep)) - 1); /* a walking lane's */
-			uint32_t om = 0;
-#pragma unroll
-			for (int q = 0; q < 8; q++)
-				om |= ballot((lm >> q) & 1u) ? 1u << q : 0u;
-			while (om) {
-				const uint32_t p = __builtin_ctz(om);
-				om &= om - 1;
-				if (COUNT)
-					nlr++;
-				if ((lm >> p) & 1u) {
-					if (w8_opaque_test_s<COUNT>(Q.w8 + ub + (p ^ K), o, d, tl, ntri, nsph)) {
-						blocked = true;
-						lm = 0;
-					}
-				}
-				if (!ballot((lm & om) != 0))
-					break;
-			}
-		} else {
-			/* the tree marks every leaf slot (built from the primitive records, emitters left out):
-			 * these are opaque, each lane tests its own.  (Dealing the wave's tests over its lanes
-			 * with ds_permute, one round for all, measured slower on scene6: 2834 vs 2806 ms, every
-			 * dealt job tested without the early break) */
-			if (COUNT) {
-				uint32_t r = 0;
-				for (uint32_t m = lm;; m &= m - 1) {
-					if (!ballot(m != 0))
-						break;
-					r++;
-				}
-				nlr += r;
-			}
-			while (lm) {
-				const uint32_t p = __builtin_ctz(lm);
-				lm &= lm - 1;
-				if (w8_opaque_test<COUNT>((const char *)(Q.w8 + base + (p ^ K)), o, d, tl, ntri, nsph)) {
-					blocked = true;
-					break;
-				}
+		while (lm) {
+			const uint32_t p = __builtin_ctz(lm);
+			lm &= lm - 1;
+			if (w8_opaque_test<COUNT>((const char *)(Q.w8 + base + (p ^ K)), o, d, tl, ntri, nsph)) {
+				blocked = true;
+				break;
 			}
 		}
 		if (blocked) { /* the queue too: a full queue left behind would keep the wave in deferred rounds */
@@ -805,8 +492,8 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 template <bool COUNT, int WALK>
 __device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restrict__ recs, const DMaterial *__restrict__ mats,
 					     const DPlane *__restrict__ planes, uint32_t num_planes, const DEmitter *__restrict__ emitters,
-					     uint32_t test_emitters, bool have_tree, bool act, f3 o, f3 d, float dist,
-					     uint32_t emit_obj, f3 &li, ShadowCount &sc)
+					     uint32_t test_emitters, bool have_tree, const DTreeFrame &tf, bool act, f3 o, f3 d,
+					     float dist, uint32_t emit_obj, f3 &li, ShadowCount &sc)
 {
 	float tl = act ? dist : -1.f;
 	for (uint32_t i = 0; i < num_planes; i++) { /* plane records are wave-uniform: s_load */
@@ -847,7 +534,21 @@ __device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restri
 	const u64 live = ballot(alive);
 	if (!live || !have_tree)
 		return act && !alive;
-	const f3 inv = safe_inv_fast(d); /* boxes are padded 2e-6 relative: a 1-ulp 1/d keeps the test conservative */
+	/* the ray in the trees' frame (rtx_device.h DTreeFrame): origin ob, direction db */
+	f3 ob = o, db = d;
+	if (uni(tf.rotated)) {
+		float r[3][3], c[3];
+#pragma unroll
+		for (int i = 0; i < 3; i++) {
+			c[i] = __uint_as_float(uni(__float_as_uint(tf.c[i])));
+#pragma unroll
+			for (int j = 0; j < 3; j++)
+				r[i][j] = __uint_as_float(uni(__float_as_uint(tf.r[i][j])));
+		}
+		ob = tf_point(r, c, o);
+		db = tf_dir(r, d);
+	}
+	const f3 inv = safe_inv_fast(db); /* boxes are padded 2e-6 relative: a 1-ulp 1/d keeps the test conservative */
 	const uint32_t oct = ((~__float_as_uint(inv.x)) >> 31) | (((~__float_as_uint(inv.y)) >> 31) << 1) |
 			     (((~__float_as_uint(inv.z)) >> 31) << 2);
 	const uint32_t lead = readlane(oct, (uint32_t)__ffsll((long long)live) - 1);
@@ -856,21 +557,17 @@ __device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restri
 #define RTX_WALK(K)                                                                            \
 	case K:                                                                                \
 		if (WALK == WALK_W8)                                                           \
-			shadow_walk8<COUNT, K>(Q, mats, o, d, inv, tl, emit_obj, li, sc);      \
-		else if (WALK == WALK_W4)                                                      \
-			shadow_walk4<COUNT, K>(Q, recs, mats, o, d, inv, tl, emit_obj, li, sc); \
+			shadow_walk8<COUNT, K>(Q, mats, o, d, ob, inv, tl, emit_obj, li, sc);  \
 		else                                                                           \
-			shadow_walk<COUNT, K>(Q, recs, mats, o, d, inv, tl, emit_obj, li, sc);  \
+			shadow_walk<COUNT, K>(Q, recs, mats, o, d, ob, inv, tl, emit_obj, li, sc); \
 		break;
 		RTX_WALK(0) RTX_WALK(1) RTX_WALK(2) RTX_WALK(3) RTX_WALK(4) RTX_WALK(5) RTX_WALK(6) RTX_WALK(7)
 #undef RTX_WALK
 	default:
 		if (WALK == WALK_W8)
-			shadow_walk8<COUNT, 8>(Q, mats, o, d, inv, tl, emit_obj, li, sc);
-		else if (WALK == WALK_W4)
-			shadow_walk4<COUNT, 8>(Q, recs, mats, o, d, inv, tl, emit_obj, li, sc);
+			shadow_walk8<COUNT, 8>(Q, mats, o, d, ob, inv, tl, emit_obj, li, sc);
 		else
-			shadow_walk<COUNT, 8>(Q, recs, mats, o, d, inv, tl, emit_obj, li, sc);
+			shadow_walk<COUNT, 8>(Q, recs, mats, o, d, ob, inv, tl, emit_obj, li, sc);
 		break;
 	}
 	return act && tl < 0.f;
@@ -883,19 +580,15 @@ __device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restri
  * compiler memory barrier, so none stays live in registers across the walk. */
 struct KShadow {
 	const DPrim *prims;   /* primitive records (DQNode leaf refs are byte offsets from `recs`) */
-	const char *recs;     /* base of the record array the leaf refs point into */
-	const DQNode *qnodes; /* threaded quantised BVH */
-	const DQNode *wnodes; /* 4-wide quantised BVH (WALK_W4 instances) */
-	const char *wtris;    /* its leaves' 48-byte triangle records */
-	const DW8 *w8;        /* 8-wide compressed BVH (WALK_W8 instances; qo / qs / qsi are then its frame) */
+	const char *recs;     /* base of the record array the leaf refs point into */	const DQNode *qnodes; /* threaded quantised BVH */
+const DW8 *w8;        /* 8-wide compressed BVH (WALK_W8 instances; qo / qs / qsi are then its frame) */
 	const DW8S *w8s;      /* its nodes' scalar-path copies */
 	uint32_t *w8spill;    /* lane-stack spill area, [entry][grid lane] */
 	uint32_t w8lstk;      /* lane-stack entries in LDS */
-	uint32_t test_emitters; /* emitters shadow_query tests linearly (the 8-wide tree leaves them out), else 0 */
-	uint32_t w8known;       /* the 8-wide tree was built from host records (leaf slots marked, no emitters) */
-	float qo[3], qs[3], qsi[3];
+	uint32_t test_emitters; /* emitters shadow_query tests linearly (the 8-wide tree leaves them out), else 0 */	float qo[3], qs[3], qsi[3];
+	DTreeFrame tf;        /* the trees' frame (their boxes are in it) */
 	const uint32_t *top; /* its top levels (rtx_device.h RTX_QTOP_CUT), copied to LDS per workgroup */
-	uint32_t ntop, nq;
+	uint32_t ntop;
 	const DMaterial *mats;
 	const DPlane *planes;
 	const DEmitter *emitters;
@@ -1038,20 +731,16 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	Q.top = top_q;
 	Q.tend = top_e;
 	Q.nt = uni(ks.ntop);
-	Q.nq = uni(ks.nq);
 	const bool have_tree = uni(ks.have_tree) != 0 && !RTX_DEBUG_NOWALK;
-	Q.w = WALK == WALK_W4 ? unip(ks.wnodes) : nullptr;
-	Q.wt = WALK == WALK_W4 ? unip(ks.wtris) : nullptr;
 	Q.w8 = WALK == WALK_W8 ? unip(ks.w8) : nullptr;
 	Q.w8s = WALK == WALK_W8 ? unip(ks.w8s) : nullptr;
 	Q.spill_stride = gridDim.x * blockDim.x;
 	Q.spill = WALK == WALK_W8 ? unip(ks.w8spill) + blockIdx.x * blockDim.x + threadIdx.x : nullptr;
 	Q.lstk = uni(ks.w8lstk);
-	Q.known = uni(ks.w8known);
 	Q.stk = stk;
 	Q.tq = stk + RTX_W8_STACK * WAVE;
 	const bool blocked = shadow_query<COUNT, WALK>(Q, unip(ks.recs), unip(ks.mats), unip(ks.planes), uni(ks.num_planes),
-						 emitters, uni(ks.test_emitters), have_tree, act, p, ldir, ldist, E.obj, li, sc);
+						 emitters, uni(ks.test_emitters), have_tree, ks.tf, act, p, ldir, ldist, E.obj, li, sc);
 	reread_barrier();
 	f3 contribution = mk3(0.f, 0.f, 0.f);
 	if (act && !blocked)
@@ -1071,8 +760,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 	constexpr bool TOP = WALK == WALK_BVH2;
 	__shared__ uint4 top_q[TOP ? RTX_TOP_MAX : 1];    /* the top records (rtx_device.h RTX_QTOP_CUT) */
 	__shared__ uint32_t top_e[TOP ? RTX_TOP_MAX : 1]; /* cut records: the DQNode index after the subtree */
-	/* the wide walks' lane stacks */
-	__shared__ uint32_t wstk[RTX_SH_NW][WALK == WALK_W4 ? RTX_W_STACK : WALK == WALK_W8 ? RTX_W8_STACK + RTX_W8_TQ : 1][WAVE];
+	/* the wide walks' lane stacks */	__shared__ uint32_t wstk[RTX_SH_NW][WALK == WALK_W8 ? RTX_W8_STACK + RTX_W8_TQ : 1][WAVE];
 	__shared__ KShadow ks_w[RTX_SH_NW];
 	/* one wave's tables in one struct, so every lane addresses them from one base register */
 	struct WaveTables {
@@ -1247,24 +935,6 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 	}
 }
 
-/* the wide walk's 48-byte triangle records (DScene.wtris): the first three float4 of every
- * DPrim (v0 | centre + eps, e1 | radius + object id, e2 + meta), 2.67 per 128-byte line */
-__global__ void k_pack_tris(const DPrim *__restrict__ prims, uint32_t n, float4 *__restrict__ out)
-{
-	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-	if (i >= 3 * n)
-		return;
-	out[i] = ldg4((const char *)(prims + i / 3), 16 * (i % 3));
-}
-
-extern "C" hipError_t rtx_launch_pack_tris(const DPrim *prims, uint32_t n, float4 *out, hipStream_t stream)
-{
-	if (!n)
-		return hipSuccess;
-	hipLaunchKernelGGL(k_pack_tris, dim3((3 * n + 255) / 256), dim3(256), 0, stream, prims, n, out);
-	return hipGetLastError();
-}
-
 /* ------------------------------------------------------------------------ */
 /* known answers of the fast device functions k_shadow runs (rtx_kat.h)     */
 /* ------------------------------------------------------------------------ */
@@ -1437,9 +1107,8 @@ template <int W> static hipError_t launch_walk(const KShadow &ka, uint32_t nw, u
 	return launch_shadow<false, RTX_SHADOW_OCC_DEFAULT, W>(ka, nw, cus, stream);
 }
 
-/* the walk k_shadow runs for a scene: the 8-wide BVH when built, else the 4-wide one, else the
- * threaded BVH2 */
-static int walk_of(const DScene *S) { return S->w8 ? WALK_W8 : S->wnodes ? WALK_W4 : WALK_BVH2; }
+/* the walk k_shadow runs for a scene: the 8-wide BVH when built, else the threaded BVH2 */
+static int walk_of(const DScene *S) { return S->w8 ? WALK_W8 : WALK_BVH2; }
 
 /* grid lanes of the largest k_shadow launch on `cus` CUs (sizes the 8-wide walk's spill area) */
 extern "C" hipError_t rtx_shadow_grid_lanes(uint32_t cus, uint32_t *lanes)
@@ -1487,8 +1156,8 @@ extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const
 	ka.qnodes = S->qnodes;
 	ka.top = S->top;
 	ka.ntop = S->num_top;
-	ka.nq = S->num_qnodes;
-	for (int a = 0; a < 3; a++) {
+	ka.tf = S->tf;
+for (int a = 0; a < 3; a++) {
 		ka.qo[a] = S->qo[a];
 		ka.qs[a] = S->qs[a];
 		ka.qsi[a] = 1.f / S->qs[a];
@@ -1511,14 +1180,11 @@ extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const
 	ka.attenuation = P->attenuation;
 	ka.reflection = P->reflection;
 	ka.att_offset = P->att_offset;
-	ka.wnodes = S->wnodes;
-	ka.wtris = (const char *)S->wtris;
 	ka.w8 = S->w8;
 	ka.w8s = S->w8s;
 	ka.w8spill = S->w8spill;
 	ka.w8lstk = S->w8lstk;
 	ka.test_emitters = 0;
-	ka.w8known = 0;
 	if (walk == WALK_W8) { /* the 8-wide tree's own frame; the emitters it leaves out are tested linearly */
 		for (int a = 0; a < 3; a++) {
 			ka.qo[a] = S->w8qo[a];
@@ -1526,11 +1192,8 @@ extern "C" hipError_t rtx_launch_shadow(const DScene *S, const DParams *P, const
 			ka.qsi[a] = 1.f / S->w8qs[a];
 		}
 		ka.test_emitters = S->w8noemit ? S->num_emitters : 0u;
-		ka.w8known = S->w8noemit;
 	}
 	if (walk == WALK_W8)
 		return launch_walk<WALK_W8>(ka, nw, cus, count, stream);
-	if (walk == WALK_W4)
-		return launch_walk<WALK_W4>(ka, nw, cus, count, stream);
 	return launch_walk<WALK_BVH2>(ka, nw, cus, count, stream);
 }

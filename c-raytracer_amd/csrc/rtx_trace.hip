@@ -78,8 +78,10 @@ __device__ void trace_closest_bvh2(const DScene &S, uint32_t *stk, bool act, f3 
 		}
 	}
 	if (act && S.root_ref != RTX_EMPTY_REF) {
-		const f3 inv = safe_inv(d);
-		const f3 oi = mul3v(o, inv);
+		/* boxes in the trees' frame (rtx_device.h DTreeFrame), primitives in world space */
+		const f3 db = S.tf.rotated ? tf_dir(S.tf.r, d) : d;
+		const f3 inv = safe_inv(db);
+		const f3 oi = mul3v(S.tf.rotated ? tf_point(S.tf.r, S.tf.c, o) : o, inv);
 		uint32_t ref = S.root_ref;
 		uint32_t sp = 0;
 		stk += lane_id();
@@ -173,12 +175,13 @@ __device__ void trace_closest_bvh2(const DScene &S, uint32_t *stk, bool act, f3 
 #endif
 template <bool COUNT, int OCT>
 __device__ __forceinline__ void closest_walk8(const DScene &S, uint32_t *stk, uint32_t *ostk, size_t ostride, f3 o, f3 d,
-					      f3 inv, float &tbest, uint32_t &hid, TraceCount &tc)
+					      f3 ob, f3 inv, float &tbest, uint32_t &hid, TraceCount &tc)
 {
 	constexpr uint32_t K = (OCT == 8 || !RTX_W8_ORDER) ? 0u : (~(uint32_t)OCT & 7u);
+	/* ob / inv: the ray's origin and inverse direction in the trees' frame; o / d the world ray */
 	const f3 qs = ld3(S.w8qs), qo = ld3(S.w8qo);
 	const f3 invq = mk3(inv.x / qs.x, inv.y / qs.y, inv.z / qs.z);
-	const f3 oq = mk3((o.x - qo.x) * qs.x, (o.y - qo.y) * qs.y, (o.z - qo.z) * qs.z);
+	const f3 oq = mk3((ob.x - qo.x) * qs.x, (ob.y - qo.y) * qs.y, (ob.z - qo.z) * qs.z);
 	const f3 oi = mul3v(oq, invq);
 	uint32_t node = 0, grp = 0, sp = 0;
 	float gt = -INFINITY; /* RTX_TRACE_CULL: least entry distance of the group in grp (-inf: unknown) */
@@ -341,7 +344,10 @@ __device__ void trace_closest_w8(const DScene &S, uint32_t *stk, bool act, f3 o,
 	}
 	const u64 live = ballot(act);
 	if (live) {
-		const f3 inv = safe_inv_fast(d);
+		/* the ray in the trees' frame (rtx_device.h DTreeFrame) for the box tests */
+		const bool rot = S.tf.rotated != 0;
+		const f3 ob = rot ? tf_point(S.tf.r, S.tf.c, o) : o;
+		const f3 inv = safe_inv_fast(rot ? tf_dir(S.tf.r, d) : d);
 		stk += lane_id();
 		uint32_t *ostk = S.ostk + (size_t)blockIdx.x * WAVE + lane_id();
 		const size_t ostride = (size_t)gridDim.x * WAVE;
@@ -353,13 +359,13 @@ __device__ void trace_closest_w8(const DScene &S, uint32_t *stk, bool act, f3 o,
 			switch (sel) {
 #define RTX_CWALK(K)                                                                    \
 	case K:                                                                             \
-		closest_walk8<COUNT, K>(S, stk, ostk, ostride, o, d, inv, tbest, hid, tc);      \
+		closest_walk8<COUNT, K>(S, stk, ostk, ostride, o, d, ob, inv, tbest, hid, tc);  \
 		break;
 				RTX_CWALK(0) RTX_CWALK(1) RTX_CWALK(2) RTX_CWALK(3) RTX_CWALK(4) RTX_CWALK(5) RTX_CWALK(6)
 				RTX_CWALK(7)
 #undef RTX_CWALK
 			default:
-				closest_walk8<COUNT, 8>(S, stk, ostk, ostride, o, d, inv, tbest, hid, tc);
+				closest_walk8<COUNT, 8>(S, stk, ostk, ostride, o, d, ob, inv, tbest, hid, tc);
 				break;
 			}
 		}

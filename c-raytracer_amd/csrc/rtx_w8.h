@@ -2,7 +2,8 @@
  * Device helpers shared by the walks of the 8-wide compressed BVH (rtx_device.h DW8 / DW8S):
  * the shadow any-hit walk (rtx_shadow.hip shadow_walk8) and the closest-hit walk
  * (rtx_trace.hip trace_closest_w8).  Both test a node's eight child boxes the same way
- * (accel.c:112-158's slab test, conservative on the quantised boxes).
+ * (accel.c:112-158's slab test, conservative on the quantised boxes), on the ray in the trees'
+ * frame (rtx_device.h DTreeFrame).
  */
 #ifndef RTX_W8_H
 #define RTX_W8_H
@@ -111,44 +112,10 @@ __device__ __forceinline__ bool w8_slab(float lx, float hx, float ly, float hy, 
 	asm("v_min_f32 %0, %0, %1" : "+v"(tf) : "v"(tl));
 	return tn <= tf;
 }
-#ifndef RTX_W8_H1024
-#define RTX_W8_H1024 0 /* measurement option (it spills the ray transform on the 64-VGPR budget) */
-#endif
-/* RTX_W8_H1024: an 8-bit plane q enters the FMA as the IEEE half 1024 + q (bits 0x6400 | q), two
- * of them built by one v_perm_b32 from the node word and taken by v_fma_mix_f32 through op_sel,
- * instead of a v_cvt_f32_ubyte and a v_fma_f32 per plane: t = (1024 + q) s + (b - 1024 s).  The
- * scalar-path copies (DW8S) hold the same halves, and both paths form b - 1024 s with the same
- * FMA (w8_off), so they still compute bit-identical box tests. */
-__device__ __forceinline__ float w8_off(float b, float s) { return RTX_W8_H1024 ? fmaf(-1024.f, s, b) : b; }
-/* the half of plane word v for byte B: 1024 + byte (H1024) */
-template <int B> __device__ __forceinline__ float w8_h(uint32_t v)
-{
-	/* bytes B&~1 and B|1 of v, each under a 0x64 exponent byte: one perm serves two children */
-	constexpr uint32_t sel = (B & 2) ? 0x04030402u : 0x04010400u;
-	const uint32_t pr = __builtin_amdgcn_perm(0x64646464u, v, sel);
-	return (float)__builtin_bit_cast(_Float16, (uint16_t)((B & 1) ? (pr >> 16) : (pr & 0xFFFFu)));
-}
-#ifndef RTX_W8_PK
-#define RTX_W8_PK 0 /* measurement option: an axis's two planes in one v_pk_fma_f32 (the same fused results) */
-#endif
-typedef float f2v __attribute__((ext_vector_type(2)));
 template <int OCT, int C>
 __device__ __forceinline__ bool w8_child(const uint32_t (&w)[16], f3 s, f3 b, float tl)
 {
 	constexpr int W = C >> 2, B = C & 3;
-	if (RTX_W8_H1024)
-		return w8_slab<OCT>(fmaf(w8_h<B>(w[4 + W]), s.x, b.x), fmaf(w8_h<B>(w[6 + W]), s.x, b.x),
-				    fmaf(w8_h<B>(w[8 + W]), s.y, b.y), fmaf(w8_h<B>(w[10 + W]), s.y, b.y),
-				    fmaf(w8_h<B>(w[12 + W]), s.z, b.z), fmaf(w8_h<B>(w[14 + W]), s.z, b.z), tl);
-	if (RTX_W8_PK) {
-		const f2v x = __builtin_elementwise_fma((f2v){ ubyte<B>(w[4 + W]), ubyte<B>(w[6 + W]) }, (f2v){ s.x, s.x },
-							(f2v){ b.x, b.x });
-		const f2v y = __builtin_elementwise_fma((f2v){ ubyte<B>(w[8 + W]), ubyte<B>(w[10 + W]) }, (f2v){ s.y, s.y },
-							(f2v){ b.y, b.y });
-		const f2v z = __builtin_elementwise_fma((f2v){ ubyte<B>(w[12 + W]), ubyte<B>(w[14 + W]) }, (f2v){ s.z, s.z },
-							(f2v){ b.z, b.z });
-		return w8_slab<OCT>(x.x, x.y, y.x, y.y, z.x, z.y, tl);
-	}
 	return w8_slab<OCT>(fmaf(ubyte<B>(w[4 + W]), s.x, b.x), fmaf(ubyte<B>(w[6 + W]), s.x, b.x),
 			    fmaf(ubyte<B>(w[8 + W]), s.y, b.y), fmaf(ubyte<B>(w[10 + W]), s.y, b.y),
 			    fmaf(ubyte<B>(w[12 + W]), s.z, b.z), fmaf(ubyte<B>(w[14 + W]), s.z, b.z), tl);
@@ -172,8 +139,8 @@ __device__ __forceinline__ void w8_frame(const uint32_t (&w)[16], f3 invq, f3 oi
 {
 	s = mk3(ldexpf(invq.x, (int)((w[1] >> 16) & 15u)), ldexpf(invq.y, (int)((w[1] >> 20) & 15u)),
 		ldexpf(invq.z, (int)((w[1] >> 24) & 15u)));
-	b = mk3(w8_off(fmaf((float)(w[0] & 0xFFFFu), invq.x, -oi.x), s.x), w8_off(fmaf((float)(w[0] >> 16), invq.y, -oi.y), s.y),
-		w8_off(fmaf((float)(w[1] & 0xFFFFu), invq.z, -oi.z), s.z));
+	b = mk3(fmaf((float)(w[0] & 0xFFFFu), invq.x, -oi.x), fmaf((float)(w[0] >> 16), invq.y, -oi.y),
+		fmaf((float)(w[1] & 0xFFFFu), invq.z, -oi.z));
 }
 
 /* hit mask of an 8-wide node's children in visit order: bit p for slot p ^ K */
@@ -265,47 +232,7 @@ __device__ __forceinline__ W8Visit w8_visit_s(const DW8S *n, f3 invq, f3 oi, flo
 	const float org0 = __uint_as_float(p0[4]), org1 = __uint_as_float(p0[5]), org2 = __uint_as_float(p0[6]);
 	const f3 s = mk3(ldexpf(invq.x, (int)((w1 >> 16) & 15u)), ldexpf(invq.y, (int)((w1 >> 20) & 15u)),
 			 ldexpf(invq.z, (int)((w1 >> 24) & 15u)));
-	const f3 b = mk3(w8_off(fmaf(org0, invq.x, -oi.x), s.x), w8_off(fmaf(org1, invq.y, -oi.y), s.y),
-			 w8_off(fmaf(org2, invq.z, -oi.z), s.z));
-	W8Visit v;
-	v.hm = w8_hits_s<OCT, K>(q, w3, s, b, tl);
-	v.base = w2 >> 8;
-	v.io = perm_xor<K>(w2 & 0xFFu);
-	v.to = perm_xor<K>((w3 >> 8) & 0xFFu);
-	v.nv = w3 & 0xFFu;
-	return v;
-}
-
-/* the same visit on the scalar-path copy read per lane (measurement option RTX_W8_VH: eight
- * 16-byte loads instead of four, v_fma_mix_f32 on the halves instead of byte conversions) */
-template <int OCT, uint32_t K>
-__device__ __forceinline__ W8Visit w8_visit_v(const DW8S *n, f3 invq, f3 oi, float tl)
-{
-	uint32_t q[24], h[8];
-	{
-		const uint4 a = ldg4u((const uint32_t *)n), b = ldg4u((const uint32_t *)n + 4);
-		h[0] = a.x;
-		h[1] = a.y;
-		h[2] = a.z;
-		h[3] = a.w;
-		h[4] = b.x;
-		h[5] = b.y;
-		h[6] = b.z;
-		h[7] = b.w;
-	}
-#pragma unroll
-	for (int k = 0; k < 6; k++) {
-		const uint4 x = ldg4u((const uint32_t *)n + 8 + 4 * k);
-		q[4 * k] = x.x;
-		q[4 * k + 1] = x.y;
-		q[4 * k + 2] = x.z;
-		q[4 * k + 3] = x.w;
-	}
-	const uint32_t w1 = h[1], w2 = h[2], w3 = h[3];
-	const f3 s = mk3(ldexpf(invq.x, (int)((w1 >> 16) & 15u)), ldexpf(invq.y, (int)((w1 >> 20) & 15u)),
-			 ldexpf(invq.z, (int)((w1 >> 24) & 15u)));
-	const f3 b = mk3(w8_off(fmaf(__uint_as_float(h[4]), invq.x, -oi.x), s.x), w8_off(fmaf(__uint_as_float(h[5]), invq.y, -oi.y), s.y),
-			 w8_off(fmaf(__uint_as_float(h[6]), invq.z, -oi.z), s.z));
+	const f3 b = mk3(fmaf(org0, invq.x, -oi.x), fmaf(org1, invq.y, -oi.y), fmaf(org2, invq.z, -oi.z));
 	W8Visit v;
 	v.hm = w8_hits_s<OCT, K>(q, w3, s, b, tl);
 	v.base = w2 >> 8;
@@ -341,7 +268,7 @@ __device__ __forceinline__ void w8_child_t(const uint32_t *w, f3 s, f3 b, float 
 		constexpr int W = C >> 2, B = C & 3;
 #pragma unroll
 		for (int k = 0; k < 6; k++)
-			l[k] = RTX_W8_H1024 ? w8_h<B>(w[4 + 2 * k + W]) : ubyte<B>(w[4 + 2 * k + W]);
+			l[k] = ubyte<B>(w[4 + 2 * k + W]);
 	}
 	float tn;
 	const bool h = w8_slab_tn<OCT>(fmaf(l[0], s.x, b.x), fmaf(l[1], s.x, b.x), fmaf(l[2], s.y, b.y), fmaf(l[3], s.y, b.y),
@@ -399,8 +326,8 @@ __device__ __forceinline__ W8VisitT w8_visit_st(const DW8S *n, f3 invq, f3 oi, f
 	const uint32_t w1 = p0[1], w2 = p0[2], w3 = p0[3];
 	const f3 s = mk3(ldexpf(invq.x, (int)((w1 >> 16) & 15u)), ldexpf(invq.y, (int)((w1 >> 20) & 15u)),
 			 ldexpf(invq.z, (int)((w1 >> 24) & 15u)));
-	const f3 b = mk3(w8_off(fmaf(__uint_as_float(p0[4]), invq.x, -oi.x), s.x), w8_off(fmaf(__uint_as_float(p0[5]), invq.y, -oi.y), s.y),
-			 w8_off(fmaf(__uint_as_float(p0[6]), invq.z, -oi.z), s.z));
+	const f3 b = mk3(fmaf(__uint_as_float(p0[4]), invq.x, -oi.x), fmaf(__uint_as_float(p0[5]), invq.y, -oi.y),
+			 fmaf(__uint_as_float(p0[6]), invq.z, -oi.z));
 	W8VisitT r;
 	w8_hits_t<OCT, K, true>(q, s, b, tl, (w2 & 0xFFu) | ((w3 & 0xFFu) << 8), r);
 	r.v.base = w2 >> 8;

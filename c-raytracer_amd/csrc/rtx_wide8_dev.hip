@@ -26,9 +26,6 @@
 #include "rtx.h"
 #include "rtx_device.h"
 #include "rtx_quant.h"
-#ifndef RTX_W8_H1024
-#define RTX_W8_H1024 0 /* keep in step with rtx_w8.h */
-#endif
 
 #ifndef RTX_W8_C_PRIM
 #define RTX_W8_C_PRIM 0.3f
@@ -380,8 +377,7 @@ __global__ __launch_bounds__(W8D_T) void k_w8d_scalar(uint32_t n, const DW8 *__r
 		for (int k = 0; k < 6; k++)
 			for (int ch = 0; ch < 8; ch++) {
 				const uint32_t q = (nd.w[4 + 2 * k + (ch >> 2)] >> (8 * (ch & 3))) & 0xFFu;
-				/* rtx_w8.h RTX_W8_H1024: the half 1024 + q, else q */
-				f.q[k][ch] = RTX_W8_H1024 ? (uint16_t)(0x6400u | q) : __builtin_bit_cast(uint16_t, (_Float16)(float)q);
+				f.q[k][ch] = __builtin_bit_cast(uint16_t, (_Float16)(float)q); /* exact: q <= 255 */
 			}
 	}
 	w8s[i] = f;

@@ -270,6 +270,17 @@ class Renderer:
             pass
 
 
+def tree_frame(scene):
+    """rtx_tree_frame (no device needed): (rotated, R (3, 3), centre (3,), cost ratio) of the frame
+    rtx_upload_scene builds the scene's BVHs in under RTX_FRAME_AUTO"""
+    rot = np.zeros(9, np.float32)
+    cen = np.zeros(3, np.float32)
+    flag = C.c_int()
+    ratio = C.c_double()
+    _check(rtx_lib().rtx_tree_frame(C.byref(scene.desc), C.byref(flag), rot.ctypes.data, cen.ctypes.data, C.byref(ratio)))
+    return bool(flag.value), rot.reshape(3, 3), cen, ratio.value
+
+
 def gpu_kat(kind, records, params=None):
     records = np.ascontiguousarray(records, dtype=np.float32).reshape(-1, abi.KAT_IN[kind])
     out = np.zeros((records.shape[0], abi.KAT_OUT[kind]), np.float32)

@@ -71,13 +71,16 @@ class Stats(C.Structure):
                 ("wide_nodes", C.c_uint32), ("wide_depth", C.c_uint32), ("shadow_leaf_rounds", C.c_uint64),
                 ("gather_ms", C.c_double), ("devices", C.c_uint32), ("pad_", C.c_uint32),
                 ("shadow_uniform_steps", C.c_uint64), ("shadow_walk", C.c_uint32), ("wide_entries", C.c_uint32),
-                ("trace_walk", C.c_uint32), ("pad2_", C.c_uint32)]
+                ("trace_walk", C.c_uint32), ("pad2_", C.c_uint32), ("tree_rotated", C.c_uint32),
+                ("pad3_", C.c_uint32), ("frame_cost", C.c_double), ("frame_ms", C.c_double)]
 
 
 RTX_BUILD_SAH_HOST, RTX_BUILD_LBVH_GPU, RTX_BUILD_PLOC_GPU, RTX_BUILD_SAH_GPU = 0, 1, 2, 3
-RTX_WALK_AUTO, RTX_WALK_BVH2, RTX_WALK_W4, RTX_WALK_W8 = -1, 0, 1, 2
+RTX_WALK_AUTO, RTX_WALK_BVH2, RTX_WALK_W8 = -1, 0, 2
+WALK_NAMES = {RTX_WALK_BVH2: "bvh2", RTX_WALK_W8: "w8"}
+RTX_FRAME_AUTO, RTX_FRAME_WORLD = 0, 1
 RTX_OPT_SHADOW_WALK, RTX_OPT_BVH_LEAF, RTX_OPT_SPSORT, RTX_OPT_SHADOW_SLOT, RTX_OPT_SHADOW_GRAB, \
-    RTX_OPT_SHADOW_LDS_STACK, RTX_OPT_TRACE_WALK = 1, 2, 3, 4, 5, 6, 7
+    RTX_OPT_SHADOW_LDS_STACK, RTX_OPT_TRACE_WALK, RTX_OPT_TREE_FRAME = 1, 2, 3, 4, 5, 6, 7, 8
 RTX_DOF_NONE, RTX_DOF_SCALE_BIAS, RTX_DOF_CAMERA = 0, 1, 2
 RTX_FALLOFF_QUAD, RTX_FALLOFF_LIN, RTX_FALLOFF_INV_QUAD = 0, 1, 2
 
@@ -105,7 +108,7 @@ RTX_SYMBOLS = ["rtx_params_default", "rtx_device_count", "rtx_open", "rtx_upload
                "rtx_postprocess_device", "rtx_set_builder", "rtx_set_option", "rtx_group_open", "rtx_group_size",
                "rtx_group_set_builder", "rtx_group_set_option", "rtx_group_upload_scene", "rtx_group_render", "rtx_group_get_stats", "rtx_group_device_stats",
                "rtx_group_close", "rtx_tile_pack_count", "rtx_tile_pack_host", "rtx_tile_unpack_host",
-               "rtx_tile_pack_device", "rtx_tile_unpack_device"]
+               "rtx_tile_pack_device", "rtx_tile_unpack_device", "rtx_tree_frame"]
 RTX_SCENE_SYMBOLS = ["rtx_scene_load", "rtx_scene_parse", "rtx_scene_desc_of", "rtx_scene_num_json_objects",
                      "rtx_scene_free", "rtx_scene_last_error", "rtx_frame_setup", "rtx_tiff_write", "rtx_hash_djb",
                      "rtx_params_from_argv", "rtx_stl_write", "rtx_tiff_read_raw", "rtx_buffer_free",
@@ -208,6 +211,9 @@ def declare_rtx(lib):
     lib.rtx_tile_unpack_device.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                            C.c_void_p, C.c_void_p, C.c_void_p]
     lib.rtx_tile_unpack_device.restype = C.c_int
+    lib.rtx_tree_frame.argtypes = [C.POINTER(SceneDesc), C.POINTER(C.c_int), C.c_void_p, C.c_void_p,
+                                   C.POINTER(C.c_double)]
+    lib.rtx_tree_frame.restype = C.c_int
 
 
 def declare_oracle(lib):

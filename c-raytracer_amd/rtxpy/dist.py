@@ -4,8 +4,8 @@ Tiles are 8x8 pixels, row-major over the frame; rank r of N renders the tiles
 t with t % N == r (rtx_params.tile_offset / tile_stride).  Interleaving deals
 the expensive centre of the frame to every rank.  After rendering, each rank
 packs its tiles (rgb + z = 16 B per pixel) into one contiguous buffer and the
-buffers are all-gathered (RCCL over xGMI with the "nccl" backend on GPUs, gloo in
-the CPU tests) to rank 0, which unpacks: one message of 16 B x max_tiles x 64 per rank
+buffers are gathered (torch.distributed.gather: RCCL over xGMI with the "nccl" backend
+on GPUs, gloo in the CPU tests) to rank 0, which unpacks: one message of 16 B x max_tiles x 64 per rank
 (4.1 MB / N at 1080p).  The only collective is this exchange: pixels are independent, so
 there is no reduction.
 """
@@ -38,7 +38,7 @@ def tile_pixel_index(width, height, tiles):
 
 
 class Gatherer:
-    """Packs / all-gathers / unpacks one rank's tiles.  Works on any device torch supports."""
+    """Packs / gathers (to rank 0) / unpacks one rank's tiles.  Works on any device torch supports."""
 
     def __init__(self, width, height, rank, world, device):
         self.w, self.h, self.rank, self.world = width, height, rank, world

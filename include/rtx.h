@@ -206,17 +206,21 @@ typedef struct rtx_stats {
 	uint64_t shadow_global_box_tests; /* ... of which read from the DQNode array (the rest from the LDS top copy) */
 	uint64_t shadow_wave_steps;       /* walk-loop iterations summed over waves (a wave steps until its longest ray ends) */
 	uint64_t shadow_wave_walks;       /* wave walks (64 lane slots each): steps / walks = the waves' mean walk length */
-	uint32_t wide_nodes;              /* 4-wide shadow-walk BVH nodes (0: k_shadow walks the threaded BVH2) */
+	uint32_t wide_nodes;              /* 8-wide BVH nodes (0: k_shadow walks the threaded BVH2) */
 	uint32_t wide_depth;
-	uint64_t shadow_leaf_rounds;      /* only with count_traversal, 4-wide walk: wave iterations of its leaf loop */
+	uint64_t shadow_leaf_rounds;      /* only with count_traversal, 8-wide walk: wave iterations of its leaf loops */
 	double gather_ms;                 /* rtx_group_render: shard pack + RCCL gather + unpack (0 on one device) */
 	uint32_t devices;                 /* devices that rendered the last frame */
 	uint32_t pad_;
-	uint64_t shadow_uniform_steps;    /* only with count_traversal, wide walks: wave steps whose active lanes all fetched one node */
-	uint32_t shadow_walk;             /* the BVH k_shadow walks: RTX_WALK_W8 / RTX_WALK_W4 / RTX_WALK_BVH2 */
+	uint64_t shadow_uniform_steps;    /* only with count_traversal, 8-wide walk: wave steps whose active lanes were all at one node */
+	uint32_t shadow_walk;             /* the BVH k_shadow walks: RTX_WALK_W8 / RTX_WALK_BVH2 */
 	uint32_t wide_entries;            /* 8-wide walk: 64-byte entries (nodes, primitive records, holes) */
 	uint32_t trace_walk;              /* the BVH k_trace walks for closest hits: RTX_WALK_W8 / RTX_WALK_BVH2 */
 	uint32_t pad2_;
+	uint32_t tree_rotated;            /* the trees are built in a rotated frame (rtx_tree_frame) */
+	uint32_t pad3_;
+	double frame_cost;                /* its sampled leaf-box surface area over the world frame's (1: world frame) */
+	double frame_ms;                  /* host time choosing the frame and taking the leaf boxes in it */
 } rtx_stats;
 
 typedef struct rtx_ctx rtx_ctx;
@@ -246,12 +250,16 @@ int rtx_get_stats(const rtx_ctx *ctx, rtx_stats *out);
 /* Builder used by subsequent rtx_upload_scene calls on this context (RTX_BUILD_*). */
 int rtx_set_builder(rtx_ctx *ctx, int builder);
 
-/* Shadow-walk BVH layouts (rtx_stats.shadow_walk, RTX_OPT_SHADOW_WALK) */
+/* Shadow-walk BVH layouts (rtx_stats.shadow_walk, RTX_OPT_SHADOW_WALK); 1 was the 4-wide walk */
 enum {
-	RTX_WALK_AUTO = -1, /* the fastest available: 8-wide when it can be built */
+	RTX_WALK_AUTO = -1, /* the fastest available: the threaded BVH2 from LDS for small scenes, else 8-wide */
 	RTX_WALK_BVH2 = 0,  /* threaded quantised BVH2 (DQNode), no stack */
-	RTX_WALK_W4 = 1,    /* 4-wide quantised BVH (global 16-bit frame) */
 	RTX_WALK_W8 = 2     /* 8-wide compressed BVH (8-bit child boxes in each node's frame) */
+};
+/* The frame the BVHs are built in (RTX_OPT_TREE_FRAME, rtx_tree_frame) */
+enum {
+	RTX_FRAME_AUTO = 0,  /* default: a rotated frame when it shrinks the leaf boxes (a rotated mesh's own axes) */
+	RTX_FRAME_WORLD = 1  /* always the world axes, as accel.c:266-315 */
 };
 /* Context options: the defaults are the tuned values; the others exist for A/B measurement and
  * tests.  Build options take effect at the next rtx_upload_scene. */
@@ -263,10 +271,16 @@ enum rtx_option {
 	RTX_OPT_SHADOW_GRAB = 5, /* lane slots per k_shadow work-queue grab, >= 1 (default 4096) */
 	RTX_OPT_SHADOW_LDS_STACK = 6, /* 8-wide walk: lane-stack entries kept in LDS, 1..8 (default 8); deeper
 	                               * ones spill to HBM (tests use 1 to exercise the spill on any tree) */
-	RTX_OPT_TRACE_WALK = 7        /* closest hits (k_trace): RTX_WALK_AUTO (the 8-wide tree when built,
+	RTX_OPT_TRACE_WALK = 7,       /* closest hits (k_trace): RTX_WALK_AUTO (the 8-wide tree when built,
 	                               * default), RTX_WALK_W8 or RTX_WALK_BVH2 (the float BVH2) */
+	RTX_OPT_TREE_FRAME = 8        /* RTX_FRAME_* (build; default RTX_FRAME_AUTO) */
 };
 int rtx_set_option(rtx_ctx *ctx, int option, int64_t value);
+/* The frame rtx_upload_scene builds the scene's BVHs in under RTX_FRAME_AUTO (a diagnostic; no
+ * device needed): *rotated = 0 for the world axes, else rot = R (rows, x' = R (x - center)) and
+ * *cost_ratio = its sampled leaf-box surface area over the world frame's.  Every primitive is
+ * still tested in world space: the frame changes which boxes a ray meets, not any hit. */
+int rtx_tree_frame(const rtx_scene_desc *scene, int *rotated, float rot[9], float center[3], double *cost_ratio);
 void rtx_close(rtx_ctx *ctx);
 const char *rtx_last_error(void);
 

@@ -3,10 +3,13 @@ import ctypes
 import os
 import re
 
+import pytest
+
 import rtxpy
 from rtxpy import abi
 
 INCLUDE = os.path.join(rtxpy.REPO_ROOT, "include")
+ROOT = rtxpy.REPO_ROOT
 
 
 def declared(header):
@@ -58,4 +61,29 @@ def test_struct_sizes_match_c():
     assert ctypes.sizeof(abi.Object) == 4 * (4 + 18 + 2)
     assert ctypes.sizeof(abi.Frame) == 4 * (2 + 12)
     assert ctypes.sizeof(abi.Params) == 56
-    assert ctypes.sizeof(abi.Stats) == 11 * 8 + 6 * 8 + 6 * 4 + 4 * 8 + 2 * 4 + 8 + 8 + 2 * 4 + 8 + 2 * 4 + 2 * 4
+    assert ctypes.sizeof(abi.Stats) == 11 * 8 + 6 * 8 + 6 * 4 + 4 * 8 + 2 * 4 + 8 + 8 + 2 * 4 + 8 + 2 * 4 + 2 * 4 + 2 * 4 + 2 * 8
+
+
+def test_struct_layouts_match_compiled_header(tmp_path):
+    """every field offset and struct size of the ctypes mirror against include/rtx.h as gcc lays it out"""
+    import shutil
+    import subprocess
+    if not shutil.which("gcc"):
+        pytest.skip("gcc not available")
+    structs = {"rtx_material": abi.Material, "rtx_object": abi.Object, "rtx_frame": abi.Frame,
+               "rtx_params": abi.Params, "rtx_stats": abi.Stats, "rtx_post": abi.Post}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "rtx.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            lines.append(f'printf("{cname}.{f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(l.split() for l in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines())
+    for cname, py in structs.items():
+        assert int(got[cname]) == ctypes.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert int(got[f"{cname}.{f}"]) == getattr(py, f).offset, (cname, f)

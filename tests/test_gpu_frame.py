@@ -1,0 +1,132 @@
+"""The trees' frame (rtx_device.h DTreeFrame, csrc/rtx_frame.cpp, RTX_OPT_TREE_FRAME).
+
+The BVHs may be built over the objects' boxes in a rotated frame (a rotated mesh's own axes);
+every walk transforms its ray once and still tests every primitive whose box it meets with the
+reference's arithmetic in world space (object.c:254-498, accel.c:317-387).  So the frame may
+change which primitives are tested, never a hit: z-buffers, ray counts and colours are the
+world-frame trees' bit for bit on opaque scenes (transparent blockers may only multiply their
+transmittances in another order), and both match the reference goldens.
+
+The CPU half checks the choice itself (rtx_tree_frame needs no device): the Menger stand-in,
+rotated by scene6.json's mesh rotation, gets a rotated frame that shrinks its leaf boxes; the
+dragon stand-in and the sphere scenes keep the world axes.
+"""
+import numpy as np
+import pytest
+
+import conftest as C
+import rtxpy
+from rtxpy import abi
+
+
+def _scene(name):
+    scene, _, _, _ = C.load_config(name)
+    return scene
+
+
+def test_tree_frame_choice():
+    rot, R, c, ratio = rtxpy.tree_frame(_scene("s6_amb"))
+    assert rot and ratio < 0.5, ratio
+    # a rotation: orthonormal rows (float)
+    assert np.allclose(R @ R.T, np.eye(3), atol=1e-6)
+    # scene6.json's mesh rotation (-0.56, 0.56, 0.78) applied ZYX (object.c:548-562): the frame's
+    # axes are the mesh's own, up to order and sign
+    rx, ry, rz = -0.56, 0.56, 0.78
+    a, b = np.cos(rz) * np.sin(ry), np.sin(rz) * np.sin(ry)
+    M = np.array([[np.cos(rz) * np.cos(ry), a * np.sin(rx) - np.sin(rz) * np.cos(rx), a * np.cos(rx) + np.sin(rz) * np.sin(rx)],
+                  [np.sin(rz) * np.cos(ry), b * np.sin(rx) + np.cos(rz) * np.cos(rx), b * np.cos(rx) - np.cos(rz) * np.sin(rx)],
+                  [-np.sin(ry), np.cos(ry) * np.sin(rx), np.cos(ry) * np.cos(rx)]])
+    P = np.abs(R.astype(np.float64) @ M)  # a signed permutation when the axes agree
+    assert np.allclose(np.sort(P, axis=1)[:, -1], 1.0, atol=1e-4), P
+    for name in ("s5_amb", "s1_amb", "s3_amb"):
+        rot, R, c, ratio = rtxpy.tree_frame(_scene(name))
+        assert not rot and ratio == 1.0 and np.array_equal(R, np.eye(3, dtype=np.float32)), name
+
+
+@pytest.fixture(scope="module")
+def renderer():
+    r = rtxpy.Renderer(0)
+    yield r
+    r.close()
+
+
+@pytest.fixture(autouse=False)
+def _defaults(renderer):
+    yield
+    renderer.set_option(abi.RTX_OPT_TREE_FRAME, abi.RTX_FRAME_AUTO)
+    renderer.set_option(abi.RTX_OPT_SHADOW_WALK, abi.RTX_WALK_AUTO)
+    renderer.set_option(abi.RTX_OPT_TRACE_WALK, abi.RTX_WALK_AUTO)
+    renderer.set_builder(abi.RTX_BUILD_SAH_GPU)
+
+
+def _render(r, scene, frame, params, frame_opt, **opts):
+    r.set_option(abi.RTX_OPT_TREE_FRAME, frame_opt)
+    for k, v in opts.items():
+        r.set_option(k, v)
+    r.upload(scene)
+    rgb, z = r.render(frame, params)
+    return rgb, z, r.stats()
+
+
+@pytest.mark.gpu
+@pytest.mark.usefixtures("_defaults")
+@pytest.mark.parametrize("name", ["s6_amb", "s6_path2", "s5_path2", "st_amb"])
+def test_gpu_rotated_trees_change_no_hit(renderer, name):
+    scene, frame, params, _ = C.load_config(name)
+    a, za, sa = _render(renderer, scene, frame, params, abi.RTX_FRAME_AUTO)
+    b, zb, sb = _render(renderer, scene, frame, params, abi.RTX_FRAME_WORLD)
+    assert sb.tree_rotated == 0 and sb.frame_cost == 1.0
+    if name.startswith("s6"):
+        assert sa.tree_rotated == 1 and sa.frame_cost < 0.5
+    assert np.array_equal(za, zb), name
+    assert (sa.closest_rays, sa.shadow_rays) == (sb.closest_rays, sb.shadow_rays)
+    if name.startswith(("s5", "s6")):  # opaque meshes: bit for bit
+        assert np.array_equal(a, b), (name, float(np.abs(a - b).max()))
+    else:
+        assert np.abs(a - b).max() <= 1e-5 * max(1.0, float(np.abs(b).max())), name
+    ref_rgb, ref_z = C.golden_frame(name + "_o2")
+    ok, info = C.compare_const(a, za, ref_rgb, ref_z)
+    assert ok, (name, info)
+
+
+@pytest.mark.gpu
+@pytest.mark.usefixtures("_defaults")
+@pytest.mark.parametrize("walks", [(abi.RTX_WALK_BVH2, abi.RTX_WALK_BVH2), (abi.RTX_WALK_W8, abi.RTX_WALK_BVH2)])
+def test_gpu_rotated_trees_every_walk(renderer, walks):
+    """the threaded BVH2 shadow walk and the float-BVH2 closest-hit walk on the rotated trees too"""
+    scene, frame, params, _ = C.load_config("s6_path2")
+    params.rng = abi.RTX_RNG_COUNTER
+    opts = {abi.RTX_OPT_SHADOW_WALK: walks[0], abi.RTX_OPT_TRACE_WALK: walks[1]}
+    a, za, sa = _render(renderer, scene, frame, params, abi.RTX_FRAME_AUTO, **opts)
+    b, zb, sb = _render(renderer, scene, frame, params, abi.RTX_FRAME_WORLD, **opts)
+    assert sa.tree_rotated == 1 and sa.shadow_walk == walks[0] and sa.trace_walk == walks[1]
+    assert np.array_equal(za, zb) and np.array_equal(a, b)
+    assert (sa.closest_rays, sa.shadow_rays) == (sb.closest_rays, sb.shadow_rays)
+
+
+@pytest.mark.gpu
+@pytest.mark.usefixtures("_defaults")
+@pytest.mark.parametrize("builder", [abi.RTX_BUILD_SAH_HOST, abi.RTX_BUILD_LBVH_GPU, abi.RTX_BUILD_PLOC_GPU])
+def test_gpu_rotated_trees_every_builder(renderer, builder):
+    scene, frame, params, _ = C.load_config("s6_amb")
+    renderer.set_builder(builder)
+    a, za, sa = _render(renderer, scene, frame, params, abi.RTX_FRAME_AUTO)
+    b, zb, sb = _render(renderer, scene, frame, params, abi.RTX_FRAME_WORLD)
+    assert sa.tree_rotated == 1 and sa.builder == builder
+    assert np.array_equal(za, zb) and np.array_equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.usefixtures("_defaults")
+def test_gpu_rotated_trees_cut_traversal(renderer):
+    """the point of the frame: fewer box tests, wave steps and leaf rounds per shadow ray on the
+    rotated Menger sponge (count_traversal)"""
+    scene, frame, params, _ = C.load_config("s6_path2")
+    params.count_traversal = 1
+    _, _, sa = _render(renderer, scene, frame, params, abi.RTX_FRAME_AUTO)
+    _, _, sb = _render(renderer, scene, frame, params, abi.RTX_FRAME_WORLD)
+    assert sa.shadow_rays == sb.shadow_rays
+    assert sa.shadow_box_tests < 0.8 * sb.shadow_box_tests
+    assert sa.shadow_wave_steps < 0.8 * sb.shadow_wave_steps
+    assert sa.shadow_leaf_rounds < 0.7 * sb.shadow_leaf_rounds
+    assert sa.shadow_tri_tests < sb.shadow_tri_tests

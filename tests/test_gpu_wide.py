@@ -1,8 +1,8 @@
 """The shadow walks over their BVH layouts (include/rtx.h RTX_WALK_*, rtx_shadow.hip):
 
   RTX_WALK_W8    8-wide compressed BVH (rtx_device.h DW8, shadow_walk8), the default
-  RTX_WALK_W4    4-wide BVH quantised in the global 16-bit frame (shadow_walk4)
-  RTX_WALK_BVH2  threaded BVH2 (shadow_walk), the fallback for trees the 8-wide layout cannot hold
+  RTX_WALK_BVH2  threaded BVH2 (shadow_walk): small scenes (its top levels fit LDS) and trees the
+                 8-wide layout cannot hold
 
 All answer is_light_blocked (render.c:126-134, accel.c:360-387) exactly: each culls only with
 conservative boxes and any-hit needs no visit order.  Only the order in which transparent
@@ -36,6 +36,7 @@ def _defaults(renderer):
     renderer.set_option(abi.RTX_OPT_SHADOW_WALK, abi.RTX_WALK_AUTO)
     renderer.set_option(abi.RTX_OPT_BVH_LEAF, 1)
     renderer.set_option(abi.RTX_OPT_SHADOW_LDS_STACK, 8)
+    renderer.set_option(abi.RTX_OPT_TREE_FRAME, abi.RTX_FRAME_AUTO)
 
 
 def render(r, scene, frame, params, walk=abi.RTX_WALK_AUTO):
@@ -58,7 +59,7 @@ def test_gpu_walks_agree(renderer, name):
     # RTX_WALK_AUTO: the LDS-resident threaded BVH2 for small scenes, the 8-wide tree otherwise
     _, _, sd = render(renderer, scene, frame, params)
     assert sd.shadow_walk == (abi.RTX_WALK_BVH2 if name in SMALL else abi.RTX_WALK_W8), name
-    for walk in (abi.RTX_WALK_W4, abi.RTX_WALK_BVH2):
+    for walk in (abi.RTX_WALK_BVH2,):
         b, zb, sb = render(renderer, scene, frame, params, walk)
         assert sb.shadow_walk == walk
         assert np.array_equal(za, zb), (name, walk)
@@ -93,14 +94,14 @@ def test_gpu_w8_lane_stack_spill(renderer, name):
 @pytest.mark.parametrize("leaf", [2, 5])
 def test_gpu_wide_walk_multi_primitive_leaves(renderer, leaf):
     """BVH2 leaves of several primitives (RTX_OPT_BVH_LEAF > 1): the 8-wide collapse opens them
-    into one slot per primitive (boxes from the records), the 4-wide tree keeps them whole."""
+    into one slot per primitive (boxes from the records), the threaded BVH2 keeps them whole."""
     renderer.set_option(abi.RTX_OPT_BVH_LEAF, leaf)
     for name in ("s5_path2", "st_amb"):
         scene, frame, params, _ = C.load_config(name)
         ref_rgb, ref_z = C.golden_frame(name + "_o2")
-        for walk in (abi.RTX_WALK_W8, abi.RTX_WALK_W4):
+        for walk in (abi.RTX_WALK_W8, abi.RTX_WALK_BVH2):
             a, za, sa = render(renderer, scene, frame, params, walk)
-            assert sa.shadow_walk == walk and sa.wide_nodes > 0
+            assert sa.shadow_walk == walk and (sa.wide_nodes > 0) == (walk == abi.RTX_WALK_W8)
             ok, info = C.compare_const(a, za, ref_rgb, ref_z)
             assert ok, (name, leaf, walk, info)
 
@@ -122,7 +123,8 @@ def test_gpu_w8_walk_counts(renderer):
 
 
 def test_gpu_options_reject_bad_values(renderer):
-    for opt, bad in ((abi.RTX_OPT_SHADOW_WALK, 3), (abi.RTX_OPT_BVH_LEAF, 0), (abi.RTX_OPT_SPSORT, 2),
+    for opt, bad in ((abi.RTX_OPT_SHADOW_WALK, 3), (abi.RTX_OPT_SHADOW_WALK, 1), (abi.RTX_OPT_TREE_FRAME, 2),
+                     (abi.RTX_OPT_BVH_LEAF, 0), (abi.RTX_OPT_SPSORT, 2),
                      (abi.RTX_OPT_SHADOW_SLOT, 3), (abi.RTX_OPT_SHADOW_GRAB, 0), (abi.RTX_OPT_SHADOW_LDS_STACK, 9),
                      (99, 1)):
         with pytest.raises(rtxpy.RtxError) as e:

@@ -27,9 +27,9 @@ for s in $STEPS; do
     testsall) run testsall 1500 python3 -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) run bench 900 python3 bench.py --verbose ;;
     benchq) run benchq 600 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --verbose ;;
-    walks) for w in ${WALKS:-w8 w4}; do run walk_$w 600 python3 bench.py --walk $w --steps 2 --warmup 1 --no-cpu-baseline --no-post --verbose; done ;;
+    walks) for w in ${WALKS:-w8 bvh2}; do run walk_$w 600 python3 bench.py --walk $w --steps 2 --warmup 1 --no-cpu-baseline --no-post --verbose; done ;;
     twalks) for w in ${TWALKS:-w8 bvh2}; do run twalk_$w 600 python3 bench.py --trace-walk $w --steps 2 --warmup 1 --no-cpu-baseline --no-post --no-count --verbose; done ;;
-    s6w4) run s6_walkw4 900 python3 bench.py --scene scene6 --width 3840 --height 2160 --spp 128 --walk w4 --steps 1 --warmup 1 --no-cpu-baseline --no-post --verbose ;;
+    s6frames) for f in ${FRAMES:-world auto}; do run s6_frame_$f 900 python3 bench.py --scene scene6 --width 3840 --height 2160 --spp 128 --frame $f --steps 1 --warmup 1 --no-cpu-baseline --no-post --verbose; done ;;
     s6var) for v in ${VARS:-$(ls c-raytracer_amd/lib/var)}; do RTX_LIBRTX=$PWD/c-raytracer_amd/lib/var/$v/librtx.so run s6var_$v 900 python3 bench.py --scene scene6 --width 3840 --height 2160 --spp 128 --steps 1 --warmup 1 --no-cpu-baseline --no-post --verbose; done ;;
     s6slot) for sl in ${SLOTS:-64 16}; do run s6slot_$sl 900 python3 bench.py --scene scene6 --width 3840 --height 2160 --spp 128 --shadow-slot $sl --steps 1 --warmup 1 --no-cpu-baseline --no-post --no-count --verbose; done ;;
     s3) run s3 600 python3 bench.py --scene scene3 --width 1920 --height 1080 --spp 16 --steps 3 --warmup 1 --no-cpu-baseline --no-post --verbose ;;

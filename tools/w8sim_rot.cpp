@@ -1,0 +1,614 @@
+/*
+ * Development tool (not product, not a test): builds a scene's BVH2 and 8-wide shadow BVH exactly
+ * as rtx_build_scene does, then simulates k_shadow's 8-wide walk (rtx_shadow.hip shadow_walk8)
+ * on the CPU for sampled shadow rays to report tree shape and per-ray / per-wave work:
+ * node visits, box tests, primitive tests, and, for packets of 64 light samples of one shade
+ * point walking in lockstep, wave steps and leaf rounds.  Shade points are sampled on the
+ * bounded objects' surfaces (area-weighted) and on the planes inside the bound; light samples
+ * are stratified like RTX_RNG_STRAT.
+ *   build: tools/w8sim.sh       run: tools/w8sim <scene.json> [base_dir] [points]
+ */
+#include <chrono>
+#include <float.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <array>
+#include <random>
+#include <vector>
+
+#include "bvh_build.h"
+#include "rtx_internal.h"
+#include "rtx_quant.h"
+#include "rtx_scene.h"
+
+int rtx_fail(int code, const char *, ...) { return code; }
+
+static float area3(const float *a, const float *b, const float *c)
+{
+	const float e1[3] = { b[0] - a[0], b[1] - a[1], b[2] - a[2] }, e2[3] = { c[0] - a[0], c[1] - a[1], c[2] - a[2] };
+	const float x = e1[1] * e2[2] - e1[2] * e2[1], y = e1[2] * e2[0] - e1[0] * e2[2], z = e1[0] * e2[1] - e1[1] * e2[0];
+	return 0.5f * sqrtf(x * x + y * y + z * z);
+}
+
+/* closest hit over planes and the BVH2 (float boxes), for camera-visible shade points */
+struct Scene2 {
+	const rtx_scene_desc *sc;
+	const std::vector<DNode> *inner;
+	const std::vector<DPrim> *prims;
+	uint32_t nnodes, root;
+};
+
+static bool tri_hit(const DPrim &p, const double o[3], const double d[3], double &t)
+{
+	const double e1[3] = { p.b[0], p.b[1], p.b[2] }, e2[3] = { p.c[0], p.c[1], p.c[2] };
+	const double h[3] = { d[1] * e2[2] - d[2] * e2[1], d[2] * e2[0] - d[0] * e2[2], d[0] * e2[1] - d[1] * e2[0] };
+	const double aa = e1[0] * h[0] + e1[1] * h[1] + e1[2] * h[2];
+	if (fabs(aa) < p.a[3])
+		return false;
+	const double f = 1 / aa, s[3] = { o[0] - p.a[0], o[1] - p.a[1], o[2] - p.a[2] };
+	const double uu = f * (s[0] * h[0] + s[1] * h[1] + s[2] * h[2]);
+	const double q[3] = { s[1] * e1[2] - s[2] * e1[1], s[2] * e1[0] - s[0] * e1[2], s[0] * e1[1] - s[1] * e1[0] };
+	const double vv = f * (d[0] * q[0] + d[1] * q[1] + d[2] * q[2]);
+	t = f * (e2[0] * q[0] + e2[1] * q[1] + e2[2] * q[2]);
+	return uu >= 0 && vv >= 0 && uu + vv <= 1 && t > p.a[3];
+}
+
+static bool box_hit(const float lo[3], const float hi[3], const double o[3], const double inv[3], double tmax)
+{
+	double tn = 0, tf = tmax;
+	for (int a = 0; a < 3; a++) {
+		const double t0 = (lo[a] - o[a]) * inv[a], t1 = (hi[a] - o[a]) * inv[a];
+		tn = std::max(tn, std::min(t0, t1));
+		tf = std::min(tf, std::max(t0, t1));
+	}
+	return tn <= tf;
+}
+
+/* closest hit: t, the normal (unnormalised for triangles) */
+static double GRT[3][3] = { { 1, 0, 0 }, { 0, 1, 0 }, { 0, 0, 1 } };
+static bool closest(const Scene2 &S, const double ow[3], const double dw[3], double &tbest, double n[3])
+{
+	const double *o = ow, *d = dw;
+	double ol[3], dl[3];
+	for (int a = 0; a < 3; a++) {
+		ol[a] = GRT[a][0] * ow[0] + GRT[a][1] * ow[1] + GRT[a][2] * ow[2];
+		dl[a] = GRT[a][0] * dw[0] + GRT[a][1] * dw[1] + GRT[a][2] * dw[2];
+	}
+	tbest = 1e30;
+	bool hit = false;
+	for (uint32_t i = 0; i < S.sc->num_objects; i++) {
+		const rtx_object &p = S.sc->objects[i];
+		if (p.type != RTX_PLANE)
+			continue;
+		const double a = p.n[0] * d[0] + p.n[1] * d[1] + p.n[2] * d[2];
+		if (fabs(a) < 1e-6)
+			continue;
+		const double t = (p.d - (p.n[0] * o[0] + p.n[1] * o[1] + p.n[2] * o[2])) / a;
+		if (t > 1e-4 && t < tbest) {
+			tbest = t;
+			hit = true;
+			for (int k = 0; k < 3; k++)
+				n[k] = p.n[k];
+		}
+	}
+	double inv[3];
+	for (int a = 0; a < 3; a++)
+		inv[a] = fabs(dl[a]) > 1e-30 ? 1.0 / dl[a] : copysign(1e30, dl[a]);
+	std::vector<uint32_t> stk{ S.root };
+	while (!stk.empty()) {
+		const uint32_t ref = stk.back();
+		stk.pop_back();
+		if (ref & RTX_REF_LEAF) {
+			const uint32_t first = (ref & RTX_REF_OFF) / 64 - S.nnodes, cnt = (ref & RTX_REF_CNT) + 1;
+			for (uint32_t k = first; k < first + cnt; k++) {
+				const DPrim &p = (*S.prims)[k];
+				uint32_t meta;
+				memcpy(&meta, &p.c[3], 4);
+				if ((meta >> 24) == RTX_SPHERE)
+					continue;
+				double t;
+				if (tri_hit(p, o, d, t) && t < tbest) {
+					tbest = t;
+					hit = true;
+					n[0] = p.b[1] * p.c[2] - p.b[2] * p.c[1];
+					n[1] = p.b[2] * p.c[0] - p.b[0] * p.c[2];
+					n[2] = p.b[0] * p.c[1] - p.b[1] * p.c[0];
+				}
+			}
+			continue;
+		}
+		const DNode &nd = (*S.inner)[(ref & RTX_REF_OFF) / 64];
+		const float l0[3] = { nd.lo0x, nd.lo0y, nd.lo0z }, h0[3] = { nd.hi0x, nd.hi0y, nd.hi0z };
+		const float l1[3] = { nd.lo1x, nd.lo1y, nd.lo1z }, h1[3] = { nd.hi1x, nd.hi1y, nd.hi1z };
+		if (box_hit(l0, h0, ol, inv, tbest))
+			stk.push_back(nd.ref0);
+		if (box_hit(l1, h1, ol, inv, tbest))
+			stk.push_back(nd.ref1);
+	}
+	return hit;
+}
+
+struct Stats {
+	double rays = 0, visits = 0, boxes = 0, tris = 0, wave_steps = 0, leaf_rounds = 0, packets = 0, blocked = 0;
+	double emit = 0;
+	/* divergent wave steps (walking lanes at more than one node): distinct 64-B node entries and
+	 * 128-B lines per step, and the line touches of the four per-lane loads vs a transposed fetch
+	 * (load k = the 16-B quarters of lanes 16k..16k+15's nodes, four lanes per node) */
+	double dsteps = 0, dnodes = 0, dlines = 0, touch_lane = 0, touch_tr = 0, walkers = 0, quad_lane = 0, quad_tr = 0;
+	double post_nodes[8] = {}, post_leaves[8] = {}; /* postponed leaf tests, threshold T = 8 * k lanes */
+};
+
+int main(int argc, char **argv)
+{
+	if (argc < 2) {
+		fprintf(stderr, "usage: %s scene.json [base_dir] [points]\n", argv[0]);
+		return 2;
+	}
+	rtx_scene *scene = nullptr;
+	if (rtx_scene_load(argv[1], nullptr, argc > 2 ? argv[2] : nullptr, &scene)) {
+		fprintf(stderr, "load: %s\n", rtx_scene_last_error());
+		return 1;
+	}
+	const int npts = argc > 3 ? atoi(argv[3]) : 4000;
+	const bool near = getenv("W8SIM_NEAR") != nullptr; /* visit the nearest hit inner child first */
+	const rtx_scene_desc *sc = rtx_scene_desc_of(scene);
+	std::vector<uint32_t> bounded;
+	for (uint32_t i = 0; i < sc->num_objects; i++)
+		if (sc->objects[i].type != RTX_PLANE)
+			bounded.push_back(i);
+	const uint32_t nb = (uint32_t)bounded.size();
+	std::vector<float> lo(3 * (size_t)nb), hi(3 * (size_t)nb);
+	/* W8SIM_ROT=rx,ry,rz: build the tree in the frame of a mesh rotated by these ZYX Euler angles
+	 * (host/scene.c), i.e. boxes of R^T v, and walk rays transformed by R^T */
+	double RT[3][3] = { { 1, 0, 0 }, { 0, 1, 0 }, { 0, 0, 1 } };
+	if (getenv("W8SIM_ROT")) {
+		float rot[3];
+		sscanf(getenv("W8SIM_ROT"), "%f,%f,%f", &rot[0], &rot[1], &rot[2]);
+		const double a = cos(rot[2]) * sin(rot[1]), b = sin(rot[2]) * sin(rot[1]);
+		const double R[3][3] = { { cos(rot[2]) * cos(rot[1]), a * sin(rot[0]) - sin(rot[2]) * cos(rot[0]), a * cos(rot[0]) + sin(rot[2]) * sin(rot[0]) },
+					 { sin(rot[2]) * cos(rot[1]), b * sin(rot[0]) + cos(rot[2]) * cos(rot[0]), b * cos(rot[0]) - cos(rot[2]) * sin(rot[0]) },
+					 { -sin(rot[1]), cos(rot[1]) * sin(rot[0]), cos(rot[1]) * cos(rot[0]) } };
+		for (int i = 0; i < 3; i++)
+			for (int j = 0; j < 3; j++)
+				RT[i][j] = R[j][i];
+	}
+	memcpy(GRT, RT, sizeof(RT));
+	auto loc = [&](const float *v, float *out) {
+		for (int i = 0; i < 3; i++)
+			out[i] = (float)(RT[i][0] * v[0] + RT[i][1] * v[1] + RT[i][2] * v[2]);
+	};
+	float blo[3] = { FLT_MAX, FLT_MAX, FLT_MAX }, bhi[3] = { -FLT_MAX, -FLT_MAX, -FLT_MAX };
+	for (uint32_t k = 0; k < nb; k++) {
+		const rtx_object &o = sc->objects[bounded[k]];
+		float l[3], h[3];
+		for (int a = 0; a < 3; a++) {
+			float q0[3], q1[3], q2[3];
+			loc(o.p0, q0);
+			loc(o.p1, q1);
+			loc(o.p2, q2);
+			if (o.type == RTX_SPHERE) {
+				l[a] = q0[a] - o.radius;
+				h[a] = q0[a] + o.radius;
+			} else {
+				l[a] = std::min(q0[a], std::min(q1[a], q2[a]));
+				h[a] = std::max(q0[a], std::max(q1[a], q2[a]));
+			}
+		}
+		const float ext = std::max(h[0] - l[0], std::max(h[1] - l[1], h[2] - l[2]));
+		for (int a = 0; a < 3; a++) {
+			lo[3 * k + a] = l[a] - (std::fabs(l[a]) + ext) * 2e-6f - 1e-30f;
+			hi[3 * k + a] = h[a] + (std::fabs(h[a]) + ext) * 2e-6f + 1e-30f;
+			blo[a] = std::min(blo[a], lo[3 * k + a]);
+			bhi[a] = std::max(bhi[a], hi[3 * k + a]);
+		}
+	}
+	BvhConfig cfg;
+	BvhOutput bvh;
+	const auto t0 = std::chrono::steady_clock::now();
+	bvh_build(BvhInput{ nb, lo.data(), hi.data() }, cfg, bvh);
+	const auto t1 = std::chrono::steady_clock::now();
+	const uint32_t nnodes = (uint32_t)bvh.nodes.size();
+	std::vector<DPrim> prims(nb);
+	for (uint32_t k = 0; k < nb; k++) {
+		const rtx_object &o = sc->objects[bounded[bvh.order[k]]];
+		DPrim &p = prims[k];
+		memset(&p, 0, sizeof(p));
+		memcpy(p.a, o.p0, 12);
+		p.a[3] = o.epsilon;
+		if (o.type == RTX_SPHERE)
+			p.b[0] = o.radius;
+		else {
+			memcpy(p.b, o.e1, 12);
+			memcpy(p.c, o.e2, 12);
+		}
+		uint32_t meta = ((uint32_t)o.type << 24) | (uint32_t)o.material;
+		if (sc->materials[o.material].transparent)
+			meta |= RTX_META_TRANSPARENT;
+		const uint32_t oi = bounded[bvh.order[k]];
+		memcpy(&p.b[3], &oi, 4);
+		memcpy(&p.c[3], &meta, 4);
+	}
+	auto dref = [&](uint32_t r) -> uint32_t {
+		if (r == RTX_EMPTY_REF)
+			return r;
+		if (r & RTX_LEAF_BIT) {
+			const uint32_t first = (r >> 4) & 0x7FFFFFFu, cnt = (r & 15u) + 1;
+			return (nnodes + first) * (uint32_t)sizeof(DNode) | RTX_REF_LEAF | (cnt - 1);
+		}
+		return r * (uint32_t)sizeof(DNode);
+	};
+	std::vector<DNode> inner = bvh.nodes;
+	for (DNode &d : inner) {
+		d.ref0 = dref(d.ref0);
+		d.ref1 = dref(d.ref1);
+	}
+	QFrame F;
+	float ext_max = 0.f;
+	for (int a = 0; a < 3; a++)
+		ext_max = std::max(ext_max, bhi[a] - blo[a]);
+	for (int a = 0; a < 3; a++) {
+		F.qo[a] = blo[a];
+		F.qs[a] = 65533.f / std::max(bhi[a] - blo[a], std::max(ext_max, 1.f) * 1e-6f);
+	}
+	std::vector<DW8> w8;
+	std::vector<uint32_t> leafmap;
+	std::vector<uint32_t> emit_objs(sc->emitters, sc->emitters + sc->num_emitters);
+	bool skipped = false;
+	const uint32_t depth = rtx_wide8_build(inner, nnodes, prims.data(), dref(bvh.root_ref), blo, bhi, emit_objs, F, skipped,
+					       w8, leafmap);
+	const auto t2 = std::chrono::steady_clock::now();
+	printf("host SAH build %.1f ms, 8-wide collapse %.1f ms\n", std::chrono::duration<double, std::milli>(t1 - t0).count(),
+	       std::chrono::duration<double, std::milli>(t2 - t1).count());
+	uint32_t nodes = 0, kids = 0, inner_kids = 0;
+	std::vector<uint32_t> hist(9, 0);
+	for (const DW8 &e : w8)
+		if (e.w[3]) {
+			nodes++;
+			kids += __builtin_popcount(e.w[3] & 0xFFu);
+			inner_kids += __builtin_popcount(e.w[2] & 0xFF);
+			hist[__builtin_popcount(e.w[3] & 0xFFu)]++;
+		}
+	printf("prims %u  bvh2 nodes %u depth %u  w8 entries %zu nodes %u depth %u  children/node %.2f (inner %.2f)  hist",
+	       nb, nnodes, bvh.depth, w8.size(), nodes, depth, (double)kids / nodes, (double)inner_kids / nodes);
+	for (int i = 1; i <= 8; i++)
+		printf(" %u", hist[i]);
+	printf("\n");
+	for (size_t i = 0; i < w8.size(); i++) /* leaf entries hold the primitive records */
+		if (leafmap[i] != RTX_NONE)
+			memcpy(&w8[i], &prims[leafmap[i]], 64);
+
+	/* shade points on bounded surfaces (area-weighted) and planes, light samples on emitter 0 */
+	std::mt19937_64 rng(12345);
+	std::uniform_real_distribution<float> U(0.f, 1.f);
+	std::vector<double> cdf;
+	double acc = 0;
+	for (uint32_t k = 0; k < nb; k++) {
+		const rtx_object &o = sc->objects[bounded[k]];
+		acc += o.type == RTX_SPHERE ? 0.0 : area3(o.p0, o.p1, o.p2);
+		cdf.push_back(acc);
+	}
+	if (!sc->num_emitters) {
+		printf("no emitters\n");
+		return 0;
+	}
+	const rtx_object &E = sc->objects[sc->emitters[0]];
+	const uint32_t nl = E.num_lights ? E.num_lights : 1;
+	Stats S;
+	const float qsi[3] = { 1.f / F.qs[0], 1.f / F.qs[1], 1.f / F.qs[2] };
+	/* shade points as the bench frame makes them: primary hits of sampled pixels, then -n GI
+	 * hits from each (uniform hemisphere about the normal, render.c:231-289) */
+	Scene2 S2{ sc, &inner, &prims, nnodes, dref(bvh.root_ref) };
+	rtx_frame fr;
+	rtx_frame_setup(&sc->camera, 1920, 1080, &fr);
+	std::vector<std::array<float, 3>> pts;
+	const int gi = 64;
+	while ((int)pts.size() < npts) {
+		const uint32_t x = (uint32_t)(U(rng) * 1920) % 1920, y = (uint32_t)(U(rng) * 1080) % 1080;
+		double o[3], d[3], dn = 0;
+		for (int a = 0; a < 3; a++) {
+			o[a] = fr.origin[a];
+			d[a] = fr.corner[a] + (x + 1) * fr.step_x[a] + y * fr.step_y[a] - o[a];
+			dn += d[a] * d[a];
+		}
+		for (int a = 0; a < 3; a++)
+			d[a] /= sqrt(dn);
+		double t, n[3];
+		if (!closest(S2, o, d, t, n))
+			continue;
+		double P0[3], nn = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+		for (int a = 0; a < 3; a++) {
+			P0[a] = o[a] + t * d[a];
+			n[a] /= nn;
+		}
+		if (n[0] * d[0] + n[1] * d[1] + n[2] * d[2] > 0)
+			for (int a = 0; a < 3; a++)
+				n[a] = -n[a];
+		pts.push_back({ (float)P0[0], (float)P0[1], (float)P0[2] });
+		for (int g = 0; g < gi && (int)pts.size() < npts; g++) {
+			double r[3], rn;
+			do {
+				for (int a = 0; a < 3; a++)
+					r[a] = 2 * U(rng) - 1;
+				rn = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
+			} while (rn > 1 || rn < 1e-6);
+			double dd = 0;
+			for (int a = 0; a < 3; a++) {
+				r[a] /= sqrt(rn);
+				dd += r[a] * n[a];
+			}
+			if (dd < 0)
+				for (int a = 0; a < 3; a++)
+					r[a] = -r[a];
+			double t2, n2[3];
+			if (closest(S2, P0, r, t2, n2))
+				pts.push_back({ (float)(P0[0] + t2 * r[0]), (float)(P0[1] + t2 * r[1]), (float)(P0[2] + t2 * r[2]) });
+		}
+	}
+	for (int pi = 0; pi < npts; pi++) {
+		const float P[3] = { pts[pi][0], pts[pi][1], pts[pi][2] };
+		/* packets of 64 light samples */
+		for (uint32_t b0 = 0; b0 < nl; b0 += 64) {
+			std::vector<uint32_t> visits_lane, leaf_at; /* per-lane per-visit leaf hits */
+			std::vector<std::vector<uint32_t>> leaves(64), seq(64);
+			uint32_t block_at[64]; /* ordinal (in discovery order) of the lane's blocking leaf test, or ~0 */
+			uint32_t maxv = 0, imm_len[64] = {};
+			for (uint32_t l = 0; l < 64 && b0 + l < nl; l++) {
+				const uint32_t j = b0 + l;
+				float u1 = ((float)j + U(rng)) / (float)nl, u2 = U(rng);
+				float Lp[3];
+				if (E.type == RTX_SPHERE) {
+					const float inc = u1 * 2.f * 3.1415927f, az = u2 * 2.f * 3.1415927f;
+					float ld[3] = { E.radius * cosf(az) * sinf(inc), E.radius * sinf(az) * sinf(inc), E.radius * cosf(inc) };
+					const float nr[3] = { E.p0[0] - P[0], E.p0[1] - P[1], E.p0[2] - P[2] };
+					if (nr[0] * ld[0] + nr[1] * ld[1] + nr[2] * ld[2] != 0.f)
+						for (int a = 0; a < 3; a++)
+							ld[a] = -ld[a];
+					for (int a = 0; a < 3; a++)
+						Lp[a] = E.p0[a] + ld[a];
+				} else {
+					if (u1 + u2 > 1) {
+						u1 = 1 - u1;
+						u2 = 1 - u2;
+					}
+					for (int a = 0; a < 3; a++)
+						Lp[a] = E.p0[a] + u1 * E.e1[a] + u2 * E.e2[a];
+				}
+				double d[3] = { Lp[0] - P[0], Lp[1] - P[1], Lp[2] - P[2] };
+				const double dist = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+				for (int a = 0; a < 3; a++)
+					d[a] /= dist;
+				double invq[3], oi[3];
+				int oct = 0;
+				double dl[3], Pl[3];
+				for (int a = 0; a < 3; a++) {
+					dl[a] = RT[a][0] * d[0] + RT[a][1] * d[1] + RT[a][2] * d[2];
+					Pl[a] = RT[a][0] * P[0] + RT[a][1] * P[1] + RT[a][2] * P[2];
+				}
+				for (int a = 0; a < 3; a++) {
+					const double inv = fabs(dl[a]) > 1e-30 ? 1.0 / dl[a] : copysign(1e30, dl[a]);
+					if (inv >= 0)
+						oct |= 1 << a;
+					invq[a] = inv * qsi[a];
+					oi[a] = (Pl[a] - F.qo[a]) * F.qs[a] * invq[a];
+				}
+				const uint32_t K = ~(uint32_t)oct & 7u;
+				/* the walk: node, group register, stack; leaf hits counted per visit */
+				std::vector<uint32_t> stk;
+				uint32_t node = 0, grp = 0, nv = 0, nleaf_total = 0;
+				block_at[l] = ~0u;
+				bool blocked = false;
+				uint32_t nv_imm = 0; /* visits of the immediate-test walk (ends at the blocker's visit) */
+				while (node != RTX_NONE) {
+					if (!blocked) {
+						nv_imm++;
+						seq[l].push_back(node);
+					}
+					const DW8 &N = w8[node];
+					nv++;
+					S.boxes += __builtin_popcount(N.w[3] & 0xFFu);
+					const double org[3] = { (double)(N.w[0] & 0xFFFF), (double)(N.w[0] >> 16), (double)(N.w[1] & 0xFFFF) };
+					const int ex[3] = { (int)((N.w[1] >> 16) & 15), (int)((N.w[1] >> 20) & 15), (int)((N.w[1] >> 24) & 15) };
+					uint32_t hm = 0, near_p = 8;
+					double near_t = 1e300;
+					for (int c = 0; c < 8; c++) {
+						if (!((N.w[3] >> c) & 1))
+							continue;
+						double tn = 0, tf = dist;
+						for (int a = 0; a < 3; a++) {
+							const uint8_t *l8 = (const uint8_t *)&N.w[4 + 4 * a], *h8 = (const uint8_t *)&N.w[6 + 4 * a];
+							const double t0 = (org[a] + ldexp(l8[c], ex[a])) * invq[a] - oi[a];
+							const double t1 = (org[a] + ldexp(h8[c], ex[a])) * invq[a] - oi[a];
+							tn = std::max(tn, std::min(t0, t1));
+							tf = std::min(tf, std::max(t0, t1));
+						}
+						if (tn <= tf) {
+							hm |= 1u << (c ^ K);
+							if (((N.w[2] >> c) & 1) && tn < near_t) {
+								near_t = tn;
+								near_p = c ^ K;
+							}
+						}
+					}
+					uint32_t io = 0;
+					for (int c = 0; c < 8; c++)
+						if ((N.w[2] >> c) & 1)
+							io |= 1u << (c ^ K);
+					const uint32_t base = N.w[2] >> 8;
+					uint32_t lm = hm & ~io, im = hm & io;
+					uint32_t nleaf = 0;
+					for (; lm; lm &= lm - 1) {
+						S.tris++;
+						const DPrim &p = *(const DPrim *)&w8[base + (__builtin_ctz(lm) ^ K)];
+						uint32_t meta;
+						memcpy(&meta, &p.c[3], 4);
+						uint32_t obj;
+						memcpy(&obj, &p.b[3], 4);
+						if (obj == sc->emitters[0]) {
+							S.emit++;
+							continue;
+						}
+						nleaf++;
+						nleaf_total++;
+						if ((meta & RTX_META_TRANSPARENT) || (meta >> 24) == RTX_SPHERE)
+							continue;
+						/* opaque triangle: Moller-Trumbore in double */
+						const double e1[3] = { p.b[0], p.b[1], p.b[2] }, e2[3] = { p.c[0], p.c[1], p.c[2] };
+						const double h[3] = { d[1] * e2[2] - d[2] * e2[1], d[2] * e2[0] - d[0] * e2[2], d[0] * e2[1] - d[1] * e2[0] };
+						const double aa = e1[0] * h[0] + e1[1] * h[1] + e1[2] * h[2];
+						if (fabs(aa) < p.a[3])
+							continue;
+						const double f = 1 / aa, s[3] = { P[0] - p.a[0], P[1] - p.a[1], P[2] - p.a[2] };
+						const double uu = f * (s[0] * h[0] + s[1] * h[1] + s[2] * h[2]);
+						const double q[3] = { s[1] * e1[2] - s[2] * e1[1], s[2] * e1[0] - s[0] * e1[2], s[0] * e1[1] - s[1] * e1[0] };
+						const double vv = f * (d[0] * q[0] + d[1] * q[1] + d[2] * q[2]);
+						const double tt = f * (e2[0] * q[0] + e2[1] * q[1] + e2[2] * q[2]);
+						if (!blocked && uu >= 0 && vv >= 0 && uu + vv <= 1 && tt > p.a[3] && tt < dist) {
+							blocked = true;
+							block_at[l] = nleaf_total - 1;
+							/* postponed tests would have kept walking: record the rest of the walk
+							 * (the leaf hits of later visits) without stopping at the blocker */
+						}
+					}
+					leaves[l].push_back(nleaf);
+					if (im) {
+						const uint32_t p0 = near ? near_p : (uint32_t)__builtin_ctz(im);
+						node = base + (p0 ^ K);
+						im &= ~(1u << p0);
+						if (im) {
+							if (grp)
+								stk.push_back(grp);
+							grp = (base << 8) | im;
+						}
+					} else if (grp) {
+						node = (grp >> 8) + (__builtin_ctz(grp) ^ K);
+						grp &= grp - 1;
+						if (!(grp & 0xFF)) {
+							grp = 0;
+							if (!stk.empty()) {
+								grp = stk.back();
+								stk.pop_back();
+							}
+						}
+					} else {
+						node = RTX_NONE;
+					}
+				}
+				S.rays++;
+				S.visits += nv_imm;
+				S.blocked += blocked;
+				maxv = std::max(maxv, nv_imm);
+				imm_len[l] = nv_imm;
+			}
+			S.packets++;
+			/* postponed leaf tests: a leaf round only when >= T lanes hold pending leaves or no lane
+			 * has node work left (emitter leaves excluded, as a tree without emitters) */
+			for (int k = 0; k < 8; k++) {
+				const uint32_t T = k ? 8 * k : 1;
+				uint32_t v[64] = {}, pend[64] = {}, tested[64] = {};
+				bool done[64] = {};
+				for (;;) {
+					uint32_t L = 0, W = 0;
+					for (int l = 0; l < 64; l++) {
+						if (done[l])
+							continue;
+						L += pend[l] > 0;
+						W += v[l] < leaves[l].size();
+					}
+					if (!L && !W)
+						break;
+					if (!W || L >= T) {
+						S.post_leaves[k]++;
+						for (int l = 0; l < 64; l++)
+							if (!done[l] && pend[l]) {
+								pend[l]--;
+								if (tested[l]++ == block_at[l])
+									done[l] = true;
+							}
+					} else {
+						S.post_nodes[k]++;
+						for (int l = 0; l < 64; l++)
+							if (!done[l] && v[l] < leaves[l].size())
+								pend[l] += leaves[l][v[l]++];
+					}
+				}
+			}
+			S.wave_steps += maxv;
+			for (uint32_t i = 0; i < maxv; i++) {
+				std::vector<uint32_t> at(64, ~0u);
+				uint32_t first = ~0u;
+				bool div = false;
+				for (int l = 0; l < 64; l++)
+					if (i < seq[l].size()) {
+						at[l] = seq[l][i];
+						if (first == ~0u)
+							first = at[l];
+						div |= at[l] != first;
+					}
+				if (!div)
+					continue;
+				S.dsteps++;
+				std::vector<uint32_t> nodes, lines;
+				for (int l = 0; l < 64; l++)
+					if (at[l] != ~0u) {
+						S.walkers++;
+						nodes.push_back(at[l]);
+						lines.push_back(at[l] >> 1);
+					}
+				auto uniq = [](std::vector<uint32_t> v) {
+					std::sort(v.begin(), v.end());
+					return (double)(std::unique(v.begin(), v.end()) - v.begin());
+				};
+				S.dnodes += uniq(nodes);
+				const double dl = uniq(lines);
+				S.dlines += dl;
+				S.touch_lane += 4 * dl;
+				/* address-path cycles if the texture unit takes 4 lanes (64 B) per cycle and one more
+				 * cycle per further distinct line in a quad: per-lane loads (x4 instructions) vs
+				 * transposed (each quad = one ray's node) */
+				for (int q = 0; q < 16; q++) {
+					std::vector<uint32_t> g;
+					for (int l = 4 * q; l < 4 * q + 4; l++)
+						if (at[l] != ~0u)
+							g.push_back(at[l] >> 1);
+					if (!g.empty())
+						S.quad_lane += 4 * uniq(g);
+				}
+				S.quad_tr += nodes.size();
+				for (int k = 0; k < 4; k++) {
+					std::vector<uint32_t> g;
+					for (int l = 16 * k; l < 16 * k + 16; l++)
+						if (at[l] != ~0u)
+							g.push_back(at[l] >> 1);
+					S.touch_tr += uniq(g);
+				}
+			}
+			for (uint32_t i = 0; i < maxv; i++) {
+				uint32_t m = 0;
+				for (int l = 0; l < 64; l++)
+					if (i < imm_len[l])
+						m = std::max(m, leaves[l][i]);
+				S.leaf_rounds += m;
+			}
+		}
+	}
+	printf("rays %.0f  visits/ray %.2f  boxes/ray %.2f  tris/ray %.3f  blocked %.3f  wave steps/packet %.2f  leaf "
+	       "rounds/packet %.2f  lanes/leaf round %.1f\n",
+	       S.rays, S.visits / S.rays, S.boxes / S.rays, S.tris / S.rays, S.blocked / S.rays, S.wave_steps / S.packets,
+	       S.leaf_rounds / S.packets, S.tris / S.leaf_rounds);
+	printf("emitter leaf hits/ray %.3f\npostponed leaf tests (no emitter leaves), per packet: T  node steps  leaf rounds  "
+	       "cost(290/step + 99/round)\n",
+	       S.emit / S.rays);
+	printf("divergent steps/packet %.2f  walking lanes %.1f  distinct nodes %.2f  lines %.2f  line touches per step: "
+	       "per-lane loads %.1f  transposed %.1f  quad cycles: per-lane %.1f  transposed %.1f\n",
+	       S.dsteps / S.packets, S.walkers / S.dsteps, S.dnodes / S.dsteps, S.dlines / S.dsteps, S.touch_lane / S.dsteps,
+	       S.touch_tr / S.dsteps, S.quad_lane / S.dsteps, S.quad_tr / S.dsteps);
+	for (int k = 0; k < 8; k++)
+		printf("  %2d  %6.2f  %6.2f  %7.0f\n", k ? 8 * k : 1, S.post_nodes[k] / S.packets, S.post_leaves[k] / S.packets,
+		       (290 * S.post_nodes[k] + 99 * S.post_leaves[k]) / S.packets);
+	rtx_scene_free(scene);
+	return 0;
+}
