@@ -64,7 +64,7 @@ def parse():
     ap.add_argument("--launch", default="group", choices=["group", "torchrun"],
                     help="--gpus N > 1 without torchrun: one process driving the C-ABI device group "
                          "(default), or N torchrun ranks")
-    ap.add_argument("--walk", default="auto", choices=["auto", "w8", "bvh2"],
+    ap.add_argument("--walk", default="auto", choices=["auto", "w8", "bvh2", "linear"],
                     help="shadow-walk BVH layout (rtx_set_option RTX_OPT_SHADOW_WALK; auto = the library default)")
     ap.add_argument("--trace-walk", default="auto", choices=["auto", "w8", "bvh2"],
                     help="closest-hit BVH layout (rtx_set_option RTX_OPT_TRACE_WALK)")
@@ -119,10 +119,7 @@ def launch_mode(a):
 
 def dry_run(a, mode):
     """Launch bring-up without a GPU: every torchrun rank joins a gloo group and rank 0 prints the
-    world size the JSON line would carry; the device-group mode prints its plan."""
-    if mode == "group":
-        print(json.dumps({"dry_run": True, "n_gpus": a.gpus, "launch": "group", "processes": 1}), flush=True)
-        return
+    world size the JSON line would carry (the device-group mode prints its line's schema: main_group)."""
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -266,6 +263,16 @@ def cpu_reference(scene_file, flags, width, height, target_s, log):
 
 
 def shadow_roofline(r, frame, params, d_rgb, d_z, stream, shadow_ms, a, world):
+    """the counting pass (count_traversal) of the same frame on renderer r, then shadow_roofline_of"""
+    from rtxpy import abi
+    import rtxpy
+    p2 = rtxpy.default_params(**{f: getattr(params, f) for f, _ in abi.Params._fields_})
+    p2.count_traversal = 1
+    r.render_device(frame, p2, d_rgb.data_ptr(), d_z.data_ptr(), stream.cuda_stream)
+    return shadow_roofline_of(r.stats(), shadow_ms, a, world)
+
+
+def shadow_roofline_of(c, shadow_ms, a, world):
     """Roofline of the dominant kernel, k_shadow (~97 % of device time).  Its counts come from a
     counting instance of the same kernel over the same frame; its duration is the HIP-event time
     of k_shadow in the timed steps (rocprofv3 agrees: profiles/).
@@ -276,13 +283,9 @@ def shadow_roofline(r, frame, params, d_rgb, d_z, stream, shadow_ms, a, world):
       hbm:    algorithmic bytes = the records k_shadow reads from memory: 16 B per box test whose
               record comes from the DQNode array (LDS top records excluded, reported apart), 48 B
               per primitive test, 96 B per shade-point record + 4 B of its Morton index + 16 B
-              written per point; traffic = PMC 2*FETCH_SIZE + WRITE_SIZE (gfx950 correction)."""
-    from rtxpy import abi
-    import rtxpy
-    p2 = rtxpy.default_params(**{f: getattr(params, f) for f, _ in abi.Params._fields_})
-    p2.count_traversal = 1
-    r.render_device(frame, p2, d_rgb.data_ptr(), d_z.data_ptr(), stream.cuda_stream)
-    c = r.stats()
+              written per point; traffic = PMC 2*FETCH_SIZE + WRITE_SIZE (gfx950 correction).
+    c: the counting render's rtx_stats (one device's), shadow_ms: that device's k_shadow time in the
+    timed steps."""
     dur = shadow_ms * 1e-3
     n_pts = int(c.shade_points)
     prim_tests = int(c.shadow_tri_tests + c.shadow_sphere_tests)
@@ -302,6 +305,8 @@ def shadow_roofline(r, frame, params, d_rgb, d_z, stream, shadow_ms, a, world):
            "plane_tests": int(c.shadow_plane_tests), "wave_steps": int(c.shadow_wave_steps),
            "wave_walks": int(c.shadow_wave_walks), "leaf_rounds": int(c.shadow_leaf_rounds),
            "uniform_steps": int(c.shadow_uniform_steps),
+           "shadow_rays_per_s": round(c.shadow_rays / dur / 1e9, 3),
+           "shadow_rays_per_s_unit": "G/s (tree-independent: the reference's is_light_blocked calls per second)",
            "k_trace": {"closest_rays": int(c.closest_rays),
                        "node_visits": int(c.node_visits - c.shadow_node_visits),
                        "prim_tests": int(c.tri_tests + c.sphere_tests - c.shadow_tri_tests - c.shadow_sphere_tests),
@@ -340,6 +345,7 @@ def shadow_roofline(r, frame, params, d_rgb, d_z, stream, shadow_ms, a, world):
             out["issued"] = round(issued, 1)
             out["issued_frac"] = round(issued / VALU_PEAK_GINST, 4)
             out["useful_over_issued"] = round(useful / valu, 4)
+            out["issued_valu_per_shadow_ray"] = round(valu * 64 / max(1, c.shadow_rays), 1)
         if "ta_busy_frac" in rec:
             out["vmem"] = {"ta_busy_frac": rec["ta_busy_frac"], "td_busy_frac": rec.get("td_busy_frac"),
                            "note": "PMC TA_TA_BUSY / TD_TD_BUSY per CU cycle: the vector-memory address / data "
@@ -348,9 +354,12 @@ def shadow_roofline(r, frame, params, d_rgb, d_z, stream, shadow_ms, a, world):
 
 
 POST_FLAGS = ["--dof", "3", "-13", "--mist", "6", "4", "lin", "0.5", "0.5", "0.6"]
+# scene6 (configs[4] "Menger sponge + procedural noise + DoF"): focus on the sponge (z ~ 2.4), the
+# back plane (z = 8) blurred by a radius-5 disc
+POST_FLAGS_SCENE = {"scene6": ["--dof", "2", "-4.8", "--mist", "6", "4", "lin", "0.5", "0.5", "0.6"]}
 
 
-def post_leg(r, d_rgb, d_z, w, h, dev, log, reps=5):
+def post_leg(r, d_rgb, d_z, w, h, dev, log, reps=5, flags=None):
     """§8(f) #1: the postprocess path (rtx_postprocess_device) on the benchmark's own rendered
     frame, next to the reference postprocessor (oracle/_ref/postprocess, single-threaded as it
     ships) on the same raw frame; the 8-bit outputs are compared byte for byte."""
@@ -360,7 +369,8 @@ def post_leg(r, d_rgb, d_z, w, h, dev, log, reps=5):
     import torch
     import rtxpy
     from rtxpy.tiffread import read_tiff
-    post = rtxpy.post_from_args(POST_FLAGS)
+    flags = flags or POST_FLAGS
+    post = rtxpy.post_from_args(flags)
     src = d_rgb.clone()
     out = torch.empty_like(d_rgb)
     stream = torch.cuda.current_stream(dev)
@@ -373,7 +383,7 @@ def post_leg(r, d_rgb, d_z, w, h, dev, log, reps=5):
         torch.cuda.synchronize(dev)
         if i:
             times.append(time.perf_counter() - t0)
-    res = {"flags": " ".join(POST_FLAGS), "gpu_ms": round(1e3 * float(np.median(times)), 3),
+    res = {"flags": " ".join(flags), "gpu_ms": round(1e3 * float(np.median(times)), 3),
            "workload": f"{w}x{h} frame rendered by this bench", "timing": "wall, median of %d, synchronised" % reps}
     ref = os.path.join(ROOT, "oracle", "_ref", "postprocess")
     if not os.path.exists(ref):
@@ -383,7 +393,7 @@ def post_leg(r, d_rgb, d_z, w, h, dev, log, reps=5):
         rgb_h = src.cpu().numpy().reshape(h, w, 3)
         rtxpy.write_tiff(raw, rgb_h, d_z.cpu().numpy().reshape(h, w), raw=True)
         try:
-            p = subprocess.run([ref, raw, o8] + POST_FLAGS, capture_output=True, text=True, timeout=300)
+            p = subprocess.run([ref, raw, o8] + flags, capture_output=True, text=True, timeout=600)
         except (subprocess.TimeoutExpired, OSError) as e:
             log(f"reference postprocess unusable: {e}")
             return res
@@ -428,7 +438,7 @@ def data_label(a):
     return f"the reference's own scenes/{a.scene}.json (no mesh)"
 
 
-WALKS = {"auto": -1, "w8": 2, "bvh2": 0}
+WALKS = {"auto": -1, "w8": 2, "bvh2": 0, "linear": 3}
 FRAMES = {"auto": 0, "world": 1}
 
 
@@ -442,11 +452,11 @@ def main():
     mode, rc = launch_mode(a)
     if mode == "exit":
         sys.exit(rc)
+    if mode == "group":
+        return main_group(a)
     if a.dry_run:
         dry_run(a, mode)
         return
-    if mode == "group":
-        return main_group(a)
     import numpy as np
     import torch
     import rtxpy
@@ -521,11 +531,12 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    rays = 0
+    rays = closest = 0
     kms, sms = [], []
     for i in range(a.steps):
         s = step()
         rays += s.closest_rays + s.shadow_rays
+        closest += s.closest_rays
         kms.append(s.kernel_ms)
         sms.append(s.shadow_ms)
     torch.cuda.synchronize(dev)
@@ -541,9 +552,9 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
-        rr = torch.tensor([rays], dtype=torch.float64, device=dev)
+        rr = torch.tensor([rays, closest], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(rr)
-        rays = int(rr.item())
+        rays, closest = int(rr[0].item()), int(rr[1].item())
 
     kernel_ms = float(np.mean(kms))
     shadow_ms = float(np.mean(sms))
@@ -602,7 +613,7 @@ def main():
     post = None
     if rank == 0 and world == 1 and not a.no_post:
         try:
-            post = post_leg(r, d_rgb, d_z, a.width, a.height, dev, log)
+            post = post_leg(r, d_rgb, d_z, a.width, a.height, dev, log, flags=POST_FLAGS_SCENE.get(a.scene))
         except Exception as e:  # never let the side leg kill the measurement
             log(f"postprocess leg failed: {e}")
 
@@ -620,6 +631,7 @@ def main():
     if rank == 0:
         value = rays / elapsed / 1e6
         out = {"metric": METRIC, "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps,
+               "closest_mrays": round(closest / elapsed / 1e6, 2),
                "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
                "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": data_label(a),
                "config": {"workload": workload(a),
@@ -654,13 +666,42 @@ def main():
         torch.distributed.destroy_process_group()
 
 
+def group_line(a, n, scene_name, objects, elapsed, rays, closest, per_dev, gather_ms, roofline):
+    """the JSON line of a device-group run (also printed by --dry-run, with None for what only a
+    GPU measures).  per_dev: one dict per device of its mean kernel / k_trace / k_shadow times
+    and rays over the timed steps."""
+    steps = a.steps
+    kms = [d["kernel_ms"] for d in per_dev if d["kernel_ms"] is not None]
+    value = rays / elapsed / 1e6 if elapsed else None
+    frame_rays = rays // steps if rays is not None else None
+    return {"metric": METRIC, "value": round(value, 2) if value is not None else None, "unit": "Mrays/s", "n_gpus": n,
+            "steps": steps, "warmup": a.warmup,
+            "ms_per_step": round(elapsed / steps * 1e3, 3) if elapsed else None,
+            "closest_mrays": round(closest / elapsed / 1e6, 2) if elapsed else None,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": data_label(a),
+            "config": {"workload": workload(a), "scene": scene_name, "width": a.width, "height": a.height,
+                       "spp": a.spp, "objects": objects, "parallelism": f"tiles{n}", "launch": "group",
+                       "rays_per_frame": frame_rays,
+                       "step": "rtx_group_render: shards on every device, RCCL send/recv to device 0, unpack, copy to "
+                               "pinned host memory (SURVEY 8(d) window)"},
+            "group": {"rtx_group_size": n, "rccl_devices": n if n > 1 else 0,
+                      "devices": per_dev,
+                      "device_kernel_ms_max": max(kms) if kms else None,
+                      "device_kernel_ms_min": min(kms) if kms else None,
+                      "gather_ms": gather_ms,
+                      "gather_message_bytes_per_device": int(16 * 64 * -(-((a.width + 7) // 8) * ((a.height + 7) // 8) // n))},
+            "roofline": roofline,
+            "cpu_baseline": None,
+            "cpu_baseline_note": "reported on the N=1 line (the reference's CPU path on this box's host cores)"}
+
+
 def main_group(a):
     """--gpus N > 1 in one process: the C-ABI device group (rtx_group_*), the path engine --gpus N
     ships.  A step is rtx_group_render: every device renders its tile shard on its own host
     thread, devices 1..N-1 pack their shards and RCCL send/recv moves them to device 0, which
-    unpacks and copies the frame to (pinned) host memory."""
+    unpacks and copies the frame to (pinned) host memory.  The line carries every device's
+    kernel times (balance) and the roofline of device 0's k_shadow from a counting render."""
     import numpy as np
-    import torch
     import rtxpy
     from rtxpy import abi
 
@@ -669,6 +710,16 @@ def main_group(a):
 
     path = scene_path(a.scene)
     scene = rtxpy.Scene.load(path, base_dir=os.path.join(ROOT, "tests", "golden"))
+    if a.dry_run:  # the schema of the line, without a GPU
+        dev0 = {"device": 0, "kernel_ms": None, "trace_ms": None, "shadow_ms": None, "rays": None}
+        out = group_line(a, a.gpus, os.path.basename(path), int(scene.num_objects), None, None, None,
+                         [dict(dev0, device=r) for r in range(a.gpus)], None,
+                         {"bound": "valu", "achieved": None, "peak": VALU_PEAK_GINST, "unit": "Ginst/s", "frac": None,
+                          "traffic": None, "kernel": "k_shadow", "device": 0})
+        out["dry_run"] = True
+        print(json.dumps(out), flush=True)
+        return
+    import torch
     frame = scene.frame(a.width, a.height)
     flags = flags_for(a.scene, a.spp)
     params = rtxpy.params_from_args(flags, seed=1)
@@ -682,7 +733,9 @@ def main_group(a):
         g.set_option(abi.RTX_OPT_SHADOW_GRAB, a.shadow_grab)
     t0 = time.perf_counter()
     g.upload(scene)
-    log(f"{n} devices, scene {os.path.basename(path)} uploaded in {time.perf_counter() - t0:.2f}s")
+    s0 = g.device_stats(0)
+    log(f"{n} devices, scene {os.path.basename(path)} uploaded in {time.perf_counter() - t0:.2f}s "
+        f"(build on device 0 {s0.build_ms:.1f} ms, tree frame {'rotated' if s0.tree_rotated else 'world'})")
     h_rgb = torch.empty((a.height, a.width, 3), dtype=torch.float32, pin_memory=True).numpy()
     h_z = torch.empty((a.height, a.width), dtype=torch.float32, pin_memory=True).numpy()
     for i in range(a.warmup):
@@ -690,30 +743,34 @@ def main_group(a):
         s = g.stats()
         log(f"warmup {i}: {s.kernel_ms:.1f} ms (slowest device), gather {s.gather_ms:.2f} ms")
     t0 = time.perf_counter()
-    rays = 0
-    per_dev = []
+    rays = closest = 0
+    dev = [[] for _ in range(n)]
+    gms = []
     for i in range(a.steps):
         g.render(frame, params, h_rgb, h_z)
         s = g.stats()
         rays += s.closest_rays + s.shadow_rays
-        per_dev.append([g.device_stats(r).kernel_ms for r in range(n)])
+        closest += s.closest_rays
+        gms.append(s.gather_ms)
+        for r in range(n):
+            d = g.device_stats(r)
+            dev[r].append((d.kernel_ms, d.trace_ms, d.shadow_ms, d.closest_rays + d.shadow_rays))
     elapsed = time.perf_counter() - t0
-    dev_ms = np.array(per_dev)
-    value = rays / elapsed / 1e6
-    out = {"metric": METRIC, "value": round(value, 2), "unit": "Mrays/s", "n_gpus": n, "steps": a.steps,
-           "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
-           "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": data_label(a),
-           "config": {"workload": workload(a), "scene": os.path.basename(path), "width": a.width, "height": a.height,
-                      "spp": a.spp, "objects": int(scene.num_objects), "parallelism": f"tiles{n}", "launch": "group",
-                      "rays_per_frame": s.closest_rays + s.shadow_rays,
-                      "step": "rtx_group_render: shards on every device, RCCL send/recv to device 0, unpack, copy to "
-                              "pinned host memory (SURVEY 8(d) window)"},
-           "group": {"rtx_group_size": n, "rccl_devices": n if n > 1 else 0,
-                     "device_kernel_ms_max": round(float(dev_ms.mean(0).max()), 3),
-                     "device_kernel_ms_min": round(float(dev_ms.mean(0).min()), 3),
-                     "gather_ms": round(s.gather_ms, 3),
-                     "gather_message_bytes_per_device": int(16 * 64 * -(-((a.width + 7) // 8) * ((a.height + 7) // 8) // n))},
-           "roofline": None, "cpu_baseline": None}
+    per_dev = []
+    for r in range(n):
+        m = np.array(dev[r], dtype=np.float64).mean(0)
+        per_dev.append({"device": r, "kernel_ms": round(m[0], 3), "trace_ms": round(m[1], 3), "shadow_ms": round(m[2], 3),
+                        "rays": int(m[3])})
+    roofline = None
+    if not a.no_count:
+        p2 = rtxpy.default_params(**{f: getattr(params, f) for f, _ in abi.Params._fields_})
+        p2.count_traversal = 1
+        g.render(frame, p2, h_rgb, h_z)
+        roofline = shadow_roofline_of(g.device_stats(0), per_dev[0]["shadow_ms"], a, n)
+        roofline["device"] = 0
+        roofline["note"] = "device 0's k_shadow over its shard (tiles t % N == 0), counts from a counting render"
+    out = group_line(a, n, os.path.basename(path), int(scene.num_objects), elapsed, rays, closest, per_dev,
+                     round(float(np.mean(gms)), 3), roofline)
     print(json.dumps(out), flush=True)
     g.close()
 

@@ -120,6 +120,7 @@ static void free_scene(rtx_ctx *c)
 	dfree(c->d_planes);
 	dfree(c->d_mats);
 	dfree(c->d_emitters);
+	dfree(c->d_lin);
 	dfree(c->d_qnodes);
 	dfree(c->d_top);
 	dfree(c->d_w8);
@@ -476,7 +477,10 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 	/* RTX_WALK_AUTO: a scene whose threaded BVH2 fits the LDS top records is walked from LDS alone
 	 * (scene3, 3 spheres: 102 ms vs 114 ms over the 8-wide tree); larger ones over the 8-wide tree */
 	const bool small = (uint64_t)2 * nb <= RTX_TOP_MAX + 1;
-	const bool want_w8 = nb && (c->opt_walk == RTX_WALK_W8 || (c->opt_walk == RTX_WALK_AUTO && !small));
+	/* a tiny scene (RTX_WALK_LINEAR): k_shadow tests its few bounded objects one by one like the planes
+	 * (scene1 / scene3: 3 spheres, one of them the light), no walk */
+	const bool linear = nb && (c->opt_walk == RTX_WALK_LINEAR || (c->opt_walk == RTX_WALK_AUTO && nb <= RTX_SHADOW_LINEAR_MAX));
+	const bool want_w8 = nb && !linear && (c->opt_walk == RTX_WALK_W8 || (c->opt_walk == RTX_WALK_AUTO && !small));
 	std::vector<DNode> inner; /* host copy of the inner-node records (threaded BVH2, host collapse) */
 	std::vector<DPrim> prims_dl; /* device builders: the primitive records read back (host collapse) */
 	const DPrim *host_prims = nullptr; /* the primitive records in leaf order on the host */
@@ -637,7 +641,26 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 	}
 	if (hs.w8.empty() && !hs.w8_on_device)
 		hs.w8depth = 0;
-	if (!hs.w8depth) {
+	if (linear) {
+		for (uint32_t k = 0; k < nb; k++) {
+			const rtx_object &o = sc->objects[bounded[k]];
+			DEmitter e;
+			memset(&e, 0, sizeof(e));
+			e.obj = bounded[k];
+			e.type = (uint32_t)o.type;
+			memcpy(e.p0, o.p0, 12);
+			memcpy(e.p1, o.p1, 12);
+			memcpy(e.p2, o.p2, 12);
+			e.radius = o.radius;
+			memcpy(e.e1, o.e1, 12);
+			memcpy(e.e2, o.e2, 12);
+			e.eps = o.epsilon;
+			e.transparent = (mats[o.material].flags & RTX_MF_TRANSPARENT) ? 1u : 0u;
+			memcpy(e.kt, mats[o.material].kt, 12);
+			e.prim = RTX_NONE;
+			hs.lin.push_back(e);
+		}
+	} else if (!hs.w8depth) {
 		std::vector<uint32_t> qdepth;
 		thread_bvh(inner, nb ? root_ref : RTX_EMPTY_REF, tlo, thi, hs.qnodes, hs.qf, qdepth);
 		if (hs.qnodes.size() >= (1u << 26))
@@ -674,7 +697,7 @@ int rtx_upload_built(rtx_ctx *c, HostScene &hs)
 	if (!(hs.recs_on_device && c->d_nodes) && (rc = upload(c->d_nodes, hs.recs)))
 		return rc;
 	if ((rc = upload(c->d_qnodes, hs.qnodes)) || (rc = upload(c->d_top, hs.qtop)) || (rc = upload(c->d_planes, hs.planes)) ||
-	    (rc = upload(c->d_mats, hs.mats)) || (rc = upload(c->d_emitters, hs.emit)))
+	    (rc = upload(c->d_mats, hs.mats)) || (rc = upload(c->d_emitters, hs.emit)) || (rc = upload(c->d_lin, hs.lin)))
 		return rc;
 	const bool have_w8 = hs.w8_on_device || !hs.w8.empty();
 	const uint32_t num_w8 = hs.w8_on_device ? hs.w8_entries : (uint32_t)hs.w8.size();
@@ -724,6 +747,8 @@ int rtx_upload_built(rtx_ctx *c, HostScene &hs)
 	S.planes = c->d_planes;
 	S.mats = c->d_mats;
 	S.emitters = c->d_emitters;
+	S.lin = hs.lin.empty() ? nullptr : c->d_lin;
+	S.num_lin = (uint32_t)hs.lin.size();
 	S.qnodes = hs.qnodes.empty() ? nullptr : c->d_qnodes;
 	S.num_qnodes = (uint32_t)hs.qnodes.size();
 	memcpy(S.qo, hs.qf.qo, 12);
@@ -753,7 +778,7 @@ int rtx_upload_built(rtx_ctx *c, HostScene &hs)
 	c->stats.bvh_depth = hs.depth;
 	c->stats.builder = (uint32_t)hs.builder;
 	c->stats.bvh_prims = hs.nb;
-	c->stats.shadow_walk = S.w8 ? RTX_WALK_W8 : RTX_WALK_BVH2;
+	c->stats.shadow_walk = S.lin ? RTX_WALK_LINEAR : S.w8 ? RTX_WALK_W8 : RTX_WALK_BVH2;
 	c->stats.tree_rotated = hs.tf.rotated;
 	c->stats.frame_cost = hs.frame_ratio;
 	c->stats.frame_ms = hs.frame_ms;
@@ -860,7 +885,8 @@ int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, floa
 	HIP_TRY(hipMemGetInfo(&free_b, &total_b));
 	/* shade points of a chunk: up to a third of free HBM (96 GB cap; 288 GB per MI355X) */
 	const uint64_t budget = std::min<uint64_t>(96ull << 30, free_b / 3);
-	const uint32_t chunk_cap = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(P.ntiles, budget / (avg_tile * 112)));
+	/* 128 B per shade point: its record (96), its light term (16) and its sort keys / values (16) */
+	const uint32_t chunk_cap = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(P.ntiles, budget / (avg_tile * 128)));
 	uint32_t chunk_tiles = chunk_cap;
 
 	auto grow = [](auto *&ptr, size_t &have, size_t need) -> hipError_t {
@@ -957,13 +983,18 @@ int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, floa
 		 * emission order (same image, bit for bit) */
 		const uint32_t *perm = nullptr;
 		if (n_sp > 1 && c->scene.root_ref != RTX_EMPTY_REF && spsort) {
+			/* keys and values (two ping-pong buffers each) sized for the chunk's capacity, like the
+			 * shade-point array: a later render with more points per chunk (its chunks sized from
+			 * this one's count) then reuses them instead of reallocating inside its frame */
 			size_t tmp = 0;
-			HIP_TRY(rtx_spsort_temp_bytes(n_sp, &tmp));
-			HIP_TRY(grow(c->d_sortbuf, c->sortbuf_bytes, (size_t)n_sp * 4 * sizeof(uint32_t)));
+			const size_t cap = std::max<size_t>(n_sp, c->sp_bytes / (6 * sizeof(float4)));
+			HIP_TRY(rtx_spsort_temp_bytes((uint32_t)std::min<size_t>(cap, 0xFFFFFFF0u), &tmp));
+			HIP_TRY(grow(c->d_sortbuf, c->sortbuf_bytes, cap * 4 * sizeof(uint32_t)));
 			HIP_TRY(grow(c->d_sorttmp, c->sorttmp_bytes, tmp));
+			const size_t q = c->sortbuf_bytes / (4 * sizeof(uint32_t)); /* the buffer's capacity in points */
 			uint32_t *b = c->d_sortbuf;
-			HIP_TRY(rtx_launch_spsort(c->d_sp, n_sp, c->bound_lo, c->bound_hi, b, b + n_sp, b + 2 * (size_t)n_sp,
-						  b + 3 * (size_t)n_sp, c->d_sorttmp, c->sorttmp_bytes, &perm, stream));
+			HIP_TRY(rtx_launch_spsort(c->d_sp, n_sp, c->bound_lo, c->bound_hi, b, b + q, b + 2 * q, b + 3 * q, c->d_sorttmp,
+						  c->sorttmp_bytes, &perm, stream));
 		}
 		HIP_TRY(hipEventRecord(c->ev[4], stream));
 		HIP_TRY(rtx_launch_shadow(&c->scene, &P, c->d_sp, perm, n_sp, per_wave, slot_b, c->d_contrib, c->d_ctr,
@@ -1141,8 +1172,8 @@ extern "C" int rtx_set_option(rtx_ctx *c, int option, int64_t value)
 		return fail(RTX_ERR_ARG, "null argument");
 	switch (option) {
 	case RTX_OPT_SHADOW_WALK:
-		if (value != RTX_WALK_AUTO && value != RTX_WALK_BVH2 && value != RTX_WALK_W8)
-			return fail(RTX_ERR_ARG, "shadow walk %lld is not AUTO, BVH2 or W8", (long long)value);
+		if (value != RTX_WALK_AUTO && value != RTX_WALK_BVH2 && value != RTX_WALK_W8 && value != RTX_WALK_LINEAR)
+			return fail(RTX_ERR_ARG, "shadow walk %lld is not AUTO, BVH2, W8 or LINEAR", (long long)value);
 		c->opt_walk = (int)value;
 		return RTX_OK;
 	case RTX_OPT_BVH_LEAF:

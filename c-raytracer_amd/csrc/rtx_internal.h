@@ -60,6 +60,7 @@ struct rtx_ctx {
 	DPlane *d_planes = nullptr;
 	DMaterial *d_mats = nullptr;
 	DEmitter *d_emitters = nullptr;
+	DEmitter *d_lin = nullptr; /* RTX_WALK_LINEAR: the bounded objects as shadow-test records */
 	DQNode *d_qnodes = nullptr;
 	uint32_t *d_top = nullptr;
 	DW8 *d_w8 = nullptr;
@@ -142,6 +143,7 @@ struct HostScene {
 	std::vector<DPlane> planes;
 	std::vector<DMaterial> mats;
 	std::vector<DEmitter> emit;
+	std::vector<DEmitter> lin;    /* RTX_WALK_LINEAR: every bounded object as a shadow-test record */
 	float bound_lo[3] = { 0, 0, 0 }, bound_hi[3] = { 0, 0, 0 }, ambient[3] = { 0, 0, 0 };
 	uint32_t num_emitters = 0;
 	DTreeFrame tf{};              /* the frame every tree's boxes are in (rtx_frame.cpp) */

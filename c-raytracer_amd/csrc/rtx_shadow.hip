@@ -491,9 +491,9 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
  * lane shares it.  Returns the lane's blocked flag; li carries the transmittance product. */
 template <bool COUNT, int WALK>
 __device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restrict__ recs, const DMaterial *__restrict__ mats,
-					     const DPlane *__restrict__ planes, uint32_t num_planes, const DEmitter *__restrict__ emitters,
-					     uint32_t test_emitters, bool have_tree, const DTreeFrame &tf, bool act, f3 o, f3 d,
-					     float dist, uint32_t emit_obj, f3 &li, ShadowCount &sc)
+					     const DPlane *__restrict__ planes, uint32_t num_planes, const DEmitter *__restrict__ lin,
+					     uint32_t num_lin, bool have_tree, const DTreeFrame &tf, bool act, f3 o, f3 d, float dist,
+					     uint32_t emit_obj, f3 &li, ShadowCount &sc)
 {
 	float tl = act ? dist : -1.f;
 	for (uint32_t i = 0; i < num_planes; i++) { /* plane records are wave-uniform: s_load */
@@ -507,10 +507,11 @@ __device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restri
 			tl = -1.f;
 		}
 	}
-	/* the emitters other than the one sampled, when the 8-wide tree leaves them out
-	 * (rtx_device.h DW8): tested like the planes, records wave-uniform (s_load) */
-	for (uint32_t i = 0; i < test_emitters; i++) {
-		const auto *e = cptr(emitters) + i;
+	/* objects tested one by one like the planes, records wave-uniform (s_load): the emitters other
+	 * than the one sampled when the 8-wide tree leaves them out (rtx_device.h DW8), or every bounded
+	 * object of a tiny scene (DScene.lin), in object order */
+	for (uint32_t i = 0; i < num_lin; i++) {
+		const auto *e = cptr(lin) + i;
 		if (e->obj == emit_obj || !(tl >= 0.f))
 			continue;
 		bool h;
@@ -585,7 +586,10 @@ const DW8 *w8;        /* 8-wide compressed BVH (WALK_W8 instances; qo / qs / qsi
 	const DW8S *w8s;      /* its nodes' scalar-path copies */
 	uint32_t *w8spill;    /* lane-stack spill area, [entry][grid lane] */
 	uint32_t w8lstk;      /* lane-stack entries in LDS */
-	uint32_t test_emitters; /* emitters shadow_query tests linearly (the 8-wide tree leaves them out), else 0 */	float qo[3], qs[3], qsi[3];
+	const DEmitter *lin;  /* objects shadow_query tests one by one: the emitters the 8-wide tree leaves out,
+	                       * or every bounded object of a tiny scene (no tree walk) */
+	uint32_t num_lin;
+	float qo[3], qs[3], qsi[3];
 	DTreeFrame tf;        /* the trees' frame (their boxes are in it) */
 	const uint32_t *top; /* its top levels (rtx_device.h RTX_QTOP_CUT), copied to LDS per workgroup */
 	uint32_t ntop;
@@ -740,7 +744,7 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	Q.stk = stk;
 	Q.tq = stk + RTX_W8_STACK * WAVE;
 	const bool blocked = shadow_query<COUNT, WALK>(Q, unip(ks.recs), unip(ks.mats), unip(ks.planes), uni(ks.num_planes),
-						 emitters, uni(ks.test_emitters), have_tree, ks.tf, act, p, ldir, ldist, E.obj, li, sc);
+						 unip(ks.lin), uni(ks.num_lin), have_tree, ks.tf, act, p, ldir, ldist, E.obj, li, sc);
 	reread_barrier();
 	f3 contribution = mk3(0.f, 0.f, 0.f);
 	if (act && !blocked)
@@ -1169,7 +1173,7 @@ for (int a = 0; a < 3; a++) {
 	ka.perm = perm;
 	ka.contrib = contrib;
 	ka.ctr = ctr;
-	ka.have_tree = S->root_ref != RTX_EMPTY_REF && S->qnodes;
+	ka.have_tree = S->root_ref != RTX_EMPTY_REF && !S->lin && (S->w8 || S->qnodes); /* the walk of walk_of(S) has its tree */
 	ka.num_planes = S->num_planes;
 	ka.num_emitters = S->num_emitters;
 	ka.n_sp = n_sp;
@@ -1184,14 +1188,16 @@ for (int a = 0; a < 3; a++) {
 	ka.w8s = S->w8s;
 	ka.w8spill = S->w8spill;
 	ka.w8lstk = S->w8lstk;
-	ka.test_emitters = 0;
+	ka.lin = S->lin; /* a tiny scene: every bounded object, no walk */
+	ka.num_lin = S->lin ? S->num_lin : 0u;
 	if (walk == WALK_W8) { /* the 8-wide tree's own frame; the emitters it leaves out are tested linearly */
 		for (int a = 0; a < 3; a++) {
 			ka.qo[a] = S->w8qo[a];
 			ka.qs[a] = S->w8qs[a];
 			ka.qsi[a] = 1.f / S->w8qs[a];
 		}
-		ka.test_emitters = S->w8noemit ? S->num_emitters : 0u;
+		ka.lin = S->emitters;
+		ka.num_lin = S->w8noemit ? S->num_emitters : 0u;
 	}
 	if (walk == WALK_W8)
 		return launch_walk<WALK_W8>(ka, nw, cus, count, stream);

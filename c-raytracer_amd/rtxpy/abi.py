@@ -76,8 +76,9 @@ class Stats(C.Structure):
 
 
 RTX_BUILD_SAH_HOST, RTX_BUILD_LBVH_GPU, RTX_BUILD_PLOC_GPU, RTX_BUILD_SAH_GPU = 0, 1, 2, 3
-RTX_WALK_AUTO, RTX_WALK_BVH2, RTX_WALK_W8 = -1, 0, 2
-WALK_NAMES = {RTX_WALK_BVH2: "bvh2", RTX_WALK_W8: "w8"}
+RTX_WALK_AUTO, RTX_WALK_BVH2, RTX_WALK_W8, RTX_WALK_LINEAR = -1, 0, 2, 3
+WALK_NAMES = {RTX_WALK_BVH2: "bvh2", RTX_WALK_W8: "w8", RTX_WALK_LINEAR: "linear"}
+RTX_SHADOW_LINEAR_MAX = 8
 RTX_FRAME_AUTO, RTX_FRAME_WORLD = 0, 1
 RTX_OPT_SHADOW_WALK, RTX_OPT_BVH_LEAF, RTX_OPT_SPSORT, RTX_OPT_SHADOW_SLOT, RTX_OPT_SHADOW_GRAB, \
     RTX_OPT_SHADOW_LDS_STACK, RTX_OPT_TRACE_WALK, RTX_OPT_TREE_FRAME = 1, 2, 3, 4, 5, 6, 7, 8

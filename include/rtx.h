@@ -213,7 +213,7 @@ typedef struct rtx_stats {
 	uint32_t devices;                 /* devices that rendered the last frame */
 	uint32_t pad_;
 	uint64_t shadow_uniform_steps;    /* only with count_traversal, 8-wide walk: wave steps whose active lanes were all at one node */
-	uint32_t shadow_walk;             /* the BVH k_shadow walks: RTX_WALK_W8 / RTX_WALK_BVH2 */
+	uint32_t shadow_walk;             /* the BVH k_shadow walks: RTX_WALK_W8 / RTX_WALK_BVH2 / RTX_WALK_LINEAR */
 	uint32_t wide_entries;            /* 8-wide walk: 64-byte entries (nodes, primitive records, holes) */
 	uint32_t trace_walk;              /* the BVH k_trace walks for closest hits: RTX_WALK_W8 / RTX_WALK_BVH2 */
 	uint32_t pad2_;
@@ -252,10 +252,14 @@ int rtx_set_builder(rtx_ctx *ctx, int builder);
 
 /* Shadow-walk BVH layouts (rtx_stats.shadow_walk, RTX_OPT_SHADOW_WALK); 1 was the 4-wide walk */
 enum {
-	RTX_WALK_AUTO = -1, /* the fastest available: the threaded BVH2 from LDS for small scenes, else 8-wide */
+	RTX_WALK_AUTO = -1, /* the fastest available: LINEAR for tiny scenes, the threaded BVH2 from LDS for
+	                     * small ones (<= 1024 bounded objects), else 8-wide */
 	RTX_WALK_BVH2 = 0,  /* threaded quantised BVH2 (DQNode), no stack */
-	RTX_WALK_W8 = 2     /* 8-wide compressed BVH (8-bit child boxes in each node's frame) */
+	RTX_WALK_W8 = 2,    /* 8-wide compressed BVH (8-bit child boxes in each node's frame) */
+	RTX_WALK_LINEAR = 3 /* no tree: every bounded object tested one by one, like the planes (AUTO for
+	                     * scenes of at most RTX_SHADOW_LINEAR_MAX bounded objects) */
 };
+#define RTX_SHADOW_LINEAR_MAX 8
 /* The frame the BVHs are built in (RTX_OPT_TREE_FRAME, rtx_tree_frame) */
 enum {
 	RTX_FRAME_AUTO = 0,  /* default: a rotated frame when it shrinks the leaf boxes (a rotated mesh's own axes) */

@@ -29,7 +29,26 @@ def test_gpus_flag_without_torchrun_drives_the_device_group():
     p = run(["--gpus", "4", "--dry-run"])
     assert p.returncode == 0, p.stderr[-2000:]
     out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
-    assert out == {"dry_run": True, "n_gpus": 4, "launch": "group", "processes": 1}
+    assert out["dry_run"] and out["n_gpus"] == 4 and out["config"]["launch"] == "group"
+
+
+def test_group_line_schema():
+    """the device-group line (--gpus N, one process): the contract's keys, every device's kernel
+    times (balance), the gather time and device 0's k_shadow roofline"""
+    p = run(["--gpus", "8", "--dry-run", "--scene", "scene3", "--spp", "16"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "closest_mrays"):
+        assert k in out, k
+    assert out["metric"].startswith("Mrays/s") and out["n_gpus"] == 8 and out["scaling"] == "strong"
+    assert out["config"]["workload"].endswith("(BASELINE configs[1])")
+    devs = out["group"]["devices"]
+    assert [d["device"] for d in devs] == list(range(8))
+    assert all({"kernel_ms", "trace_ms", "shadow_ms", "rays"} <= set(d) for d in devs)
+    assert "gather_ms" in out["group"] and out["group"]["rccl_devices"] == 8
+    rl = out["roofline"]
+    assert rl["kernel"] == "k_shadow" and rl["device"] == 0 and {"bound", "achieved", "peak", "unit", "frac", "traffic"} <= set(rl)
 
 
 def test_workload_labels_name_the_baseline_config():

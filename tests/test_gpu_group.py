@@ -1,11 +1,17 @@
 """Multi-device C-ABI (include/rtx.h rtx_group_*, csrc/rtx_group.cpp) on the one-GPU box.
 
-A group of one device is the same render as rtx_render, bit for bit (the BVH built once on the
-host, uploaded through the group path).  The gather's device kernels (rtx_tile_pack_device /
-rtx_tile_unpack_device, csrc/rtx_gather.hip) are checked on one device: packing the shards of
-a rendered frame equals the host reference records, and unpacking every shard rebuilds the
-frame; the RCCL send/recv between them is exercised by the driver's multi-GPU runs (the
-torch.distributed bench path gathers the same records, tests/test_distributed.py).
+A group of one device is the same render as rtx_render, bit for bit, with the same upload (the
+BVHs built on device 0: device SAH and the 8-wide collapse, the same tree as a single context).
+The gather's device kernels (rtx_tile_pack_device / rtx_tile_unpack_device, csrc/rtx_gather.hip)
+are checked on one device: packing the shards of a rendered frame equals the host reference
+records, and unpacking every shard rebuilds the frame.
+
+NOT exercised here: a group of n > 1 devices, i.e. the peer copies of the built trees
+(hipMemcpyPeer in rtx_group_upload_scene) and the grouped RCCL ncclSend / ncclRecv of the
+shards.  This box has one GPU, and the driver's multi-GPU runs have so far been skipped (no 8-GPU
+node), so that path has never run.  What stands in for it: the shard deal and record layout on
+the host (tests/test_gather.py), the same records gathered over torch.distributed with gloo
+(tests/test_distributed.py), and the group line's schema (tests/test_bench_cli.py).
 """
 import numpy as np
 import pytest
@@ -34,6 +40,10 @@ def test_gpu_group_of_one_matches_render(name):
     assert (sa.closest_rays, sa.shadow_rays) == (sb.closest_rays, sb.shadow_rays)
     assert sb.devices == 1 and sb.gather_ms == 0.0
     assert sb.wide_nodes == sa.wide_nodes and sb.bvh_nodes == sa.bvh_nodes
+    # the group's upload is the single context's: device SAH + device 8-wide collapse
+    assert sb.builder == sa.builder == abi.RTX_BUILD_SAH_GPU
+    assert (sb.shadow_walk, sb.wide_entries, sb.wide_depth, sb.tree_rotated) == \
+        (sa.shadow_walk, sa.wide_entries, sa.wide_depth, sa.tree_rotated)
 
 
 def test_gpu_group_rejects_shard_params_and_bad_devices():

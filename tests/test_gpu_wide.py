@@ -3,6 +3,7 @@
   RTX_WALK_W8    8-wide compressed BVH (rtx_device.h DW8, shadow_walk8), the default
   RTX_WALK_BVH2  threaded BVH2 (shadow_walk): small scenes (its top levels fit LDS) and trees the
                  8-wide layout cannot hold
+  RTX_WALK_LINEAR no tree: every bounded object tested one by one (tiny scenes, <= 8 objects)
 
 All answer is_light_blocked (render.c:126-134, accel.c:360-387) exactly: each culls only with
 conservative boxes and any-hit needs no visit order.  Only the order in which transparent
@@ -49,6 +50,13 @@ def render(r, scene, frame, params, walk=abi.RTX_WALK_AUTO):
 SMALL = {"s1_amb", "s3_path2", "st_amb", "st2_r2"}  # threaded BVH2 within the LDS top (<= 1024 primitives)
 
 
+def auto_walk(scene, name):
+    nb = sum(1 for o in scene.objects() if o.type != abi.RTX_PLANE)
+    if nb <= abi.RTX_SHADOW_LINEAR_MAX:
+        return abi.RTX_WALK_LINEAR
+    return abi.RTX_WALK_BVH2 if name in SMALL else abi.RTX_WALK_W8
+
+
 @pytest.mark.parametrize("name", CONFIGS)
 def test_gpu_walks_agree(renderer, name):
     scene, frame, params, _ = C.load_config(name)
@@ -56,10 +64,13 @@ def test_gpu_walks_agree(renderer, name):
     assert sa.shadow_walk == abi.RTX_WALK_W8 and sa.wide_nodes > 0 and sa.wide_depth >= 1
     assert sa.wide_entries >= 8 * sa.wide_nodes
     ref_rgb, ref_z = C.golden_frame(name + "_o2")
-    # RTX_WALK_AUTO: the LDS-resident threaded BVH2 for small scenes, the 8-wide tree otherwise
+    # RTX_WALK_AUTO: no tree for tiny scenes, the LDS-resident threaded BVH2 for small ones, the
+    # 8-wide tree otherwise
     _, _, sd = render(renderer, scene, frame, params)
-    assert sd.shadow_walk == (abi.RTX_WALK_BVH2 if name in SMALL else abi.RTX_WALK_W8), name
-    for walk in (abi.RTX_WALK_BVH2,):
+    assert sd.shadow_walk == auto_walk(scene, name), name
+    for walk in (abi.RTX_WALK_BVH2, abi.RTX_WALK_LINEAR):
+        if walk == abi.RTX_WALK_LINEAR and len(scene.objects()) > 64:
+            continue  # one by one over a mesh: correct, but not a walk anyone would run
         b, zb, sb = render(renderer, scene, frame, params, walk)
         assert sb.shadow_walk == walk
         assert np.array_equal(za, zb), (name, walk)
@@ -123,7 +134,7 @@ def test_gpu_w8_walk_counts(renderer):
 
 
 def test_gpu_options_reject_bad_values(renderer):
-    for opt, bad in ((abi.RTX_OPT_SHADOW_WALK, 3), (abi.RTX_OPT_SHADOW_WALK, 1), (abi.RTX_OPT_TREE_FRAME, 2),
+    for opt, bad in ((abi.RTX_OPT_SHADOW_WALK, 4), (abi.RTX_OPT_SHADOW_WALK, 1), (abi.RTX_OPT_TREE_FRAME, 2),
                      (abi.RTX_OPT_BVH_LEAF, 0), (abi.RTX_OPT_SPSORT, 2),
                      (abi.RTX_OPT_SHADOW_SLOT, 3), (abi.RTX_OPT_SHADOW_GRAB, 0), (abi.RTX_OPT_SHADOW_LDS_STACK, 9),
                      (99, 1)):

@@ -32,6 +32,14 @@ for s in $STEPS; do
     s6frames) for f in ${FRAMES:-world auto}; do run s6_frame_$f 900 python3 bench.py --scene scene6 --width 3840 --height 2160 --spp 128 --frame $f --steps 1 --warmup 1 --no-cpu-baseline --no-post --verbose; done ;;
     s6var) for v in ${VARS:-$(ls c-raytracer_amd/lib/var)}; do RTX_LIBRTX=$PWD/c-raytracer_amd/lib/var/$v/librtx.so run s6var_$v 900 python3 bench.py --scene scene6 --width 3840 --height 2160 --spp 128 --steps 1 --warmup 1 --no-cpu-baseline --no-post --verbose; done ;;
     s6slot) for sl in ${SLOTS:-64 16}; do run s6slot_$sl 900 python3 bench.py --scene scene6 --width 3840 --height 2160 --spp 128 --shadow-slot $sl --steps 1 --warmup 1 --no-cpu-baseline --no-post --no-count --verbose; done ;;
+    cfgs) # every BASELINE config on one GPU, each line with the reference CPU baseline and closest-only rate
+      run cfg0_scene1_512 600 python3 bench.py --scene scene1 --width 512 --height 512 --steps 5 --warmup 1 --verbose &&
+      run cfg1_scene3_1080p_n16 600 python3 bench.py --scene scene3 --spp 16 --steps 3 --warmup 1 --verbose &&
+      run cfg2_scene5_1080p_n64 600 python3 bench.py --steps 3 --warmup 1 --verbose &&
+      run cfg3_scene5_1080p_n256 900 python3 bench.py --spp 256 --steps 1 --warmup 1 --verbose &&
+      run cfg4_scene6_2160p_n128 900 python3 bench.py --scene scene6 --width 3840 --height 2160 --spp 128 --steps 2 --warmup 1 --verbose &&
+      run cfgl8_scene5_l8 900 python3 bench.py --scene scene5_l8 --steps 2 --warmup 1 --verbose ;;
+    s3walks) for w in ${S3WALKS:-linear bvh2}; do run s3_walk_$w 600 python3 bench.py --scene scene3 --spp 16 --walk $w --steps 3 --warmup 1 --no-cpu-baseline --no-post --verbose; done ;;
     s3) run s3 600 python3 bench.py --scene scene3 --width 1920 --height 1080 --spp 16 --steps 3 --warmup 1 --no-cpu-baseline --no-post --verbose ;;
     l8) run l8 900 python3 bench.py --scene scene5_l8 --steps 1 --warmup 1 --no-cpu-baseline --no-post --verbose ;;
     s6) for w in ${TWALKS:-w8}; do run s6_$w 900 python3 bench.py --scene scene6 --width 3840 --height 2160 --spp 128 --trace-walk $w --steps 1 --warmup 1 --no-cpu-baseline --no-post --verbose; done ;;
