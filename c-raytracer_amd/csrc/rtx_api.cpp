@@ -398,7 +398,7 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 	memcpy(tlo, c->bound_lo, 12);
 	memcpy(thi, c->bound_hi, 12);
 	if (tf.rotated) {
-		const double pad = rtx_frame_pad(rtx_frame_radius(sc, bounded, tf));
+		const double pad = hs.frame_pad = rtx_frame_pad(rtx_frame_radius(sc, bounded, tf));
 		for (int a = 0; a < 3; a++) {
 			tlo[a] = FLT_MAX;
 			thi[a] = -FLT_MAX;
@@ -636,8 +636,8 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 		std::vector<uint32_t> emit_objs;
 		for (const DEmitter &e : emit)
 			emit_objs.push_back(e.obj);
-		hs.w8depth = rtx_wide8_build(inner, nnodes, host_prims, root_ref, tlo, thi, emit_objs, hs.w8f, hs.w8noemit, hs.w8,
-					     hs.w8leaf);
+		hs.w8depth = rtx_wide8_build(inner, nnodes, host_prims, root_ref, tlo, thi, emit_objs, tf, hs.frame_pad, hs.w8f,
+					     hs.w8noemit, hs.w8, hs.w8leaf);
 	}
 	if (hs.w8.empty() && !hs.w8_on_device)
 		hs.w8depth = 0;

@@ -148,6 +148,7 @@ struct HostScene {
 	uint32_t num_emitters = 0;
 	DTreeFrame tf{};              /* the frame every tree's boxes are in (rtx_frame.cpp) */
 	double frame_ratio = 1.0;     /* its sampled leaf-box cost over the identity's */
+	double frame_pad = 0;         /* the leaf boxes' padding for the ray transform (rtx_frame.cpp) */
 	double frame_ms = 0;          /* choosing it and the leaf boxes in it */
 	double build_ms = 0;
 	HostScene() = default;
@@ -167,10 +168,11 @@ struct HostScene {
 /* flatten sc and build its BVHs (on c's device for the device builder), then upload to c */
 int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs);
 int rtx_upload_built(rtx_ctx *c, HostScene &hs);
-/* rtx_wide8.cpp: the 8-wide shadow BVH collapsed from the BVH2 (0 = not built) */
+/* rtx_wide8.cpp: the 8-wide shadow BVH collapsed from the BVH2 (0 = not built); boxes it takes
+ * from primitive records (leaves of several primitives) in the trees' frame tf, padded by fpad */
 uint32_t rtx_wide8_build(const std::vector<DNode> &inner, uint32_t nnodes, const DPrim *prims, uint32_t root_ref,
-			 const float lo[3], const float hi[3], const std::vector<uint32_t> &skip_objs, QFrame &F,
-			 bool &skipped, std::vector<DW8> &out, std::vector<uint32_t> &leafmap);
+			 const float lo[3], const float hi[3], const std::vector<uint32_t> &skip_objs, const DTreeFrame &tf,
+			 double fpad, QFrame &F, bool &skipped, std::vector<DW8> &out, std::vector<uint32_t> &leafmap);
 /* one frame (or tile shard) into device buffers on stream */
 int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, float *d_rgb, float *d_z, hipStream_t stream);
 

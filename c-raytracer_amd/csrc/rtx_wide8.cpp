@@ -55,6 +55,8 @@ struct Builder {
 	const DPrim *prims;
 	const std::vector<uint32_t> &skip_objs;
 	QFrame F;
+	DTreeFrame tf{};   /* the frame the tree's boxes are in (rtx_device.h DTreeFrame) */
+	double fpad = 0;   /* its transform padding (rtx_frame.cpp) */
 	std::vector<DW8> &out;
 	std::vector<uint32_t> &leafmap;
 	std::vector<TNode> tree;
@@ -68,27 +70,51 @@ struct Builder {
 		return dx * dy + dy * dz + dz * dx;
 	}
 
-	/* a primitive's box from its record, padded like the leaf boxes of rtx_build_scene */
+	/* a primitive's box from its record, in the trees' frame, padded like the leaf boxes of
+	 * rtx_build_scene (twice the relative padding: v0 + e1 is v1 only to float rounding) */
 	void prim_box(uint32_t i, float lo[3], float hi[3]) const
 	{
 		const DPrim &p = prims[i];
 		uint32_t meta;
 		memcpy(&meta, &p.c[3], 4);
-		float l[3], h[3];
+		const bool sph = (meta >> 24) == RTX_SPHERE;
+		double l[3], h[3];
 		for (int a = 0; a < 3; a++) {
-			if ((meta >> 24) == RTX_SPHERE) {
-				l[a] = p.a[a] - p.b[0];
-				h[a] = p.a[a] + p.b[0];
+			if (!tf.rotated) {
+				if (sph) {
+					l[a] = (float)(p.a[a] - p.b[0]);
+					h[a] = (float)(p.a[a] + p.b[0]);
+				} else {
+					const float v1 = p.a[a] + p.b[a], v2 = p.a[a] + p.c[a];
+					l[a] = std::min(p.a[a], std::min(v1, v2));
+					h[a] = std::max(p.a[a], std::max(v1, v2));
+				}
+				continue;
+			}
+			/* x' = R (x - c) of the vertices (or the sphere's centre +- its radius along row a) */
+			auto rot = [&](const float v[3]) {
+				double y = 0;
+				for (int j = 0; j < 3; j++)
+					y += (double)tf.r[a][j] * ((double)v[j] - tf.c[j]);
+				return y;
+			};
+			if (sph) {
+				double rn = 0;
+				for (int j = 0; j < 3; j++)
+					rn += (double)tf.r[a][j] * tf.r[a][j];
+				l[a] = rot(p.a) - p.b[0] * std::sqrt(rn);
+				h[a] = rot(p.a) + p.b[0] * std::sqrt(rn);
 			} else {
-				const float v1 = p.a[a] + p.b[a], v2 = p.a[a] + p.c[a];
-				l[a] = std::min(p.a[a], std::min(v1, v2));
-				h[a] = std::max(p.a[a], std::max(v1, v2));
+				const float v1[3] = { p.a[0] + p.b[0], p.a[1] + p.b[1], p.a[2] + p.b[2] };
+				const float v2[3] = { p.a[0] + p.c[0], p.a[1] + p.c[1], p.a[2] + p.c[2] };
+				l[a] = std::min(rot(p.a), std::min(rot(v1), rot(v2)));
+				h[a] = std::max(rot(p.a), std::max(rot(v1), rot(v2)));
 			}
 		}
-		const float ext = std::max(h[0] - l[0], std::max(h[1] - l[1], h[2] - l[2]));
+		const double ext = std::max(h[0] - l[0], std::max(h[1] - l[1], h[2] - l[2]));
 		for (int a = 0; a < 3; a++) {
-			lo[a] = l[a] - (std::fabs(l[a]) + ext) * 4e-6f - 1e-30f;
-			hi[a] = h[a] + (std::fabs(h[a]) + ext) * 4e-6f + 1e-30f;
+			lo[a] = (float)(l[a] - (std::fabs(l[a]) + ext) * 4e-6 - fpad) - 1e-30f;
+			hi[a] = (float)(h[a] + (std::fabs(h[a]) + ext) * 4e-6 + fpad) + 1e-30f;
 		}
 	}
 
@@ -376,15 +402,15 @@ struct Builder {
  * cannot be built (empty tree, more than 2^24 entries, a leaf of several primitives without
  * host records). */
 uint32_t rtx_wide8_build(const std::vector<DNode> &inner, uint32_t nnodes, const DPrim *prims, uint32_t root_ref,
-			 const float lo[3], const float hi[3], const std::vector<uint32_t> &skip_objs, QFrame &F,
-			 bool &skipped, std::vector<DW8> &out, std::vector<uint32_t> &leafmap)
+			 const float lo[3], const float hi[3], const std::vector<uint32_t> &skip_objs, const DTreeFrame &tf,
+			 double fpad, QFrame &F, bool &skipped, std::vector<DW8> &out, std::vector<uint32_t> &leafmap)
 {
 	out.clear();
 	leafmap.clear();
 	skipped = false;
 	if (root_ref == RTX_EMPTY_REF)
 		return 0;
-	Builder b{ inner, nnodes, prims, skip_objs, QFrame{}, out, leafmap };
+	Builder b{ inner, nnodes, prims, skip_objs, QFrame{}, tf, fpad, out, leafmap };
 	b.tree.reserve(2 * (size_t)nnodes + 2);
 	const int32_t root = b.add(root_ref, lo, hi);
 	if (!b.ok || root < 0) {

@@ -130,3 +130,20 @@ def test_gpu_rotated_trees_cut_traversal(renderer):
     assert sa.shadow_wave_steps < 0.8 * sb.shadow_wave_steps
     assert sa.shadow_leaf_rounds < 0.7 * sb.shadow_leaf_rounds
     assert sa.shadow_tri_tests < sb.shadow_tri_tests
+
+
+@pytest.mark.gpu
+@pytest.mark.usefixtures("_defaults")
+@pytest.mark.parametrize("leaf", [3])
+def test_gpu_rotated_trees_multi_primitive_leaves(renderer, leaf):
+    """BVH2 leaves of several primitives: the 8-wide collapse (on the host then) takes their boxes
+    from the primitive records, in the trees' frame"""
+    scene, frame, params, _ = C.load_config("s6_amb")
+    renderer.set_option(abi.RTX_OPT_BVH_LEAF, leaf)
+    try:
+        a, za, sa = _render(renderer, scene, frame, params, abi.RTX_FRAME_AUTO)
+        b, zb, sb = _render(renderer, scene, frame, params, abi.RTX_FRAME_WORLD)
+    finally:
+        renderer.set_option(abi.RTX_OPT_BVH_LEAF, 1)
+    assert sa.tree_rotated == 1 and sa.shadow_walk == abi.RTX_WALK_W8
+    assert np.array_equal(za, zb) and np.array_equal(a, b)

@@ -228,8 +228,9 @@ int main(int argc, char **argv)
 	std::vector<uint32_t> leafmap;
 	std::vector<uint32_t> emit_objs(sc->emitters, sc->emitters + sc->num_emitters);
 	bool skipped = false;
-	const uint32_t depth = rtx_wide8_build(inner, nnodes, prims.data(), dref(bvh.root_ref), blo, bhi, emit_objs, F, skipped,
-					       w8, leafmap);
+	const DTreeFrame tf{};
+	const uint32_t depth = rtx_wide8_build(inner, nnodes, prims.data(), dref(bvh.root_ref), blo, bhi, emit_objs, tf, 0.0, F,
+					       skipped, w8, leafmap);
 	const auto t2 = std::chrono::steady_clock::now();
 	printf("host SAH build %.1f ms, 8-wide collapse %.1f ms\n", std::chrono::duration<double, std::milli>(t1 - t0).count(),
 	       std::chrono::duration<double, std::milli>(t2 - t1).count());
