@@ -59,9 +59,9 @@ def _defaults(renderer):
     renderer.set_builder(abi.RTX_BUILD_SAH_GPU)
 
 
-def _render(r, scene, frame, params, frame_opt, **opts):
+def _render(r, scene, frame, params, frame_opt, opts=None):
     r.set_option(abi.RTX_OPT_TREE_FRAME, frame_opt)
-    for k, v in opts.items():
+    for k, v in (opts or {}).items():
         r.set_option(k, v)
     r.upload(scene)
     rgb, z = r.render(frame, params)
@@ -97,8 +97,8 @@ def test_gpu_rotated_trees_every_walk(renderer, walks):
     scene, frame, params, _ = C.load_config("s6_path2")
     params.rng = abi.RTX_RNG_COUNTER
     opts = {abi.RTX_OPT_SHADOW_WALK: walks[0], abi.RTX_OPT_TRACE_WALK: walks[1]}
-    a, za, sa = _render(renderer, scene, frame, params, abi.RTX_FRAME_AUTO, **opts)
-    b, zb, sb = _render(renderer, scene, frame, params, abi.RTX_FRAME_WORLD, **opts)
+    a, za, sa = _render(renderer, scene, frame, params, abi.RTX_FRAME_AUTO, opts)
+    b, zb, sb = _render(renderer, scene, frame, params, abi.RTX_FRAME_WORLD, opts)
     assert sa.tree_rotated == 1 and sa.shadow_walk == walks[0] and sa.trace_walk == walks[1]
     assert np.array_equal(za, zb) and np.array_equal(a, b)
     assert (sa.closest_rays, sa.shadow_rays) == (sb.closest_rays, sb.shadow_rays)
