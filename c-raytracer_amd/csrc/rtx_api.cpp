@@ -70,6 +70,24 @@ extern "C" hipError_t rtx_shadow_grid_lanes(uint32_t cus, uint32_t *lanes);
 
 static thread_local char g_err[512] = "";
 
+/* measurement builds (EXTRA=-DRTX_MEASURE=1): host-side phase times of an upload on stderr */
+#if RTX_MEASURE
+struct PhaseClock {
+	std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+	void mark(const char *what, hipStream_t st)
+	{
+		(void)hipStreamSynchronize(st);
+		const auto n = std::chrono::steady_clock::now();
+		fprintf(stderr, "[rtx upload] %-24s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
+		t = n;
+	}
+};
+#define PHASE(clk, what, st) clk.mark(what, st)
+#else
+struct PhaseClock {};
+#define PHASE(clk, what, st) ((void)clk)
+#endif
+
 int rtx_fail(int code, const char *fmt, ...)
 {
 	va_list ap;
@@ -389,6 +407,7 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 			c->bound_lo[a] = std::min(c->bound_lo[a], lo[3 * (size_t)k + a]);
 			c->bound_hi[a] = std::max(c->bound_hi[a], hi[3 * (size_t)k + a]);
 		}
+	PhaseClock clk;
 	const auto tf0 = std::chrono::steady_clock::now();
 	DTreeFrame &tf = hs.tf;
 	hs.frame_ratio = c->opt_frame == RTX_FRAME_AUTO ? rtx_frame_choose(sc, bounded, c->bound_lo, c->bound_hi, tf) : 1.0;
@@ -498,12 +517,14 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 		float *d_lo = nullptr, *d_hi = nullptr;
 		DPrim *d_in = nullptr;
 		DNode *recs = nullptr;
+		PHASE(clk, "frame + boxes + records", c->stream);
 		if ((rc = upload(d_lo, lo)) || (rc = upload(d_hi, hi)) || (rc = upload(d_in, prims_in))) {
 			dfree(d_lo);
 			dfree(d_hi);
 			dfree(d_in);
 			return rc;
 		}
+		PHASE(clk, "upload boxes + records", c->stream);
 		uint32_t rounds = 0;
 		hipError_t e = c->builder == RTX_BUILD_PLOC_GPU
 				       ? rtx_ploc_build(nb, d_lo, d_hi, d_in, tlo, thi, cfg.max_leaf, &recs, &nnodes,
@@ -518,6 +539,7 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 		dfree(d_in);
 		if (e != hipSuccess)
 			return fail(RTX_ERR_HIP, "GPU BVH build failed: %s", hipGetErrorString(e));
+		PHASE(clk, "device BVH2 build", c->stream);
 		c->d_nodes = recs;
 		hs.recs_on_device = true;
 		if (root_ref == RTX_EMPTY_REF) /* nb <= max_leaf: a single leaf */
@@ -539,6 +561,7 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 			dfree(d_skip);
 			if (e != hipSuccess)
 				return fail(RTX_ERR_HIP, "8-wide BVH collapse on the device failed: %s", hipGetErrorString(e));
+			PHASE(clk, "device 8-wide collapse", c->stream);
 			if (dep) {
 				hs.w8_on_device = true;
 				hs.w8depth = dep;
@@ -578,6 +601,7 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 				return fail(RTX_ERR_HIP, "emitter record lookup failed: %s", hipGetErrorString(e));
 			for (size_t i = 0; i < emit.size(); i++)
 				emit[i].prim = at[i];
+			PHASE(clk, "emitter records", c->stream);
 		}
 	} else {
 		BvhOutput bvh;
@@ -667,6 +691,7 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 			return fail(RTX_ERR_SCENE, "scene too large: %zu threaded BVH nodes (max 2^26)", hs.qnodes.size());
 		hs.ntop = thread_top(hs.qnodes, qdepth, hs.qtop);
 	}
+	PHASE(clk, "host trees", c->stream);
 	hs.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count();
 	hs.mats = std::move(mats);
 	hs.planes = std::move(planes);
@@ -688,6 +713,7 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 int rtx_upload_built(rtx_ctx *c, HostScene &hs)
 {
 	int rc;
+	PhaseClock clk;
 	/* a failure below leaves the context without a scene (RTX_ERR_STATE on render), never with a
 	 * mix of old and new buffers */
 	c->have_scene = false;
@@ -728,6 +754,7 @@ int rtx_upload_built(rtx_ctx *c, HostScene &hs)
 			return fail(RTX_ERR_HIP, "8-wide BVH scalar copies failed: %s", hipGetErrorString(e));
 		}
 	}
+	PHASE(clk, "upload host parts", c->stream);
 	if (have_w8) { /* the 8-wide tree's leaf entries: copies of their primitive records */
 		hipError_t e = rtx_launch_w8_fill((const DPrim *)(c->d_nodes + hs.nnodes), c->d_mats, d_map, num_w8, c->d_w8, c->stream);
 		if (e == hipSuccess)
@@ -737,6 +764,7 @@ int rtx_upload_built(rtx_ctx *c, HostScene &hs)
 			return fail(RTX_ERR_HIP, "8-wide BVH leaf fill failed: %s", hipGetErrorString(e));
 	}
 	dfree(d_map);
+	PHASE(clk, "8-wide leaf fill", c->stream);
 	memcpy(c->bound_lo, hs.bound_lo, 12);
 	memcpy(c->bound_hi, hs.bound_hi, 12);
 	DScene &S = c->scene;
