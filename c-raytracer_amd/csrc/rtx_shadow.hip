@@ -135,8 +135,8 @@ struct ShadowCount {
 	u64 pln;       /* plane tests */
 	u64 steps;     /* walk-loop iterations of the waves (a wave runs until its longest ray ends) */
 	u64 walks;     /* wave walks (64 rays each) */
-	u64 lrounds;   /* 4-wide walk: wave iterations of the leaf loop */
-	u64 unif;      /* 4-wide walk: wave steps with one node for all active lanes */
+	u64 lrounds;   /* 8-wide walk: wave iterations of the leaf loops (immediate and deferred) */
+	u64 unif;      /* 8-wide walk: wave steps with one node for all walking lanes (scalar path) */
 };
 
 /* one primitive record (a, b, c = its first 48 bytes) against this lane's shadow ray

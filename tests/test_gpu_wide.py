@@ -86,7 +86,7 @@ def test_gpu_walks_agree(renderer, name):
 def test_gpu_w8_lane_stack_spill(renderer, name):
     """Trees deeper than the LDS lane stack walk on with the deeper entries in HBM: with one LDS
     entry every wide node below the second level spills (the path the depth-cliff fallback of
-    the 4-wide walk never had); the frame is bit-identical to the all-LDS walk and matches the
+    the round-2 4-wide walk never had); the frame is bit-identical to the all-LDS walk and matches the
     reference."""
     scene, frame, params, _ = C.load_config(name)
     params.rng = abi.RTX_RNG_COUNTER
