@@ -336,7 +336,9 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 	if (sc->num_emitters && !sc->emitters)
 		return fail(RTX_ERR_ARG, "emitters pointer is null");
 	HIP_TRY(hipSetDevice(c->device));
+	PhaseClock clk0;
 	free_scene(c);
+	PHASE(clk0, "free the old scene", c->stream);
 	hs.builder = c->builder;
 
 	if (sc->num_materials > RTX_META_MAT)
@@ -396,17 +398,9 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 	 * shade-point sort's frame), then in the trees' frame (rtx_frame.cpp) for the builders */
 	const uint32_t nb = (uint32_t)bounded.size();
 	std::vector<float> lo(3 * (size_t)nb), hi(3 * (size_t)nb);
-	for (uint32_t k = 0; k < nb; k++)
-		rtx_world_box(sc->objects[bounded[k]], &lo[3 * (size_t)k], &hi[3 * (size_t)k]);
-	for (int a = 0; a < 3; a++) {
-		c->bound_lo[a] = FLT_MAX;
-		c->bound_hi[a] = -FLT_MAX;
-	}
-	for (uint32_t k = 0; k < nb; k++)
-		for (int a = 0; a < 3; a++) {
-			c->bound_lo[a] = std::min(c->bound_lo[a], lo[3 * (size_t)k + a]);
-			c->bound_hi[a] = std::max(c->bound_hi[a], hi[3 * (size_t)k + a]);
-		}
+	PHASE(clk0, "materials + planes", c->stream);
+	rtx_world_boxes(sc, bounded, lo.data(), hi.data(), c->bound_lo, c->bound_hi);
+	PHASE(clk0, "world boxes", c->stream);
 	PhaseClock clk;
 	const auto tf0 = std::chrono::steady_clock::now();
 	DTreeFrame &tf = hs.tf;
@@ -418,18 +412,7 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 	memcpy(thi, c->bound_hi, 12);
 	if (tf.rotated) {
 		const double pad = hs.frame_pad = rtx_frame_pad(rtx_frame_radius(sc, bounded, tf));
-		for (int a = 0; a < 3; a++) {
-			tlo[a] = FLT_MAX;
-			thi[a] = -FLT_MAX;
-		}
-		for (uint32_t k = 0; k < nb; k++) {
-			float *l = &lo[3 * (size_t)k], *h = &hi[3 * (size_t)k];
-			rtx_frame_box(sc->objects[bounded[k]], tf, pad, l, h);
-			for (int a = 0; a < 3; a++) {
-				tlo[a] = std::min(tlo[a], l[a]);
-				thi[a] = std::max(thi[a], h[a]);
-			}
-		}
+		rtx_frame_boxes(sc, bounded, tf, pad, lo.data(), hi.data(), tlo, thi);
 	}
 	hs.frame_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf0).count();
 	BvhConfig cfg;
@@ -508,17 +491,19 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 	if ((c->builder == RTX_BUILD_LBVH_GPU || c->builder == RTX_BUILD_PLOC_GPU || c->builder == RTX_BUILD_SAH_GPU) && nb) {
 		/* GPU builders (rtx_build.hip): primitives uploaded in input order, records emitted on the device */
 		std::vector<DPrim> prims_in(nb);
+		rtx_host_parallel(nb, [&](size_t b, size_t e, unsigned) {
+			for (size_t k = b; k < e; k++)
+				prims_in[k] = make_prim(bounded[k]);
+		});
 		uint32_t sph = 0;
-		for (uint32_t k = 0; k < nb; k++) {
-			prims_in[k] = make_prim(bounded[k]);
-			if (is_sphere(prims_in[k]))
+		for (uint32_t k = 0; k < nb && !sph; k++)
+			if (sc->objects[bounded[k]].type == RTX_SPHERE)
 				sph = RTX_REF_SPH;
-		}
 		float *d_lo = nullptr, *d_hi = nullptr;
 		DPrim *d_in = nullptr;
 		DNode *recs = nullptr;
 		PHASE(clk, "frame + boxes + records", c->stream);
-		if ((rc = upload(d_lo, lo)) || (rc = upload(d_hi, hi)) || (rc = upload(d_in, prims_in))) {
+		if ((rc = upload(d_lo, lo, c->stream)) || (rc = upload(d_hi, hi, c->stream)) || (rc = upload(d_in, prims_in, c->stream))) {
 			dfree(d_lo);
 			dfree(d_hi);
 			dfree(d_in);
@@ -553,7 +538,7 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 			for (uint32_t i = 0; i < sc->num_emitters; i++)
 				skip[sc->emitters[i] >> 5] |= 1u << (sc->emitters[i] & 31u);
 			uint32_t *d_skip = nullptr;
-			if ((rc = upload(d_skip, skip)))
+			if ((rc = upload(d_skip, skip, c->stream)))
 				return rc;
 			uint32_t ent = 0, dep = 0, wide = 0;
 			e = rtx_w8_collapse_device(recs, nnodes, nb, d_skip, sc->num_objects, &hs.dev_w8, &hs.dev_w8s, &hs.dev_w8leaf, &ent,
@@ -586,7 +571,7 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 			for (size_t i = 0; i < emit.size(); i++)
 				objs[i] = emit[i].obj;
 			uint32_t *d_objs = nullptr, *d_at = nullptr;
-			if ((rc = upload(d_objs, objs)) || (rc = upload(d_at, at))) {
+			if ((rc = upload(d_objs, objs, c->stream)) || (rc = upload(d_at, at, c->stream))) {
 				dfree(d_objs);
 				return rc;
 			}
@@ -720,11 +705,18 @@ int rtx_upload_built(rtx_ctx *c, HostScene &hs)
 	c->sp_tile_seen = 0.0; /* the next render sizes its chunks from the static bound */
 	c->sp_tile_key = SpKey{};
 	HIP_TRY(hipSetDevice(c->device));
-	if (!(hs.recs_on_device && c->d_nodes) && (rc = upload(c->d_nodes, hs.recs)))
+	if (!(hs.recs_on_device && c->d_nodes) && (rc = upload(c->d_nodes, hs.recs, c->stream)))
 		return rc;
-	if ((rc = upload(c->d_qnodes, hs.qnodes)) || (rc = upload(c->d_top, hs.qtop)) || (rc = upload(c->d_planes, hs.planes)) ||
-	    (rc = upload(c->d_mats, hs.mats)) || (rc = upload(c->d_emitters, hs.emit)) || (rc = upload(c->d_lin, hs.lin)))
+	PHASE(clk, "upload: set device", c->stream);
+	if ((rc = upload(c->d_qnodes, hs.qnodes, c->stream)) || (rc = upload(c->d_top, hs.qtop, c->stream)))
 		return rc;
+	PHASE(clk, "upload threaded BVH2", c->stream);
+	if ((rc = upload(c->d_planes, hs.planes, c->stream)))
+		return rc;
+	PHASE(clk, "upload planes", c->stream);
+	if ((rc = upload(c->d_mats, hs.mats, c->stream)) || (rc = upload(c->d_emitters, hs.emit, c->stream)) || (rc = upload(c->d_lin, hs.lin, c->stream)))
+		return rc;
+	PHASE(clk, "upload scene tables", c->stream);
 	const bool have_w8 = hs.w8_on_device || !hs.w8.empty();
 	const uint32_t num_w8 = hs.w8_on_device ? hs.w8_entries : (uint32_t)hs.w8.size();
 	uint32_t *d_map = nullptr; /* entry -> primitive index of the 8-wide tree's leaf entries */
@@ -739,10 +731,11 @@ int rtx_upload_built(rtx_ctx *c, HostScene &hs)
 		hs.dev_w8 = nullptr;
 		hs.dev_w8s = nullptr;
 		hs.dev_w8leaf = nullptr;
+		PHASE(clk, "8-wide tree handover", c->stream);
 	} else {
-		if ((rc = upload(c->d_w8, hs.w8)))
+		if ((rc = upload(c->d_w8, hs.w8, c->stream)))
 			return rc;
-		if ((rc = upload(d_map, hs.w8leaf)))
+		if ((rc = upload(d_map, hs.w8leaf, c->stream)))
 			return rc;
 		dfree(c->d_w8s);
 		/* the scalar-path node copies (rtx_device.h DW8S) */

@@ -774,14 +774,46 @@ __global__ __launch_bounds__(SB_T) void k_sb_reset(uint32_t M, uint32_t nb, uint
 	acc[i] = v;
 }
 
-/* node boxes and centroid bounds.  A wave whose positions all lie in one node reduces first. */
+/* the batch's node of position q (RTX_NONE: a leaf, or another batch's node) */
+__device__ __forceinline__ uint32_t sb_node(uint32_t q, uint32_t n, uint32_t s0b, uint32_t sn, const uint32_t *__restrict__ seg)
+{
+	const uint32_t s = q < n ? seg[q] : RTX_NONE;
+	return (s != RTX_NONE && s - s0b < sn) ? s - s0b : RTX_NONE;
+}
+
+/* the least and greatest batch node of the workgroup's positions (a node's positions are one
+ * contiguous range, so every position between two of one node's is that node's); lo = RTX_NONE:
+ * none */
+__device__ __forceinline__ void sb_span(uint32_t s, uint32_t *sh, uint32_t &lo, uint32_t &hi)
+{
+	if (threadIdx.x == 0) {
+		sh[0] = RTX_NONE;
+		sh[1] = 0u;
+	}
+	__syncthreads();
+	if (s != RTX_NONE) {
+		atomicMin(&sh[0], s);
+		atomicMax(&sh[1], s);
+	}
+	__syncthreads();
+	lo = sh[0];
+	hi = sh[1];
+}
+
+/* node boxes and centroid bounds.  A wave whose positions all lie in one node reduces first; a
+ * workgroup whose positions all lie in one node reduces its waves in LDS and sends one set of
+ * atomics (the top levels: every workgroup's positions in the root, or one of a few nodes). */
 __global__ __launch_bounds__(SB_T) void k_sb_bounds(uint32_t n, uint32_t nb, uint32_t s0b, uint32_t sn,
 						     const uint32_t *__restrict__ seg, const uint32_t *__restrict__ pidx,
 						     const float *__restrict__ lo, const float *__restrict__ hi, uint32_t *__restrict__ acc)
 {
+	__shared__ uint32_t span[2], red[12];
 	const uint32_t q = blockIdx.x * SB_T + threadIdx.x;
-	uint32_t s = q < n ? seg[q] : RTX_NONE;
-	s = (s != RTX_NONE && s - s0b < sn) ? s - s0b : RTX_NONE; /* this batch's nodes only */
+	const uint32_t s = sb_node(q, n, s0b, sn, seg);
+	uint32_t smin, smax;
+	sb_span(s, span, smin, smax);
+	if (smin == RTX_NONE)
+		return;
 	float v[12];
 	if (s != RTX_NONE) {
 		const uint32_t p = pidx[q];
@@ -795,6 +827,26 @@ __global__ __launch_bounds__(SB_T) void k_sb_bounds(uint32_t n, uint32_t nb, uin
 			v[a] = v[6 + a] = FLT_MAX;
 			v[3 + a] = v[9 + a] = -FLT_MAX;
 		}
+	}
+	if (smin == smax) { /* one node: waves reduce, then the workgroup in LDS */
+		if (threadIdx.x < 12)
+			red[threadIdx.x] = (threadIdx.x % 6) < 3 ? f2o(FLT_MAX) : f2o(-FLT_MAX);
+		for (int k = 0; k < 12; k++)
+			for (int m = 32; m > 0; m >>= 1) {
+				const float o = __shfl_xor(v[k], m);
+				v[k] = ((k % 6) < 3) ? fminf(v[k], o) : fmaxf(v[k], o);
+			}
+		__syncthreads();
+		if ((threadIdx.x & 63u) == 0)
+			for (int k = 0; k < 12; k++)
+				((k % 6) < 3) ? atomicMin(&red[k], f2o(v[k])) : atomicMax(&red[k], f2o(v[k]));
+		__syncthreads();
+		if (threadIdx.x < 12) {
+			uint32_t *A = acc + (size_t)smin * SB_ACC(nb);
+			const int k = (int)threadIdx.x;
+			((k % 6) < 3) ? atomicMin(&A[k], red[k]) : atomicMax(&A[k], red[k]);
+		}
+		return;
 	}
 	const uint32_t s0 = __shfl(s, 0);
 	if (__all(s == s0)) {
@@ -826,36 +878,75 @@ __device__ __forceinline__ int sb_bin(float c, float clo, float k, int nb)
 	return min(max(bi, 0), nb - 1);
 }
 
+/* the bins of a position's centroid, per axis: 6 bounds and a count.  A workgroup whose
+ * positions lie in at most SB_LK nodes accumulates in LDS first and sends one atomic per bin
+ * word it touched (the top levels: thousands of positions per bin word, which serialised on the
+ * L2 atomics); otherwise every position sends its own.  Min / max of order-preserving encodings
+ * and integer counts: the same result in any order. */
+#define SB_LK 2
+__device__ __forceinline__ uint32_t sb_ident(uint32_t k) /* bin word k's identity (k < 7 * 3 * nb) */
+{
+	const uint32_t j = k % 7;
+	return j == 6 ? 0u : j < 3 ? f2o(FLT_MAX) : f2o(-FLT_MAX);
+}
 __global__ __launch_bounds__(SB_T) void k_sb_bins(uint32_t n, uint32_t nb, uint32_t s0b, uint32_t sn,
 						   const uint32_t *__restrict__ seg, const uint32_t *__restrict__ pidx,
 						   const float *__restrict__ lo, const float *__restrict__ hi, uint32_t *__restrict__ acc)
 {
+	__shared__ uint32_t span[2];
+	__shared__ uint32_t L[SB_LK][3 * SB_NBMAX * 7];
 	const uint32_t q = blockIdx.x * SB_T + threadIdx.x;
-	if (q >= n)
+	const uint32_t s = sb_node(q, n, s0b, sn, seg);
+	uint32_t smin, smax;
+	sb_span(s, span, smin, smax);
+	if (smin == RTX_NONE)
 		return;
-	uint32_t s = seg[q];
-	if (s == RTX_NONE || s - s0b >= sn)
-		return;
-	s -= s0b;
-	uint32_t *A = acc + (size_t)s * SB_ACC(nb);
-	const uint32_t p = pidx[q];
-	float b[6];
-	for (int a = 0; a < 3; a++) {
-		b[a] = lo[3 * (size_t)p + a];
-		b[3 + a] = hi[3 * (size_t)p + a];
+	const bool local = smax - smin < SB_LK;
+	const uint32_t nw = 3 * nb * 7; /* bin words per node */
+	if (local) {
+		for (uint32_t i = threadIdx.x; i < SB_LK * nw; i += SB_T)
+			L[i / nw][i % nw] = sb_ident(i % nw);
+		__syncthreads();
 	}
-	for (int ax = 0; ax < 3; ax++) {
-		const float clo = o2f(A[6 + ax]), chi = o2f(A[9 + ax]), ext = chi - clo;
-		if (!(ext > 0.f))
-			continue;
-		const float k = (float)nb * (1.f - 1e-6f) / ext;
-		const int bi = sb_bin(0.5f * (b[ax] + b[3 + ax]), clo, k, (int)nb);
-		uint32_t *B = A + 12 + ((size_t)ax * nb + bi) * 7;
+	if (s != RTX_NONE) {
+		const uint32_t *A = acc + (size_t)s * SB_ACC(nb);
+		uint32_t *D = local ? L[s - smin] : acc + (size_t)s * SB_ACC(nb) + 12;
+		const uint32_t p = pidx[q];
+		float b[6];
 		for (int a = 0; a < 3; a++) {
-			atomicMin(&B[a], f2o(b[a]));
-			atomicMax(&B[3 + a], f2o(b[3 + a]));
+			b[a] = lo[3 * (size_t)p + a];
+			b[3 + a] = hi[3 * (size_t)p + a];
 		}
-		atomicAdd(&B[6], 1u);
+		for (int ax = 0; ax < 3; ax++) {
+			const float clo = o2f(A[6 + ax]), chi = o2f(A[9 + ax]), ext = chi - clo;
+			if (!(ext > 0.f))
+				continue;
+			const float k = (float)nb * (1.f - 1e-6f) / ext;
+			const int bi = sb_bin(0.5f * (b[ax] + b[3 + ax]), clo, k, (int)nb);
+			uint32_t *B = D + ((size_t)ax * nb + bi) * 7;
+			for (int a = 0; a < 3; a++) {
+				atomicMin(&B[a], f2o(b[a]));
+				atomicMax(&B[3 + a], f2o(b[3 + a]));
+			}
+			atomicAdd(&B[6], 1u);
+		}
+	}
+	if (!local)
+		return;
+	__syncthreads();
+	const uint32_t nl = smax - smin + 1;
+	for (uint32_t i = threadIdx.x; i < nl * nw; i += SB_T) {
+		const uint32_t w = i % nw, v = L[i / nw][w];
+		if (v == sb_ident(w))
+			continue;
+		uint32_t *G = acc + (size_t)(smin + i / nw) * SB_ACC(nb) + 12 + w;
+		const uint32_t j = w % 7;
+		if (j == 6)
+			atomicAdd(G, v);
+		else if (j < 3)
+			atomicMin(G, v);
+		else
+			atomicMax(G, v);
 	}
 }
 

@@ -28,9 +28,12 @@
  */
 #include <float.h>
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <functional>
+#include <thread>
 #include <vector>
 
 #include "rtx_frame.h"
@@ -40,6 +43,63 @@
 #define RTX_FRAME_CANDS 16     /* largest sampled triangles whose frames are tried */
 #define RTX_FRAME_GAIN 0.75    /* a rotated frame must cost at most this fraction of the identity's */
 
+/* host threads for the per-object loops: RTX_HOST_THREADS, else OMP_NUM_THREADS, else at most 16
+ * (plain threads, not an OpenMP runtime: its first start-up cost ~0.3 s on a GPU box's host) */
+static unsigned host_threads()
+{
+	for (const char *k : { "RTX_HOST_THREADS", "OMP_NUM_THREADS" })
+		if (const char *v = getenv(k))
+			if (atoi(v) > 0)
+				return (unsigned)std::min(atoi(v), 256);
+	return std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+}
+
+/* f(begin, end, chunk) over [0, n) in contiguous chunks, one per thread (serially below 32K) */
+template <class F> static unsigned parallel_chunks(size_t n, F f)
+{
+	const unsigned t = n < 32768 ? 1u : (unsigned)std::min<size_t>(host_threads(), (n + 16383) / 16384);
+	if (t <= 1) {
+		f((size_t)0, n, 0u);
+		return 1;
+	}
+	std::vector<std::thread> th;
+	for (unsigned k = 1; k < t; k++)
+		th.emplace_back(f, n * k / t, n * (k + 1) / t, k);
+	f((size_t)0, n / t, 0u);
+	for (auto &x : th)
+		x.join();
+	return t;
+}
+
+unsigned rtx_host_parallel(size_t n, const std::function<void(size_t, size_t, unsigned)> &f) { return parallel_chunks(n, f); }
+
+/* per-object boxes lo / hi (3 floats each) by box(k, l, h) and their union blo / bhi */
+template <class B> static void boxes_and_union(size_t nb, float *lo, float *hi, float blo[3], float bhi[3], B box)
+{
+	std::vector<float> part(6 * 256);
+	const unsigned t = parallel_chunks(nb, [&](size_t b, size_t e, unsigned c) {
+		float P[6] = { FLT_MAX, FLT_MAX, FLT_MAX, -FLT_MAX, -FLT_MAX, -FLT_MAX }; /* the chunk's union, written once */
+		for (size_t k = b; k < e; k++) {
+			float *l = lo + 3 * k, *h = hi + 3 * k;
+			box(k, l, h);
+			for (int a = 0; a < 3; a++) {
+				P[a] = std::min(P[a], l[a]);
+				P[3 + a] = std::max(P[3 + a], h[a]);
+			}
+		}
+		std::copy(P, P + 6, &part[6 * (size_t)c]);
+	});
+	for (int a = 0; a < 3; a++) {
+		blo[a] = FLT_MAX;
+		bhi[a] = -FLT_MAX;
+	}
+	for (unsigned c = 0; c < t; c++)
+		for (int a = 0; a < 3; a++) {
+			blo[a] = std::min(blo[a], part[6 * (size_t)c + a]);
+			bhi[a] = std::max(bhi[a], part[6 * (size_t)c + 3 + a]);
+		}
+}
+
 static double half_area(const double lo[3], const double hi[3])
 {
 	const double x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
@@ -47,7 +107,7 @@ static double half_area(const double lo[3], const double hi[3])
 }
 
 /* sum of the sampled triangles' box half-areas in the frame with rows r */
-static double frame_cost(const rtx_scene_desc *sc, const std::vector<uint32_t> &tris, const double r[3][3])
+static double frame_cost(const rtx_scene_desc *sc, const std::vector<uint32_t> &tris, const double (*r)[3])
 {
 	double cost = 0;
 	for (uint32_t oi : tris) {
@@ -138,24 +198,40 @@ double rtx_frame_choose(const rtx_scene_desc *sc, const std::vector<uint32_t> &b
 		by_area.push_back({ -(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]), oi });
 	}
 	std::sort(by_area.begin(), by_area.end());
-	const double id[3][3] = { { 1, 0, 0 }, { 0, 1, 0 }, { 0, 0, 1 } };
-	const double c_id = frame_cost(sc, sample, id);
-	double c_best = c_id, r_best[3][3];
-	memcpy(r_best, id, sizeof(id));
-	for (size_t k = 0; k < by_area.size() && k < RTX_FRAME_CANDS; k++) {
+	/* frame 0 the identity, frame k the k-th largest sampled triangle's (as the device holds it:
+	 * float rows); each frame's cost summed by one thread in sample order (deterministic) */
+	const size_t nc = std::min<size_t>(by_area.size(), RTX_FRAME_CANDS) + 1;
+	std::vector<double> rs(9 * nc, 0.0), cost(nc, -1.0);
+	for (int i = 0; i < 3; i++)
+		rs[4 * i] = 1.0;
+	for (size_t k = 1; k < nc; k++) {
 		double r[3][3];
-		if (!tri_frame(sc->objects[by_area[k].second], r))
+		if (!tri_frame(sc->objects[by_area[k - 1].second], r))
 			continue;
-		/* the frame as the device holds it (float rows) */
 		for (int i = 0; i < 3; i++)
 			for (int j = 0; j < 3; j++)
-				r[i][j] = (double)(float)r[i][j];
-		const double cost = frame_cost(sc, sample, r);
-		if (cost < c_best) {
-			c_best = cost;
-			memcpy(r_best, r, sizeof(r));
-		}
+				rs[9 * k + 3 * i + j] = (double)(float)r[i][j];
+		cost[k] = 0.0;
 	}
+	cost[0] = 0.0;
+	{
+		std::vector<std::thread> th;
+		for (size_t k = 0; k < nc; k++)
+			if (cost[k] == 0.0)
+				th.emplace_back([&, k] { cost[k] = frame_cost(sc, sample, (const double(*)[3]) & rs[9 * k]); });
+		for (auto &x : th)
+			x.join();
+	}
+	const double c_id = cost[0];
+	double c_best = c_id;
+	size_t best = 0;
+	for (size_t k = 1; k < nc; k++)
+		if (cost[k] >= 0.0 && cost[k] < c_best) {
+			c_best = cost[k];
+			best = k;
+		}
+	double r_best[3][3];
+	memcpy(r_best, &rs[9 * best], sizeof(r_best));
 	if (!(c_id > 0) || !(c_best <= RTX_FRAME_GAIN * c_id))
 		return 1.0;
 	for (int i = 0; i < 3; i++) {
@@ -167,34 +243,48 @@ double rtx_frame_choose(const rtx_scene_desc *sc, const std::vector<uint32_t> &b
 	return c_best / c_id;
 }
 
-/* the largest float <= x / >= x */
+/* the float next to f towards -inf / +inf (nextafterf by its bits; f not a NaN) */
+static float next_down(float f)
+{
+	if (f == 0.f)
+		return -FLT_TRUE_MIN;
+	uint32_t b;
+	memcpy(&b, &f, 4);
+	if (b == 0xFF800000u) /* -inf */
+		return f;
+	b = f > 0.f ? b - 1 : b + 1;
+	memcpy(&f, &b, 4);
+	return f;
+}
+static float next_up(float f) { return -next_down(-f); }
+/* the largest float <= x / least float >= x */
 static float down(double x)
 {
-	float f = (float)x;
-	if ((double)f > x)
-		f = nextafterf(f, -FLT_MAX);
-	return f;
+	const float f = (float)x;
+	return (double)f > x ? next_down(f) : f;
 }
 static float up(double x)
 {
-	float f = (float)x;
-	if ((double)f < x)
-		f = nextafterf(f, FLT_MAX);
-	return f;
+	const float f = (float)x;
+	return (double)f < x ? next_up(f) : f;
 }
 
 double rtx_frame_radius(const rtx_scene_desc *sc, const std::vector<uint32_t> &bounded, const DTreeFrame &F)
 {
-	double rad = 0;
-	for (uint32_t oi : bounded) {
-		const rtx_object &o = sc->objects[oi];
-		const int n = o.type == RTX_SPHERE ? 1 : 3;
-		const float *p[3] = { o.p0, o.p1, o.p2 };
-		for (int k = 0; k < n; k++)
-			for (int i = 0; i < 3; i++)
-				rad = std::max(rad, fabs((double)p[k][i] - F.c[i]) + (o.type == RTX_SPHERE ? (double)o.radius : 0.0));
-	}
-	return rad;
+	std::vector<double> part(256, 0.0);
+	const unsigned t = parallel_chunks(bounded.size(), [&](size_t b, size_t e, unsigned c) {
+		double rad = 0;
+		for (size_t q = b; q < e; q++) {
+			const rtx_object &o = sc->objects[bounded[q]];
+			const int n = o.type == RTX_SPHERE ? 1 : 3;
+			const float *p[3] = { o.p0, o.p1, o.p2 };
+			for (int k = 0; k < n; k++)
+				for (int i = 0; i < 3; i++)
+					rad = std::max(rad, fabs((double)p[k][i] - F.c[i]) + (o.type == RTX_SPHERE ? (double)o.radius : 0.0));
+		}
+		part[c] = rad;
+	});
+	return *std::max_element(part.begin(), part.begin() + t);
 }
 
 void rtx_frame_box(const rtx_object &o, const DTreeFrame &F, double pad, float lo[3], float hi[3])
@@ -234,6 +324,13 @@ void rtx_frame_box(const rtx_object &o, const DTreeFrame &F, double pad, float l
 
 double rtx_frame_pad(double radius) { return RTX_FRAME_PAD * radius; }
 
+void rtx_frame_boxes(const rtx_scene_desc *sc, const std::vector<uint32_t> &bounded, const DTreeFrame &F, double pad,
+		     float *lo, float *hi, float blo[3], float bhi[3])
+{
+	boxes_and_union(bounded.size(), lo, hi, blo, bhi,
+			[&](size_t k, float *l, float *h) { rtx_frame_box(sc->objects[bounded[k]], F, pad, l, h); });
+}
+
 void rtx_world_box(const rtx_object &o, float lo[3], float hi[3])
 {
 	float l[3], h[3];
@@ -252,6 +349,12 @@ void rtx_world_box(const rtx_object &o, float lo[3], float hi[3])
 		lo[a] = l[a] - (std::fabs(l[a]) + ext) * 2e-6f - 1e-30f;
 		hi[a] = h[a] + (std::fabs(h[a]) + ext) * 2e-6f + 1e-30f;
 	}
+}
+
+void rtx_world_boxes(const rtx_scene_desc *sc, const std::vector<uint32_t> &bounded, float *lo, float *hi, float blo[3],
+		     float bhi[3])
+{
+	boxes_and_union(bounded.size(), lo, hi, blo, bhi, [&](size_t k, float *l, float *h) { rtx_world_box(sc->objects[bounded[k]], l, h); });
 }
 
 extern "C" int rtx_tree_frame(const rtx_scene_desc *sc, int *rotated, float rot[9], float center[3], double *cost_ratio)

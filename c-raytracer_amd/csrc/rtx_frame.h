@@ -5,6 +5,7 @@
 #ifndef RTX_FRAME_H
 #define RTX_FRAME_H
 
+#include <functional>
 #include <vector>
 
 #include "rtx.h"
@@ -12,6 +13,9 @@
 
 int rtx_fail(int code, const char *fmt, ...);
 
+/* f(begin, end, chunk) over [0, n) in contiguous chunks on host threads (RTX_HOST_THREADS, else
+ * OMP_NUM_THREADS, else at most 16; serially below 32K); returns the chunk count */
+unsigned rtx_host_parallel(size_t n, const std::function<void(size_t, size_t, unsigned)> &f);
 /* object o's world box (sphere_get_corners / triangle_get_corners, object.c:277-282, 375-388),
  * padded for the walks' FMA slab test */
 void rtx_world_box(const rtx_object &o, float lo[3], float hi[3]);
@@ -26,5 +30,12 @@ double rtx_frame_pad(double radius);
 /* object o's box in frame F (F.rotated), rounded outward and padded by pad plus the relative
  * padding of rtx_world_box */
 void rtx_frame_box(const rtx_object &o, const DTreeFrame &F, double pad, float lo[3], float hi[3]);
+/* rtx_frame_box of every object in `bounded` (lo / hi: 3 floats each), and their union blo / bhi
+ * (host threads; the boxes do not depend on the thread count) */
+void rtx_frame_boxes(const rtx_scene_desc *sc, const std::vector<uint32_t> &bounded, const DTreeFrame &F, double pad,
+		     float *lo, float *hi, float blo[3], float bhi[3]);
+/* rtx_world_box of every object in `bounded`, and their union */
+void rtx_world_boxes(const rtx_scene_desc *sc, const std::vector<uint32_t> &bounded, float *lo, float *hi, float blo[3],
+		     float bhi[3]);
 
 #endif

@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <vector>
 
 #include "rtx.h"
@@ -32,13 +34,29 @@ template <class T> static inline void dfree(T *&p)
 	p = nullptr;
 }
 
-template <class T> static inline int upload(T *&dst, const std::vector<T> &v)
+/* a host vector into a fresh device buffer, copied on `stream` (the context's own: no
+ * synchronisation with the null stream) and complete on return */
+template <class T> static inline int upload(T *&dst, const std::vector<T> &v, hipStream_t stream)
 {
+#if RTX_MEASURE
+	const auto t0 = std::chrono::steady_clock::now();
+#endif
 	dfree(dst);
 	size_t n = std::max<size_t>(v.size(), 1);
 	HIP_TRY(hipMalloc(&dst, n * sizeof(T)));
-	if (!v.empty())
-		HIP_TRY(hipMemcpy(dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+#if RTX_MEASURE
+	const auto t1 = std::chrono::steady_clock::now();
+#endif
+	if (!v.empty()) {
+		HIP_TRY(hipMemcpyAsync(dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, stream));
+		HIP_TRY(hipStreamSynchronize(stream));
+	}
+#if RTX_MEASURE
+	const auto t2 = std::chrono::steady_clock::now();
+	const double a = std::chrono::duration<double, std::milli>(t1 - t0).count(), b = std::chrono::duration<double, std::milli>(t2 - t1).count();
+	if (a + b > 1.0)
+		fprintf(stderr, "[rtx upload]   upload of %zu B: free + malloc %.2f ms, copy %.2f ms\n", v.size() * sizeof(T), a, b);
+#endif
 	return RTX_OK;
 }
 

@@ -679,15 +679,43 @@ __device__ __forceinline__ f3 shade_light(const KShadow &ks, const float4 *rec, 
 		li = mul3s(li, sh_rcp(ks.att_offset + ldist));
 	else if (att == RTX_ATT_SQR)
 		li = mul3s(li, sh_rcp(ks.att_offset + dsq));
-	const DMaterial &m = unip(ks.mats)[__float_as_uint(q3.w)];
+	f3 ks3;
+	float shin;
+	if (UNI) { /* the material of a wave-uniform record: scalar reads */
+		const auto &m = cptr(unip(ks.mats))[__float_as_uint(q3.w)];
+		ks3 = mk3(m.ks[0], m.ks[1], m.ks[2]);
+		shin = m.shininess;
+	} else {
+		const DMaterial &m = unip(ks.mats)[__float_as_uint(q3.w)];
+		ks3 = ld3(m.ks);
+		shin = m.shininess;
+	}
 	const f3 diff = mul3s(mul3v(mk3(q3.x, q3.y, q3.z), li), fmaxf(0.f, a));
 	float sm;
 	if ((int32_t)uni((uint32_t)ks.reflection) == RTX_BLINN)
 		sm = -dot3(n, norm3(add3(mul3s(ldir, -1.f), dir)));
 	else
 		sm = -dot3(sub3(mul3s(n, 2.f * a), ldir), dir);
-	const f3 spec = mul3s(mul3v(ld3(m.ks), li), fmaxf(0.f, sh_pow(sm, m.shininess)));
+	const f3 spec = mul3s(mul3v(ks3, li), fmaxf(0.f, sh_pow(sm, shin)));
 	return add3(diff, spec);
+}
+
+/* the light point of sample j of emitter number e, E (object.c:293-304, 403-419: stratified per
+ * the rng mode), its shadow ray's direction and length, and the sample's intensity */
+__device__ __forceinline__ void emitter_sample(const KShadow &ks, const DEmitter &E, uint32_t e, uint32_t j, uint32_t ka, uint32_t kb,
+					       f3 p, f3 &ldir, float &ldist, float &dsq, f3 &li)
+{
+	float u1 = 0.5f, u2 = 0.5f;
+	if (uni(ks.rng) != RTX_RNG_CONST) /* the key already carries the seed (rtx_key_pixel) */
+		rtx_draw2(key_of(ka, kb), e, j, &u1, &u2);
+	if (uni(ks.rng) == RTX_RNG_STRAT) /* stratum j of the emitter's lights (IEEE, as the oracle) */
+		u1 = ((float)j + u1) / (float)E.num_lights;
+	const f3 lp = light_point_sh(E, p, u1, u2);
+	const f3 dv = sub3(lp, p);
+	ldist = mag3(dv);
+	dsq = magsqr3(dv);
+	ldir = mul3s(dv, sh_rcp(ldist));
+	li = ld3(E.li);
 }
 
 /* one light sample per lane of the shade point `rec` (render.c:170-229): the light point of
@@ -702,31 +730,43 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	const f3 p = mk3(q0.x, q0.y, q0.z);
 	const uint32_t obj = __float_as_uint(q4.x);
 	const DEmitter *emitters = unip(ks.emitters);
+	const auto *EM = cptr(emitters);
 	const uint32_t num_emitters = uni(ks.num_emitters);
-	uint32_t j = idx;
-	uint32_t e = 0;
-	for (; e < num_emitters; e++) {
-		const uint32_t eo = emitters[e].obj, enl = emitters[e].num_lights;
-		if (eo == obj)
+	/* the sample's emitter: one pass over the emitter table, read through the scalar cache */
+	uint32_t j = idx, e = RTX_NONE;
+	for (uint32_t k = 0; k < num_emitters; k++) {
+		const uint32_t eo = EM[k].obj, enl = EM[k].num_lights;
+		if (eo == obj || e != RTX_NONE)
 			continue;
 		if (j < enl)
-			break;
-		j -= enl;
+			e = k;
+		else
+			j -= enl;
 	}
-	if (e >= num_emitters)
+	if (e == RTX_NONE)
 		e = 0;
-	const DEmitter &E = emitters[e];
-	float u1 = 0.5f, u2 = 0.5f;
-	if (uni(ks.rng) != RTX_RNG_CONST) /* the key already carries the seed (rtx_key_pixel) */
-		rtx_draw2(key_of(__float_as_uint(q4.y), __float_as_uint(q4.z)), e, j, &u1, &u2);
-	if (uni(ks.rng) == RTX_RNG_STRAT) /* stratum j of the emitter's lights (IEEE, as the oracle) */
-		u1 = ((float)j + u1) / (float)E.num_lights;
-	const f3 lp = light_point_sh(E, p, u1, u2);
-	const f3 dv = sub3(lp, p);
-	const float ldist = mag3(dv);
-	const float dsq = magsqr3(dv);
-	const f3 ldir = mul3s(dv, sh_rcp(ldist));
-	f3 li = ld3(E.li);
+	/* every live lane's emitter the same (a packet inside one emitter's samples: the usual case):
+	 * its record through the scalar cache too, else per lane */
+	const u64 am = ballot(act);
+	const uint32_t lead = readlane(e, am ? (uint32_t)__ffsll((long long)am) - 1 : 0u);
+	f3 ldir, li;
+	float ldist, dsq;
+	uint32_t eobj;
+	if (!ballot(act && e != lead)) {
+		uint32_t w[sizeof(DEmitter) / 4];
+		const auto *W = (const __attribute__((address_space(4))) uint32_t *)(EM + lead);
+#pragma unroll
+		for (int i = 0; i < (int)(sizeof(DEmitter) / 4); i++)
+			w[i] = W[i];
+		DEmitter Eu;
+		__builtin_memcpy(&Eu, w, sizeof(Eu));
+		emitter_sample(ks, Eu, lead, j, __float_as_uint(q4.y), __float_as_uint(q4.z), p, ldir, ldist, dsq, li);
+		eobj = Eu.obj;
+	} else {
+		const DEmitter &E = emitters[e];
+		emitter_sample(ks, E, e, j, __float_as_uint(q4.y), __float_as_uint(q4.z), p, ldir, ldist, dsq, li);
+		eobj = E.obj;
+	}
 	QBvh Q;
 	Q.q = unip(ks.qnodes);
 	Q.qo = mk3(ks.qo[0], ks.qo[1], ks.qo[2]);
@@ -744,7 +784,7 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	Q.stk = stk;
 	Q.tq = stk + RTX_W8_STACK * WAVE;
 	const bool blocked = shadow_query<COUNT, WALK>(Q, unip(ks.recs), unip(ks.mats), unip(ks.planes), uni(ks.num_planes),
-						 unip(ks.lin), uni(ks.num_lin), have_tree, ks.tf, act, p, ldir, ldist, E.obj, li, sc);
+						 unip(ks.lin), uni(ks.num_lin), have_tree, ks.tf, act, p, ldir, ldist, eobj, li, sc);
 	reread_barrier();
 	f3 contribution = mk3(0.f, 0.f, 0.f);
 	if (act && !blocked)

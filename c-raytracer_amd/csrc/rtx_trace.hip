@@ -84,20 +84,21 @@ __device__ void trace_closest_bvh2(const DScene &S, uint32_t *stk, bool act, f3 
 		const f3 oi = mul3v(S.tf.rotated ? tf_point(S.tf.r, S.tf.c, o) : o, inv);
 		uint32_t ref = S.root_ref;
 		uint32_t sp = 0;
-		stk += lane_id();
-		/* entries from RTX_TRACE_LSTK on live in HBM, [entry][grid lane] */
-		uint32_t *ostk = S.ostk + (size_t)blockIdx.x * WAVE + lane_id();
+		/* entries from RTX_TRACE_LSTK on live in HBM, [entry][grid lane]; lane addresses formed at
+		 * each use (lane_id), none kept live across the walk */
+		lds_u32 *ls = (lds_u32 *)stk;
+		uint32_t *ostk = S.ostk + (size_t)blockIdx.x * WAVE;
 		const size_t ostride = (size_t)gridDim.x * WAVE;
 		auto push = [&](uint32_t v) {
 			if (sp < RTX_TRACE_LSTK)
-				stk[sp * WAVE] = v;
+				ls[sp * WAVE + lane_id()] = v;
 			else
-				ostk[(sp - RTX_TRACE_LSTK) * ostride] = v;
+				ostk[(sp - RTX_TRACE_LSTK) * ostride + lane_id()] = v;
 			sp++;
 		};
 		auto pop = [&]() -> uint32_t {
 			sp--;
-			return sp < RTX_TRACE_LSTK ? stk[sp * WAVE] : ostk[(sp - RTX_TRACE_LSTK) * ostride];
+			return sp < RTX_TRACE_LSTK ? ls[sp * WAVE + lane_id()] : ostk[(sp - RTX_TRACE_LSTK) * ostride + lane_id()];
 		};
 		for (;;) {
 			if (ref & RTX_REF_LEAF) {
@@ -174,16 +175,30 @@ __device__ void trace_closest_bvh2(const DScene &S, uint32_t *stk, bool act, f3 
 #define RTX_TRACE_EMPTYCOUNT 0 /* measurement builds: count only the visits that hit no child */
 #endif
 template <bool COUNT, int OCT>
-__device__ __forceinline__ void closest_walk8(const DScene &S, uint32_t *stk, uint32_t *ostk, size_t ostride, f3 o, f3 d,
+__device__ __forceinline__ void closest_walk8(const DScene &S, lds_u32 *stk, uint32_t *ostk, size_t ostride, f3 o, f3 d,
 					      f3 ob, f3 inv, float &tbest, uint32_t &hid, TraceCount &tc)
 {
+	/* the lane stack: stk / ostk are the wave's bases (LDS, then HBM [entry][grid lane]); a lane's
+	 * address is formed at each use (lane_id), none kept live across the walk */
+	uint32_t sp = 0;
+	auto push = [&](uint32_t v) {
+		if (sp < RTX_TRACE_LSTK)
+			stk[sp * WAVE + lane_id()] = v;
+		else
+			ostk[(sp - RTX_TRACE_LSTK) * ostride + lane_id()] = v;
+		sp++;
+	};
+	auto pop = [&]() -> uint32_t {
+		sp--;
+		return sp < RTX_TRACE_LSTK ? stk[sp * WAVE + lane_id()] : ostk[(sp - RTX_TRACE_LSTK) * ostride + lane_id()];
+	};
 	constexpr uint32_t K = (OCT == 8 || !RTX_W8_ORDER) ? 0u : (~(uint32_t)OCT & 7u);
 	/* ob / inv: the ray's origin and inverse direction in the trees' frame; o / d the world ray */
 	const f3 qs = ld3(S.w8qs), qo = ld3(S.w8qo);
 	const f3 invq = mk3(inv.x / qs.x, inv.y / qs.y, inv.z / qs.z);
 	const f3 oq = mk3((ob.x - qo.x) * qs.x, (ob.y - qo.y) * qs.y, (ob.z - qo.z) * qs.z);
 	const f3 oi = mul3v(oq, invq);
-	uint32_t node = 0, grp = 0, sp = 0;
+	uint32_t node = 0, grp = 0;
 	float gt = -INFINITY; /* RTX_TRACE_CULL: least entry distance of the group in grp (-inf: unknown) */
 	constexpr bool T = RTX_TRACE_NEAR || RTX_TRACE_CULL;
 	while (node != RTX_NONE) {
@@ -251,34 +266,21 @@ __device__ __forceinline__ void closest_walk8(const DScene &S, uint32_t *stk, ui
 			node = v.base + (p0 ^ K);
 			im &= ~(1u << p0);
 			if (im) {
-				if (grp) {
-					if (sp < RTX_TRACE_LSTK)
-						stk[sp * WAVE] = grp;
-					else
-						ostk[(sp - RTX_TRACE_LSTK) * ostride] = grp;
-					sp++;
-				}
+				if (grp)
+					push(grp);
 				grp = (v.base << 8) | im;
 				gt = tin;
 			}
 		} else {
 			if (RTX_TRACE_CULL && grp && gt > tbest) { /* the kept group starts beyond the closest hit */
-				grp = 0;
-				if (sp) {
-					sp--;
-					grp = sp < RTX_TRACE_LSTK ? stk[sp * WAVE] : ostk[(sp - RTX_TRACE_LSTK) * ostride];
-				}
+				grp = sp ? pop() : 0u;
 				gt = -INFINITY;
 			}
 			if (grp) {
 				node = (grp >> 8) + (__builtin_ctz(grp) ^ K);
 				grp &= grp - 1;
 				if (!(grp & 0xFFu)) {
-					grp = 0;
-					if (sp) {
-						sp--;
-						grp = sp < RTX_TRACE_LSTK ? stk[sp * WAVE] : ostk[(sp - RTX_TRACE_LSTK) * ostride];
-					}
+					grp = sp ? pop() : 0u;
 					gt = -INFINITY;
 				}
 			} else {
@@ -348,8 +350,8 @@ __device__ void trace_closest_w8(const DScene &S, uint32_t *stk, bool act, f3 o,
 		const bool rot = S.tf.rotated != 0;
 		const f3 ob = rot ? tf_point(S.tf.r, S.tf.c, o) : o;
 		const f3 inv = safe_inv_fast(rot ? tf_dir(S.tf.r, d) : d);
-		stk += lane_id();
-		uint32_t *ostk = S.ostk + (size_t)blockIdx.x * WAVE + lane_id();
+		lds_u32 *ls = (lds_u32 *)stk;
+		uint32_t *ostk = S.ostk + (size_t)blockIdx.x * WAVE;
 		const size_t ostride = (size_t)gridDim.x * WAVE;
 		const uint32_t oct = ((~__float_as_uint(inv.x)) >> 31) | (((~__float_as_uint(inv.y)) >> 31) << 1) |
 				     (((~__float_as_uint(inv.z)) >> 31) << 2);
@@ -359,13 +361,13 @@ __device__ void trace_closest_w8(const DScene &S, uint32_t *stk, bool act, f3 o,
 			switch (sel) {
 #define RTX_CWALK(K)                                                                    \
 	case K:                                                                             \
-		closest_walk8<COUNT, K>(S, stk, ostk, ostride, o, d, ob, inv, tbest, hid, tc);  \
+		closest_walk8<COUNT, K>(S, ls, ostk, ostride, o, d, ob, inv, tbest, hid, tc);   \
 		break;
 				RTX_CWALK(0) RTX_CWALK(1) RTX_CWALK(2) RTX_CWALK(3) RTX_CWALK(4) RTX_CWALK(5) RTX_CWALK(6)
 				RTX_CWALK(7)
 #undef RTX_CWALK
 			default:
-				closest_walk8<COUNT, 8>(S, stk, ostk, ostride, o, d, ob, inv, tbest, hid, tc);
+				closest_walk8<COUNT, 8>(S, ls, ostk, ostride, o, d, ob, inv, tbest, hid, tc);
 				break;
 			}
 		}

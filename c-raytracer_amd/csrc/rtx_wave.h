@@ -22,7 +22,14 @@ typedef unsigned long long u64;
 
 __device__ __forceinline__ u64 ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ uint32_t popc64(u64 m) { return (uint32_t)__popcll(m); }
-__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+/* recomputed at every use (two VALU), never a value kept live across the walks (the register
+ * allocator spilled it and reloaded it inside the walk loop) */
+__device__ __forceinline__ uint32_t lane_id()
+{
+	uint32_t l;
+	asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+	return l;
+}
 __device__ __forceinline__ uint32_t mbcnt(u64 m)
 {
 	return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));

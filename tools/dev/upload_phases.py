@@ -7,7 +7,9 @@ import rtxpy
 import standins
 which = sys.argv[1] if len(sys.argv) > 1 else "scene5"
 scene = rtxpy.Scene.load(standins.ensure_scene(which), base_dir=os.path.join(ROOT, "tests", "golden"))
+t0 = time.perf_counter()
 r = rtxpy.Renderer(0)
+print(f"open: {1e3 * (time.perf_counter() - t0):.1f} ms", file=sys.stderr, flush=True)
 for i in range(3):
     t0 = time.perf_counter()
     r.upload(scene)

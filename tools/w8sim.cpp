@@ -133,6 +133,9 @@ struct Stats {
 	 * (load k = the 16-B quarters of lanes 16k..16k+15's nodes, four lanes per node) */
 	double dsteps = 0, dnodes = 0, dlines = 0, touch_lane = 0, touch_tr = 0, walkers = 0, quad_lane = 0, quad_tr = 0;
 	double post_nodes[8] = {}, post_leaves[8] = {}; /* postponed leaf tests, threshold T = 8 * k lanes */
+	/* lane visits of divergent steps by the node's level (root 0), and of steps where every walking
+	 * lane's node is at level <= L (a top-of-tree LDS copy of levels 0..L would serve them all) */
+	double dlevel[16] = {}, dstep_top[16] = {};
 };
 
 int main(int argc, char **argv)
@@ -247,6 +250,26 @@ int main(int argc, char **argv)
 	       nb, nnodes, bvh.depth, w8.size(), nodes, depth, (double)kids / nodes, (double)inner_kids / nodes);
 	for (int i = 1; i <= 8; i++)
 		printf(" %u", hist[i]);
+	printf("\n");
+	/* every node entry's level (root 0) and the node count per level */
+	std::vector<uint32_t> level(w8.size(), ~0u), per_level(16, 0);
+	{
+		std::vector<uint32_t> q{ 0u };
+		level[0] = 0;
+		for (size_t h = 0; h < q.size(); h++) {
+			const DW8 &e = w8[q[h]];
+			per_level[std::min<uint32_t>(level[q[h]], 15)]++;
+			for (int c = 0; c < 8; c++)
+				if ((e.w[2] >> c) & 1) {
+					const uint32_t ch = (e.w[2] >> 8) + c;
+					level[ch] = level[q[h]] + 1;
+					q.push_back(ch);
+				}
+		}
+	}
+	printf("nodes per level:");
+	for (int i = 0; i < 16 && per_level[i]; i++)
+		printf(" %u", per_level[i]);
 	printf("\n");
 	for (size_t i = 0; i < w8.size(); i++) /* leaf entries hold the primitive records */
 		if (leafmap[i] != RTX_NONE)
@@ -517,6 +540,14 @@ int main(int argc, char **argv)
 				if (!div)
 					continue;
 				S.dsteps++;
+				uint32_t maxlev = 0;
+				for (int l = 0; l < 64; l++)
+					if (at[l] != ~0u) {
+						S.dlevel[std::min<uint32_t>(level[at[l]], 15)]++;
+						maxlev = std::max(maxlev, level[at[l]]);
+					}
+				for (uint32_t L = maxlev; L < 16; L++)
+					S.dstep_top[L]++;
 				std::vector<uint32_t> nodes, lines;
 				for (int l = 0; l < 64; l++)
 					if (at[l] != ~0u) {
@@ -572,6 +603,14 @@ int main(int argc, char **argv)
 	       "per-lane loads %.1f  transposed %.1f  quad cycles: per-lane %.1f  transposed %.1f\n",
 	       S.dsteps / S.packets, S.walkers / S.dsteps, S.dnodes / S.dsteps, S.dlines / S.dsteps, S.touch_lane / S.dsteps,
 	       S.touch_tr / S.dsteps, S.quad_lane / S.dsteps, S.quad_tr / S.dsteps);
+	printf("divergent-step lane visits by level:");
+	for (int i = 0; i < 16; i++)
+		if (S.dlevel[i])
+			printf(" L%d %.1f%%", i, 100 * S.dlevel[i] / S.walkers);
+	printf("\ndivergent steps with every walking lane at level <= L:");
+	for (int i = 0; i < 8; i++)
+		printf(" L%d %.1f%%", i, 100 * S.dstep_top[i] / S.dsteps);
+	printf("\n");
 	for (int k = 0; k < 8; k++)
 		printf("  %2d  %6.2f  %6.2f  %7.0f\n", k ? 8 * k : 1, S.post_nodes[k] / S.packets, S.post_leaves[k] / S.packets,
 		       (290 * S.post_nodes[k] + 99 * S.post_leaves[k]) / S.packets);
