@@ -485,7 +485,9 @@ def main():
     params = rtxpy.params_from_args(flags, seed=1)
     params.tile_offset, params.tile_stride = rank, world
 
+    t_open = time.perf_counter()
     r = rtxpy.Renderer(local)
+    open_ms = (time.perf_counter() - t_open) * 1e3  # rtx_open: the device code loaded, copies primed
     r.set_option(abi.RTX_OPT_SHADOW_WALK, WALKS[a.walk])
     r.set_option(abi.RTX_OPT_TRACE_WALK, WALKS[a.trace_walk])
     r.set_option(abi.RTX_OPT_SHADOW_SLOT, a.shadow_slot)
@@ -494,6 +496,7 @@ def main():
         r.set_option(abi.RTX_OPT_SHADOW_GRAB, a.shadow_grab)
     t0 = time.perf_counter()
     r.upload(scene)
+    upload_ms = (time.perf_counter() - t0) * 1e3
     st = r.stats()
     log(f"scene {os.path.basename(path)}: {scene.num_objects} objects, BVH {st.bvh_nodes} nodes depth {st.bvh_depth}, "
         f"shadow walk {walk_name(st.shadow_walk)}: {st.wide_nodes} wide nodes depth {st.wide_depth}, "
@@ -585,7 +588,11 @@ def main():
             names = {abi.RTX_BUILD_SAH_HOST: "sah_host", abi.RTX_BUILD_LBVH_GPU: "lbvh", abi.RTX_BUILD_PLOC_GPU: "ploc",
                      abi.RTX_BUILD_SAH_GPU: "sah_gpu"}
             d = names[int(st.builder)]
-            build = {"default": d, f"{d}_ms": round(st.build_ms, 1), f"{d}_nodes": int(st.bvh_nodes),
+            build = {"default": d, "first_upload_wall_ms": round(upload_ms, 1), "open_ms": round(open_ms, 1),
+                     "note": f"{d}_ms: the BVH build of this process's first upload (device build + 8-wide collapse); "
+                             "first_upload_wall_ms: the whole rtx_upload_scene call; open_ms: rtx_open, which "
+                             "loads the library's device code and primes host->device copies once per context",
+                     f"{d}_ms": round(st.build_ms, 1), f"{d}_nodes": int(st.bvh_nodes),
                      f"{d}_depth": int(st.bvh_depth), f"{d}_wide_nodes": int(st.wide_nodes),
                      f"{d}_wide_depth": int(st.wide_depth), f"{d}_shadow_walk": walk_name(st.shadow_walk),
                      f"{d}_shadow_ms": round(float(np.mean(sms)), 1)}

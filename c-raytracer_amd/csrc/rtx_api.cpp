@@ -47,8 +47,8 @@ extern "C" hipError_t rtx_sah_build(uint32_t n, const float *d_lo, const float *
 				    uint32_t *levels_out, hipStream_t st);
 extern "C" hipError_t rtx_w8_collapse_device(const DNode *recs, uint32_t nnodes, uint32_t nb, const uint32_t *skip_obj,
 					     uint32_t num_objects, DW8 **w8_out, DW8S **w8s_out, uint32_t **leafmap_out,
-					     uint32_t *entries_out, uint32_t *depth_out, uint32_t *wide_out, float qo[3],
-					     float qs[3], hipStream_t st);
+					     uint32_t *entries_out, uint32_t *depth_out, uint32_t *wide_out, uint32_t *top_out,
+					     float qo[3], float qs[3], hipStream_t st);
 extern "C" hipError_t rtx_launch_w8_scalar(uint32_t n, const DW8 *w8, const uint32_t *leafmap, DW8S *w8s, hipStream_t st);
 extern "C" hipError_t rtx_lbvh_build(uint32_t n, const float *d_lo, const float *d_hi, const DPrim *d_prims_in,
 				     const float blo[3], const float bhi[3], uint32_t max_leaf, DNode **recs_out,
@@ -67,6 +67,15 @@ extern "C" hipError_t rtx_launch_kat_shadow(int kind, uint32_t n, const float *i
 extern "C" hipError_t rtx_launch_w8_fill(const DPrim *prims, const DMaterial *mats, const uint32_t *leafmap, uint32_t n, DW8 *out,
 					  hipStream_t stream);
 extern "C" hipError_t rtx_shadow_grid_lanes(uint32_t cus, uint32_t *lanes);
+
+/* the code objects of the library's device files (each file's rtx_load_*) */
+extern "C" hipError_t rtx_load_build(void);
+extern "C" hipError_t rtx_load_wide8_dev(void);
+extern "C" hipError_t rtx_load_shadow(void);
+extern "C" hipError_t rtx_load_trace(void);
+extern "C" hipError_t rtx_load_sort(void);
+extern "C" hipError_t rtx_load_post(void);
+extern "C" hipError_t rtx_load_gather(void);
 
 static thread_local char g_err[512] = "";
 
@@ -211,6 +220,32 @@ extern "C" int rtx_open(int device, rtx_ctx **out)
 	    (e = hipMalloc(&c->d_ctr, sizeof(unsigned long long) * RTX_C_N)) != hipSuccess) {
 		rtx_close(c);
 		return fail(RTX_ERR_HIP, "context setup failed: %s", hipGetErrorString(e));
+	}
+	/* one-time device set-up here rather than inside the first upload or render: every code object
+	 * of the library loaded on this device (the runtime loads one at its first launch otherwise,
+	 * ~30 ms inside the first BVH build), and the runtime's pageable-copy path primed */
+	for (hipError_t (*load)(void) : { rtx_load_build, rtx_load_wide8_dev, rtx_load_shadow, rtx_load_trace, rtx_load_sort,
+					  rtx_load_post, rtx_load_gather })
+		if ((e = load()) != hipSuccess) {
+			rtx_close(c);
+			return fail(RTX_ERR_HIP, "loading the device code failed: %s", hipGetErrorString(e));
+		}
+	{
+		std::vector<uint8_t> h((size_t)4 << 20, 0);
+		void *d = nullptr;
+		e = hipMalloc(&d, h.size());
+		if (e == hipSuccess)
+			e = hipMemcpyAsync(d, h.data(), h.size(), hipMemcpyHostToDevice, c->stream);
+		if (e == hipSuccess)
+			e = hipMemcpyAsync(h.data(), d, 64, hipMemcpyDeviceToHost, c->stream);
+		if (e == hipSuccess)
+			e = hipStreamSynchronize(c->stream);
+		if (d)
+			(void)hipFree(d);
+		if (e != hipSuccess) {
+			rtx_close(c);
+			return fail(RTX_ERR_HIP, "context setup failed: %s", hipGetErrorString(e));
+		}
 	}
 	*out = c;
 	return RTX_OK;
@@ -411,7 +446,7 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 	memcpy(tlo, c->bound_lo, 12);
 	memcpy(thi, c->bound_hi, 12);
 	if (tf.rotated) {
-		const double pad = hs.frame_pad = rtx_frame_pad(rtx_frame_radius(sc, bounded, tf));
+		const double pad = hs.frame_pad = rtx_frame_pad(rtx_frame_radius(c->bound_lo, c->bound_hi, tf));
 		rtx_frame_boxes(sc, bounded, tf, pad, lo.data(), hi.data(), tlo, thi);
 	}
 	hs.frame_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf0).count();
@@ -540,9 +575,9 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 			uint32_t *d_skip = nullptr;
 			if ((rc = upload(d_skip, skip, c->stream)))
 				return rc;
-			uint32_t ent = 0, dep = 0, wide = 0;
+			uint32_t ent = 0, dep = 0, wide = 0, top = 0;
 			e = rtx_w8_collapse_device(recs, nnodes, nb, d_skip, sc->num_objects, &hs.dev_w8, &hs.dev_w8s, &hs.dev_w8leaf, &ent,
-						   &dep, &wide, hs.w8f.qo, hs.w8f.qs, c->stream);
+						   &dep, &wide, &top, hs.w8f.qo, hs.w8f.qs, c->stream);
 			dfree(d_skip);
 			if (e != hipSuccess)
 				return fail(RTX_ERR_HIP, "8-wide BVH collapse on the device failed: %s", hipGetErrorString(e));
@@ -552,6 +587,7 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 				hs.w8depth = dep;
 				hs.w8_entries = ent;
 				hs.w8_wide = wide;
+				hs.w8top = top;
 				hs.w8noemit = sc->num_emitters > 0;
 			}
 		}
@@ -779,6 +815,7 @@ int rtx_upload_built(rtx_ctx *c, HostScene &hs)
 	S.w8 = have_w8 ? c->d_w8 : nullptr;
 	S.num_w8 = num_w8;
 	S.w8depth = hs.w8depth;
+	S.w8top = hs.w8_on_device ? hs.w8top : 0u; /* the device collapse's breadth-first layout only */
 	memcpy(S.w8qo, hs.w8f.qo, 12);
 	memcpy(S.w8qs, hs.w8f.qs, 12);
 	S.w8noemit = hs.w8noemit ? 1u : 0u;

@@ -1351,3 +1351,11 @@ extern "C" hipError_t rtx_launch_find_prims(const DPrim *prims, uint32_t n, cons
 	hipLaunchKernelGGL(k_find_prims, dim3((n + 255) / 256), dim3(256), 0, stream, prims, n, objs, nobj, out);
 	return hipGetLastError();
 }
+
+/* the code object of this file on the current device, loaded now (rtx_open) rather than at the
+ * first launch inside an upload or a render */
+extern "C" __attribute__((visibility("hidden"))) hipError_t rtx_load_build(void)
+{
+	hipFuncAttributes a;
+	return hipFuncGetAttributes(&a, (const void *)k_sb_reset);
+}

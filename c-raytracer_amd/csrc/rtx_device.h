@@ -148,6 +148,8 @@ typedef struct DTreeFrame {
 #define RTX_W8_STACK 8     /* k_shadow lane-stack entries in LDS; deeper ones spill to HBM (DScene.w8spill) */
 #endif
 #define RTX_W8_MAX_ENTRIES (1u << 24)
+#define RTX_W8_TOP_LEVELS 3 /* levels of the 8-wide tree k_shadow serves from LDS (root, 8, 64 nodes) */
+#define RTX_W8_TOP_MAX 80   /* entries of them at most: 2 + 8 + 64 */
 typedef struct __attribute__((aligned(64))) DW8 {
 	uint32_t w[16];
 } DW8;
@@ -216,6 +218,8 @@ typedef struct DScene {
 	uint32_t num_top;
 	const DW8 *w8;          /* 8-wide compressed BVH (num_w8 entries), null when not built */
 	uint32_t num_w8, w8depth;
+	uint32_t w8top;         /* entries [0, w8top): the tree's levels 0..RTX_W8_TOP_LEVELS-1 (the device collapse
+	                         * lays levels out breadth-first), which k_shadow copies to LDS; 0: none */
 	float w8qo[3], w8qs[3]; /* its 16-bit frame */
 	const DW8S *w8s;        /* scalar-path copies of its nodes (num_w8 slots, node entries filled) */
 	uint32_t trace_w8;      /* k_trace walks the 8-wide tree for closest hits (else the float BVH2) */

@@ -39,7 +39,7 @@
 #include "rtx_frame.h"
 
 #define RTX_FRAME_PAD 4e-6     /* leaf-box padding for the ray transform, times the scene radius */
-#define RTX_FRAME_SAMPLE 16384 /* triangles the cost is summed over (every k-th) */
+#define RTX_FRAME_SAMPLE 16384 /* objects the cost is sampled over (every k-th bounded object; its triangles) */
 #define RTX_FRAME_CANDS 16     /* largest sampled triangles whose frames are tried */
 #define RTX_FRAME_GAIN 0.75    /* a rotated frame must cost at most this fraction of the identity's */
 
@@ -178,16 +178,14 @@ double rtx_frame_choose(const rtx_scene_desc *sc, const std::vector<uint32_t> &b
 	memset(&F, 0, sizeof(F));
 	for (int i = 0; i < 3; i++)
 		F.r[i][i] = 1.f;
-	std::vector<uint32_t> tris;
-	for (uint32_t oi : bounded)
-		if (sc->objects[oi].type == RTX_TRIANGLE)
-			tris.push_back(oi);
-	if (tris.size() < 16)
-		return 1.0;
-	const size_t stride = (tris.size() + RTX_FRAME_SAMPLE - 1) / RTX_FRAME_SAMPLE;
+	/* the triangles among every stride-th bounded object (one pass over the sample, not the scene) */
+	const size_t stride = (bounded.size() + RTX_FRAME_SAMPLE - 1) / RTX_FRAME_SAMPLE;
 	std::vector<uint32_t> sample;
-	for (size_t k = 0; k < tris.size(); k += stride)
-		sample.push_back(tris[k]);
+	for (size_t k = 0; k < bounded.size(); k += std::max<size_t>(stride, 1))
+		if (sc->objects[bounded[k]].type == RTX_TRIANGLE)
+			sample.push_back(bounded[k]);
+	if (sample.size() < 16)
+		return 1.0;
 	/* candidates: the frames of the largest sampled triangles (ties: lower object index) */
 	std::vector<std::pair<double, uint32_t>> by_area;
 	for (uint32_t oi : sample) {
@@ -269,22 +267,14 @@ static float up(double x)
 	return (double)f < x ? next_up(f) : f;
 }
 
-double rtx_frame_radius(const rtx_scene_desc *sc, const std::vector<uint32_t> &bounded, const DTreeFrame &F)
+double rtx_frame_radius(const float world_lo[3], const float world_hi[3], const DTreeFrame &F)
 {
-	std::vector<double> part(256, 0.0);
-	const unsigned t = parallel_chunks(bounded.size(), [&](size_t b, size_t e, unsigned c) {
-		double rad = 0;
-		for (size_t q = b; q < e; q++) {
-			const rtx_object &o = sc->objects[bounded[q]];
-			const int n = o.type == RTX_SPHERE ? 1 : 3;
-			const float *p[3] = { o.p0, o.p1, o.p2 };
-			for (int k = 0; k < n; k++)
-				for (int i = 0; i < 3; i++)
-					rad = std::max(rad, fabs((double)p[k][i] - F.c[i]) + (o.type == RTX_SPHERE ? (double)o.radius : 0.0));
-		}
-		part[c] = rad;
-	});
-	return *std::max_element(part.begin(), part.begin() + t);
+	/* the largest |x - c| component over the bounded objects' world box: it holds every vertex and
+	 * every sphere with its radius */
+	double rad = 0;
+	for (int i = 0; i < 3; i++)
+		rad = std::max(rad, std::max(fabs((double)world_lo[i] - F.c[i]), fabs((double)world_hi[i] - F.c[i])));
+	return rad;
 }
 
 void rtx_frame_box(const rtx_object &o, const DTreeFrame &F, double pad, float lo[3], float hi[3])
@@ -364,19 +354,12 @@ extern "C" int rtx_tree_frame(const rtx_scene_desc *sc, int *rotated, float rot[
 	if (sc->num_objects && !sc->objects)
 		return rtx_fail(RTX_ERR_ARG, "objects pointer is null");
 	std::vector<uint32_t> bounded;
-	float lo[3] = { FLT_MAX, FLT_MAX, FLT_MAX }, hi[3] = { -FLT_MAX, -FLT_MAX, -FLT_MAX };
-	for (uint32_t i = 0; i < sc->num_objects; i++) {
-		const rtx_object &o = sc->objects[i];
-		if (o.type != RTX_SPHERE && o.type != RTX_TRIANGLE)
-			continue;
-		bounded.push_back(i);
-		float l[3], h[3];
-		rtx_world_box(o, l, h);
-		for (int a = 0; a < 3; a++) {
-			lo[a] = std::min(lo[a], l[a]);
-			hi[a] = std::max(hi[a], h[a]);
-		}
-	}
+	for (uint32_t i = 0; i < sc->num_objects; i++)
+		if (sc->objects[i].type == RTX_SPHERE || sc->objects[i].type == RTX_TRIANGLE)
+			bounded.push_back(i);
+	std::vector<float> bl(3 * bounded.size()), bh(3 * bounded.size());
+	float lo[3], hi[3];
+	rtx_world_boxes(sc, bounded, bl.data(), bh.data(), lo, hi);
 	DTreeFrame F;
 	const double ratio = rtx_frame_choose(sc, bounded, lo, hi, F);
 	memcpy(rot, F.r, 36);

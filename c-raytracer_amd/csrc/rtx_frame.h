@@ -23,8 +23,9 @@ void rtx_world_box(const rtx_object &o, float lo[3], float hi[3]);
  * leaf-box cost relative to the identity's (1.0: the identity, F.rotated = 0) */
 double rtx_frame_choose(const rtx_scene_desc *sc, const std::vector<uint32_t> &bounded, const float world_lo[3],
 			const float world_hi[3], DTreeFrame &F);
-/* the largest |x - c| component over the bounded objects (spheres: + radius) */
-double rtx_frame_radius(const rtx_scene_desc *sc, const std::vector<uint32_t> &bounded, const DTreeFrame &F);
+/* the largest |x - c| component over the bounded objects' world box world_lo / world_hi (every
+ * vertex, every sphere with its radius) */
+double rtx_frame_radius(const float world_lo[3], const float world_hi[3], const DTreeFrame &F);
 /* the transform's leaf-box padding for a scene of that radius */
 double rtx_frame_pad(double radius);
 /* object o's box in frame F (F.rotated), rounded outward and padded by pad plus the relative

@@ -61,3 +61,11 @@ extern "C" hipError_t rtx_launch_tile_unpack(const float4 *in, uint32_t w, uint3
 	hipLaunchKernelGGL(k_tile_unpack, dim3((nrec + 255) / 256), dim3(256), 0, stream, in, w, h, off, stride, nrec, rgb, z);
 	return hipGetLastError();
 }
+
+/* the code object of this file on the current device, loaded now (rtx_open) rather than at the
+ * first launch inside an upload or a render */
+extern "C" __attribute__((visibility("hidden"))) hipError_t rtx_load_gather(void)
+{
+	hipFuncAttributes a;
+	return hipFuncGetAttributes(&a, (const void *)k_tile_pack);
+}

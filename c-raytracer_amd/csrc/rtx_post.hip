@@ -192,3 +192,11 @@ extern "C" hipError_t rtx_launch_post(uint32_t w, uint32_t h, const rtx_post *pp
 				   pp->mist_falloff, pp->mist_color[0], pp->mist_color[1], pp->mist_color[2]);
 	return hipGetLastError();
 }
+
+/* the code object of this file on the current device, loaded now (rtx_open) rather than at the
+ * first launch inside an upload or a render */
+extern "C" __attribute__((visibility("hidden"))) hipError_t rtx_load_post(void)
+{
+	hipFuncAttributes a;
+	return hipFuncGetAttributes(&a, (const void *)k_post_prep);
+}

@@ -195,6 +195,8 @@ struct QBvh {
 	uint32_t nt;          /* top records */
 	const DW8 *w8;        /* the 8-wide BVH (rtx_device.h DW8), WALK_W8 */
 	const DW8S *w8s;      /* ... its nodes' scalar-path copies */
+	const uint4 *t8;      /* the workgroup's LDS copy of its entries [0, nt8) (top levels) */
+	uint32_t nt8;
 	uint32_t *spill;      /* this lane's stack entries from lstk on: entry k at spill[(k - lstk) * spill_stride] */
 	uint32_t spill_stride;
 	uint32_t lstk;        /* lane-stack entries in LDS (<= RTX_W8_STACK) */
@@ -289,6 +291,9 @@ __device__ __forceinline__ void shadow_walk(const QBvh &Q, const char *__restric
  *    register, the older groups in the lane's LDS stack (entries from Q.lstk on in HBM,
  *    Q.spill), at most one per level, so any depth walks.
  * tl < 0 on entry: inactive lane.  On an opaque hit tl becomes -1. */
+#ifndef RTX_W8_TOP
+#define RTX_W8_TOP 1 /* divergent steps read the tree's top levels (DScene.w8top entries) from an LDS copy */
+#endif
 #ifndef RTX_W8_TQ
 #define RTX_W8_TQ 4 /* deferred leaf groups per lane in LDS (besides the one in a register) */
 #endif
@@ -377,14 +382,25 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 				v = w8_visit_s<OCT, K>(Q.w8s + (size_t)un, invq, oi, tl);
 			} else {
 				uint32_t w[16];
-				const DW8 *N = Q.w8 + (size_t)node;
+				if (node < Q.nt8) { /* a top-level node: the workgroup's LDS copy (no texture-path traffic) */
 #pragma unroll
-				for (int k = 0; k < 4; k++) {
-					const uint4 x = ldg4u((const uint32_t *)N + 4 * k);
-					w[4 * k] = x.x;
-					w[4 * k + 1] = x.y;
-					w[4 * k + 2] = x.z;
-					w[4 * k + 3] = x.w;
+					for (int k = 0; k < 4; k++) {
+						const uint4 x = lds4u(Q.t8 + 4 * node + k);
+						w[4 * k] = x.x;
+						w[4 * k + 1] = x.y;
+						w[4 * k + 2] = x.z;
+						w[4 * k + 3] = x.w;
+					}
+				} else {
+					const DW8 *N = Q.w8 + (size_t)node;
+#pragma unroll
+					for (int k = 0; k < 4; k++) {
+						const uint4 x = ldg4u((const uint32_t *)N + 4 * k);
+						w[4 * k] = x.x;
+						w[4 * k + 1] = x.y;
+						w[4 * k + 2] = x.z;
+						w[4 * k + 3] = x.w;
+					}
 				}
 				v = w8_visit<OCT, K, false>(w, invq, oi, tl);
 			}
@@ -586,6 +602,7 @@ const DW8 *w8;        /* 8-wide compressed BVH (WALK_W8 instances; qo / qs / qsi
 	const DW8S *w8s;      /* its nodes' scalar-path copies */
 	uint32_t *w8spill;    /* lane-stack spill area, [entry][grid lane] */
 	uint32_t w8lstk;      /* lane-stack entries in LDS */
+	uint32_t w8top;       /* entries of the 8-wide tree's top levels, copied to LDS per workgroup (DScene.w8top) */
 	const DEmitter *lin;  /* objects shadow_query tests one by one: the emitters the 8-wide tree leaves out,
 	                       * or every bounded object of a tiny scene (no tree walk) */
 	uint32_t num_lin;
@@ -723,7 +740,7 @@ __device__ __forceinline__ void emitter_sample(const KShadow &ks, const DEmitter
  * and Phong / Blinn.  Argument-block fields are read from LDS behind reread barriers. */
 template <bool COUNT, int WALK, bool UNI>
 __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec, uint32_t idx, bool act, ShadowCount &sc,
-					   const uint4 *top_q, const uint32_t *top_e, lds_u32 *stk)
+					   const uint4 *top_q, const uint32_t *top_e, lds_u32 *stk, const uint4 *t8)
 {
 	reread_barrier();
 	const float4 q0 = sp_field<UNI && RTX_SH_SPUNI>(rec, 0), q4 = sp_field<UNI && RTX_SH_SPUNI>(rec, 4);
@@ -778,6 +795,8 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	const bool have_tree = uni(ks.have_tree) != 0 && !RTX_DEBUG_NOWALK;
 	Q.w8 = WALK == WALK_W8 ? unip(ks.w8) : nullptr;
 	Q.w8s = WALK == WALK_W8 ? unip(ks.w8s) : nullptr;
+	Q.t8 = t8;
+	Q.nt8 = (WALK == WALK_W8 && RTX_W8_TOP) ? min(uni(ks.w8top), (uint32_t)RTX_W8_TOP_MAX) : 0u;
 	Q.spill_stride = gridDim.x * blockDim.x;
 	Q.spill = WALK == WALK_W8 ? unip(ks.w8spill) + blockIdx.x * blockDim.x + threadIdx.x : nullptr;
 	Q.lstk = uni(ks.w8lstk);
@@ -805,7 +824,9 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 	__shared__ uint4 top_q[TOP ? RTX_TOP_MAX : 1];    /* the top records (rtx_device.h RTX_QTOP_CUT) */
 	__shared__ uint32_t top_e[TOP ? RTX_TOP_MAX : 1]; /* cut records: the DQNode index after the subtree */
 	/* the wide walks' lane stacks */	__shared__ uint32_t wstk[RTX_SH_NW][WALK == WALK_W8 ? RTX_W8_STACK + RTX_W8_TQ : 1][WAVE];
-	__shared__ KShadow ks_w[RTX_SH_NW];
+	__shared__ KShadow ks_s; /* the arguments, one copy for the workgroup */
+	/* WALK_W8: the 8-wide tree's top levels (RTX_W8_TOP_LEVELS), read by divergent steps from LDS */
+	__shared__ uint4 t8[WALK == WALK_W8 && RTX_W8_TOP ? RTX_W8_TOP_MAX * 4 : 1];
 	/* one wave's tables in one struct, so every lane addresses them from one base register */
 	struct WaveTables {
 		uint32_t off[WAVE + 1]; /* first lane slot of each shade point, total */
@@ -819,11 +840,14 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 		top_q[i] = ldg4u(ka.top + 4 * i);
 		top_e[i] = gptr(ka.top)[4 * ntop + i];
 	}
+	const uint32_t nt8 = (WALK == WALK_W8 && RTX_W8_TOP) ? min(ka.w8top, (uint32_t)RTX_W8_TOP_MAX) : 0u;
+	for (uint32_t i = threadIdx.x; i < 4 * nt8; i += WAVE * RTX_SH_NW)
+		t8[i] = ldg4u((const uint32_t *)ka.w8 + 4 * i);
 	const uint32_t wv = uni(threadIdx.x / WAVE);
-	if (lane_id() == 0)
-		ks_w[wv] = ka;
+	if (threadIdx.x == 0)
+		ks_s = ka;
 	__syncthreads();
-	KShadow &ks = ks_w[wv];
+	KShadow &ks = ks_s;
 	uint32_t *off = wt_w[wv].off, *nls = wt_w[wv].nls, *sid = wt_w[wv].sid;
 	float(*Ls)[WAVE] = wt_w[wv].Ls;
 	lds_u32 *stk = (lds_u32 *)&wstk[wv][0][lane_id()];
@@ -867,7 +891,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 				f3 acc = mk3(0.f, 0.f, 0.f);
 				for (uint32_t base = 0; base < nl; base += WAVE) {
 					const uint32_t idx = base + lane_id();
-					acc = add3(acc, light_sample<COUNT, WALK, true>(ks, rec, idx, idx < nl, sc, top_q, top_e, stk));
+					acc = add3(acc, light_sample<COUNT, WALK, true>(ks, rec, idx, idx < nl, sc, top_q, top_e, stk, t8));
 				}
 				const float sx = wave_sum(acc.x), sy = wave_sum(acc.y), sz = wave_sum(acc.z);
 				if (lane_id() == 0) {
@@ -890,7 +914,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 				const uint32_t idx = ((slot - off[k]) << slot_lg) + (lane_id() & (slot_b - 1));
 				const bool act = slot < tot && idx < nls[k];
 				const float4 *rec = unip(ks.sp) + (size_t)sid[k] * SPREC;
-				const f3 contribution = light_sample<COUNT, WALK, false>(ks, rec, idx, act, sc, top_q, top_e, stk);
+				const f3 contribution = light_sample<COUNT, WALK, false>(ks, rec, idx, act, sc, top_q, top_e, stk, t8);
 				/* per-shade-point sums.  Each slot's B lanes reduce in a fixed butterfly (masks B/2 .. 1),
 				 * then the slot sums are added to their point's total one slot at a time in slot order, so a
 				 * point whose slots straddle packets gets the same sum whatever its neighbours (with one slot
@@ -1228,6 +1252,7 @@ for (int a = 0; a < 3; a++) {
 	ka.w8s = S->w8s;
 	ka.w8spill = S->w8spill;
 	ka.w8lstk = S->w8lstk;
+	ka.w8top = S->w8top;
 	ka.lin = S->lin; /* a tiny scene: every bounded object, no walk */
 	ka.num_lin = S->lin ? S->num_lin : 0u;
 	if (walk == WALK_W8) { /* the 8-wide tree's own frame; the emitters it leaves out are tested linearly */
@@ -1242,4 +1267,12 @@ for (int a = 0; a < 3; a++) {
 	if (walk == WALK_W8)
 		return launch_walk<WALK_W8>(ka, nw, cus, count, stream);
 	return launch_walk<WALK_BVH2>(ka, nw, cus, count, stream);
+}
+
+/* the code object of this file on the current device, loaded now (rtx_open) rather than at the
+ * first launch inside an upload or a render */
+extern "C" __attribute__((visibility("hidden"))) hipError_t rtx_load_shadow(void)
+{
+	hipFuncAttributes a;
+	return hipFuncGetAttributes(&a, (const void *)k_w8_fill);
 }

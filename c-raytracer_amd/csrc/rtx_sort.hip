@@ -74,3 +74,11 @@ extern "C" hipError_t rtx_launch_spsort(const float4 *sp, uint32_t n, const floa
 	*perm = v.Current();
 	return e;
 }
+
+/* the code object of this file on the current device, loaded now (rtx_open) rather than at the
+ * first launch inside an upload or a render */
+extern "C" __attribute__((visibility("hidden"))) hipError_t rtx_load_sort(void)
+{
+	hipFuncAttributes a;
+	return hipFuncGetAttributes(&a, (const void *)k_spkey);
+}

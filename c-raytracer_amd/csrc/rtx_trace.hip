@@ -1029,3 +1029,11 @@ extern "C" hipError_t rtx_launch_kat(int kind, uint32_t n, const float *in, floa
 	hipLaunchKernelGGL(k_kat, dim3((n + 255) / 256), dim3(256), 0, stream, kind, n, in, out, u32mode);
 	return hipGetLastError();
 }
+
+/* the code object of this file on the current device, loaded now (rtx_open) rather than at the
+ * first launch inside an upload or a render */
+extern "C" __attribute__((visibility("hidden"))) hipError_t rtx_load_trace(void)
+{
+	hipFuncAttributes a;
+	return hipFuncGetAttributes(&a, (const void *)k_accum);
+}

@@ -399,14 +399,14 @@ extern "C" hipError_t rtx_launch_w8_scalar(uint32_t n, const DW8 *w8, const uint
  * *depth_out = 0 when nothing is left or the tree exceeds RTX_W8_MAX_ENTRIES. */
 extern "C" hipError_t rtx_w8_collapse_device(const DNode *recs, uint32_t nnodes, uint32_t nb, const uint32_t *skip_obj,
 					     uint32_t num_objects, DW8 **w8_out, DW8S **w8s_out, uint32_t **leafmap_out,
-					     uint32_t *entries_out, uint32_t *depth_out, uint32_t *wide_out, float qo[3],
-					     float qs[3], hipStream_t st)
+					     uint32_t *entries_out, uint32_t *depth_out, uint32_t *wide_out, uint32_t *top_out,
+					     float qo[3], float qs[3], hipStream_t st)
 {
 	hipError_t e = hipSuccess;
 	*w8_out = nullptr;
 	*w8s_out = nullptr;
 	*leafmap_out = nullptr;
-	*entries_out = *depth_out = *wide_out = 0;
+	*entries_out = *depth_out = *wide_out = *top_out = 0;
 	if (!nnodes || !nb)
 		return hipErrorInvalidValue;
 	const size_t nt = (size_t)nnodes + nb;
@@ -474,7 +474,7 @@ extern "C" hipError_t rtx_w8_collapse_device(const DNode *recs, uint32_t nnodes,
 		hst[1] = root;
 		hst[2] = 0;
 		TRY(hipMemcpyAsync(items, &hst[1], 8, hipMemcpyHostToDevice, st));
-		uint32_t m = 1, blk = 2, depth = 0, wide = 0;
+		uint32_t m = 1, blk = 2, depth = 0, wide = 0, top = 0;
 		while (m) {
 			if (blk + 8 * (size_t)m > RTX_W8_MAX_ENTRIES || blk + 8 * (size_t)m > cap) {
 				depth = 0;
@@ -493,6 +493,8 @@ extern "C" hipError_t rtx_w8_collapse_device(const DNode *recs, uint32_t nnodes,
 			wide += m;
 			depth++;
 			blk += 8 * m;
+			if (depth == RTX_W8_TOP_LEVELS - 1) /* every entry of levels 0 .. RTX_W8_TOP_LEVELS-1 */
+				top = blk;
 			m = hst[4] + hst[5];
 			uint2 *ti = items;
 			items = items2;
@@ -514,6 +516,7 @@ extern "C" hipError_t rtx_w8_collapse_device(const DNode *recs, uint32_t nnodes,
 		w8s = nullptr;
 		lmf = nullptr;
 		*entries_out = blk;
+		*top_out = std::min<uint32_t>(top ? top : blk, RTX_W8_TOP_MAX);
 		*depth_out = depth;
 		*wide_out = wide;
 	}
@@ -540,4 +543,12 @@ done:
 	(void)hipFree(lmf);
 	(void)hipHostFree(hst);
 	return e;
+}
+
+/* the code object of this file on the current device, loaded now (rtx_open) rather than at the
+ * first launch inside an upload or a render */
+extern "C" __attribute__((visibility("hidden"))) hipError_t rtx_load_wide8_dev(void)
+{
+	hipFuncAttributes a;
+	return hipFuncGetAttributes(&a, (const void *)k_w8d_parent);
 }
