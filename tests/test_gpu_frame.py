@@ -43,6 +43,22 @@ def test_tree_frame_choice():
         assert not rot and ratio == 1.0 and np.array_equal(R, np.eye(3, dtype=np.float32)), name
 
 
+def test_tree_frame_independent_of_host_threads():
+    """the frame choice and the boxes behind it run on host threads (rtx_host_parallel): the same
+    frame whatever their number"""
+    import subprocess, sys, os
+    code = ("import sys; sys.path[:0] = [%r, %r]; import conftest as C, rtxpy, numpy as np; "
+            "rot, R, c, ratio = rtxpy.tree_frame(C.load_config('s6_amb')[0]); "
+            "print(int(rot), R.tobytes().hex(), c.tobytes().hex(), repr(ratio))") % (
+        os.path.dirname(os.path.abspath(__file__)), os.path.join(C.ROOT, "c-raytracer_amd"))
+    outs = []
+    for n in ("1", "3", "8"):
+        env = dict(os.environ, RTX_HOST_THREADS=n)
+        outs.append(subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                                   check=True).stdout.split()[-4:])
+    assert outs[0] == outs[1] == outs[2], outs
+
+
 @pytest.fixture(scope="module")
 def renderer():
     r = rtxpy.Renderer(0)
