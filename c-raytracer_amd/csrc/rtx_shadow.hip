@@ -10,11 +10,16 @@
  * The walk: every lane walks its own shadow ray over the 8-wide compressed BVH
  * (rtx_device.h DW8, shadow_walk8): one 64-byte node per step, eight box tests
  * per memory round trip, pending siblings as (base, slot mask) groups in a
- * register, an LDS lane stack and HBM below it (any depth).  Small scenes (the
- * whole threaded BVH2 fits the LDS top copy) walk the threaded BVH2 instead
- * (shadow_walk: one 16-byte record per step, no stack, read from LDS).  Both
- * walks test boxes in the tree's frame (DScene.tf: the rotation the uploader
- * chose for the leaf boxes) and primitives in world space.
+ * register, an LDS lane stack and HBM below it (any depth).  A step whose walking
+ * lanes share one node reads it through the scalar cache; other steps read the
+ * tree's top three levels from the workgroup's LDS copy (DScene.w8top) and the
+ * rest from memory.  Small scenes (the whole threaded BVH2 fits the LDS top copy)
+ * may walk the threaded BVH2 instead (shadow_walk: one 16-byte record per step,
+ * no stack, read from LDS), and tiny ones test their few objects one by one
+ * (DScene.lin, no walk).  The walks test boxes in the tree's frame (DScene.tf:
+ * the rotation the uploader chose for the leaf boxes) and primitives in world
+ * space.  The emitter and material records of a one-point packet are read
+ * through the scalar cache.
  *
  * Scheduling: persistent workgroups; each wave takes `per_wave` shade points at
  * a time from a global queue in Morton order of their position (rtx_sort.hip),
