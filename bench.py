@@ -43,12 +43,16 @@ SHADOW_SRCS = ["c-raytracer_amd/csrc/rtx_shadow.hip", "c-raytracer_amd/csrc/rtx_
 
 
 def shadow_src_sha():
-    """sha1 over k_shadow's sources: ties a committed PMC summary to the kernel it measured"""
+    """sha1 over k_shadow's sources with comments and blank space stripped: ties a committed PMC
+    summary to the kernel code it measured (a comment edit keeps the tie, a code edit breaks it)"""
     import hashlib
+    import re
     h = hashlib.sha1()
     for f in SHADOW_SRCS:
-        with open(os.path.join(ROOT, f), "rb") as fh:
-            h.update(fh.read())
+        with open(os.path.join(ROOT, f), encoding="utf-8") as fh:
+            code = re.sub(r"/\*.*?\*/", " ", fh.read(), flags=re.S)
+        code = re.sub(r"//[^\n]*", " ", code)
+        h.update(" ".join(code.split()).encode())
     return h.hexdigest()[:16]
 
 
