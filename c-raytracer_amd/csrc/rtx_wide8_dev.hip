@@ -5,7 +5,8 @@
  * builder left in HBM, so a GPU build never round-trips the tree through the host.
  *
  *   k_w8d_parent  parent of every BVH2 node; leaf boxes from their parent's record
- *   k_w8d_up      bottom-up (atomic arrival counters, as the builders' refit): the emitters'
+ *   k_w8d_leaves / k_w8d_depth / k_w8d_bucket / k_w8d_level
+ *                 bottom-up, one launch per BVH2 depth from the deepest: the emitters'
  *                 primitives left out, boxes refitted over what remains, and the cost table
  *                 C(n, 1..8) with its choices per node (a node with one side left becomes an
  *                 alias of that side, as the host collapse's join)
@@ -16,12 +17,14 @@
  *   k_w8d_scalar  the scalar-path copies (DW8S) of the inner entries
  * Levels are laid out breadth-first (the host collapse: depth-first); the walk reads either.
  * Single-primitive BVH2 leaves only (the default RTX_OPT_BVH_LEAF 1); rtx_api.cpp keeps the
- * host collapse for larger leaves and for device groups.
+ * host collapse for larger leaves.
  */
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <float.h>
 #include <stdint.h>
+
+#include <vector>
 
 #include "rtx.h"
 #include "rtx_device.h"
@@ -43,17 +46,6 @@ __device__ __forceinline__ float area6(const float (&b)[6])
 	return dx * dy + dy * dz + dz * dx;
 }
 
-__device__ __forceinline__ float ald(const float *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ uint32_t ald(const uint32_t *p)
-{
-	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void ast(float *p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ void ast(uint32_t *p, uint32_t v)
-{
-	__hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 /* tree node id of a BVH2 child ref: inner record index, or nnodes + primitive index */
 __device__ __forceinline__ uint32_t child_id(uint32_t ref, uint32_t nnodes)
 {
@@ -70,7 +62,6 @@ struct W8Tree {
 	uint2 *ekids;     /* [nnodes]: effective children of full inner nodes */
 	float *cost;      /* [nnodes + nb][8]: C(n, j) for j = 1..8 */
 	int8_t *pick;     /* [nnodes + nb][8] */
-	uint32_t *arrive; /* [nnodes] */
 };
 
 } // namespace
@@ -94,95 +85,149 @@ __global__ __launch_bounds__(W8D_T) void k_w8d_parent(W8Tree T)
 	}
 	if (i == 0)
 		T.parent[0] = RTX_NONE;
-	T.arrive[i] = 0;
 }
 
-/* bottom-up: one thread per primitive climbs while it is the second to arrive at a node */
-__global__ __launch_bounds__(W8D_T) void k_w8d_up(W8Tree T, const uint32_t *__restrict__ skip_obj, uint32_t num_objects)
+/* a primitive's tree node: left out (an emitter) or a leaf slot of cost A * c_prim */
+__device__ __forceinline__ void w8d_leaf(const W8Tree &T, uint32_t k, const uint32_t *__restrict__ skip_obj, uint32_t num_objects)
 {
-	const uint32_t k = blockIdx.x * W8D_T + threadIdx.x;
-	if (k >= T.nb)
-		return;
 	const uint32_t leaf = T.nnodes + k;
 	const DPrim &p = *(const DPrim *)(T.recs + leaf);
 	const uint32_t obj = __float_as_uint(p.b[3]);
 	const bool skip = obj < num_objects && ((skip_obj[obj >> 5] >> (obj & 31u)) & 1u);
 	if (skip) {
-		ast(&T.state[leaf], W8D_EMPTY);
-		ast(&T.eff[leaf], RTX_NONE);
-	} else {
-		float b[6];
-		for (int a = 0; a < 6; a++)
-			b[a] = T.box[6 * (size_t)leaf + a];
-		const float c = area6(b) * RTX_W8_C_PRIM;
-		for (int j = 0; j < 8; j++) {
-			ast(&T.cost[8 * (size_t)leaf + j], c);
-			T.pick[8 * (size_t)leaf + j] = 0;
-		}
-		ast(&T.state[leaf], W8D_FULL);
-		ast(&T.eff[leaf], leaf);
+		T.state[leaf] = W8D_EMPTY;
+		T.eff[leaf] = RTX_NONE;
+		return;
 	}
-	uint32_t node = T.parent[leaf];
-	while (node != RTX_NONE) {
-		__threadfence();
-		if (atomicAdd(&T.arrive[node], 1u) == 0)
-			return; /* the sibling's thread finishes this node */
-		__threadfence();
-		const DNode &d = T.recs[node];
-		const uint32_t ea = ald(&T.eff[child_id(d.ref0, T.nnodes)]), eb = ald(&T.eff[child_id(d.ref1, T.nnodes)]);
-		if (ea == RTX_NONE && eb == RTX_NONE) {
-			ast(&T.state[node], W8D_EMPTY);
-			ast(&T.eff[node], RTX_NONE);
-		} else if (ea == RTX_NONE || eb == RTX_NONE) { /* one side left: the node is that side */
-			ast(&T.state[node], W8D_ALIAS);
-			ast(&T.eff[node], ea == RTX_NONE ? eb : ea);
+	float b[6];
+	for (int a = 0; a < 6; a++)
+		b[a] = T.box[6 * (size_t)leaf + a];
+	const float c = area6(b) * RTX_W8_C_PRIM;
+	for (int j = 0; j < 8; j++) {
+		T.cost[8 * (size_t)leaf + j] = c;
+		T.pick[8 * (size_t)leaf + j] = 0;
+	}
+	T.state[leaf] = W8D_FULL;
+	T.eff[leaf] = leaf;
+}
+
+/* an inner BVH2 node once both children are done: empty, an alias of its one remaining side, or
+ * a full node with its refitted box and cost table C(n, 1..8) (the host programme,
+ * rtx_wide8.cpp Builder::solve) */
+__device__ __forceinline__ void w8d_node(const W8Tree &T, uint32_t node)
+{
+	const DNode &d = T.recs[node];
+	const uint32_t ea = T.eff[child_id(d.ref0, T.nnodes)], eb = T.eff[child_id(d.ref1, T.nnodes)];
+	if (ea == RTX_NONE && eb == RTX_NONE) {
+		T.state[node] = W8D_EMPTY;
+		T.eff[node] = RTX_NONE;
+		return;
+	}
+	if (ea == RTX_NONE || eb == RTX_NONE) { /* one side left: the node is that side */
+		T.state[node] = W8D_ALIAS;
+		T.eff[node] = ea == RTX_NONE ? eb : ea;
+		return;
+	}
+	float b[6], L[9], R[9];
+	for (int a = 0; a < 3; a++) {
+		b[a] = fminf(T.box[6 * (size_t)ea + a], T.box[6 * (size_t)eb + a]);
+		b[3 + a] = fmaxf(T.box[6 * (size_t)ea + 3 + a], T.box[6 * (size_t)eb + 3 + a]);
+	}
+	for (int j = 1; j <= 8; j++) {
+		L[j] = T.cost[8 * (size_t)ea + j - 1];
+		R[j] = T.cost[8 * (size_t)eb + j - 1];
+	}
+	float D[9], C[9];
+	int8_t K[9], P[9];
+	for (int j = 2; j <= 8; j++) {
+		D[j] = FLT_MAX;
+		K[j] = 1;
+		for (int q = 1; q < j; q++) {
+			const float v = L[q] + R[j - q];
+			if (v < D[j]) {
+				D[j] = v;
+				K[j] = (int8_t)q;
+			}
+		}
+	}
+	C[1] = area6(b) * 1.0f + D[8];
+	P[1] = -1;
+	for (int j = 2; j <= 8; j++) {
+		if (D[j] < C[j - 1]) {
+			C[j] = D[j];
+			P[j] = K[j];
 		} else {
-			float b[6], L[9], R[9];
-			for (int a = 0; a < 3; a++) {
-				b[a] = fminf(ald(&T.box[6 * (size_t)ea + a]), ald(&T.box[6 * (size_t)eb + a]));
-				b[3 + a] = fmaxf(ald(&T.box[6 * (size_t)ea + 3 + a]), ald(&T.box[6 * (size_t)eb + 3 + a]));
-			}
-			for (int j = 1; j <= 8; j++) {
-				L[j] = ald(&T.cost[8 * (size_t)ea + j - 1]);
-				R[j] = ald(&T.cost[8 * (size_t)eb + j - 1]);
-			}
-			/* the host programme (rtx_wide8.cpp Builder::solve) */
-			float D[9], C[9];
-			int8_t K[9], P[9];
-			for (int j = 2; j <= 8; j++) {
-				D[j] = FLT_MAX;
-				K[j] = 1;
-				for (int q = 1; q < j; q++) {
-					const float v = L[q] + R[j - q];
-					if (v < D[j]) {
-						D[j] = v;
-						K[j] = (int8_t)q;
-					}
-				}
-			}
-			C[1] = area6(b) * 1.0f + D[8];
-			P[1] = -1;
-			for (int j = 2; j <= 8; j++) {
-				if (D[j] < C[j - 1]) {
-					C[j] = D[j];
-					P[j] = K[j];
-				} else {
-					C[j] = C[j - 1];
-					P[j] = 0;
-				}
-			}
-			for (int a = 0; a < 6; a++)
-				ast(&T.box[6 * (size_t)node + a], b[a]);
-			for (int j = 1; j <= 8; j++) {
-				ast(&T.cost[8 * (size_t)node + j - 1], C[j]);
-				T.pick[8 * (size_t)node + j - 1] = P[j];
-			}
-			T.ekids[node] = make_uint2(ea, eb);
-			ast(&T.state[node], W8D_FULL);
-			ast(&T.eff[node], node);
+			C[j] = C[j - 1];
+			P[j] = 0;
 		}
-		node = T.parent[node];
 	}
+	for (int a = 0; a < 6; a++)
+		T.box[6 * (size_t)node + a] = b[a];
+	for (int j = 1; j <= 8; j++) {
+		T.cost[8 * (size_t)node + j - 1] = C[j];
+		T.pick[8 * (size_t)node + j - 1] = P[j];
+	}
+	T.ekids[node] = make_uint2(ea, eb);
+	T.state[node] = W8D_FULL;
+	T.eff[node] = node;
+}
+
+/* bottom-up, level by level (no arrival counters or device-scope fences): every primitive's
+ * leaf, then each inner node's depth (its parent chain) bucketed by depth, then one launch per
+ * depth from the deepest, each node's children finished by the launches before */
+__global__ __launch_bounds__(W8D_T) void k_w8d_leaves(W8Tree T, const uint32_t *__restrict__ skip_obj, uint32_t num_objects)
+{
+	const uint32_t k = blockIdx.x * W8D_T + threadIdx.x;
+	if (k < T.nb)
+		w8d_leaf(T, k, skip_obj, num_objects);
+}
+#define W8D_MAXDEPTH 1024
+/* each inner node's depth (its parent chain), counted per depth: a workgroup counts in LDS and
+ * adds its counts once (one global atomic per depth per workgroup, not per node: the few depth
+ * counters serialised 327K atomics, 1.6 ms) */
+__global__ __launch_bounds__(W8D_T) void k_w8d_depth(W8Tree T, uint32_t *__restrict__ depth, uint32_t *__restrict__ hist)
+{
+	__shared__ uint32_t h[W8D_MAXDEPTH + 1];
+	for (uint32_t b = threadIdx.x; b <= W8D_MAXDEPTH; b += W8D_T)
+		h[b] = 0;
+	__syncthreads();
+	const uint32_t i = blockIdx.x * W8D_T + threadIdx.x;
+	if (i < T.nnodes) {
+		uint32_t d = 0;
+		for (uint32_t n = T.parent[i]; n != RTX_NONE && d < W8D_MAXDEPTH; n = T.parent[n])
+			d++;
+		depth[i] = d;
+		atomicAdd(&h[d], 1u); /* d = W8D_MAXDEPTH: too deep, the host gives up */
+	}
+	__syncthreads();
+	for (uint32_t b = threadIdx.x; b <= W8D_MAXDEPTH; b += W8D_T)
+		if (h[b])
+			atomicAdd(&hist[b], h[b]);
+}
+/* the inner nodes bucketed by depth: a workgroup ranks its nodes per depth in LDS and reserves
+ * each depth's range with one global atomic */
+__global__ __launch_bounds__(W8D_T) void k_w8d_bucket(uint32_t n, const uint32_t *__restrict__ depth, uint32_t *__restrict__ cursor,
+						      uint32_t *__restrict__ order)
+{
+	__shared__ uint32_t cnt[W8D_MAXDEPTH], base[W8D_MAXDEPTH];
+	for (uint32_t b = threadIdx.x; b < W8D_MAXDEPTH; b += W8D_T)
+		cnt[b] = 0;
+	__syncthreads();
+	const uint32_t i = blockIdx.x * W8D_T + threadIdx.x;
+	const uint32_t d = i < n ? depth[i] : 0u, r = i < n ? atomicAdd(&cnt[d], 1u) : 0u;
+	__syncthreads();
+	for (uint32_t b = threadIdx.x; b < W8D_MAXDEPTH; b += W8D_T)
+		if (cnt[b])
+			base[b] = atomicAdd(&cursor[b], cnt[b]);
+	__syncthreads();
+	if (i < n)
+		order[base[d] + r] = i;
+}
+__global__ __launch_bounds__(W8D_T) void k_w8d_level(W8Tree T, const uint32_t *__restrict__ nodes, uint32_t m)
+{
+	const uint32_t i = blockIdx.x * W8D_T + threadIdx.x;
+	if (i < m)
+		w8d_node(T, nodes[i]);
 }
 
 /* one wide node of a level: its slots, their order, the quantised entry, its inner children */
@@ -414,13 +459,14 @@ extern "C" hipError_t rtx_w8_collapse_device(const DNode *recs, uint32_t nnodes,
 	T.recs = recs;
 	T.nnodes = nnodes;
 	T.nb = nb;
-	T.parent = T.state = T.eff = T.arrive = nullptr;
+	T.parent = T.state = T.eff = nullptr;
 	T.box = T.cost = nullptr;
 	T.ekids = nullptr;
 	T.pick = nullptr;
 	DW8 *w8 = nullptr, *w8f = nullptr;
 	DW8S *w8s = nullptr;
 	uint32_t *lm = nullptr, *lmf = nullptr, *nxt = nullptr, *ncnt = nullptr, *noff = nullptr, *hst = nullptr;
+	uint32_t *hhist = nullptr, *dhist = nullptr, *ddepth = nullptr, *dorder = nullptr; /* the bottom-up pass's depth buckets */
 	uint2 *items = nullptr, *items2 = nullptr;
 	void *temp = nullptr;
 	const size_t cap = 2 + 8 * (size_t)nnodes; /* entries: at most one wide node per inner record */
@@ -437,7 +483,6 @@ extern "C" hipError_t rtx_w8_collapse_device(const DNode *recs, uint32_t nnodes,
 	TRY(hipMalloc(&T.ekids, (size_t)nnodes * 8));
 	TRY(hipMalloc(&T.cost, nt * 32));
 	TRY(hipMalloc(&T.pick, nt * 8));
-	TRY(hipMalloc(&T.arrive, (size_t)nnodes * 4));
 	TRY(hipMalloc(&w8, cap * sizeof(DW8)));
 	TRY(hipMalloc(&lm, cap * 4));
 	TRY(hipMalloc(&nxt, 8 * (size_t)nnodes * 4));
@@ -446,12 +491,44 @@ extern "C" hipError_t rtx_w8_collapse_device(const DNode *recs, uint32_t nnodes,
 	TRY(hipMalloc(&items, (size_t)nnodes * 8));
 	TRY(hipMalloc(&items2, (size_t)nnodes * 8));
 	TRY(hipHostMalloc(&hst, 16 * 4));
+	TRY(hipHostMalloc(&hhist, (W8D_MAXDEPTH + 1) * 4));
+	TRY(hipMalloc(&dhist, (W8D_MAXDEPTH + 1) * 4));
+	TRY(hipMalloc(&ddepth, (size_t)nnodes * 4));
+	TRY(hipMalloc(&dorder, (size_t)nnodes * 4));
 	TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, ncnt, noff, (int)nnodes, st));
 	TRY(hipMalloc(&temp, tb));
 	hipLaunchKernelGGL(k_w8d_parent, dim3((nnodes + W8D_T - 1) / W8D_T), dim3(W8D_T), 0, st, T);
 	TRY(hipGetLastError());
-	hipLaunchKernelGGL(k_w8d_up, dim3((nb + W8D_T - 1) / W8D_T), dim3(W8D_T), 0, st, T, skip_obj, num_objects);
+	hipLaunchKernelGGL(k_w8d_leaves, dim3((nb + W8D_T - 1) / W8D_T), dim3(W8D_T), 0, st, T, skip_obj, num_objects);
+	TRY(hipMemsetAsync(dhist, 0, (W8D_MAXDEPTH + 1) * 4, st));
+	hipLaunchKernelGGL(k_w8d_depth, dim3((nnodes + W8D_T - 1) / W8D_T), dim3(W8D_T), 0, st, T, ddepth, dhist);
 	TRY(hipGetLastError());
+	TRY(hipMemcpyAsync(hhist, dhist, (W8D_MAXDEPTH + 1) * 4, hipMemcpyDeviceToHost, st));
+	TRY(hipStreamSynchronize(st));
+	{
+		if (hhist[W8D_MAXDEPTH]) { /* a BVH2 deeper than W8D_MAXDEPTH: no tree (the walks fall back) */
+			e = hipSuccess;
+			goto done;
+		}
+		uint32_t maxd = 0, acc = 0;
+		std::vector<uint32_t> off(W8D_MAXDEPTH + 1, 0);
+		for (uint32_t d = 0; d < W8D_MAXDEPTH; d++) {
+			off[d] = acc;
+			acc += hhist[d];
+			if (hhist[d])
+				maxd = d;
+		}
+		TRY(hipMemcpyAsync(dhist, off.data(), W8D_MAXDEPTH * 4, hipMemcpyHostToDevice, st));
+		hipLaunchKernelGGL(k_w8d_bucket, dim3((nnodes + W8D_T - 1) / W8D_T), dim3(W8D_T), 0, st, nnodes, ddepth, dhist, dorder);
+		TRY(hipGetLastError());
+		for (uint32_t d = maxd + 1; d-- > 0;)
+			if (hhist[d]) {
+				hipLaunchKernelGGL(k_w8d_level, dim3((hhist[d] + W8D_T - 1) / W8D_T), dim3(W8D_T), 0, st, T, dorder + off[d],
+						   hhist[d]);
+				TRY(hipGetLastError());
+			}
+		TRY(hipStreamSynchronize(st)); /* off (host memory) stays alive until the copy has run */
+	}
 	/* the root: its effective node and box -> the frame (rtx_wide8_build's) */
 	TRY(hipMemcpyAsync(&hst[0], T.eff, 4, hipMemcpyDeviceToHost, st));
 	TRY(hipStreamSynchronize(st));
@@ -529,7 +606,6 @@ done:
 	(void)hipFree(T.ekids);
 	(void)hipFree(T.cost);
 	(void)hipFree(T.pick);
-	(void)hipFree(T.arrive);
 	(void)hipFree(w8);
 	(void)hipFree(lm);
 	(void)hipFree(nxt);
@@ -542,6 +618,10 @@ done:
 	(void)hipFree(w8s);
 	(void)hipFree(lmf);
 	(void)hipHostFree(hst);
+	(void)hipHostFree(hhist);
+	(void)hipFree(dhist);
+	(void)hipFree(ddepth);
+	(void)hipFree(dorder);
 	return e;
 }
 
