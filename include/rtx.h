@@ -234,7 +234,8 @@ enum {
 };
 
 int rtx_device_count(int *count);
-/* Open a context on HIP device `device` (must be gfx950). */
+/* Open a context on HIP device `device` (must be gfx950).  Loads the library's device code on
+ * that device and primes host-to-device copies once (~0.1 s), so uploads and renders do not. */
 int rtx_open(int device, rtx_ctx **out);
 /* Flatten + copy the scene to the device, build the BVH (replaces accel_init). */
 int rtx_upload_scene(rtx_ctx *ctx, const rtx_scene_desc *scene);
