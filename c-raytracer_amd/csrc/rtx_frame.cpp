@@ -54,24 +54,34 @@ static unsigned host_threads()
 	return std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
 }
 
-/* f(begin, end, chunk) over [0, n) in contiguous chunks, one per thread (serially below 32K) */
-template <class F> static unsigned parallel_chunks(size_t n, F f)
+/* f(begin, end, chunk) over [0, n) in contiguous chunks, one per thread, each of at least `grain`
+ * items (serially when n < 2 grain) */
+template <class F> static unsigned parallel_chunks(size_t n, F f, size_t grain = 16384)
 {
-	const unsigned t = n < 32768 ? 1u : (unsigned)std::min<size_t>(host_threads(), (n + 16383) / 16384);
+	const unsigned t = n < 2 * grain ? 1u : (unsigned)std::min<size_t>(host_threads(), (n + grain - 1) / grain);
 	if (t <= 1) {
 		f((size_t)0, n, 0u);
 		return 1;
 	}
 	std::vector<std::thread> th;
-	for (unsigned k = 1; k < t; k++)
-		th.emplace_back(f, n * k / t, n * (k + 1) / t, k);
+	unsigned k = 1;
+	try {
+		for (; k < t; k++)
+			th.emplace_back(f, n * k / t, n * (k + 1) / t, k);
+	} catch (...) { /* no more threads: the rest of the chunks on this one */
+		for (; k < t; k++)
+			f(n * k / t, n * (k + 1) / t, k);
+	}
 	f((size_t)0, n / t, 0u);
 	for (auto &x : th)
 		x.join();
 	return t;
 }
 
-unsigned rtx_host_parallel(size_t n, const std::function<void(size_t, size_t, unsigned)> &f) { return parallel_chunks(n, f); }
+unsigned rtx_host_parallel(size_t n, const std::function<void(size_t, size_t, unsigned)> &f, size_t grain)
+{
+	return parallel_chunks(n, f, grain);
+}
 
 /* per-object boxes lo / hi (3 floats each) by box(k, l, h) and their union blo / bhi */
 template <class B> static void boxes_and_union(size_t nb, float *lo, float *hi, float blo[3], float bhi[3], B box)
@@ -106,13 +116,13 @@ static double half_area(const double lo[3], const double hi[3])
 	return x * y + y * z + z * x;
 }
 
-/* sum of the sampled triangles' box half-areas in the frame with rows r */
-static double frame_cost(const rtx_scene_desc *sc, const std::vector<uint32_t> &tris, const double (*r)[3])
+/* sum of the sampled triangles' box half-areas in the frame with rows r; v: the sample's
+ * vertices, 9 floats per triangle (gathered once, so the candidates do not chase the objects) */
+static double frame_cost(const std::vector<float> &v, const double (*r)[3])
 {
 	double cost = 0;
-	for (uint32_t oi : tris) {
-		const rtx_object &o = sc->objects[oi];
-		const float *p[3] = { o.p0, o.p1, o.p2 };
+	for (size_t t = 0; t < v.size(); t += 9) {
+		const float *p[3] = { &v[t], &v[t + 3], &v[t + 6] };
 		double lo[3] = { DBL_MAX, DBL_MAX, DBL_MAX }, hi[3] = { -DBL_MAX, -DBL_MAX, -DBL_MAX };
 		for (int k = 0; k < 3; k++)
 			for (int i = 0; i < 3; i++) {
@@ -188,8 +198,13 @@ double rtx_frame_choose(const rtx_scene_desc *sc, const std::vector<uint32_t> &b
 		return 1.0;
 	/* candidates: the frames of the largest sampled triangles (ties: lower object index) */
 	std::vector<std::pair<double, uint32_t>> by_area;
+	std::vector<float> sv;
+	sv.reserve(9 * sample.size());
 	for (uint32_t oi : sample) {
 		const rtx_object &o = sc->objects[oi];
+		sv.insert(sv.end(), o.p0, o.p0 + 3);
+		sv.insert(sv.end(), o.p1, o.p1 + 3);
+		sv.insert(sv.end(), o.p2, o.p2 + 3);
 		const double c[3] = { (double)o.e1[1] * o.e2[2] - (double)o.e1[2] * o.e2[1],
 				      (double)o.e1[2] * o.e2[0] - (double)o.e1[0] * o.e2[2],
 				      (double)o.e1[0] * o.e2[1] - (double)o.e1[1] * o.e2[0] };
@@ -212,14 +227,11 @@ double rtx_frame_choose(const rtx_scene_desc *sc, const std::vector<uint32_t> &b
 		cost[k] = 0.0;
 	}
 	cost[0] = 0.0;
-	{
-		std::vector<std::thread> th;
-		for (size_t k = 0; k < nc; k++)
+	rtx_host_parallel(nc, [&](size_t b, size_t e, unsigned) {
+		for (size_t k = b; k < e; k++)
 			if (cost[k] == 0.0)
-				th.emplace_back([&, k] { cost[k] = frame_cost(sc, sample, (const double(*)[3]) & rs[9 * k]); });
-		for (auto &x : th)
-			x.join();
-	}
+				cost[k] = frame_cost(sv, (const double(*)[3]) & rs[9 * k]);
+	}, 1);
 	const double c_id = cost[0];
 	double c_best = c_id;
 	size_t best = 0;

@@ -13,9 +13,10 @@
 
 int rtx_fail(int code, const char *fmt, ...);
 
-/* f(begin, end, chunk) over [0, n) in contiguous chunks on host threads (RTX_HOST_THREADS, else
- * OMP_NUM_THREADS, else at most 16; serially below 32K); returns the chunk count */
-unsigned rtx_host_parallel(size_t n, const std::function<void(size_t, size_t, unsigned)> &f);
+/* f(begin, end, chunk) over [0, n) in contiguous chunks of at least `grain` items on host threads
+ * (RTX_HOST_THREADS, else OMP_NUM_THREADS, else at most 16; serially when n < 2 grain, and on this
+ * thread when no more can start); returns the chunk count */
+unsigned rtx_host_parallel(size_t n, const std::function<void(size_t, size_t, unsigned)> &f, size_t grain = 16384);
 /* object o's world box (sphere_get_corners / triangle_get_corners, object.c:277-282, 375-388),
  * padded for the walks' FMA slab test */
 void rtx_world_box(const rtx_object &o, float lo[3], float hi[3]);
