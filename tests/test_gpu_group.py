@@ -23,7 +23,7 @@ from rtxpy import abi
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("name", ["s5_path2", "st_amb"])
+@pytest.mark.parametrize("name", ["s5_path2", "st_amb", "s6_amb"])
 def test_gpu_group_of_one_matches_render(name):
     scene, frame, params, _ = C.load_config(name)
     r = rtxpy.Renderer(0)
