@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "bvh_build.h"
+#include "rtx_frame.h"
 #include "rtx_internal.h"
 #include "rtx_quant.h"
 #include "rtx_scene.h"
@@ -179,60 +180,94 @@ int main(int argc, char **argv)
 			bhi[a] = std::max(bhi[a], hi[3 * k + a]);
 		}
 	}
-	BvhConfig cfg;
-	BvhOutput bvh;
-	const auto t0 = std::chrono::steady_clock::now();
-	bvh_build(BvhInput{ nb, lo.data(), hi.data() }, cfg, bvh);
-	const auto t1 = std::chrono::steady_clock::now();
-	const uint32_t nnodes = (uint32_t)bvh.nodes.size();
-	std::vector<DPrim> prims(nb);
-	for (uint32_t k = 0; k < nb; k++) {
-		const rtx_object &o = sc->objects[bounded[bvh.order[k]]];
-		DPrim &p = prims[k];
-		memset(&p, 0, sizeof(p));
-		memcpy(p.a, o.p0, 12);
-		p.a[3] = o.epsilon;
-		if (o.type == RTX_SPHERE)
-			p.b[0] = o.radius;
-		else {
-			memcpy(p.b, o.e1, 12);
-			memcpy(p.c, o.e2, 12);
-		}
-		uint32_t meta = ((uint32_t)o.type << 24) | (uint32_t)o.material;
-		if (sc->materials[o.material].transparent)
-			meta |= RTX_META_TRANSPARENT;
-		const uint32_t oi = bounded[bvh.order[k]];
-		memcpy(&p.b[3], &oi, 4);
-		memcpy(&p.c[3], &meta, 4);
-	}
-	auto dref = [&](uint32_t r) -> uint32_t {
-		if (r == RTX_EMPTY_REF)
-			return r;
-		if (r & RTX_LEAF_BIT) {
-			const uint32_t first = (r >> 4) & 0x7FFFFFFu, cnt = (r & 15u) + 1;
-			return (nnodes + first) * (uint32_t)sizeof(DNode) | RTX_REF_LEAF | (cnt - 1);
-		}
-		return r * (uint32_t)sizeof(DNode);
+	/* a BVH2 over boxes bl / bh with its primitive records in leaf order (rtx_build_scene's host path) */
+	struct Tree2 {
+		BvhOutput bvh;
+		std::vector<DPrim> prims;
+		std::vector<DNode> inner;
+		uint32_t nnodes = 0, root = RTX_EMPTY_REF;
 	};
-	std::vector<DNode> inner = bvh.nodes;
-	for (DNode &d : inner) {
-		d.ref0 = dref(d.ref0);
-		d.ref1 = dref(d.ref1);
+	auto build2 = [&](const float *bl, const float *bh, Tree2 &T) {
+		BvhConfig cfg;
+		bvh_build(BvhInput{ nb, bl, bh }, cfg, T.bvh);
+		T.nnodes = (uint32_t)T.bvh.nodes.size();
+		T.prims.assign(nb, DPrim{});
+		for (uint32_t k = 0; k < nb; k++) {
+			const rtx_object &o = sc->objects[bounded[T.bvh.order[k]]];
+			DPrim &p = T.prims[k];
+			memset(&p, 0, sizeof(p));
+			memcpy(p.a, o.p0, 12);
+			p.a[3] = o.epsilon;
+			if (o.type == RTX_SPHERE)
+				p.b[0] = o.radius;
+			else {
+				memcpy(p.b, o.e1, 12);
+				memcpy(p.c, o.e2, 12);
+			}
+			uint32_t meta = ((uint32_t)o.type << 24) | (uint32_t)o.material;
+			if (sc->materials[o.material].transparent)
+				meta |= RTX_META_TRANSPARENT;
+			const uint32_t oi = bounded[T.bvh.order[k]];
+			memcpy(&p.b[3], &oi, 4);
+			memcpy(&p.c[3], &meta, 4);
+		}
+		const uint32_t nn = T.nnodes;
+		auto dref = [nn](uint32_t r) -> uint32_t {
+			if (r == RTX_EMPTY_REF)
+				return r;
+			if (r & RTX_LEAF_BIT) {
+				const uint32_t first = (r >> 4) & 0x7FFFFFFu, cnt = (r & 15u) + 1;
+				return (nn + first) * (uint32_t)sizeof(DNode) | RTX_REF_LEAF | (cnt - 1);
+			}
+			return r * (uint32_t)sizeof(DNode);
+		};
+		T.inner = T.bvh.nodes;
+		for (DNode &d : T.inner) {
+			d.ref0 = dref(d.ref0);
+			d.ref1 = dref(d.ref1);
+		}
+		T.root = dref(T.bvh.root_ref);
+	};
+	const auto t0 = std::chrono::steady_clock::now();
+	Tree2 W; /* world boxes: the shade points' closest hits */
+	build2(lo.data(), hi.data(), W);
+	const auto t1 = std::chrono::steady_clock::now();
+	const BvhOutput &bvh = W.bvh;
+	const uint32_t nnodes = W.nnodes;
+	std::vector<DPrim> &prims = W.prims;
+	std::vector<DNode> &inner = W.inner;
+	/* the trees' frame as the uploader chooses it (rtx_frame.cpp; W8SIM_FRAME=0: the world axes),
+	 * the 8-wide tree built over the leaf boxes in it */
+	DTreeFrame tf;
+	const double fratio = getenv("W8SIM_FRAME") && !atoi(getenv("W8SIM_FRAME")) ? (rtx_frame_choose(sc, {}, blo, bhi, tf), 1.0)
+										 : rtx_frame_choose(sc, bounded, blo, bhi, tf);
+	double fpad = 0.0;
+	float tlo[3], thi[3];
+	memcpy(tlo, blo, 12);
+	memcpy(thi, bhi, 12);
+	Tree2 Fr;
+	const Tree2 *WT = &W;
+	std::vector<float> flo(3 * (size_t)nb), fhi(3 * (size_t)nb);
+	if (tf.rotated) {
+		fpad = rtx_frame_pad(rtx_frame_radius(blo, bhi, tf));
+		rtx_frame_boxes(sc, bounded, tf, fpad, flo.data(), fhi.data(), tlo, thi);
+		build2(flo.data(), fhi.data(), Fr);
+		WT = &Fr;
 	}
+	printf("tree frame: %s (leaf-box cost x%.3f)\n", tf.rotated ? "rotated" : "world", fratio);
 	QFrame F;
 	float ext_max = 0.f;
 	for (int a = 0; a < 3; a++)
-		ext_max = std::max(ext_max, bhi[a] - blo[a]);
+		ext_max = std::max(ext_max, thi[a] - tlo[a]);
 	for (int a = 0; a < 3; a++) {
-		F.qo[a] = blo[a];
-		F.qs[a] = 65533.f / std::max(bhi[a] - blo[a], std::max(ext_max, 1.f) * 1e-6f);
+		F.qo[a] = tlo[a];
+		F.qs[a] = 65533.f / std::max(thi[a] - tlo[a], std::max(ext_max, 1.f) * 1e-6f);
 	}
 	std::vector<DW8> w8;
 	std::vector<uint32_t> leafmap;
 	std::vector<uint32_t> emit_objs(sc->emitters, sc->emitters + sc->num_emitters);
 	bool skipped = false;
-	const DTreeFrame tf{};
-	const uint32_t depth = rtx_wide8_build(inner, nnodes, prims.data(), dref(bvh.root_ref), blo, bhi, emit_objs, tf, 0.0, F,
+	const uint32_t depth = rtx_wide8_build(WT->inner, WT->nnodes, WT->prims.data(), WT->root, tlo, thi, emit_objs, tf, fpad, F,
 					       skipped, w8, leafmap);
 	const auto t2 = std::chrono::steady_clock::now();
 	printf("host SAH build %.1f ms, 8-wide collapse %.1f ms\n", std::chrono::duration<double, std::milli>(t1 - t0).count(),
@@ -273,7 +308,7 @@ int main(int argc, char **argv)
 	printf("\n");
 	for (size_t i = 0; i < w8.size(); i++) /* leaf entries hold the primitive records */
 		if (leafmap[i] != RTX_NONE)
-			memcpy(&w8[i], &prims[leafmap[i]], 64);
+			memcpy(&w8[i], &WT->prims[leafmap[i]], 64);
 
 	/* shade points on bounded surfaces (area-weighted) and planes, light samples on emitter 0 */
 	std::mt19937_64 rng(12345);
@@ -295,7 +330,7 @@ int main(int argc, char **argv)
 	const float qsi[3] = { 1.f / F.qs[0], 1.f / F.qs[1], 1.f / F.qs[2] };
 	/* shade points as the bench frame makes them: primary hits of sampled pixels, then -n GI
 	 * hits from each (uniform hemisphere about the normal, render.c:231-289) */
-	Scene2 S2{ sc, &inner, &prims, nnodes, dref(bvh.root_ref) };
+	Scene2 S2{ sc, &inner, &prims, nnodes, W.root };
 	rtx_frame fr;
 	rtx_frame_setup(&sc->camera, 1920, 1080, &fr);
 	std::vector<std::array<float, 3>> pts;
@@ -375,14 +410,18 @@ int main(int argc, char **argv)
 				const double dist = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
 				for (int a = 0; a < 3; a++)
 					d[a] /= dist;
-				double invq[3], oi[3];
+				double invq[3], oi[3], ob[3], db[3];
+				for (int a = 0; a < 3; a++) { /* the ray in the trees' frame (boxes); primitives in world space */
+					ob[a] = tf.rotated ? tf.r[a][0] * (P[0] - tf.c[0]) + tf.r[a][1] * (P[1] - tf.c[1]) + tf.r[a][2] * (P[2] - tf.c[2]) : P[a];
+					db[a] = tf.rotated ? tf.r[a][0] * d[0] + tf.r[a][1] * d[1] + tf.r[a][2] * d[2] : d[a];
+				}
 				int oct = 0;
 				for (int a = 0; a < 3; a++) {
-					const double inv = fabs(d[a]) > 1e-30 ? 1.0 / d[a] : copysign(1e30, d[a]);
+					const double inv = fabs(db[a]) > 1e-30 ? 1.0 / db[a] : copysign(1e30, db[a]);
 					if (inv >= 0)
 						oct |= 1 << a;
 					invq[a] = inv * qsi[a];
-					oi[a] = (P[a] - F.qo[a]) * F.qs[a] * invq[a];
+					oi[a] = (ob[a] - F.qo[a]) * F.qs[a] * invq[a];
 				}
 				const uint32_t K = ~(uint32_t)oct & 7u;
 				/* the walk: node, group register, stack; leaf hits counted per visit */
