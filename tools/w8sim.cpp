@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <array>
+#include <tuple>
 #include <random>
 #include <vector>
 
@@ -157,7 +158,7 @@ int main(int argc, char **argv)
 	for (uint32_t i = 0; i < sc->num_objects; i++)
 		if (sc->objects[i].type != RTX_PLANE)
 			bounded.push_back(i);
-	const uint32_t nb = (uint32_t)bounded.size();
+	uint32_t nb = (uint32_t)bounded.size();
 	std::vector<float> lo(3 * (size_t)nb), hi(3 * (size_t)nb);
 	float blo[3] = { FLT_MAX, FLT_MAX, FLT_MAX }, bhi[3] = { -FLT_MAX, -FLT_MAX, -FLT_MAX };
 	for (uint32_t k = 0; k < nb; k++) {
@@ -248,10 +249,57 @@ int main(int argc, char **argv)
 	Tree2 Fr;
 	const Tree2 *WT = &W;
 	std::vector<float> flo(3 * (size_t)nb), fhi(3 * (size_t)nb);
+	/* W8SIM_PAIRS=1: triangles whose frame boxes are identical (the two halves of an axis-aligned
+	 * face), same material, same epsilon, share one leaf slot; partner[k] = the other one */
+	std::vector<uint32_t> partner(sc->num_objects, RTX_NONE);
+	const bool pairs = getenv("W8SIM_PAIRS") && atoi(getenv("W8SIM_PAIRS"));
 	if (tf.rotated) {
 		fpad = rtx_frame_pad(rtx_frame_radius(blo, bhi, tf));
 		rtx_frame_boxes(sc, bounded, tf, fpad, flo.data(), fhi.data(), tlo, thi);
-		build2(flo.data(), fhi.data(), Fr);
+		if (pairs) {
+			std::vector<uint32_t> idx(nb);
+			for (uint32_t k = 0; k < nb; k++)
+				idx[k] = k;
+			const double g = 1e-4 * rtx_frame_radius(blo, bhi, tf); /* boxes equal to a 1e-4 radius grid */
+			auto key = [&](uint32_t k) {
+				const rtx_object &o = sc->objects[bounded[k]];
+				auto r = [&](float v) { return (long long)llround(v / g); };
+				return std::make_tuple(o.type, o.material, o.epsilon, r(flo[3 * k]), r(flo[3 * k + 1]), r(flo[3 * k + 2]),
+						       r(fhi[3 * k]), r(fhi[3 * k + 1]), r(fhi[3 * k + 2]));
+			};
+			std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return key(a) < key(b); });
+			std::vector<uint32_t> keep;
+			std::vector<uint32_t> blist;
+			for (size_t i = 0; i < nb;) {
+				size_t j = i + 1;
+				while (j < nb && key(idx[j]) == key(idx[i]))
+					j++;
+				if (j - i == 2 && sc->objects[bounded[idx[i]]].type == RTX_TRIANGLE) {
+					partner[bounded[idx[i]]] = bounded[idx[i + 1]];
+					keep.push_back(idx[i]);
+					for (int a = 0; a < 3; a++) { /* the slot's box: the union */
+						flo[3 * idx[i] + a] = std::min(flo[3 * idx[i] + a], flo[3 * idx[i + 1] + a]);
+						fhi[3 * idx[i] + a] = std::max(fhi[3 * idx[i] + a], fhi[3 * idx[i + 1] + a]);
+					}
+				} else
+					for (size_t q = i; q < j; q++)
+						keep.push_back(idx[q]);
+				i = j;
+			}
+			std::sort(keep.begin(), keep.end());
+			std::vector<float> plo, phi;
+			for (uint32_t k : keep) {
+				blist.push_back(bounded[k]);
+				plo.insert(plo.end(), &flo[3 * k], &flo[3 * k] + 3);
+				phi.insert(phi.end(), &fhi[3 * k], &fhi[3 * k] + 3);
+			}
+			printf("pairs: %zu units for %u primitives\n", keep.size(), nb);
+			bounded.swap(blist); /* build2 reads `bounded` and `nb` */
+			nb = (uint32_t)bounded.size();
+			build2(plo.data(), phi.data(), Fr);
+		} else {
+			build2(flo.data(), fhi.data(), Fr);
+		}
 		WT = &Fr;
 	}
 	printf("tree frame: %s (leaf-box cost x%.3f)\n", tf.rotated ? "rotated" : "world", fratio);
@@ -483,6 +531,17 @@ int main(int argc, char **argv)
 						nleaf_total++;
 						if ((meta & RTX_META_TRANSPARENT) || (meta >> 24) == RTX_SPHERE)
 							continue;
+						for (int half = 0; half < (partner[obj] != RTX_NONE ? 2 : 1); half++) {
+						DPrim pp = p;
+						if (half) { /* the pair's other triangle, in the same leaf round */
+							S.tris++;
+							const rtx_object &o2 = sc->objects[partner[obj]];
+							memcpy(pp.a, o2.p0, 12);
+							pp.a[3] = o2.epsilon;
+							memcpy(pp.b, o2.e1, 12);
+							memcpy(pp.c, o2.e2, 12);
+						}
+						const DPrim &p = pp;
 						/* opaque triangle: Moller-Trumbore in double */
 						const double e1[3] = { p.b[0], p.b[1], p.b[2] }, e2[3] = { p.c[0], p.c[1], p.c[2] };
 						const double h[3] = { d[1] * e2[2] - d[2] * e2[1], d[2] * e2[0] - d[0] * e2[2], d[0] * e2[1] - d[1] * e2[0] };
@@ -499,6 +558,7 @@ int main(int argc, char **argv)
 							block_at[l] = nleaf_total - 1;
 							/* postponed tests would have kept walking: record the rest of the walk
 							 * (the leaf hits of later visits) without stopping at the blocker */
+						}
 						}
 					}
 					leaves[l].push_back(nleaf);
