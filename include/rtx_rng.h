@@ -50,12 +50,27 @@ RTX_HD uint64_t rtx_key_child(uint64_t key, uint32_t tag)
 	return rtx_mix64(key + 0x9e3779b97f4a7c15ull * ((uint64_t)tag + 1u));
 }
 
-/* two uniform floats in [0,1) */
+/* 32-bit integer hash (C. Wellons' "lowbias32": two multiplies, full avalanche) */
+RTX_HD uint32_t rtx_hash32(uint32_t x)
+{
+	x ^= x >> 16;
+	x *= 0x21f0aaadu;
+	x ^= x >> 15;
+	x *= 0x735a2d97u;
+	x ^= x >> 15;
+	return x;
+}
+
+/* two uniform floats in [0,1).  The (key, stream) part is one splitmix64 round, the same for every
+ * index, so a wave whose lanes share the key and the stream (the 64 light samples of one shade
+ * point) computes it once in scalar registers; each index then costs two 32-bit hashes. */
 RTX_HD void rtx_draw2(uint64_t key, uint32_t stream, uint32_t index, float *u1, float *u2)
 {
-	uint64_t h = rtx_mix64(key ^ (((uint64_t)stream << 32) | index) * 0xd1b54a32d192ed03ull);
-	*u1 = (float)(uint32_t)(h >> 40) * (1.0f / 16777216.0f);
-	*u2 = (float)(uint32_t)((h >> 8) & 0xFFFFFFu) * (1.0f / 16777216.0f);
+	const uint64_t s = rtx_mix64(key ^ ((uint64_t)stream + 1u) * 0xd1b54a32d192ed03ull);
+	const uint32_t a = rtx_hash32((uint32_t)s ^ index);
+	const uint32_t b = rtx_hash32((uint32_t)(s >> 32) ^ a);
+	*u1 = (float)(a >> 8) * (1.0f / 16777216.0f);
+	*u2 = (float)(b >> 8) * (1.0f / 16777216.0f);
 }
 
 #endif
