@@ -1,0 +1,40 @@
+"""The drop-in, built and run: oracle/Makefile `dropin` compiles the reference's own main,
+scene loader (cJSON + its STL reader), camera and image writer from /root/reference with
+integration/rtx_render.c in place of accel.c and render.c, linked
+against lib/librtx.so.  That program renders the same frames as this repository's engine
+(lib/engine: our own scene loader and TIFF writer over the same library), float for float, so
+the scene the reference loads into its globals reaches the library unchanged through the
+adapter's flattening (rtx_export.h accessors).  Skipped where the binary was not built (no
+/root/reference when __graft_entry__.build() ran)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import conftest as C
+import rtxpy
+import standins
+
+pytestmark = pytest.mark.gpu
+
+DROPIN = os.path.join(C.ROOT, "oracle", "_ref", "engine_dropin")
+
+
+@pytest.mark.skipif(not os.path.exists(DROPIN), reason="oracle/_ref/engine_dropin not built")
+@pytest.mark.parametrize("name", ["s1_amb", "s2_blinn_lin", "s3_path2", "s5_path2", "s6_amb"])
+def test_gpu_dropin_renders_what_the_engine_renders(name, tmp_path):
+    m = C.manifest()[name]
+    if "standin" in m["scene"]:
+        standins.ensure_scene(m["scene"].split("_standin")[0])
+    frames = []
+    for exe in (DROPIN, rtxpy.ENGINE):
+        out = str(tmp_path / (os.path.basename(exe) + ".tif"))
+        cmd = [exe, os.path.join("scenes", m["scene"]), out, str(m["width"]), str(m["height"]), "-f"] + m["flags"]
+        p = subprocess.run(cmd, cwd=C.GOLDEN, capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0, (exe, p.stdout[-2000:] + p.stderr[-2000:])
+        frames.append(rtxpy.read_tiff_raw(out))
+    (a, za), (b, zb) = frames
+    assert np.array_equal(za, zb), name
+    assert np.array_equal(a, b), (name, float(np.abs(a - b).max()))
+    assert (za > 0).any()

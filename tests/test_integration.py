@@ -49,3 +49,16 @@ def test_integration_md_carries_the_adapter_verbatim():
     for f in ("rtx_render.c", "rtx_export.h", "object_export.inc", "texture_export.inc"):
         text = open(os.path.join(INTEG, f)).read().strip()
         assert text in doc, f
+
+
+def test_dropin_binary_links_and_starts():
+    """oracle/Makefile `dropin` (built by __graft_entry__.build() where /root/reference exists):
+    the reference's main linked with the adapter and lib/librtx.so resolves every symbol and
+    starts (its --help exits before any device work).  The frames it renders are checked on the
+    GPU (tests/test_gpu_dropin.py)."""
+    import subprocess
+    exe = os.path.join(ROOT, "oracle", "_ref", "engine_dropin")
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref/engine_dropin not built (no /root/reference)")
+    p = subprocess.run([exe, "--help"], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0 and "Usage: ./engine <input> <output> <resolution>" in p.stdout
