@@ -1,11 +1,14 @@
 """The drop-in, built and run: oracle/Makefile `dropin` compiles the reference's own main,
 scene loader (cJSON + its STL reader), camera and image writer from /root/reference with
 integration/rtx_render.c in place of accel.c and render.c, linked
-against lib/librtx.so.  That program renders the same frames as this repository's engine
-(lib/engine: our own scene loader and TIFF writer over the same library), float for float, so
-the scene the reference loads into its globals reaches the library unchanged through the
-adapter's flattening (rtx_export.h accessors).  Skipped where the binary was not built (no
-/root/reference when __graft_entry__.build() ran)."""
+against lib/librtx.so, at -O2 (IEEE scene set-up).  That program renders the frames this
+repository's engine renders (lib/engine: our own scene loader and TIFF writer over the same
+library, the same counter RNG), bit for bit: the scene the reference loads into its globals
+reaches the library unchanged through the adapter's flattening (rtx_export.h accessors).
+(Built with Makefile.rt's -Ofast instead, the reference's camera and edge set-up carries its own
+contraction noise; frames then agree within SURVEY §8(c)'s -Ofast-vs-O2 floor on s1/s3/s5/s6
+and at relL1 5e-5 on s2.)  Skipped where the binary was not built (no /root/reference when
+__graft_entry__.build() ran)."""
 import os
 import subprocess
 
@@ -35,6 +38,6 @@ def test_gpu_dropin_renders_what_the_engine_renders(name, tmp_path):
         assert p.returncode == 0, (exe, p.stdout[-2000:] + p.stderr[-2000:])
         frames.append(rtxpy.read_tiff_raw(out))
     (a, za), (b, zb) = frames
-    assert np.array_equal(za, zb), name
-    assert np.array_equal(a, b), (name, float(np.abs(a - b).max()))
     assert (za > 0).any()
+    ok, info = C.compare_const(a, za, b, zb, **C.floor_tolerance(m))
+    assert np.array_equal(za, zb) and np.array_equal(a, b), (name, info, float(np.abs(a - b).max()))
