@@ -138,7 +138,51 @@ struct Stats {
 	/* lane visits of divergent steps by the node's level (root 0), and of steps where every walking
 	 * lane's node is at level <= L (a top-of-tree LDS copy of levels 0..L would serve them all) */
 	double dlevel[16] = {}, dstep_top[16] = {};
+	/* lane refill simulation (refill threshold RF_T[k]) */
+	double rf_steps[6] = {}, rf_usteps[6] = {}, rf_refills[6] = {};
 };
+static const int RF_T[6] = { 64, 48, 32, 16, 8, 1 };
+
+/* one point's light samples (their node-visit sequences) over one wave of 64 lanes that takes a
+ * new sample into a finished lane whenever at least T lanes are idle (T = 64: packets, today) */
+static void refill_sim(const std::vector<std::vector<uint32_t>> &seqs, int T, double &steps, double &usteps, double &refills)
+{
+	const size_t n = seqs.size();
+	size_t q = 0;
+	long cur[64];
+	size_t pos[64];
+	for (int l = 0; l < 64; l++)
+		cur[l] = -1;
+	for (;;) {
+		int walking = 0;
+		for (int l = 0; l < 64; l++)
+			if (cur[l] >= 0 && pos[l] < seqs[cur[l]].size())
+				walking++;
+		if (!walking && q >= n)
+			break;
+		if (q < n && (64 - walking >= T || !walking)) {
+			for (int l = 0; l < 64 && q < n; l++)
+				if (cur[l] < 0 || pos[l] >= seqs[cur[l]].size()) {
+					cur[l] = (long)q++;
+					pos[l] = 0;
+				}
+			refills++;
+			continue;
+		}
+		steps++;
+		uint32_t first = ~0u;
+		bool uni = true;
+		for (int l = 0; l < 64; l++)
+			if (cur[l] >= 0 && pos[l] < seqs[cur[l]].size()) {
+				const uint32_t nd = seqs[cur[l]][pos[l]];
+				if (first == ~0u)
+					first = nd;
+				uni &= nd == first;
+				pos[l]++;
+			}
+		usteps += uni;
+	}
+}
 
 int main(int argc, char **argv)
 {
@@ -428,6 +472,7 @@ int main(int argc, char **argv)
 	for (int pi = 0; pi < npts; pi++) {
 		const float P[3] = { pts[pi][0], pts[pi][1], pts[pi][2] };
 		/* packets of 64 light samples */
+		std::vector<std::vector<uint32_t>> allseq; /* every sample's node visits (immediate-test walk) */
 		for (uint32_t b0 = 0; b0 < nl; b0 += 64) {
 			std::vector<uint32_t> visits_lane, leaf_at; /* per-lane per-visit leaf hits */
 			std::vector<std::vector<uint32_t>> leaves(64), seq(64);
@@ -591,6 +636,8 @@ int main(int argc, char **argv)
 				maxv = std::max(maxv, nv_imm);
 				imm_len[l] = nv_imm;
 			}
+			for (uint32_t l = 0; l < 64 && b0 + l < nl; l++)
+				allseq.emplace_back(seq[l].begin(), seq[l].begin() + std::min<size_t>(seq[l].size(), imm_len[l]));
 			S.packets++;
 			/* postponed leaf tests: a leaf round only when >= T lanes hold pending leaves or no lane
 			 * has node work left (emitter leaves excluded, as a tree without emitters) */
@@ -690,7 +737,15 @@ int main(int argc, char **argv)
 				S.leaf_rounds += m;
 			}
 		}
+		for (int r = 0; r < 6; r++)
+			refill_sim(allseq, RF_T[r], S.rf_steps[r], S.rf_usteps[r], S.rf_refills[r]);
 	}
+	printf("lane refill (a finished lane takes the point's next light sample when >= T lanes are idle), per point:\n"
+	       "   T   wave steps (uniform)   refill rounds   cost (178/divergent + 95/uniform step + 220/refill)\n");
+	for (int k = 0; k < 6; k++)
+		printf("  %2d   %8.2f (%6.2f)   %8.2f   %9.0f\n", RF_T[k], S.rf_steps[k] / npts, S.rf_usteps[k] / npts,
+		       S.rf_refills[k] / npts,
+		       (178.0 * (S.rf_steps[k] - S.rf_usteps[k]) + 95.0 * S.rf_usteps[k] + 220.0 * S.rf_refills[k]) / npts);
 	printf("rays %.0f  visits/ray %.2f  boxes/ray %.2f  tris/ray %.3f  blocked %.3f  wave steps/packet %.2f  leaf "
 	       "rounds/packet %.2f  lanes/leaf round %.1f\n",
 	       S.rays, S.visits / S.rays, S.boxes / S.rays, S.tris / S.rays, S.blocked / S.rays, S.wave_steps / S.packets,
