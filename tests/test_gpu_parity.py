@@ -347,6 +347,47 @@ def test_gpu_edge_scene(renderer, args):
     assert abs(st.shadow_rays - ns) <= 0.005 * ns + 100
 
 
+ONE_OBJECT_SCENE = """{
+ "AmbientLight": [0.2, 0.2, 0.2],
+ "Camera": {"position": [0, 0, -3], "vector_x": [1, 0, 0], "vector_y": [0, 1, 0], "fov": 70, "focal_length": 1},
+ "Materials": [
+  {"id": 0, "ks": [0.2,0.2,0.2], "ka": [0.3,0.3,0.3], "kr": [0.2,0.2,0.2], "kt": [0,0,0], "ke": [0,0,0],
+   "shininess": 3, "refractive_index": 1, "texture": {"type": "uniform", "color": [0.8,0.5,0.2]}},
+  {"id": 1, "ks": [0,0,0], "ka": [0,0,0], "kr": [0,0,0], "kt": [0,0,0], "ke": [2,2,2],
+   "shininess": 1, "refractive_index": 1, "texture": {"type": "uniform", "color": [1,1,1]}}],
+ "Objects": [
+  {"type": "Plane", "parameters": {"material": 0, "position": [0, -1, 0], "normal": [0, 1, 0]}},
+  {"type": "Sphere", "parameters": {"material": 1, "lights": 4, "position": [0, 1, 1], "radius": 0.3}}
+ ]
+}"""
+
+
+@pytest.mark.parametrize("builder", [abi.RTX_BUILD_SAH_HOST, abi.RTX_BUILD_LBVH_GPU, abi.RTX_BUILD_PLOC_GPU,
+                                     abi.RTX_BUILD_SAH_GPU])
+@pytest.mark.parametrize("walk", [abi.RTX_WALK_AUTO, abi.RTX_WALK_BVH2, abi.RTX_WALK_W8])
+@pytest.mark.parametrize("args", [[], ["-g", "path", "-n", "3"]])
+def test_gpu_one_bounded_object(renderer, builder, walk, args):
+    """The smallest scene the reference accepts (scene.c needs one object and one emitter): one
+    bounded object, so the tree is a single leaf, under every builder and shadow walk (auto: the
+    linear test; the threaded BVH2; the 8-wide tree over a root leaf); shadow rays from the plane
+    to the sphere emitter."""
+    scene = rtxpy.Scene.parse(ONE_OBJECT_SCENE)
+    frame = scene.frame(24, 16)
+    params = rtxpy.params_from_args(args, rng=abi.RTX_RNG_COUNTER, seed=5)
+    renderer.set_builder(builder)
+    renderer.set_option(abi.RTX_OPT_SHADOW_WALK, walk)
+    try:
+        rgb, z, st = render(renderer, scene, frame, params)
+    finally:
+        renderer.set_builder(abi.RTX_BUILD_SAH_GPU)
+        renderer.set_option(abi.RTX_OPT_SHADOW_WALK, abi.RTX_WALK_AUTO)
+    o_rgb, o_z, (nc, ns) = oracle.render(scene, frame, params)
+    ok, info = C.compare_const(rgb, z, o_rgb, o_z)
+    assert ok, info
+    assert st.bvh_nodes == 0 and st.bvh_prims == 1
+    assert ns > 0 and abs(st.shadow_rays - ns) <= 0.005 * ns + 100
+
+
 def test_gpu_errors():
     r = rtxpy.Renderer(0)
     scene = rtxpy.Scene.load(os.path.join(C.SCENES, "scene1.json"))
