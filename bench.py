@@ -197,7 +197,13 @@ def cpu_reference(scene_file, flags, width, height, target_s, log):
     same scene and flags (Mrays/s is intensive: scale the resolution, not the spp).
     Both thread modes SURVEY §8(d) asks for are timed, `-m 1` and `-m max` (all host threads), each
     on a frame sized for ~target_s/2 of rendering; the faster is the baseline.  Rays are counted by
-    the instrumented build (engine_count_*) on the same config."""
+    the instrumented build (engine_count_*) on the same config.
+
+    The reference's row loop is OpenMP's static schedule (render.c:349-352: each thread gets a
+    contiguous block of ceil(H / threads) rows), so a frame with few rows leaves threads idle.  The
+    `-m max` frame (and its calibration frame) therefore has H a multiple of the thread count and at
+    least 4 rows per thread, H = 4·threads·k; only its width is fitted to the time target (the
+    reference's image plane keeps the horizontal field of view, image.c:41-42)."""
     import subprocess
     import tempfile
     refdir = os.path.join(ROOT, "oracle", "_ref")
@@ -238,19 +244,24 @@ def cpu_reference(scene_file, flags, width, height, target_s, log):
             modes = {}
             try:
                 for nthreads in (1, threads):
-                    # calibrate on a tiny frame, then size the frame for ~target_s/2 of rendering
-                    w, h = 16, 9
+                    # calibrate (pixels per second), then size the frame for ~target_s/2 of rendering
+                    w, h = (16, 9) if nthreads == 1 else (8, 4 * nthreads)
                     _, tr, _ = run(eng, w, h, nthreads)
-                    _, _, rays = run(cnt, w, h, nthreads)
-                    rate = rays / max(tr, 0.05)
-                    scale = min(64.0, max(1.0, rate * target_s / 2 / rays) ** 0.5)
-                    w, h = max(16, int(w * scale)), max(9, int(h * scale))
+                    px = w * h / max(tr, 0.05) * target_s / 2
+                    if nthreads == 1:
+                        scale = min(64.0, max(1.0, px / (w * h)) ** 0.5)
+                        w, h = max(16, int(w * scale)), max(9, int(h * scale))
+                    else:  # H = 4·threads·k rows (static row schedule), aspect at most 16:9
+                        k = max(1, int((px * 9 / 16) ** 0.5 / (4 * nthreads)))
+                        h = 4 * nthreads * k
+                        w = max(8, min((16 * h) // 9, int(round(px / h))))
                     _, tr, _ = run(eng, w, h, nthreads)
                     _, _, rays = run(cnt, w, h, nthreads)
                     log(f"cpu reference ({arch}, -m {'1' if nthreads == 1 else 'max'}): {w}x{h} "
                         f"{' '.join(flags)}: {rays} rays in {tr:.2f}s on {nthreads} threads")
                     modes[nthreads] = {"value": round(rays / tr / 1e6, 4), "cores": nthreads,
-                                       "seconds": round(tr, 2), "rays": rays, "frame": f"{w}x{h}"}
+                                       "seconds": round(tr, 2), "rays": rays, "frame": f"{w}x{h}",
+                                       "rows_per_thread": h / nthreads}
             except (RuntimeError, subprocess.TimeoutExpired, OSError) as e:
                 log(f"reference {arch} unusable here: {e}")
                 continue
@@ -258,7 +269,8 @@ def cpu_reference(scene_file, flags, width, height, target_s, log):
             return {"value": best["value"], "unit": "Mrays/s", "cores": best["cores"], "kind": "reference",
                     "sample": f"reference engine (Makefile.rt flags, -march={'native' if arch == 'native' else 'x86-64-v3'}"
                               f") on the same scene and flags at a reduced resolution, timed at -m 1 and -m max "
-                              f"({threads} host threads); the faster is the value; render window = its own "
+                              f"({threads} host threads; the -m max frame has 4k rows per thread for the static "
+                              f"OpenMP row schedule); the faster is the value; render window = its own "
                               f"'Commencing raytracing' -> 'Saving image' log stamps; rays from the instrumented "
                               f"build on the same config",
                     "seconds": best["seconds"], "rays": best["rays"],
@@ -487,6 +499,7 @@ def main():
     frame = scene.frame(a.width, a.height)
     flags = flags_for(a.scene, a.spp)
     params = rtxpy.params_from_args(flags, seed=1)
+    params.rng = abi.RTX_RNG_COUNTER  # the reference's i.i.d. light samples (system.c:93-96, object.c:298-299)
     params.tile_offset, params.tile_stride = rank, world
 
     t_open = time.perf_counter()
@@ -569,21 +582,23 @@ def main():
     if not a.no_count:
         roofline = shadow_roofline(r, frame, params, d_rgb, d_z, stream, shadow_ms, a, world)
 
-    faithful = None
+    strat = None
     if rank == 0 and world == 1 and not a.no_post:
-        # the reference-faithful i.i.d. light samples (RTX_RNG_COUNTER) beside the stratified default
+        # side leg: the opt-in stratified light samples (RTX_RNG_STRAT, another estimator of the same
+        # expectation; not the reference's sampling), one frame after the timed loop
         p2 = rtxpy.default_params(**{f: getattr(params, f) for f, _ in abi.Params._fields_})
-        p2.rng = abi.RTX_RNG_COUNTER
+        p2.rng = abi.RTX_RNG_STRAT
+        r.render_device(frame, p2, d_rgb.data_ptr(), d_z.data_ptr(), stream.cuda_stream)  # warm its chunk size
         torch.cuda.synchronize(dev)
         t1 = time.perf_counter()
         r.render_device(frame, p2, d_rgb.data_ptr(), d_z.data_ptr(), stream.cuda_stream)
         torch.cuda.synchronize(dev)
         sc_ = r.stats()
         dt = time.perf_counter() - t1
-        faithful = {"rng": "counter (i.i.d. light samples, the reference's sampling)", "frame_ms": round(dt * 1e3, 1),
-                    "shadow_ms": round(sc_.shadow_ms, 1),
-                    "mrays_per_s": round((sc_.closest_rays + sc_.shadow_rays) / dt / 1e6, 1)}
-        log(f"counter-RNG frame: {faithful}")
+        strat = {"rng": "counter, stratified light samples (RTX_RNG_STRAT, opt-in; not the reference's estimator)",
+                 "frame_ms": round(dt * 1e3, 1), "shadow_ms": round(sc_.shadow_ms, 1),
+                 "mrays_per_s": round((sc_.closest_rays + sc_.shadow_rays) / dt / 1e6, 1)}
+        log(f"stratified-RNG frame: {strat}")
 
     build = None
     if rank == 0 and world == 1 and not a.no_post:
@@ -657,12 +672,13 @@ def main():
                                          "choose_ms": round(st.frame_ms, 1)},
                           "step": "render into HBM, tile shards gathered to rank 0 over RCCL (N > 1), frame copied "
                                   "to pinned host memory (SURVEY 8(d): render window up to the framebuffer on the host)",
-                          "rng": "counter, stratified light samples (library default)"},
+                          "rng": "counter, i.i.d. light samples (RTX_RNG_COUNTER, the library default; the "
+                                 "reference's rand_flt sampling, system.c:93-96, object.c:298-299)"},
                "roofline": roofline, "cpu_baseline": cpu}
         if gat is not None:
             out["config"]["gather_message_bytes_per_rank"] = gat.message_bytes
-        if faithful:
-            out["rng_counter_frame"] = faithful
+        if strat:
+            out["rng_strat_frame"] = strat
         if cpu:
             out["config"]["gpu_over_cpu"] = round(value / cpu["value"], 1)
         if port:
@@ -677,7 +693,8 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-def group_line(a, n, scene_name, objects, elapsed, rays, closest, per_dev, gather_ms, roofline):
+def group_line(a, n, scene_name, objects, elapsed, rays, closest, per_dev, gather_ms, roofline, cpu=None,
+               upload=None):
     """the JSON line of a device-group run (also printed by --dry-run, with None for what only a
     GPU measures).  per_dev: one dict per device of its mean kernel / k_trace / k_shadow times
     and rays over the timed steps."""
@@ -693,6 +710,7 @@ def group_line(a, n, scene_name, objects, elapsed, rays, closest, per_dev, gathe
             "config": {"workload": workload(a), "scene": scene_name, "width": a.width, "height": a.height,
                        "spp": a.spp, "objects": objects, "parallelism": f"tiles{n}", "launch": "group",
                        "rays_per_frame": frame_rays,
+                       "rng": "counter, i.i.d. light samples (RTX_RNG_COUNTER, the library default)",
                        "step": "rtx_group_render: shards on every device, RCCL send/recv to device 0, unpack, copy to "
                                "pinned host memory (SURVEY 8(d) window)"},
             "group": {"rtx_group_size": n, "rccl_devices": n if n > 1 else 0,
@@ -700,10 +718,12 @@ def group_line(a, n, scene_name, objects, elapsed, rays, closest, per_dev, gathe
                       "device_kernel_ms_max": max(kms) if kms else None,
                       "device_kernel_ms_min": min(kms) if kms else None,
                       "gather_ms": gather_ms,
-                      "gather_message_bytes_per_device": int(16 * 64 * -(-((a.width + 7) // 8) * ((a.height + 7) // 8) // n))},
+                      "gather_message_bytes_per_device": int(16 * 64 * -(-((a.width + 7) // 8) * ((a.height + 7) // 8) // n)),
+                      "upload": upload},
             "roofline": roofline,
-            "cpu_baseline": None,
-            "cpu_baseline_note": "reported on the N=1 line (the reference's CPU path on this box's host cores)"}
+            "cpu_baseline": cpu,
+            "cpu_baseline_note": "the reference's own CPU path on this box's host cores, timed after the GPU steps "
+                                 "(the same measurement as the N=1 line's)"}
 
 
 def main_group(a):
@@ -734,6 +754,7 @@ def main_group(a):
     frame = scene.frame(a.width, a.height)
     flags = flags_for(a.scene, a.spp)
     params = rtxpy.params_from_args(flags, seed=1)
+    params.rng = abi.RTX_RNG_COUNTER  # the reference's i.i.d. light samples
     g = rtxpy.Group(list(range(a.gpus)))
     n = g.size()
     g.set_option(abi.RTX_OPT_SHADOW_WALK, WALKS[a.walk])
@@ -744,6 +765,7 @@ def main_group(a):
         g.set_option(abi.RTX_OPT_SHADOW_GRAB, a.shadow_grab)
     t0 = time.perf_counter()
     g.upload(scene)
+    upload_ms = (time.perf_counter() - t0) * 1e3
     s0 = g.device_stats(0)
     log(f"{n} devices, scene {os.path.basename(path)} uploaded in {time.perf_counter() - t0:.2f}s "
         f"(build on device 0 {s0.build_ms:.1f} ms, tree frame {'rotated' if s0.tree_rotated else 'world'})")
@@ -780,10 +802,20 @@ def main_group(a):
         roofline = shadow_roofline_of(g.device_stats(0), per_dev[0]["shadow_ms"], a, n)
         roofline["device"] = 0
         roofline["note"] = "device 0's k_shadow over its shard (tiles t % N == 0), counts from a counting render"
-    out = group_line(a, n, os.path.basename(path), int(scene.num_objects), elapsed, rays, closest, per_dev,
-                     round(float(np.mean(gms)), 3), roofline)
-    print(json.dumps(out), flush=True)
+    upload = {"wall_ms": round(upload_ms, 1), "build_ms_device0": round(s0.build_ms, 1),
+              "peer_copy_ms": [round(g.device_stats(r).upload_copy_ms, 1) for r in range(n)]}
     g.close()
+    cpu = None
+    if not a.no_cpu_baseline:
+        try:
+            cpu = cpu_reference(path, flags, a.width, a.height, a.cpu_target_s, log)
+        except Exception as e:  # never let the baseline kill the measurement
+            log(f"reference baseline failed: {e}")
+    out = group_line(a, n, os.path.basename(path), int(scene.num_objects), elapsed, rays, closest, per_dev,
+                     round(float(np.mean(gms)), 3), roofline, cpu, upload)
+    if cpu and out["value"]:
+        out["config"]["gpu_over_cpu"] = round(out["value"] / cpu["value"], 1)
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

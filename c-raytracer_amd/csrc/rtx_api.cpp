@@ -122,7 +122,7 @@ extern "C" void rtx_params_default(rtx_params *p)
 	p->samples = 1;
 	p->attenuation = RTX_ATT_SQR;
 	p->attenuation_offset = 1.f;
-	p->rng = RTX_RNG_STRAT;
+	p->rng = RTX_RNG_COUNTER;
 	p->seed = 1;
 	p->u32conv = RTX_U32_SAT;
 	p->tile_offset = 0;
@@ -733,6 +733,20 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
  * collapsed on the device) change hands to c */
 int rtx_upload_built(rtx_ctx *c, HostScene &hs)
 {
+	DevTree t{ hs.dev_w8, hs.dev_w8s, hs.dev_w8leaf, hs.device };
+	hs.dev_w8 = nullptr;
+	hs.dev_w8s = nullptr;
+	hs.dev_w8leaf = nullptr;
+	const int rc = rtx_upload_built(c, hs, &t);
+	/* whatever was not handed over goes back to hs, whose destructor frees it */
+	hs.dev_w8 = t.w8;
+	hs.dev_w8s = t.w8s;
+	hs.dev_w8leaf = t.leaf;
+	return rc;
+}
+
+int rtx_upload_built(rtx_ctx *c, const HostScene &hs, DevTree *take)
+{
 	int rc;
 	PhaseClock clk;
 	/* a failure below leaves the context without a scene (RTX_ERR_STATE on render), never with a
@@ -756,17 +770,17 @@ int rtx_upload_built(rtx_ctx *c, HostScene &hs)
 	const bool have_w8 = hs.w8_on_device || !hs.w8.empty();
 	const uint32_t num_w8 = hs.w8_on_device ? hs.w8_entries : (uint32_t)hs.w8.size();
 	uint32_t *d_map = nullptr; /* entry -> primitive index of the 8-wide tree's leaf entries */
-	if (hs.w8_on_device) { /* collapsed on this device: the buffers change hands */
-		if (hs.device != c->device)
-			return fail(RTX_ERR_STATE, "8-wide tree built on device %d uploaded to device %d", hs.device, c->device);
+	if (hs.w8_on_device) { /* collapsed on the device (or peer-copied to it): the buffers change hands */
+		if (!take || take->device != c->device)
+			return fail(RTX_ERR_STATE, "8-wide tree on device %d uploaded to device %d", take ? take->device : -1, c->device);
 		dfree(c->d_w8);
 		dfree(c->d_w8s);
-		c->d_w8 = hs.dev_w8;
-		c->d_w8s = hs.dev_w8s;
-		d_map = hs.dev_w8leaf;
-		hs.dev_w8 = nullptr;
-		hs.dev_w8s = nullptr;
-		hs.dev_w8leaf = nullptr;
+		c->d_w8 = take->w8;
+		c->d_w8s = take->w8s;
+		d_map = take->leaf;
+		take->w8 = nullptr;
+		take->w8s = nullptr;
+		take->leaf = nullptr;
 		PHASE(clk, "8-wide tree handover", c->stream);
 	} else {
 		if ((rc = upload(c->d_w8, hs.w8, c->stream)))
@@ -1003,6 +1017,7 @@ int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, floa
 	const uint32_t grab = c->opt_grab; /* lane slots per k_shadow queue grab (1024 -> 4096: 903 -> 885 ms) */
 	const uint32_t per_wave = std::max<uint32_t>(1, std::min<uint32_t>(64, grab / (slot_b * slots_per_point)));
 	const bool spsort = c->opt_spsort;
+	bool overflowed = false; /* a chunk of this frame overflowed the shade-point array */
 	for (uint32_t begin = 0; begin < P.ntiles;) {
 		const uint32_t end = std::min<uint32_t>(P.ntiles, begin + chunk_tiles);
 		const uint64_t sp_cap64 = std::min<uint64_t>((uint64_t)(end - begin) * avg_tile + staging_cap, 0xFFFFFFF0ull);
@@ -1033,6 +1048,7 @@ int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, floa
 			if (end - begin == 1)
 				return fail(RTX_ERR_STATE, "shade-point array overflow on a single tile");
 			chunk_tiles = std::max<uint32_t>(1, (end - begin) / 2);
+			overflowed = true;
 			continue;
 		}
 		const uint32_t n_sp = (uint32_t)head[RTX_C_SPCOUNT];
@@ -1076,7 +1092,10 @@ int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, floa
 		t_accum += cc;
 		chunks++;
 		begin = end;
-		chunk_tiles = std::min<uint32_t>(chunk_cap, 2 * chunk_tiles); /* grows back after an overflow halved it */
+		/* a chunk an overflow halved grows back by a quarter per chunk that fits, so a dense region of
+		 * the image does not overflow (and re-trace) every other chunk */
+		if (overflowed)
+			chunk_tiles = std::min<uint32_t>(chunk_cap, chunk_tiles + std::max<uint32_t>(1, chunk_tiles / 4));
 	}
 	HIP_TRY(hipEventRecord(c->ev1, stream));
 	HIP_TRY(hipStreamSynchronize(stream));

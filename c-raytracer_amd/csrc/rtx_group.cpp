@@ -3,9 +3,12 @@
  * one process.  Replaces the reference's parallel point, the OpenMP row loop of render()
  * (render.c:349-352), with a tile deal over devices:
  *
+ *   open     peer access enabled between device 0 and every other device (the tree copies
+ *            then go device to device over xGMI, not through host memory)
  *   upload   the scene is flattened and its BVHs built ONCE, on device 0 (rtx_build_scene,
  *            the work of accel_init, accel.c:266-315: device SAH build + 8-wide collapse); the
- *            other devices get peer copies of the device-built records and tree over xGMI
+ *            other devices copy the device-built records and tree from it, one host thread
+ *            per device, each on its own stream
  *   render   device r renders tiles t = r (mod n) on its own host thread (rtx_render_common
  *            with tile_offset r, tile_stride n), into its own HBM framebuffer
  *   gather   devices r > 0 pack their shard into 16-byte {r, g, b, z} tile records
@@ -15,6 +18,10 @@
  *
  * At 1080p a shard is 4.1 MB / n per device; the gather is a few tens of microseconds of
  * link time.  With n = 1 no communicator is created.
+ *
+ * rtx_group_open_loopback: n shards as n contexts on one device, the gather a device-to-device
+ * copy instead of RCCL; the rest of the path is the one above (tests/test_gpu_group.py runs it
+ * at n = 2, 3, 8 on a one-GPU box against rtx_render).
  */
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -42,6 +49,8 @@ extern "C" hipError_t rtx_launch_tile_unpack(const float4 *in, uint32_t w, uint3
 
 struct rtx_group {
 	int n = 0;
+	bool loopback = false;         /* rtx_group_open_loopback: every context on one device */
+	std::vector<uint32_t> peer;    /* peer access between device r and device 0 enabled */
 	std::vector<rtx_ctx *> ctx;
 	std::vector<ncclComm_t> comm;  /* n > 1: one per device, rank r = ctx[r] */
 	std::vector<float4 *> d_buf;   /* r > 0: shard r's packed records on device r */
@@ -75,6 +84,23 @@ extern "C" void rtx_group_close(rtx_group *g)
 	delete g;
 }
 
+/* let device `dev` access `peer`'s memory (already enabled counts); false when the pair has no
+ * peer path (copies then stage through the host, which is slower but correct) */
+static bool enable_peer(int dev, int peer)
+{
+	int can = 0;
+	if (hipDeviceCanAccessPeer(&can, dev, peer) != hipSuccess || !can)
+		return false;
+	if (hipSetDevice(dev) != hipSuccess)
+		return false;
+	hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+	if (e == hipErrorPeerAccessAlreadyEnabled) {
+		(void)hipGetLastError(); /* clear the sticky "already enabled" */
+		return true;
+	}
+	return e == hipSuccess;
+}
+
 extern "C" int rtx_group_open(int n, const int *devices, rtx_group **out)
 {
 	if (!out)
@@ -103,6 +129,9 @@ extern "C" int rtx_group_open(int n, const int *devices, rtx_group **out)
 			return rc;
 		}
 	}
+	g->peer.assign(n, 1u);
+	for (int r = 1; r < n; r++) /* the upload's tree copies go device to device */
+		g->peer[r] = enable_peer(dev[r], dev[0]) && enable_peer(dev[0], dev[r]);
 	if (n > 1) {
 		g->comm.assign(n, nullptr);
 		ncclResult_t e = ncclCommInitAll(g->comm.data(), n, dev.data());
@@ -111,6 +140,39 @@ extern "C" int rtx_group_open(int n, const int *devices, rtx_group **out)
 			rtx_group_close(g);
 			return fail(RTX_ERR_HIP, "ncclCommInitAll over %d devices failed: %s", n, ncclGetErrorString(e));
 		}
+	}
+	for (int r = 0; r < n; r++) {
+		g->ctx[r]->stats.transport = n > 1 ? RTX_TRANSPORT_RCCL : RTX_TRANSPORT_NONE;
+		g->ctx[r]->stats.peer_access = g->peer[r];
+	}
+	*out = g;
+	return RTX_OK;
+}
+
+extern "C" int rtx_group_open_loopback(int n, int device, rtx_group **out)
+{
+	if (!out)
+		return fail(RTX_ERR_ARG, "null out");
+	*out = nullptr;
+	if (n < 1 || n > 64)
+		return fail(RTX_ERR_ARG, "loopback group of %d shards (1..64)", n);
+	rtx_group *g = new rtx_group();
+	g->n = n;
+	g->loopback = true;
+	g->ctx.assign(n, nullptr);
+	g->d_buf.assign(n, nullptr);
+	g->d_recv.assign(n, nullptr);
+	g->buf_cap.assign(n, 0);
+	g->recv_cap.assign(n, 0);
+	g->peer.assign(n, 1u);
+	for (int r = 0; r < n; r++) {
+		int rc = rtx_open(device, &g->ctx[r]);
+		if (rc) {
+			rtx_group_close(g);
+			return rc;
+		}
+		g->ctx[r]->stats.transport = n > 1 ? RTX_TRANSPORT_LOOPBACK : RTX_TRANSPORT_NONE;
+		g->ctx[r]->stats.peer_access = 1u;
 	}
 	*out = g;
 	return RTX_OK;
@@ -142,20 +204,53 @@ extern "C" int rtx_group_set_option(rtx_group *g, int option, int64_t value)
 	return RTX_OK;
 }
 
-/* a device buffer of `bytes` on device dst, copied from src on device sd (xGMI peer copy) */
-template <class T> static int peer_copy(T *&out, int dst, const T *src, int sd, size_t bytes)
+/* a device buffer of `bytes` on device dst, copied from src on device sd on dst's stream (xGMI
+ * with peer access; a plain device-to-device copy when sd == dst, the loopback group) */
+template <class T> static int peer_copy(T *&out, int dst, const T *src, int sd, size_t bytes, hipStream_t s)
 {
 	out = nullptr;
 	if (!src || !bytes)
 		return RTX_OK;
 	HIP_TRY(hipSetDevice(dst));
 	HIP_TRY(hipMalloc(&out, bytes));
-	hipError_t e = hipMemcpyPeer(out, dst, src, sd, bytes);
+	hipError_t e = hipMemcpyPeerAsync(out, dst, src, sd, bytes, s);
 	if (e != hipSuccess) {
 		dfree(out);
 		return fail(RTX_ERR_HIP, "peer copy of %zu bytes from device %d to %d failed: %s", bytes, sd, dst, hipGetErrorString(e));
 	}
 	return RTX_OK;
+}
+
+/* device r of the group takes copies of what device 0's build left in HBM, on its own host thread:
+ * the records, the 8-wide tree (entries, scalar copies, leaf map), then the host parts */
+static int upload_copy(rtx_group *g, int r, const HostScene &hs, const DevTree &src)
+{
+	rtx_ctx *c0 = g->ctx[0], *c = g->ctx[r];
+	const auto t0 = std::chrono::steady_clock::now();
+	HIP_TRY(hipSetDevice(c->device));
+	dfree(c->d_nodes);
+	c->have_scene = false;
+	const size_t rec_bytes = ((size_t)hs.nnodes + hs.nb) * sizeof(DNode);
+	const size_t ent = hs.w8_on_device ? hs.w8_entries : 0;
+	DevTree t;
+	t.device = c->device;
+	int rc = RTX_OK;
+	if ((!hs.recs_on_device || !(rc = peer_copy(c->d_nodes, c->device, c0->d_nodes, c0->device, rec_bytes, c->stream))) &&
+	    !(rc = peer_copy(t.w8, c->device, src.w8, src.device, ent * sizeof(DW8), c->stream)) &&
+	    !(rc = peer_copy(t.w8s, c->device, src.w8s, src.device, ent * sizeof(DW8S), c->stream)) &&
+	    !(rc = peer_copy(t.leaf, c->device, src.leaf, src.device, ent * sizeof(uint32_t), c->stream))) {
+		hipError_t e = hipStreamSynchronize(c->stream);
+		if (e != hipSuccess)
+			rc = fail(RTX_ERR_HIP, "device %d: scene copies: %s", c->device, hipGetErrorString(e));
+	}
+	c->stats.upload_copy_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+	if (!rc)
+		rc = rtx_upload_built(c, hs, &t); /* takes the copies */
+	(void)hipSetDevice(c->device); /* copies a failure left behind */
+	dfree(t.w8);
+	dfree(t.w8s);
+	dfree(t.leaf);
+	return rc;
 }
 
 extern "C" int rtx_group_upload_scene(rtx_group *g, const rtx_scene_desc *sc)
@@ -170,45 +265,27 @@ extern "C" int rtx_group_upload_scene(rtx_group *g, const rtx_scene_desc *sc)
 	int rc = rtx_build_scene(c0, sc, hs);
 	if (rc)
 		return rc;
-	const bool recs_dev = hs.recs_on_device;
-	const size_t rec_bytes = ((size_t)hs.nnodes + hs.nb) * sizeof(DNode);
-	DW8 *w8 = hs.dev_w8;
-	DW8S *w8s = hs.dev_w8s;
-	uint32_t *leaf = hs.dev_w8leaf;
-	const size_t ent = hs.w8_on_device ? hs.w8_entries : 0;
-	for (int r = 1; r < g->n; r++) {
-		rtx_ctx *c = g->ctx[r];
-		HIP_TRY(hipSetDevice(c->device));
-		dfree(c->d_nodes);
-		c->have_scene = false;
-		if (recs_dev && (rc = peer_copy(c->d_nodes, c->device, c0->d_nodes, c0->device, rec_bytes)))
-			return rc;
-		hs.dev_w8 = nullptr;
-		hs.dev_w8s = nullptr;
-		hs.dev_w8leaf = nullptr;
-		hs.device = c->device;
-		if (!(rc = peer_copy(hs.dev_w8, c->device, w8, c0->device, ent * sizeof(DW8))) &&
-		    !(rc = peer_copy(hs.dev_w8s, c->device, w8s, c0->device, ent * sizeof(DW8S))) &&
-		    !(rc = peer_copy(hs.dev_w8leaf, c->device, leaf, c0->device, ent * sizeof(uint32_t)))) {
-			hs.recs_on_device = recs_dev;
-			rc = rtx_upload_built(c, hs); /* takes the copies */
-		}
-		if (rc) { /* copies a failure left behind */
-			(void)hipSetDevice(c->device);
-			dfree(hs.dev_w8);
-			dfree(hs.dev_w8s);
-			dfree(hs.dev_w8leaf);
-			break;
-		}
+	const DevTree src{ hs.dev_w8, hs.dev_w8s, hs.dev_w8leaf, c0->device };
+	/* devices 1..n-1 copy from device 0 concurrently, one host thread each; hs is only read */
+	std::vector<int> rcs(g->n, RTX_OK);
+	std::vector<std::string> errs(g->n);
+	{
+		std::vector<std::thread> th;
+		for (int r = 1; r < g->n; r++)
+			th.emplace_back([&, r] {
+				rcs[r] = upload_copy(g, r, hs, src);
+				if (rcs[r])
+					errs[r] = rtx_last_error();
+			});
+		for (auto &t : th)
+			t.join();
 	}
-	/* device 0 last: it takes the original buffers (hs frees whatever a failure left) */
-	hs.dev_w8 = w8;
-	hs.dev_w8s = w8s;
-	hs.dev_w8leaf = leaf;
-	hs.device = c0->device;
-	if (rc)
-		return rc;
-	hs.recs_on_device = recs_dev;
+	for (int r = 1; r < g->n; r++)
+		if (rcs[r])
+			return fail(rcs[r], "device %d: %s", g->ctx[r]->device, errs[r].c_str());
+	/* device 0 last: it takes the original buffers (hs frees whatever a failure left), after every
+	 * copy of them has completed */
+	c0->stats.upload_copy_ms = 0.0;
 	return rtx_upload_built(c0, hs);
 }
 
@@ -302,15 +379,26 @@ extern "C" int rtx_group_render(rtx_group *g, const rtx_frame *fr, const rtx_par
 			HIP_TRY(hipSetDevice(c->device));
 			HIP_TRY(rtx_launch_tile_pack(c->d_rgb, c->d_z, w, h, (uint32_t)r, (uint32_t)n, g->d_buf[r], c->stream));
 		}
-		NCCL_TRY(ncclGroupStart());
-		for (int r = 1; r < n; r++) {
-			const size_t floats = rtx_tile_pack_count(w, h, (uint32_t)r, (uint32_t)n) * 4;
-			if (!floats)
-				continue;
-			NCCL_TRY(ncclSend(g->d_buf[r], floats, ncclFloat, 0, g->comm[r], g->ctx[r]->stream));
-			NCCL_TRY(ncclRecv(g->d_recv[r], floats, ncclFloat, r, g->comm[0], c0->stream));
+		if (g->loopback) { /* the test transport: a device-to-device copy per shard, then device 0 waits */
+			for (int r = 1; r < n; r++) {
+				const size_t recs = rtx_tile_pack_count(w, h, (uint32_t)r, (uint32_t)n);
+				if (!recs)
+					continue;
+				HIP_TRY(hipMemcpyAsync(g->d_recv[r], g->d_buf[r], recs * sizeof(float4), hipMemcpyDeviceToDevice,
+						       g->ctx[r]->stream));
+				HIP_TRY(hipStreamSynchronize(g->ctx[r]->stream));
+			}
+		} else {
+			NCCL_TRY(ncclGroupStart());
+			for (int r = 1; r < n; r++) {
+				const size_t floats = rtx_tile_pack_count(w, h, (uint32_t)r, (uint32_t)n) * 4;
+				if (!floats)
+					continue;
+				NCCL_TRY(ncclSend(g->d_buf[r], floats, ncclFloat, 0, g->comm[r], g->ctx[r]->stream));
+				NCCL_TRY(ncclRecv(g->d_recv[r], floats, ncclFloat, r, g->comm[0], c0->stream));
+			}
+			NCCL_TRY(ncclGroupEnd());
 		}
-		NCCL_TRY(ncclGroupEnd());
 		HIP_TRY(hipSetDevice(c0->device));
 		for (int r = 1; r < n; r++)
 			HIP_TRY(rtx_launch_tile_unpack(g->d_recv[r], w, h, (uint32_t)r, (uint32_t)n, c0->d_rgb, c0->d_z, c0->stream));
@@ -356,6 +444,8 @@ extern "C" int rtx_group_render(rtx_group *g, const rtx_frame *fr, const rtx_par
 		s.shadow_ms = std::max(s.shadow_ms, o.shadow_ms);
 		s.accum_ms = std::max(s.accum_ms, o.accum_ms);
 		s.sort_ms = std::max(s.sort_ms, o.sort_ms);
+		s.upload_copy_ms = std::max(s.upload_copy_ms, o.upload_copy_ms);
+		s.peer_access = s.peer_access && o.peer_access;
 	}
 	s.gather_ms = n > 1 ? gather_ms : 0.0;
 	s.devices = (uint32_t)n;

@@ -187,6 +187,19 @@ struct HostScene {
 /* flatten sc and build its BVHs (on c's device for the device builder), then upload to c */
 int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs);
 int rtx_upload_built(rtx_ctx *c, HostScene &hs);
+/* a device-collapsed 8-wide tree's buffers on one device (hs.w8_on_device): the building device's
+ * own, or a device group's peer copies of them */
+struct DevTree {
+	DW8 *w8 = nullptr;
+	DW8S *w8s = nullptr;
+	uint32_t *leaf = nullptr;
+	int device = 0;
+};
+/* upload a built scene to c, taking the device tree from `take` (c's device; c owns the buffers
+ * after the call and take's pointers are cleared once handed over: on failure the caller frees
+ * whatever take still holds).  hs is only read, so several contexts may upload one scene at once
+ * from their own host threads. */
+int rtx_upload_built(rtx_ctx *c, const HostScene &hs, DevTree *take);
 /* rtx_wide8.cpp: the 8-wide shadow BVH collapsed from the BVH2 (0 = not built); boxes it takes
  * from primitive records (leaves of several primitives) in the trees' frame tf, padded by fpad */
 uint32_t rtx_wide8_build(const std::vector<DNode> &inner, uint32_t nnodes, const DPrim *prims, uint32_t root_ref,

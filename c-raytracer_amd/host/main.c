@@ -13,7 +13,8 @@
  *   --device D   first device (default 0)
  *   --seed S     counter-RNG seed (default 1)
  *   --rng const  every rand_flt() draw = 0.5 (the oracle's REF_CONST_RNG)
- *   --rng counter  counter-based draws without the light-sample stratification (default: strat)
+ *   --rng counter  counter-based i.i.d. draws like rand_flt (the default)
+ *   --rng strat    the same stream with the light samples stratified (opt-in, another estimator)
  *   --u32 wrap   float->uint32 texture conversion of a generic x86-64 build
  *                (default: AVX-512 saturating, like -march=native on AVX-512 hosts)
  */
@@ -45,7 +46,7 @@ static const char *HELPTEXT =
 	"[-p] (\"real\" | \"cpu\")            : DEFAULT = real    : time to print with status messages.\n"
 	"[-g] (string)                    : DEFAULT = ambient : global illumination model (ambient | path).\n"
 	"[-f]                             : DEFAULT = OFF     : save raw output for post-processing.\n"
-	"[--gpus N] [--device D] [--seed S] [--rng strat|counter|const] [--u32 sat|wrap]\n";
+	"[--gpus N] [--device D] [--seed S] [--rng counter|strat|const] [--u32 sat|wrap]\n";
 
 static struct timespec t0;
 static int log_cpu = 0;
@@ -98,6 +99,8 @@ int main(int argc, char **argv)
 		p.rng = RTX_RNG_CONST;
 	if ((idx = argv_find(argc, argv, "--rng", 1)) && !strcmp(argv[idx + 1], "counter"))
 		p.rng = RTX_RNG_COUNTER;
+	if ((idx = argv_find(argc, argv, "--rng", 1)) && !strcmp(argv[idx + 1], "strat"))
+		p.rng = RTX_RNG_STRAT;
 	if ((idx = argv_find(argc, argv, "--u32", 1)) && !strcmp(argv[idx + 1], "wrap"))
 		p.u32conv = RTX_U32_WRAP;
 	if (ngpu < 1)

@@ -129,7 +129,7 @@ def default_params(**kw):
     p.samples = 1
     p.attenuation = abi.RTX_ATT_SQR
     p.attenuation_offset = 1.0
-    p.rng = abi.RTX_RNG_STRAT
+    p.rng = abi.RTX_RNG_COUNTER
     p.seed = 1
     p.u32conv = abi.RTX_U32_SAT
     p.tile_offset = 0
@@ -291,14 +291,19 @@ def gpu_kat(kind, records, params=None):
 
 class Group:
     """Several HIP devices rendering one frame (rtx_group_open .. rtx_group_close): tiles dealt
-    round-robin over the devices, gathered to the first one over RCCL."""
+    round-robin over the devices, gathered to the first one over RCCL.  loopback=n: n shards as
+    n contexts on device devices[0] (rtx_group_open_loopback, the test transport)."""
 
-    def __init__(self, devices):
+    def __init__(self, devices, loopback=None):
         self.lib = rtx_lib()
         self._g = C.c_void_p()
-        devs = (C.c_int * len(devices))(*devices)
-        _check(self.lib.rtx_group_open(len(devices), devs, C.byref(self._g)))
-        self.devices = list(devices)
+        if loopback:
+            _check(self.lib.rtx_group_open_loopback(int(loopback), int(devices[0]), C.byref(self._g)))
+            self.devices = [devices[0]] * int(loopback)
+        else:
+            devs = (C.c_int * len(devices))(*devices)
+            _check(self.lib.rtx_group_open(len(devices), devs, C.byref(self._g)))
+            self.devices = list(devices)
 
     def set_builder(self, builder):
         _check(self.lib.rtx_group_set_builder(self._g, builder))

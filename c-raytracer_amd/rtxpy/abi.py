@@ -72,7 +72,11 @@ class Stats(C.Structure):
                 ("gather_ms", C.c_double), ("devices", C.c_uint32), ("pad_", C.c_uint32),
                 ("shadow_uniform_steps", C.c_uint64), ("shadow_walk", C.c_uint32), ("wide_entries", C.c_uint32),
                 ("trace_walk", C.c_uint32), ("pad2_", C.c_uint32), ("tree_rotated", C.c_uint32),
-                ("pad3_", C.c_uint32), ("frame_cost", C.c_double), ("frame_ms", C.c_double)]
+                ("pad3_", C.c_uint32), ("frame_cost", C.c_double), ("frame_ms", C.c_double),
+                ("upload_copy_ms", C.c_double), ("transport", C.c_uint32), ("peer_access", C.c_uint32)]
+
+
+RTX_TRANSPORT_NONE, RTX_TRANSPORT_RCCL, RTX_TRANSPORT_LOOPBACK = 0, 1, 2
 
 
 RTX_BUILD_SAH_HOST, RTX_BUILD_LBVH_GPU, RTX_BUILD_PLOC_GPU, RTX_BUILD_SAH_GPU = 0, 1, 2, 3
@@ -106,7 +110,7 @@ KAT_NAMES = ["moller", "sphere", "plane", "slab", "noise", "texture", "sph_light
 # symbols include/rtx.h declares (checked by tests/test_abi.py)
 RTX_SYMBOLS = ["rtx_params_default", "rtx_device_count", "rtx_open", "rtx_upload_scene", "rtx_render",
                "rtx_render_device", "rtx_get_stats", "rtx_close", "rtx_last_error", "rtx_kat", "rtx_postprocess",
-               "rtx_postprocess_device", "rtx_set_builder", "rtx_set_option", "rtx_group_open", "rtx_group_size",
+               "rtx_postprocess_device", "rtx_set_builder", "rtx_set_option", "rtx_group_open", "rtx_group_open_loopback", "rtx_group_size",
                "rtx_group_set_builder", "rtx_group_set_option", "rtx_group_upload_scene", "rtx_group_render", "rtx_group_get_stats", "rtx_group_device_stats",
                "rtx_group_close", "rtx_tile_pack_count", "rtx_tile_pack_host", "rtx_tile_unpack_host",
                "rtx_tile_pack_device", "rtx_tile_unpack_device", "rtx_tree_frame"]
@@ -184,6 +188,8 @@ def declare_rtx(lib):
     lib.rtx_postprocess_device.restype = C.c_int
     lib.rtx_group_open.argtypes = [C.c_int, C.c_void_p, C.POINTER(C.c_void_p)]
     lib.rtx_group_open.restype = C.c_int
+    lib.rtx_group_open_loopback.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_void_p)]
+    lib.rtx_group_open_loopback.restype = C.c_int
     lib.rtx_group_size.argtypes = [C.c_void_p]
     lib.rtx_group_size.restype = C.c_int
     lib.rtx_group_set_builder.argtypes = [C.c_void_p, C.c_int]

@@ -137,12 +137,14 @@ enum rtx_gi { RTX_GI_AMBIENT = 0, RTX_GI_PATH = 1 };                        /* r
 enum rtx_attenuation { RTX_ATT_NONE = 0, RTX_ATT_LIN = 1, RTX_ATT_SQR = 2 }; /* render.c:42-46 */
 /* rand_flt (system.c:93-96) replacement */
 enum rtx_rng {
-	RTX_RNG_COUNTER = 0,  /* counter-based hash of (seed, pixel, ray-tree node, draw) */
+	RTX_RNG_COUNTER = 0,  /* counter-based hash of (seed, pixel, ray-tree node, draw): i.i.d. draws like
+	                       * rand_flt, two per light sample (object.c:298-299, 403-419); the default */
 	RTX_RNG_CONST = 1,    /* every draw == 0.5f (the oracle's REF_CONST_RNG) */
-	RTX_RNG_STRAT = 2,    /* RTX_RNG_COUNTER with the light samples stratified (the default): sample j
+	RTX_RNG_STRAT = 2,    /* RTX_RNG_COUNTER with the light samples stratified (opt-in): sample j
 	                       * of an emitter's n draws its first number (the sphere's inclination, the
 	                       * triangle's p) from [j/n, (j+1)/n) as ((float)j + u) / n; each stratum is
-	                       * sampled uniformly, so the estimator keeps render.c:170-229's expectation */
+	                       * sampled uniformly, so the estimator keeps render.c:170-229's expectation
+	                       * (a different estimator from the reference's i.i.d. one, lower variance) */
 };
 /* (uint32_t)float in texture_get_color_checkerboard/brick (material.c:164,173)
  * is UB for negatives; its result depends on the host ISA. */
@@ -221,6 +223,11 @@ typedef struct rtx_stats {
 	uint32_t pad3_;
 	double frame_cost;                /* its sampled leaf-box surface area over the world frame's (1: world frame) */
 	double frame_ms;                  /* host time choosing the frame and taking the leaf boxes in it */
+	double upload_copy_ms;            /* device groups: this device's copies of the scene built on device 0
+	                                   * (last rtx_group_upload_scene; 0 on device 0 and for single contexts) */
+	uint32_t transport;               /* device groups: RTX_TRANSPORT_* of the shard gather */
+	uint32_t peer_access;             /* device groups: this device and device 0 have peer access enabled
+	                                   * (hipDeviceEnablePeerAccess both ways; 1 on device 0 itself) */
 } rtx_stats;
 
 typedef struct rtx_ctx rtx_ctx;
@@ -291,18 +298,26 @@ const char *rtx_last_error(void);
 
 /*
  * Several devices rendering one frame (the reference's own parallel point is
- * the OpenMP row loop of render.c:349-352).  The group builds the scene's BVHs once on the
- * host (rtx_upload_scene's work) and uploads them to every device; rtx_group_render deals the
- * frame's 8x8 tiles round-robin (tile t -> device t % n), renders every shard on its own host
- * thread, packs each shard into 16-byte {r, g, b, z} records (64 per tile) and gathers them
- * to the first device over RCCL (grouped ncclSend / ncclRecv on xGMI), which unpacks the frame
- * and copies it to the caller.  Pixels are independent and the RNG is counter-based, so the
- * frame is bit-identical for any n.  One host thread calls the group; it must not be shared.
+ * the OpenMP row loop of render.c:349-352).  The group builds the scene's BVHs once, on its
+ * first device (rtx_upload_scene's work: device SAH build, 8-wide collapse), and the other
+ * devices copy the built records and trees from it over xGMI (peer access enabled at open, one
+ * host thread per device); rtx_group_render deals the frame's 8x8 tiles round-robin (tile t ->
+ * device t % n), renders every shard on its own host thread, packs each shard into 16-byte
+ * {r, g, b, z} records (64 per tile) and gathers them to the first device over RCCL (grouped
+ * ncclSend / ncclRecv on xGMI), which unpacks the frame and copies it to the caller.  Pixels
+ * are independent and the RNG is counter-based, so the frame is bit-identical for any n.  One
+ * host thread calls the group; it must not be shared.
  */
 typedef struct rtx_group rtx_group;
+enum { RTX_TRANSPORT_NONE = 0, RTX_TRANSPORT_RCCL = 1, RTX_TRANSPORT_LOOPBACK = 2 };
 
 /* n devices: devices[0..n-1], or 0..n-1 when devices is NULL (each must be gfx950, distinct) */
 int rtx_group_open(int n, const int *devices, rtx_group **out);
+/* Test transport: a group of n shards as n contexts on ONE device.  Everything is the group's
+ * own path (scene built once and copied to every context from one host thread each, one host
+ * thread per shard, tile pack, unpack, statistics) except the gather, which is a device-to-device
+ * copy in place of RCCL send/recv.  Lets a one-GPU machine check rtx_group_render at any n. */
+int rtx_group_open_loopback(int n, int device, rtx_group **out);
 int rtx_group_size(const rtx_group *g);
 int rtx_group_set_builder(rtx_group *g, int builder);
 int rtx_group_set_option(rtx_group *g, int option, int64_t value); /* rtx_set_option on every device */

@@ -838,7 +838,7 @@ void rtx_oracle_params_default(rtx_params *p)
 	p->samples = 1;
 	p->attenuation = RTX_ATT_SQR;
 	p->attenuation_offset = 1.f;
-	p->rng = RTX_RNG_STRAT;
+	p->rng = RTX_RNG_COUNTER;
 	p->seed = 1;
 	p->u32conv = RTX_U32_SAT;
 	p->tile_offset = 0;

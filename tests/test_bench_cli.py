@@ -47,6 +47,9 @@ def test_group_line_schema():
     assert [d["device"] for d in devs] == list(range(8))
     assert all({"kernel_ms", "trace_ms", "shadow_ms", "rays"} <= set(d) for d in devs)
     assert "gather_ms" in out["group"] and out["group"]["rccl_devices"] == 8
+    assert "upload" in out["group"]  # per-device copy times of the scene built on device 0
+    assert "i.i.d." in out["config"]["rng"]  # the reference's sampling (system.c:93-96)
+    assert "cpu_baseline_note" in out  # the same reference CPU leg as the N=1 line, after the GPU steps
     rl = out["roofline"]
     assert rl["kernel"] == "k_shadow" and rl["device"] == 0 and {"bound", "achieved", "peak", "unit", "frac", "traffic"} <= set(rl)
 

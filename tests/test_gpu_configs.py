@@ -1,7 +1,7 @@
 """Parity at the BASELINE.json workloads themselves (the frames bench.py and the scaling runs time).
 
 Each config renders on the GPU through the C-ABI at its full size, flags and spp, with the
-default RNG (counter-based, stratified light samples, seed 1, as bench.py).  The oracle
+default RNG (counter-based i.i.d. light samples, seed 1, as bench.py).  The oracle
 (oracle/restate.c, bit-exact with the reference built at -O2, tests/test_oracle.py) renders an evenly spaced sample of the same frame's 8x8
 tiles with the same RNG stream, and the GPU pixels of those tiles must agree within SURVEY
 §8(c)'s tolerances (conftest.compare_const):
@@ -47,7 +47,7 @@ def load(name):
 
 def params_for(spp, offset=0, stride=1):
     p = rtxpy.params_from_args(["-g", "path", "-n", str(spp)], seed=1)
-    p.rng = abi.RTX_RNG_STRAT  # bench.py's mode (the library default)
+    p.rng = abi.RTX_RNG_COUNTER  # bench.py's mode (the library default: i.i.d. like rand_flt)
     p.tile_offset, p.tile_stride = offset, stride
     return p
 

@@ -6,12 +6,19 @@ The gather's device kernels (rtx_tile_pack_device / rtx_tile_unpack_device, csrc
 are checked on one device: packing the shards of a rendered frame equals the host reference
 records, and unpacking every shard rebuilds the frame.
 
-NOT exercised here: a group of n > 1 devices, i.e. the peer copies of the built trees
-(hipMemcpyPeer in rtx_group_upload_scene) and the grouped RCCL ncclSend / ncclRecv of the
-shards.  This box has one GPU, and the driver's multi-GPU runs have so far been skipped (no 8-GPU
-node), so that path has never run.  What stands in for it: the shard deal and record layout on
-the host (tests/test_gather.py), the same records gathered over torch.distributed with gloo
-(tests/test_distributed.py), and the group line's schema (tests/test_bench_cli.py).
+A group of n > 1 shards runs here through the loopback transport (rtx_group_open_loopback: n
+contexts on device 0).  That is the group's own orchestration at n = 2, 3 and 8: the scene built
+once and copied to every context from one host thread each, one host thread per shard rendering
+tiles t % n == r, the shard pack on each context, the unpack on the first and the statistics
+summed over the shards; only the transport differs (a device-to-device copy instead of grouped
+RCCL ncclSend / ncclRecv).  The frame must equal rtx_render's bit for bit, with equal summed ray
+counts (render.c:349-352 is the parallel point the shards replace).
+
+NOT exercised here: RCCL itself and peer copies between distinct devices (this box has one GPU,
+and the driver's 8-GPU runs have been skipped for want of a node).  What stands in for them: the
+loopback group above, the record layout on the host (tests/test_gather.py), the same records
+gathered over torch.distributed with gloo (tests/test_distributed.py), and the group line's
+schema (tests/test_bench_cli.py).
 """
 import numpy as np
 import pytest
@@ -91,3 +98,52 @@ def test_gpu_tile_pack_unpack_device():
     torch.cuda.synchronize()
     assert np.array_equal(o_rgb.cpu().numpy(), rgb) and np.array_equal(o_z.cpu().numpy(), z)
     r.close()
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+@pytest.mark.parametrize("name", ["s5_path2", "s6_amb", "s3_path2"])
+def test_gpu_loopback_group_matches_render(name, n):
+    """rtx_group_render at n shards (loopback transport) is rtx_render, bit for bit, with the ray
+    counts of the shards summing to the single render's"""
+    scene, frame, params, _ = C.load_config(name)
+    r = rtxpy.Renderer(0)
+    r.upload(scene)
+    a, za = r.render(frame, params)
+    sa = r.stats()
+    r.close()
+    g = rtxpy.Group([0], loopback=n)
+    assert g.size() == n
+    g.upload(scene)
+    b, zb = g.render(frame, params)
+    sb = g.stats()
+    per = [g.device_stats(k) for k in range(n)]
+    # a second frame through the same group (buffers reused, chunk sizes from the first)
+    b2, zb2 = g.render(frame, params)
+    g.close()
+    assert np.array_equal(a, b) and np.array_equal(za, zb)
+    assert np.array_equal(b, b2) and np.array_equal(zb, zb2)
+    assert (sb.closest_rays, sb.shadow_rays, sb.shade_points) == (sa.closest_rays, sa.shadow_rays, sa.shade_points)
+    assert sum(p.closest_rays for p in per) == sa.closest_rays
+    assert sum(p.shadow_rays for p in per) == sa.shadow_rays
+    assert sb.devices == n and sb.gather_ms > 0.0 and sb.transport == abi.RTX_TRANSPORT_LOOPBACK
+    for k, p in enumerate(per):  # every context holds the tree built on the first one
+        assert (p.wide_nodes, p.wide_entries, p.wide_depth, p.bvh_nodes, p.tree_rotated, p.shadow_walk) == \
+            (sa.wide_nodes, sa.wide_entries, sa.wide_depth, sa.bvh_nodes, sa.tree_rotated, sa.shadow_walk)
+        assert (p.upload_copy_ms > 0.0) == (k > 0)
+        assert p.closest_rays > 0
+
+
+def test_gpu_loopback_group_sharding_of_a_tall_ragged_frame():
+    """a frame whose tile count is not a multiple of n (and smaller than n in one dimension)"""
+    scene, _, params, _ = C.load_config("s1_amb")
+    frame = scene.frame(20, 61)
+    r = rtxpy.Renderer(0)
+    r.upload(scene)
+    a, za = r.render(frame, params)
+    r.close()
+    for n in (5, 16):  # 3 x 8 = 24 tiles over 5 shards; 16 shards, some with 1 tile
+        g = rtxpy.Group([0], loopback=n)
+        g.upload(scene)
+        b, zb = g.render(frame, params)
+        g.close()
+        assert np.array_equal(a, b) and np.array_equal(za, zb), n

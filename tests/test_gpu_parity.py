@@ -236,7 +236,7 @@ def test_gpu_statistical_vs_reference_seeds(renderer, name, rng):
     """Against the reference's own glibc rand() stream: the GPU image averaged over
     as many counter-RNG seeds as the reference fixture averages glibc seeds (16-256), per-channel
     means within 1 % and 8x8 box-filtered relL1 <= 3 %, for the plain counter RNG and for
-    stratified light samples (RTX_RNG_STRAT, the default).  Fixture sigma of the seed-averaged
+    stratified light samples (RTX_RNG_STRAT, opt-in).  Fixture sigma of the seed-averaged
     mean <= 0.2 % (tests/golden/seeds/manifest.json)."""
     scene, frame, params, m, g = C.load_seedset(name)
     params.rng = rng

@@ -3,9 +3,10 @@
  * as rtx_build_scene does, then simulates k_shadow's 8-wide walk (rtx_shadow.hip shadow_walk8)
  * on the CPU for sampled shadow rays to report tree shape and per-ray / per-wave work:
  * node visits, box tests, primitive tests, and, for packets of 64 light samples of one shade
- * point walking in lockstep, wave steps and leaf rounds.  Shade points are sampled on the
- * bounded objects' surfaces (area-weighted) and on the planes inside the bound; light samples
- * are stratified like RTX_RNG_STRAT.
+ * point walking in lockstep, wave steps and leaf rounds.  Shade points are the primary hits of
+ * sampled 1080p pixels and their -n 64 GI hits; light samples are i.i.d. like the library's
+ * default RTX_RNG_COUNTER (W8SIM_STRAT=1: stratified like RTX_RNG_STRAT).  W8SIM_OCC=1 adds the
+ * occluder-first tests (a cached opaque blocker tested before the walk).
  *   build: tools/w8sim.sh       run: tools/w8sim <scene.json> [base_dir] [points]
  */
 #include <chrono>
@@ -140,6 +141,11 @@ struct Stats {
 	double dlevel[16] = {}, dstep_top[16] = {};
 	/* lane refill simulation (refill threshold RF_T[k]) */
 	double rf_steps[6] = {}, rf_usteps[6] = {}, rf_refills[6] = {};
+	/* occluder-first tests (opaque blockers): samples a cached occluder resolves, and the packets'
+	 * wave steps / leaf rounds once those lanes skip their walk.  [0] probe ray to the light's
+	 * centre, [1] the point's last blocker from an earlier packet, [2] the lane's blocker of the
+	 * previous point (Morton neighbour), [3] probe + last blocker */
+	double occ_hit[4] = {}, occ_steps[4] = {}, occ_rounds[4] = {}, probe_visits = 0, blocked_samples = 0;
 };
 static const int RF_T[6] = { 64, 48, 32, 16, 8, 1 };
 
@@ -182,6 +188,28 @@ static void refill_sim(const std::vector<std::vector<uint32_t>> &seqs, int T, do
 			}
 		usteps += uni;
 	}
+}
+
+/* the opaque triangle `obj` blocks the segment P + t d, eps < t < dist (Moller-Trumbore in double,
+ * as the walk's leaf test) */
+static bool occ_blocks(const rtx_scene_desc *sc, uint32_t obj, const float P[3], const double d[3], double dist)
+{
+	if (obj == RTX_NONE)
+		return false;
+	const rtx_object &o = sc->objects[obj];
+	if (o.type != RTX_TRIANGLE || sc->materials[o.material].transparent)
+		return false;
+	const double e1[3] = { o.e1[0], o.e1[1], o.e1[2] }, e2[3] = { o.e2[0], o.e2[1], o.e2[2] };
+	const double h[3] = { d[1] * e2[2] - d[2] * e2[1], d[2] * e2[0] - d[0] * e2[2], d[0] * e2[1] - d[1] * e2[0] };
+	const double aa = e1[0] * h[0] + e1[1] * h[1] + e1[2] * h[2];
+	if (fabs(aa) < o.epsilon)
+		return false;
+	const double f = 1 / aa, s[3] = { P[0] - o.p0[0], P[1] - o.p0[1], P[2] - o.p0[2] };
+	const double uu = f * (s[0] * h[0] + s[1] * h[1] + s[2] * h[2]);
+	const double q[3] = { s[1] * e1[2] - s[2] * e1[1], s[2] * e1[0] - s[0] * e1[2], s[0] * e1[1] - s[1] * e1[0] };
+	const double vv = f * (d[0] * q[0] + d[1] * q[1] + d[2] * q[2]);
+	const double tt = f * (e2[0] * q[0] + e2[1] * q[1] + e2[2] * q[2]);
+	return uu >= 0 && vv >= 0 && uu + vv <= 1 && tt > o.epsilon && tt < dist;
 }
 
 int main(int argc, char **argv)
@@ -469,18 +497,84 @@ int main(int argc, char **argv)
 				pts.push_back({ (float)(P0[0] + t2 * r[0]), (float)(P0[1] + t2 * r[1]), (float)(P0[2] + t2 * r[2]) });
 		}
 	}
+	/* the first opaque blocker of the segment P + t d (t < dist) in the walk's slot order (the
+	 * occluder-first probe), and the node visits it took */
+	auto probe_blocker = [&](const float P[3], const double d[3], double dist, double &visits) -> uint32_t {
+		double ob[3], db[3], invq[3], oi[3];
+		for (int a = 0; a < 3; a++) {
+			ob[a] = tf.rotated ? tf.r[a][0] * (P[0] - tf.c[0]) + tf.r[a][1] * (P[1] - tf.c[1]) + tf.r[a][2] * (P[2] - tf.c[2]) : P[a];
+			db[a] = tf.rotated ? tf.r[a][0] * d[0] + tf.r[a][1] * d[1] + tf.r[a][2] * d[2] : d[a];
+		}
+		for (int a = 0; a < 3; a++) {
+			const double inv = fabs(db[a]) > 1e-30 ? 1.0 / db[a] : copysign(1e30, db[a]);
+			invq[a] = inv * qsi[a];
+			oi[a] = (ob[a] - F.qo[a]) * F.qs[a] * invq[a];
+		}
+		std::vector<uint32_t> stk{ 0u };
+		while (!stk.empty()) {
+			const uint32_t node = stk.back();
+			stk.pop_back();
+			const DW8 &N = w8[node];
+			visits++;
+			const double org[3] = { (double)(N.w[0] & 0xFFFF), (double)(N.w[0] >> 16), (double)(N.w[1] & 0xFFFF) };
+			const int ex[3] = { (int)((N.w[1] >> 16) & 15), (int)((N.w[1] >> 20) & 15), (int)((N.w[1] >> 24) & 15) };
+			const uint32_t base = N.w[2] >> 8;
+			for (int c = 7; c >= 0; c--) { /* pushed in reverse: popped in slot order */
+				if (!((N.w[3] >> c) & 1))
+					continue;
+				double tn = 0, tfar = dist;
+				for (int a = 0; a < 3; a++) {
+					const uint8_t *l8 = (const uint8_t *)&N.w[4 + 4 * a], *h8 = (const uint8_t *)&N.w[6 + 4 * a];
+					const double t0 = (org[a] + ldexp(l8[c], ex[a])) * invq[a] - oi[a];
+					const double t1 = (org[a] + ldexp(h8[c], ex[a])) * invq[a] - oi[a];
+					tn = std::max(tn, std::min(t0, t1));
+					tfar = std::min(tfar, std::max(t0, t1));
+				}
+				if (tn > tfar)
+					continue;
+				if ((N.w[2] >> c) & 1) {
+					stk.push_back(base + c);
+					continue;
+				}
+				const DPrim &p = *(const DPrim *)&w8[base + c];
+				uint32_t obj;
+				memcpy(&obj, &p.b[3], 4);
+				if (occ_blocks(sc, obj, P, d, dist))
+					return obj;
+			}
+		}
+		return RTX_NONE;
+	};
+	const bool occ_sim = getenv("W8SIM_OCC") && atoi(getenv("W8SIM_OCC"));
+	const bool strat = getenv("W8SIM_STRAT") && atoi(getenv("W8SIM_STRAT")); /* RTX_RNG_STRAT light samples */
+	uint32_t prev_lane_blk[64];
+	for (int l = 0; l < 64; l++)
+		prev_lane_blk[l] = RTX_NONE;
 	for (int pi = 0; pi < npts; pi++) {
 		const float P[3] = { pts[pi][0], pts[pi][1], pts[pi][2] };
+		uint32_t probe_occ = RTX_NONE, last_blk = RTX_NONE;
+		if (occ_sim) {
+			float Lc[3];
+			for (int a = 0; a < 3; a++)
+				Lc[a] = E.type == RTX_SPHERE ? E.p0[a] : E.p0[a] + (E.e1[a] + E.e2[a]) / 3.f;
+			double d[3] = { Lc[0] - P[0], Lc[1] - P[1], Lc[2] - P[2] };
+			const double dist = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+			for (int a = 0; a < 3; a++)
+				d[a] /= dist;
+			probe_occ = probe_blocker(P, d, dist, S.probe_visits);
+		}
 		/* packets of 64 light samples */
 		std::vector<std::vector<uint32_t>> allseq; /* every sample's node visits (immediate-test walk) */
 		for (uint32_t b0 = 0; b0 < nl; b0 += 64) {
 			std::vector<uint32_t> visits_lane, leaf_at; /* per-lane per-visit leaf hits */
 			std::vector<std::vector<uint32_t>> leaves(64), seq(64);
 			uint32_t block_at[64]; /* ordinal (in discovery order) of the lane's blocking leaf test, or ~0 */
+			uint32_t blk_obj[64]; /* the lane's blocking primitive (object index), or RTX_NONE */
+			float lane_d[64][3], lane_dist[64];
 			uint32_t maxv = 0, imm_len[64] = {};
 			for (uint32_t l = 0; l < 64 && b0 + l < nl; l++) {
 				const uint32_t j = b0 + l;
-				float u1 = ((float)j + U(rng)) / (float)nl, u2 = U(rng);
+				float u1 = strat ? ((float)j + U(rng)) / (float)nl : U(rng), u2 = U(rng);
 				float Lp[3];
 				if (E.type == RTX_SPHERE) {
 					const float inc = u1 * 2.f * 3.1415927f, az = u2 * 2.f * 3.1415927f;
@@ -503,6 +597,10 @@ int main(int argc, char **argv)
 				const double dist = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
 				for (int a = 0; a < 3; a++)
 					d[a] /= dist;
+				for (int a = 0; a < 3; a++)
+					lane_d[l][a] = (float)d[a];
+				lane_dist[l] = (float)dist;
+				blk_obj[l] = RTX_NONE;
 				double invq[3], oi[3], ob[3], db[3];
 				for (int a = 0; a < 3; a++) { /* the ray in the trees' frame (boxes); primitives in world space */
 					ob[a] = tf.rotated ? tf.r[a][0] * (P[0] - tf.c[0]) + tf.r[a][1] * (P[1] - tf.c[1]) + tf.r[a][2] * (P[2] - tf.c[2]) : P[a];
@@ -601,6 +699,7 @@ int main(int argc, char **argv)
 						if (!blocked && uu >= 0 && vv >= 0 && uu + vv <= 1 && tt > p.a[3] && tt < dist) {
 							blocked = true;
 							block_at[l] = nleaf_total - 1;
+							blk_obj[l] = half ? partner[obj] : obj;
 							/* postponed tests would have kept walking: record the rest of the walk
 							 * (the leaf hits of later visits) without stopping at the blocker */
 						}
@@ -639,6 +738,39 @@ int main(int argc, char **argv)
 			for (uint32_t l = 0; l < 64 && b0 + l < nl; l++)
 				allseq.emplace_back(seq[l].begin(), seq[l].begin() + std::min<size_t>(seq[l].size(), imm_len[l]));
 			S.packets++;
+			if (occ_sim) {
+				const uint32_t nlanes = std::min<uint32_t>(64, nl - b0);
+				for (uint32_t l = 0; l < nlanes; l++)
+					S.blocked_samples += blk_obj[l] != RTX_NONE;
+				for (int v = 0; v < 4; v++) {
+					bool res[64] = {};
+					for (uint32_t l = 0; l < nlanes; l++) {
+						const double dd[3] = { lane_d[l][0], lane_d[l][1], lane_d[l][2] };
+						const uint32_t o1 = v == 0 || v == 3 ? probe_occ : v == 1 ? last_blk : prev_lane_blk[l];
+						res[l] = occ_blocks(sc, o1, P, dd, lane_dist[l]) ||
+							 (v == 3 && occ_blocks(sc, last_blk, P, dd, lane_dist[l]));
+						S.occ_hit[v] += res[l];
+					}
+					uint32_t mv = 0;
+					for (uint32_t l = 0; l < nlanes; l++)
+						if (!res[l])
+							mv = std::max(mv, imm_len[l]);
+					S.occ_steps[v] += mv;
+					for (uint32_t i = 0; i < mv; i++) {
+						uint32_t m = 0;
+						for (uint32_t l = 0; l < nlanes; l++)
+							if (!res[l] && i < imm_len[l])
+								m = std::max(m, leaves[l][i]);
+						S.occ_rounds[v] += m;
+					}
+				}
+				for (uint32_t l = 0; l < nlanes; l++)
+					if (blk_obj[l] != RTX_NONE) {
+						if (last_blk == RTX_NONE || true)
+							last_blk = blk_obj[l]; /* the packet's last blocked lane: the cache of the next packet */
+						prev_lane_blk[l] = blk_obj[l];
+					}
+			}
 			/* postponed leaf tests: a leaf round only when >= T lanes hold pending leaves or no lane
 			 * has node work left (emitter leaves excluded, as a tree without emitters) */
 			for (int k = 0; k < 8; k++) {
@@ -746,6 +878,17 @@ int main(int argc, char **argv)
 		printf("  %2d   %8.2f (%6.2f)   %8.2f   %9.0f\n", RF_T[k], S.rf_steps[k] / npts, S.rf_usteps[k] / npts,
 		       S.rf_refills[k] / npts,
 		       (178.0 * (S.rf_steps[k] - S.rf_usteps[k]) + 95.0 * S.rf_usteps[k] + 220.0 * S.rf_refills[k]) / npts);
+	if (occ_sim) {
+		static const char *nm[4] = { "probe to the light centre", "the point's last blocker (earlier packet)",
+					     "the lane's blocker of the previous point", "probe + last blocker" };
+		printf("occluder-first (opaque blockers; %.3f of samples blocked; probe %.2f node visits per point):\n"
+		       "  occluder                                       resolves (of samples / of blocked)  wave steps/packet  leaf rounds/packet\n",
+		       S.blocked_samples / S.rays, S.probe_visits / npts);
+		printf("  %-46s %8s %8s          %8.2f          %8.2f\n", "none", "-", "-", S.wave_steps / S.packets, S.leaf_rounds / S.packets);
+		for (int v = 0; v < 4; v++)
+			printf("  %-46s %8.3f %8.3f          %8.2f          %8.2f\n", nm[v], S.occ_hit[v] / S.rays,
+			       S.occ_hit[v] / std::max(1.0, S.blocked_samples), S.occ_steps[v] / S.packets, S.occ_rounds[v] / S.packets);
+	}
 	printf("rays %.0f  visits/ray %.2f  boxes/ray %.2f  tris/ray %.3f  blocked %.3f  wave steps/packet %.2f  leaf "
 	       "rounds/packet %.2f  lanes/leaf round %.1f\n",
 	       S.rays, S.visits / S.rays, S.boxes / S.rays, S.tris / S.rays, S.blocked / S.rays, S.wave_steps / S.packets,
