@@ -169,7 +169,10 @@ struct Builder {
 			float ext = cb.hi[best_axis] - cb.lo[best_axis];
 			float k = NB * (1.f - 1e-6f) / ext;
 			const int ax = best_axis;
-			uint32_t *pm = std::partition(idx.data() + b, idx.data() + e, [&](uint32_t p) {
+			/* stable, like the device builder's prefix-scan partition (rtx_build.hip): primitives
+			 * with equal centroids (a rotated mesh face's two triangles) keep their order, so both
+			 * builders put the same primitive in the same leaf */
+			uint32_t *pm = std::stable_partition(idx.data() + b, idx.data() + e, [&](uint32_t p) {
 				int bi = (int)((cent[3 * (size_t)p + ax] - cb.lo[ax]) * k);
 				bi = std::min(std::max(bi, 0), (int)NB - 1);
 				return (uint32_t)bi <= best_split;

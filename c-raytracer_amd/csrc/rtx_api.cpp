@@ -446,7 +446,9 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 	memcpy(tlo, c->bound_lo, 12);
 	memcpy(thi, c->bound_hi, 12);
 	if (tf.rotated) {
-		const double pad = hs.frame_pad = rtx_frame_pad(rtx_frame_radius(c->bound_lo, c->bound_hi, tf));
+		const double rad = rtx_frame_radius(c->bound_lo, c->bound_hi, tf);
+		tf.rad = std::nextafter((float)rad, FLT_MAX); /* rounded up (rtx_math.h tf_far) */
+		const double pad = hs.frame_pad = rtx_frame_pad(rad);
 		rtx_frame_boxes(sc, bounded, tf, pad, lo.data(), hi.data(), tlo, thi);
 	}
 	hs.frame_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf0).count();
@@ -1290,6 +1292,25 @@ extern "C" int rtx_set_option(rtx_ctx *c, int option, int64_t value)
 		return RTX_OK;
 	}
 	return fail(RTX_ERR_ARG, "unknown option %d", option);
+}
+
+extern "C" int rtx_read_wide_tree(rtx_ctx *c, void *entries, uint32_t capacity, uint32_t *count, float frame[6])
+{
+	if (!c || !count)
+		return fail(RTX_ERR_ARG, "null argument");
+	if (!c->have_scene)
+		return fail(RTX_ERR_STATE, "rtx_read_wide_tree before rtx_upload_scene");
+	const DScene &S = c->scene;
+	*count = S.w8 ? S.num_w8 : 0u;
+	if (frame) {
+		memcpy(frame, S.w8qo, 12);
+		memcpy(frame + 3, S.w8qs, 12);
+	}
+	if (entries && S.w8 && capacity) {
+		HIP_TRY(hipSetDevice(c->device));
+		HIP_TRY(hipMemcpy(entries, S.w8, (size_t)std::min(capacity, S.num_w8) * sizeof(DW8), hipMemcpyDeviceToHost));
+	}
+	return RTX_OK;
 }
 
 extern "C" int rtx_get_stats(const rtx_ctx *c, rtx_stats *out)

@@ -117,6 +117,10 @@ typedef struct DTreeFrame {
 	float r[3][3];
 	float c[3];
 	uint32_t rotated;
+	float rad; /* the largest |x - c| component over the bounded objects' world box (rtx_frame_radius):
+	            * ray origins farther than RTX_FRAME_FAR * rad from c are handled by tf_shift /
+	            * tf_far_end (rtx_math.h), as the boxes' padding covers the transform's rounding only
+	            * near c */
 } DTreeFrame;
 
 /* 8-wide compressed BVH for the shadow walk (rtx_shadow.hip shadow_walk8), in the style of

@@ -24,7 +24,10 @@
  * ray point at parameter t.  Every leaf box is computed exactly (double) from the same float R
  * and c, rounded outward, and padded by RTX_FRAME_PAD times the scene's radius about c on top
  * of the world trees' own relative padding and one 16-bit quantisation step: ample for rays that
- * start within a few scene radii of c (shade points, the camera of any reference scene).
+ * start within a few scene radii of c (shade points, the camera of any reference scene).  Rays
+ * from farther away (a distant camera, a point far out on a plane) get a frame origin near c
+ * computed in double (rtx_math.h tf_shift for closest hits, tf_point_at at the segment's other end
+ * for shadow rays), so the padding covers them too.
  */
 #include <float.h>
 #include <math.h>

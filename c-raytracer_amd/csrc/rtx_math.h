@@ -168,6 +168,35 @@ __device__ __forceinline__ f3 tf_point(const float (&r)[3][3], const float (&c)[
 	return tf_dir(r, mk3(x.x - c[0], x.y - c[1], x.z - c[2]));
 }
 
+/* Ray origins far from the trees' frame centre.  The transform's rounding grows with |x - c|
+ * (about 3 * 2^-24 (|x - c| + t)), and the leaf boxes are padded for origins within a few radii
+ * of c (rtx_frame.cpp).  An origin beyond RTX_FRAME_FAR radii (|x'| max-norm) gets a frame origin
+ * near c computed in double, so the box tests stay conservative for any origin; the world ray
+ * the primitives are tested with is untouched, so no hit changes. */
+#define RTX_FRAME_FAR 4.f
+__device__ __forceinline__ bool tf_far(f3 ob, float rad)
+{
+	return fmaxf(fabsf(ob.x), fmaxf(fabsf(ob.y), fabsf(ob.z))) > RTX_FRAME_FAR * rad;
+}
+/* x' = R (x - c) of the world point x + s d, the sum and product formed in double */
+__device__ __forceinline__ f3 tf_point_at(const float (&r)[3][3], const float (&c)[3], f3 x, f3 d, float s)
+{
+	const double v0 = ((double)x.x - c[0]) + (double)s * d.x, v1 = ((double)x.y - c[1]) + (double)s * d.y,
+		     v2 = ((double)x.z - c[2]) + (double)s * d.z;
+	return mk3((float)(r[0][0] * v0 + r[0][1] * v1 + r[0][2] * v2), (float)(r[1][0] * v0 + r[1][1] * v1 + r[1][2] * v2),
+		   (float)(r[2][0] * v0 + r[2][1] * v1 + r[2][2] * v2));
+}
+/* closest-hit rays (k_trace): the frame origin moved along the ray to t0, 2 radii before its
+ * closest approach to c (every bounded object lies within sqrt(3) radii of c, so no hit comes
+ * before t0); the walk then tests boxes against tbest - t0.  t0 = 0 for a ray leaving the scene. */
+__device__ __forceinline__ f3 tf_shift(const float (&r)[3][3], const float (&c)[3], float rad, f3 o, f3 d, float &t0)
+{
+	const double tca = -(((double)o.x - c[0]) * d.x + ((double)o.y - c[1]) * d.y + ((double)o.z - c[2]) * d.z);
+	const double ts = tca - 2.0 * (double)rad;
+	t0 = ts > 0.0 ? (float)ts : 0.f;
+	return tf_point_at(r, c, o, d, t0);
+}
+
 /* slab test on the traversal path: hit iff [max(tnear,0), min(tfar,tlim)] non-empty */
 __device__ __forceinline__ bool slab(float lox, float hix, float loy, float hiy, float loz, float hiz, f3 oi, f3 inv,
 				     float tlim, float &tnear)

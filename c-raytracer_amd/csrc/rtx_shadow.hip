@@ -350,7 +350,9 @@ template <bool COUNT, int OCT>
 __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__restrict__ mats, f3 o, f3 d, f3 ob, f3 inv,
 					     float &tl, uint32_t emit_obj, f3 &li, ShadowCount &sc)
 {
-	constexpr uint32_t K = (OCT == 8 || !RTX_W8_SORDER) ? 0u : (~(uint32_t)OCT & 7u);
+	/* visit order of hit children: plain slot order (0), front to back from the shade point (1), or
+	 * front to back from the light (2) */
+	constexpr uint32_t K = (OCT == 8 || !RTX_W8_SORDER) ? 0u : RTX_W8_SORDER == 2 ? ((uint32_t)OCT & 7u) : (~(uint32_t)OCT & 7u);
 	/* the ray in the tree's 16-bit frame: ob / inv are its origin and inverse direction in the
 	 * tree's rotated frame (shadow_query), o / d the world ray the primitives are tested with */
 	const f3 invq = mk3(inv.x * Q.qsi.x, inv.y * Q.qsi.y, inv.z * Q.qsi.z);
@@ -569,6 +571,13 @@ __device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restri
 		}
 		ob = tf_point(r, c, o);
 		db = tf_dir(r, d);
+		/* a far origin (a plane point far from the bounded objects, rtx_math.h tf_far): the walk runs
+		 * the segment from its other end, x' computed in double there; the same boxes meet the
+		 * segment [0, dist] from either end, and the primitives are still tested from o along d */
+		if (tf_far(ob, __uint_as_float(uni(__float_as_uint(tf.rad))))) {
+			ob = tf_point_at(r, c, o, d, dist);
+			db = mk3(-db.x, -db.y, -db.z);
+		}
 	}
 	const f3 inv = safe_inv_fast(db); /* boxes are padded 2e-6 relative: a 1-ulp 1/d keeps the test conservative */
 	const uint32_t oct = ((~__float_as_uint(inv.x)) >> 31) | (((~__float_as_uint(inv.y)) >> 31) << 1) |

@@ -78,10 +78,15 @@ __device__ void trace_closest_bvh2(const DScene &S, uint32_t *stk, bool act, f3 
 		}
 	}
 	if (act && S.root_ref != RTX_EMPTY_REF) {
-		/* boxes in the trees' frame (rtx_device.h DTreeFrame), primitives in world space */
+		/* boxes in the trees' frame (rtx_device.h DTreeFrame), primitives in world space; a far
+		 * origin's frame origin moves to t0 along the ray (tf_shift: boxes tested against tbest - t0) */
 		const f3 db = S.tf.rotated ? tf_dir(S.tf.r, d) : d;
 		const f3 inv = safe_inv(db);
-		const f3 oi = mul3v(S.tf.rotated ? tf_point(S.tf.r, S.tf.c, o) : o, inv);
+		float t0 = 0.f;
+		f3 ob = S.tf.rotated ? tf_point(S.tf.r, S.tf.c, o) : o;
+		if (S.tf.rotated && tf_far(ob, S.tf.rad))
+			ob = tf_shift(S.tf.r, S.tf.c, S.tf.rad, o, d, t0);
+		const f3 oi = mul3v(ob, inv);
 		uint32_t ref = S.root_ref;
 		uint32_t sp = 0;
 		/* entries from RTX_TRACE_LSTK on live in HBM, [entry][grid lane]; lane addresses formed at
@@ -134,8 +139,9 @@ __device__ void trace_closest_bvh2(const DScene &S, uint32_t *stk, bool act, f3 
 				if (COUNT)
 					tc.nodes++;
 				float tn0, tn1;
-				const bool h0 = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, oi, inv, tbest, tn0) && tn0 < tbest;
-				const bool h1 = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, oi, inv, tbest, tn1) && tn1 < tbest;
+				const float tlim = tbest - t0; /* tbest itself when t0 = 0 */
+				const bool h0 = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, oi, inv, tlim, tn0) && tn0 < tlim;
+				const bool h1 = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, oi, inv, tlim, tn1) && tn1 < tlim;
 				if (h0 && h1) {
 					/* nearer child first; tie -> right first (accel.c:341-345) */
 					const bool l_first = tn0 < tn1;
@@ -176,7 +182,7 @@ __device__ void trace_closest_bvh2(const DScene &S, uint32_t *stk, bool act, f3 
 #endif
 template <bool COUNT, int OCT>
 __device__ __forceinline__ void closest_walk8(const DScene &S, lds_u32 *stk, uint32_t *ostk, size_t ostride, f3 o, f3 d,
-					      f3 ob, f3 inv, float &tbest, uint32_t &hid, TraceCount &tc)
+					      f3 ob, f3 inv, float t0, float &tbest, uint32_t &hid, TraceCount &tc)
 {
 	/* the lane stack: stk / ostk are the wave's bases (LDS, then HBM [entry][grid lane]); a lane's
 	 * address is formed at each use (lane_id), none kept live across the walk */
@@ -193,7 +199,8 @@ __device__ __forceinline__ void closest_walk8(const DScene &S, lds_u32 *stk, uin
 		return sp < RTX_TRACE_LSTK ? stk[sp * WAVE + lane_id()] : ostk[(sp - RTX_TRACE_LSTK) * ostride + lane_id()];
 	};
 	constexpr uint32_t K = (OCT == 8 || !RTX_W8_ORDER) ? 0u : (~(uint32_t)OCT & 7u);
-	/* ob / inv: the ray's origin and inverse direction in the trees' frame; o / d the world ray */
+	/* ob / inv: the ray's origin and inverse direction in the trees' frame, ob at parameter t0 of
+	 * the world ray o / d (tf_shift; 0 unless the origin is far): boxes are tested against tbest - t0 */
 	const f3 qs = ld3(S.w8qs), qo = ld3(S.w8qo);
 	const f3 invq = mk3(inv.x / qs.x, inv.y / qs.y, inv.z / qs.z);
 	const f3 oq = mk3((ob.x - qo.x) * qs.x, (ob.y - qo.y) * qs.y, (ob.z - qo.z) * qs.z);
@@ -208,12 +215,12 @@ __device__ __forceinline__ void closest_walk8(const DScene &S, lds_u32 *stk, uin
 		const uint32_t un = uni(node);
 		if (!ballot(node != un)) {
 			if (T) {
-				const W8VisitT r = w8_visit_st<OCT, K>(S.w8s + (size_t)un, invq, oi, tbest);
+				const W8VisitT r = w8_visit_st<OCT, K>(S.w8s + (size_t)un, invq, oi, tbest - t0);
 				v = r.v;
 				nearp = r.near;
 				tin = r.tin;
 			} else {
-				v = w8_visit_s<OCT, K>(S.w8s + (size_t)un, invq, oi, tbest);
+				v = w8_visit_s<OCT, K>(S.w8s + (size_t)un, invq, oi, tbest - t0);
 			}
 		} else {
 			uint32_t w[16];
@@ -227,12 +234,12 @@ __device__ __forceinline__ void closest_walk8(const DScene &S, lds_u32 *stk, uin
 				w[4 * k + 3] = x.w;
 			}
 			if (T) {
-				const W8VisitT r = w8_visit_t<OCT, K>(w, invq, oi, tbest);
+				const W8VisitT r = w8_visit_t<OCT, K>(w, invq, oi, tbest - t0);
 				v = r.v;
 				nearp = r.near;
 				tin = r.tin;
 			} else {
-				v = w8_visit<OCT, K, false>(w, invq, oi, tbest);
+				v = w8_visit<OCT, K, false>(w, invq, oi, tbest - t0);
 			}
 		}
 		if (COUNT && (!RTX_TRACE_EMPTYCOUNT || !v.hm))
@@ -348,7 +355,10 @@ __device__ void trace_closest_w8(const DScene &S, uint32_t *stk, bool act, f3 o,
 	if (live) {
 		/* the ray in the trees' frame (rtx_device.h DTreeFrame) for the box tests */
 		const bool rot = S.tf.rotated != 0;
-		const f3 ob = rot ? tf_point(S.tf.r, S.tf.c, o) : o;
+		float t0 = 0.f;
+		f3 ob = rot ? tf_point(S.tf.r, S.tf.c, o) : o;
+		if (rot && tf_far(ob, S.tf.rad)) /* a far origin (tf_shift) */
+			ob = tf_shift(S.tf.r, S.tf.c, S.tf.rad, o, d, t0);
 		const f3 inv = safe_inv_fast(rot ? tf_dir(S.tf.r, d) : d);
 		lds_u32 *ls = (lds_u32 *)stk;
 		uint32_t *ostk = S.ostk + (size_t)blockIdx.x * WAVE;
@@ -361,13 +371,13 @@ __device__ void trace_closest_w8(const DScene &S, uint32_t *stk, bool act, f3 o,
 			switch (sel) {
 #define RTX_CWALK(K)                                                                    \
 	case K:                                                                             \
-		closest_walk8<COUNT, K>(S, ls, ostk, ostride, o, d, ob, inv, tbest, hid, tc);   \
+		closest_walk8<COUNT, K>(S, ls, ostk, ostride, o, d, ob, inv, t0, tbest, hid, tc); \
 		break;
 				RTX_CWALK(0) RTX_CWALK(1) RTX_CWALK(2) RTX_CWALK(3) RTX_CWALK(4) RTX_CWALK(5) RTX_CWALK(6)
 				RTX_CWALK(7)
 #undef RTX_CWALK
 			default:
-				closest_walk8<COUNT, 8>(S, ls, ostk, ostride, o, d, ob, inv, tbest, hid, tc);
+				closest_walk8<COUNT, 8>(S, ls, ostk, ostride, o, d, ob, inv, t0, tbest, hid, tc);
 				break;
 			}
 		}

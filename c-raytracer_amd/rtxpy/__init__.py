@@ -253,6 +253,16 @@ class Renderer:
         _check(self.lib.rtx_postprocess_device(self._ctx, width, height, C.byref(post), C.c_void_p(d_rgb),
                                                C.c_void_p(d_z), C.c_void_p(stream) if stream else None))
 
+    def wide_tree(self):
+        """the uploaded 8-wide tree (rtx_read_wide_tree): (entries uint32 (n, 16), frame float32 (6,))"""
+        n = C.c_uint32(0)
+        frame = np.zeros(6, np.float32)
+        _check(self.lib.rtx_read_wide_tree(self._ctx, None, 0, C.byref(n), frame.ctypes.data))
+        ent = np.zeros((n.value, 16), np.uint32)
+        if n.value:
+            _check(self.lib.rtx_read_wide_tree(self._ctx, ent.ctypes.data, n.value, C.byref(n), frame.ctypes.data))
+        return ent, frame
+
     def stats(self):
         s = Stats()
         _check(self.lib.rtx_get_stats(self._ctx, C.byref(s)))

@@ -295,6 +295,10 @@ int rtx_set_option(rtx_ctx *ctx, int option, int64_t value);
 int rtx_tree_frame(const rtx_scene_desc *scene, int *rotated, float rot[9], float center[3], double *cost_ratio);
 void rtx_close(rtx_ctx *ctx);
 const char *rtx_last_error(void);
+/* Diagnostics (tests): the uploaded 8-wide tree's 64-byte entries (csrc/rtx_device.h DW8) copied to
+ * host memory, at most `capacity` of them; *count = the tree's entry count (0: no 8-wide tree),
+ * frame[6] = its 16-bit frame (origin, scale per axis).  entries may be NULL to query the count. */
+int rtx_read_wide_tree(rtx_ctx *ctx, void *entries, uint32_t capacity, uint32_t *count, float frame[6]);
 
 /*
  * Several devices rendering one frame (the reference's own parallel point is

@@ -5,10 +5,11 @@ against lib/librtx.so, at -O2 (IEEE scene set-up).  That program renders the fra
 repository's engine renders (lib/engine: our own scene loader and TIFF writer over the same
 library, the same counter RNG), bit for bit: the scene the reference loads into its globals
 reaches the library unchanged through the adapter's flattening (rtx_export.h accessors).
-(Built with Makefile.rt's -Ofast instead, the reference's camera and edge set-up carries its own
-contraction noise; frames then agree within SURVEY §8(c)'s -Ofast-vs-O2 floor on s1/s3/s5/s6
-and at relL1 5e-5 on s2.)  Skipped where the binary was not built (no /root/reference when
-__graft_entry__.build() ran)."""
+The drop-in as a user builds it from INTEGRATION.md (oracle/Makefile engine_dropin_rt: Makefile.rt's
+own -Ofast -flto flags, no determinism shim) carries the reference's -Ofast contraction noise in
+its camera and scene set-up, so its frames are checked against the -O2 build's within SURVEY
+§8(c)'s -Ofast-vs-O2 floor of each config (tests/golden/frames/manifest.json).  Skipped where the
+binaries were not built (no /root/reference when __graft_entry__.build() ran)."""
 import os
 import subprocess
 
@@ -22,6 +23,15 @@ import standins
 pytestmark = pytest.mark.gpu
 
 DROPIN = os.path.join(C.ROOT, "oracle", "_ref", "engine_dropin")
+DROPIN_RT = os.path.join(C.ROOT, "oracle", "_ref", "engine_dropin_rt")
+
+
+def render_with(exe, m, tmp_path):
+    out = str(tmp_path / (os.path.basename(exe) + ".tif"))
+    cmd = [exe, os.path.join("scenes", m["scene"]), out, str(m["width"]), str(m["height"]), "-f"] + m["flags"]
+    p = subprocess.run(cmd, cwd=C.GOLDEN, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, (exe, p.stdout[-2000:] + p.stderr[-2000:])
+    return rtxpy.read_tiff_raw(out)
 
 
 @pytest.mark.skipif(not os.path.exists(DROPIN), reason="oracle/_ref/engine_dropin not built")
@@ -41,3 +51,18 @@ def test_gpu_dropin_renders_what_the_engine_renders(name, tmp_path):
     assert (za > 0).any()
     ok, info = C.compare_const(a, za, b, zb, **C.floor_tolerance(m))
     assert np.array_equal(za, zb) and np.array_equal(a, b), (name, info, float(np.abs(a - b).max()))
+
+
+@pytest.mark.skipif(not (os.path.exists(DROPIN_RT) and os.path.exists(DROPIN)), reason="drop-in binaries not built")
+@pytest.mark.parametrize("name", ["s1_amb", "s2_blinn_lin", "s3_path2", "s5_path2", "s6_amb"])
+def test_gpu_dropin_user_recipe(name, tmp_path):
+    """INTEGRATION.md's own build (Makefile.rt flags, -Ofast, no shim) against the -O2 drop-in:
+    the same library and RNG, only the reference's scene set-up rounding differs"""
+    m = C.manifest()[name]
+    if "standin" in m["scene"]:
+        standins.ensure_scene(m["scene"].split("_standin")[0])
+    a, za = render_with(DROPIN_RT, m, tmp_path)
+    b, zb = render_with(DROPIN, m, tmp_path)
+    assert (za > 0).any()
+    ok, info = C.compare_const(a, za, b, zb, **C.floor_tolerance(m))
+    assert ok, (name, info)

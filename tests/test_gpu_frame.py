@@ -11,6 +11,8 @@ The CPU half checks the choice itself (rtx_tree_frame needs no device): the Meng
 rotated by scene6.json's mesh rotation, gets a rotated frame that shrinks its leaf boxes; the
 dragon stand-in and the sphere scenes keep the world axes.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -163,3 +165,49 @@ def test_gpu_rotated_trees_multi_primitive_leaves(renderer, leaf):
         renderer.set_option(abi.RTX_OPT_BVH_LEAF, 1)
     assert sa.tree_rotated == 1 and sa.shadow_walk == abi.RTX_WALK_W8
     assert np.array_equal(za, zb) and np.array_equal(a, b)
+
+
+def far_camera_scene(tmp_path, dist):
+    """a small rotated mesh (a level-1 Menger sponge: 20 cubes, the closest-hit walk's float BVH2
+    and the shadow walk's threaded BVH2) seen from `dist` along -z with a field of view that
+    frames it, a sphere light beside it and scene6's back plane behind it"""
+    import json
+    import standins
+    os.makedirs(tmp_path / "meshes", exist_ok=True)
+    standins.write_stl(str(tmp_path / "meshes" / "m1.stl"), standins.menger_standin(level=1))
+    with open(os.path.join(C.SCENES, "scene6_standin.json")) as fh:
+        d = json.load(fh)
+    centre = [0.0, -0.13, 2.4]
+    for o in d["Objects"]:
+        p = o["parameters"]
+        if o["type"] == "Mesh":
+            p["filename"] = "meshes/m1.stl"
+        elif o["type"] == "Sphere":  # the light: beside the sponge, on the camera's side
+            p["position"], p["radius"] = [1.6, 1.2, 1.4], 0.5
+    d["Camera"]["position"] = [centre[0], centre[1], centre[2] - dist]
+    d["Camera"]["fov"] = float(np.degrees(2 * np.arctan(1.6 / dist)))
+    path = tmp_path / "far.json"
+    path.write_text(json.dumps(d))
+    return rtxpy.Scene.load(str(path), base_dir=str(tmp_path))
+
+
+@pytest.mark.gpu
+@pytest.mark.usefixtures("_defaults")
+@pytest.mark.parametrize("dist", [3.0, 60.0, 2000.0])
+@pytest.mark.parametrize("walks", [(abi.RTX_WALK_AUTO, abi.RTX_WALK_BVH2), (abi.RTX_WALK_W8, abi.RTX_WALK_W8)])
+def test_gpu_rotated_trees_far_camera(renderer, tmp_path, dist, walks):
+    """rays from far outside the trees' frame (a distant camera, points far out on the
+    back plane): the frame origin of a far ray is formed in double near the frame's centre
+    (rtx_math.h tf_shift / tf_point_at), so the rotated trees' boxes stay conservative and the
+    frame is the world trees' bit for bit, z-buffer and colours, at 3, 60 and 2000 scene radii"""
+    scene = far_camera_scene(tmp_path, dist)
+    frame = scene.frame(96, 96)
+    params = rtxpy.params_from_args([], seed=1)
+    opts = {abi.RTX_OPT_SHADOW_WALK: walks[0], abi.RTX_OPT_TRACE_WALK: walks[1]}
+    a, za, sa = _render(renderer, scene, frame, params, abi.RTX_FRAME_AUTO, opts)
+    b, zb, sb = _render(renderer, scene, frame, params, abi.RTX_FRAME_WORLD, opts)
+    assert sa.tree_rotated == 1 and sb.tree_rotated == 0 and sa.trace_walk == walks[1]
+    sponge = (za > 0) & (za < dist + 3.0)  # the back plane lies 5.6 beyond the sponge's centre
+    assert 0.2 < sponge.mean() < 0.95, sponge.mean()  # the sponge fills the frame, the plane around it
+    assert np.array_equal(za, zb), (dist, int((za != zb).sum()))
+    assert np.array_equal(a, b), (dist, int((a != b).any(axis=2).sum()))

@@ -146,6 +146,10 @@ struct Stats {
 	 * centre, [1] the point's last blocker from an earlier packet, [2] the lane's blocker of the
 	 * previous point (Morton neighbour), [3] probe + last blocker */
 	double occ_hit[4] = {}, occ_steps[4] = {}, occ_rounds[4] = {}, probe_visits = 0, blocked_samples = 0;
+	/* packet cull at uniform steps (every walking lane at one node): the node's children, those
+	 * some walking lane hits, and those an interval test of the packet's shared origin and
+	 * direction bounds keeps: [0] bounds over the packet's 64 rays, [1] over the walking lanes */
+	double u_steps = 0, u_kids = 0, u_union = 0, u_cull[2] = {}, u_mixed = 0;
 };
 static const int RF_T[6] = { 64, 48, 32, 16, 8, 1 };
 
@@ -546,6 +550,7 @@ int main(int argc, char **argv)
 		return RTX_NONE;
 	};
 	const bool occ_sim = getenv("W8SIM_OCC") && atoi(getenv("W8SIM_OCC"));
+	const int order = getenv("W8SIM_ORDER") ? atoi(getenv("W8SIM_ORDER")) : 0;
 	const bool strat = getenv("W8SIM_STRAT") && atoi(getenv("W8SIM_STRAT")); /* RTX_RNG_STRAT light samples */
 	uint32_t prev_lane_blk[64];
 	for (int l = 0; l < 64; l++)
@@ -570,6 +575,7 @@ int main(int argc, char **argv)
 			std::vector<std::vector<uint32_t>> leaves(64), seq(64);
 			uint32_t block_at[64]; /* ordinal (in discovery order) of the lane's blocking leaf test, or ~0 */
 			uint32_t blk_obj[64]; /* the lane's blocking primitive (object index), or RTX_NONE */
+			double lane_invq[64][3], lane_oq[64][3], lane_tl[64];
 			float lane_d[64][3], lane_dist[64];
 			uint32_t maxv = 0, imm_len[64] = {};
 			for (uint32_t l = 0; l < 64 && b0 + l < nl; l++) {
@@ -613,8 +619,13 @@ int main(int argc, char **argv)
 						oct |= 1 << a;
 					invq[a] = inv * qsi[a];
 					oi[a] = (ob[a] - F.qo[a]) * F.qs[a] * invq[a];
+					lane_invq[l][a] = invq[a];
+					lane_oq[l][a] = (ob[a] - F.qo[a]) * F.qs[a];
 				}
-				const uint32_t K = ~(uint32_t)oct & 7u;
+				lane_tl[l] = dist;
+				/* W8SIM_ORDER: 0 front to back from the shade point (octant order), 1 plain slot order
+				 * (k_shadow's RTX_W8_SORDER 0), 2 back to front (front to back from the light) */
+				const uint32_t K = order == 1 ? 0u : order == 2 ? (uint32_t)oct & 7u : ~(uint32_t)oct & 7u;
 				/* the walk: node, group register, stack; leaf hits counted per visit */
 				std::vector<uint32_t> stk;
 				uint32_t node = 0, grp = 0, nv = 0, nleaf_total = 0;
@@ -815,8 +826,82 @@ int main(int argc, char **argv)
 							first = at[l];
 						div |= at[l] != first;
 					}
-				if (!div)
+				if (!div) {
+					if (first == ~0u)
+						continue;
+					/* a uniform step at node `first` */
+					const DW8 &N = w8[first];
+					const double org[3] = { (double)(N.w[0] & 0xFFFF), (double)(N.w[0] >> 16), (double)(N.w[1] & 0xFFFF) };
+					const int ex[3] = { (int)((N.w[1] >> 16) & 15), (int)((N.w[1] >> 20) & 15), (int)((N.w[1] >> 24) & 15) };
+					const uint32_t nl2 = std::min<uint32_t>(64, nl - b0);
+					S.u_steps++;
+					S.u_kids += __builtin_popcount(N.w[3] & 0xFFu);
+					double imn[2][3], imx[2][3], tlx[2] = { 0, 0 };
+					for (int v = 0; v < 2; v++)
+						for (int a = 0; a < 3; a++) {
+							imn[v][a] = 1e300;
+							imx[v][a] = -1e300;
+						}
+					for (uint32_t l = 0; l < nl2; l++)
+						for (int v = 0; v < 2; v++) {
+							if (v == 1 && at[l] == ~0u)
+								continue;
+							for (int a = 0; a < 3; a++) {
+								imn[v][a] = std::min(imn[v][a], lane_invq[l][a]);
+								imx[v][a] = std::max(imx[v][a], lane_invq[l][a]);
+							}
+							tlx[v] = std::max(tlx[v], lane_tl[l]);
+						}
+					bool mixed = false;
+					for (int a = 0; a < 3; a++)
+						mixed |= imn[0][a] < 0 && imx[0][a] > 0;
+					S.u_mixed += mixed;
+					const double *oq = lane_oq[0]; /* one origin per packet (one shade point) */
+					for (int c = 0; c < 8; c++) {
+						if (!((N.w[3] >> c) & 1))
+							continue;
+						double lo[3], hi[3];
+						for (int a = 0; a < 3; a++) {
+							const uint8_t *l8 = (const uint8_t *)&N.w[4 + 4 * a], *h8 = (const uint8_t *)&N.w[6 + 4 * a];
+							lo[a] = org[a] + ldexp(l8[c], ex[a]);
+							hi[a] = org[a] + ldexp(h8[c], ex[a]);
+						}
+						bool any = false; /* some walking lane hits the child */
+						for (uint32_t l = 0; l < nl2 && !any; l++) {
+							if (at[l] == ~0u)
+								continue;
+							double tn = 0, tf = lane_tl[l];
+							for (int a = 0; a < 3; a++) {
+								const double t0 = (lo[a] - oq[a]) * lane_invq[l][a], t1 = (hi[a] - oq[a]) * lane_invq[l][a];
+								tn = std::max(tn, std::min(t0, t1));
+								tf = std::min(tf, std::max(t0, t1));
+							}
+							any = tn <= tf;
+						}
+						S.u_union += any;
+						for (int v = 0; v < 2; v++) {
+							double tn = 0, tf = tlx[v];
+							for (int a = 0; a < 3; a++) {
+								if (imn[v][a] < 0 && imx[v][a] > 0)
+									continue; /* the packet's directions straddle the axis: no bound */
+								const double e[4] = { (lo[a] - oq[a]) * imn[v][a], (lo[a] - oq[a]) * imx[v][a],
+										      (hi[a] - oq[a]) * imn[v][a], (hi[a] - oq[a]) * imx[v][a] };
+								/* near: the lesser plane's least t; far: the greater plane's largest t */
+								const double nlo = std::min(std::min(e[0], e[1]), std::min(e[2], e[3]));
+								const double fhi = std::max(std::max(e[0], e[1]), std::max(e[2], e[3]));
+								/* per ray the near plane is min(t_lo, t_hi) and the far max: bound each
+								 * over the interval by the planes' own ranges */
+								const double near_max_lo = std::min(std::max(e[0], e[1]) , std::max(e[2], e[3]));
+								(void)near_max_lo;
+								tn = std::max(tn, nlo);
+								tf = std::min(tf, fhi);
+							}
+							if (tn <= tf)
+								S.u_cull[v]++;
+						}
+					}
 					continue;
+				}
 				S.dsteps++;
 				uint32_t maxlev = 0;
 				for (int l = 0; l < 64; l++)
@@ -878,6 +963,10 @@ int main(int argc, char **argv)
 		printf("  %2d   %8.2f (%6.2f)   %8.2f   %9.0f\n", RF_T[k], S.rf_steps[k] / npts, S.rf_usteps[k] / npts,
 		       S.rf_refills[k] / npts,
 		       (178.0 * (S.rf_steps[k] - S.rf_usteps[k]) + 95.0 * S.rf_usteps[k] + 220.0 * S.rf_refills[k]) / npts);
+	printf("uniform steps %.2f per packet: children %.2f, hit by some walking lane %.2f, kept by the packet interval "
+	       "test %.2f (bounds over the packet) / %.2f (over the walking lanes); steps with mixed-sign directions %.1f%%\n",
+	       S.u_steps / S.packets, S.u_kids / S.u_steps, S.u_union / S.u_steps, S.u_cull[0] / S.u_steps, S.u_cull[1] / S.u_steps,
+	       100 * S.u_mixed / std::max(1.0, S.u_steps));
 	if (occ_sim) {
 		static const char *nm[4] = { "probe to the light centre", "the point's last blocker (earlier packet)",
 					     "the lane's blocker of the previous point", "probe + last blocker" };
