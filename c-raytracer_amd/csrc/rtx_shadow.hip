@@ -346,167 +346,199 @@ __device__ __forceinline__ bool w8_opaque_test(const char *pr, f3 o, f3 d, float
 	return any_tri(mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z), mk3(c.x, c.y, c.z), o, d, a.w, tl);
 }
 
+/* the visit order of hit children: plain slot order (RTX_W8_SORDER 0), front to back from the
+ * shade point (1), or front to back from the light (2) */
+template <int OCT> __device__ __forceinline__ constexpr uint32_t w8_sorder()
+{
+	return (OCT == 8 || !RTX_W8_SORDER) ? 0u : RTX_W8_SORDER == 2 ? ((uint32_t)OCT & 7u) : (~(uint32_t)OCT & 7u);
+}
+
+/* one lane's 8-wide any-hit walk: the node it is at (RTX_NONE: no node work), the kept sibling
+ * group and the stack depth below it, the deferred transparent-leaf group and the queue depth */
+struct W8Walk {
+	uint32_t node, grp, sp, tgrp, tn;
+};
+/* the walk's counters (COUNT instances) */
+struct W8Ctr {
+	uint32_t nbox, ntri, nsph, nstep, nlr, nun;
+};
+
+/* One iteration of the 8-wide any-hit walk for the wave: a round of deferred transparent-leaf
+ * tests, or one node step with its opaque leaf tests (see shadow_walk8).  walking / holding: the
+ * lanes with node work / deferred tests; at least one lane has one or the other.  o / d: the
+ * world ray; invq / oi: its inverse direction and origin term in the tree's 16-bit frame. */
+template <bool COUNT, int OCT>
+__device__ __forceinline__ void w8_iter(const QBvh &Q, f3 o, f3 d, f3 invq, f3 oi, float &tl, f3 &li, W8Walk &w, W8Ctr &c,
+					u64 walking, u64 holding)
+{
+	constexpr uint32_t K = w8_sorder<OCT>();
+	lds_u32 *stk = Q.stk, *tq = Q.tq;
+	if (!walking || popc64(holding) >= RTX_W8_DEFER || ballot(w.tn == RTX_W8_TQ)) {
+		/* a round of deferred transparent-leaf tests */
+		if (COUNT)
+			c.nlr++;
+		if (w.tgrp) {
+			const char *pr = (const char *)(Q.w8 + (w.tgrp >> 8) + (__builtin_ctz(w.tgrp) ^ K));
+			w.tgrp &= w.tgrp - 1;
+			if (!(w.tgrp & 0xFFu))
+				w.tgrp = w.tn ? tq[--w.tn * WAVE] : 0u;
+			w8_defer_test<COUNT>(pr, o, d, tl, li, c.ntri, c.nsph);
+		}
+		return;
+	}
+	uint32_t lm = 0, base = 0; /* this step's opaque leaf hits (visit order) and their block */
+	if (w.node != RTX_NONE) {
+		const uint32_t un = uni(w.node);
+		W8Visit v;
+		if (!ballot(w.node != un)) {
+			/* every walking lane is at one node: its scalar-path copy through the scalar cache,
+			 * the planes as SGPR float operands (no vector-memory address / data cycles) */
+			v = w8_visit_s<OCT, K>(Q.w8s + (size_t)un, invq, oi, tl);
+		} else {
+			uint32_t wd[16];
+			if (w.node < Q.nt8) { /* a top-level node: the workgroup's LDS copy (no texture-path traffic) */
+#pragma unroll
+				for (int k = 0; k < 4; k++) {
+					const uint4 x = lds4u(Q.t8 + 4 * w.node + k);
+					wd[4 * k] = x.x;
+					wd[4 * k + 1] = x.y;
+					wd[4 * k + 2] = x.z;
+					wd[4 * k + 3] = x.w;
+				}
+			} else {
+				const DW8 *N = Q.w8 + (size_t)w.node;
+#pragma unroll
+				for (int k = 0; k < 4; k++) {
+					const uint4 x = ldg4u((const uint32_t *)N + 4 * k);
+					wd[4 * k] = x.x;
+					wd[4 * k + 1] = x.y;
+					wd[4 * k + 2] = x.z;
+					wd[4 * k + 3] = x.w;
+				}
+			}
+			v = w8_visit<OCT, K, false>(wd, invq, oi, tl);
+		}
+		const uint32_t hm = v.hm;
+		base = v.base;
+		lm = hm & ~v.io & ~v.to;
+		uint32_t im = hm & v.io;
+		const uint32_t dm = hm & v.to;
+		if (COUNT) {
+			c.nstep++;
+			c.nbox += popc64(v.nv);
+			c.nun += ballot(w.node != uni(w.node)) ? 0u : 1u;
+		}
+		if (dm) { /* transparent leaves: deferred */
+			const uint32_t g = (base << 8) | dm;
+			if (w.tgrp)
+				tq[w.tn++ * WAVE] = g;
+			else
+				w.tgrp = g;
+		}
+		/* the next node (a lane the opaque leaves below block drops it again) */
+		if (im) {
+			w.node = base + (__builtin_ctz(im) ^ K);
+			im &= im - 1;
+			if (im) {
+				if (w.grp) {
+					if (w.sp < Q.lstk)
+						stk[w.sp * WAVE] = w.grp;
+					else
+						gptrw(Q.spill)[(size_t)(w.sp - Q.lstk) * Q.spill_stride] = w.grp;
+					w.sp++;
+				}
+				w.grp = (base << 8) | im;
+			}
+		} else if (w.grp) {
+			w.node = (w.grp >> 8) + (__builtin_ctz(w.grp) ^ K);
+			w.grp &= w.grp - 1;
+			if (!(w.grp & 0xFFu)) {
+				w.grp = 0;
+				if (w.sp) {
+					w.sp--;
+					w.grp = w.sp < Q.lstk ? stk[w.sp * WAVE] : gptr(Q.spill)[(size_t)(w.sp - Q.lstk) * Q.spill_stride];
+				}
+			}
+		} else {
+			w.node = RTX_NONE;
+		}
+	}
+	/* opaque leaves, at once (an opaque hit ends the ray): the tree marks every leaf slot (built
+	 * from the primitive records, emitters left out), each lane tests its own.  (Dealing the
+	 * wave's tests over its lanes with ds_permute, one round for all, measured slower on scene6:
+	 * 2834 vs 2806 ms, every dealt job tested without the early break) */
+	if (!ballot(lm != 0))
+		return;
+	if (COUNT) {
+		uint32_t r = 0;
+		for (uint32_t m = lm;; m &= m - 1) {
+			if (!ballot(m != 0))
+				break;
+			r++;
+		}
+		c.nlr += r;
+	}
+	bool blocked = false;
+	while (lm) {
+		const uint32_t p = __builtin_ctz(lm);
+		lm &= lm - 1;
+		if (w8_opaque_test<COUNT>((const char *)(Q.w8 + base + (p ^ K)), o, d, tl, c.ntri, c.nsph)) {
+			blocked = true;
+			break;
+		}
+	}
+	if (blocked) { /* the queue too: a full queue left behind would keep the wave in deferred rounds */
+		tl = -1.f;
+		w.node = RTX_NONE;
+		w.tgrp = 0;
+		w.tn = 0;
+	}
+}
+
+/* the walk's counters summed over the wave into sc (walks: wave walks of 64 lane slots) */
+template <bool COUNT> __device__ __forceinline__ void w8_count(W8Ctr c, ShadowCount &sc, uint32_t walks)
+{
+	if (!COUNT)
+		return;
+	uint32_t a = c.nbox, bb = c.ntri, cc = c.nsph, nstep = c.nstep, nun = c.nun, nlr = c.nlr;
+#pragma unroll
+	for (int k = 32; k > 0; k >>= 1) {
+		a += __shfl_xor(a, k, WAVE);
+		bb += __shfl_xor(bb, k, WAVE);
+		cc += __shfl_xor(cc, k, WAVE);
+		nstep = max(nstep, (uint32_t)__shfl_xor(nstep, k, WAVE));
+		nun = max(nun, (uint32_t)__shfl_xor(nun, k, WAVE));
+		nlr = max(nlr, (uint32_t)__shfl_xor(nlr, k, WAVE));
+	}
+	sc.boxes += uni(a);
+	sc.gboxes += uni(a);
+	sc.lrounds += uni(nlr);
+	sc.unif += uni(nun);
+	sc.tris += uni(bb);
+	sc.sph += uni(cc);
+	sc.steps += uni(nstep);
+	sc.walks += walks;
+}
+
 template <bool COUNT, int OCT>
 __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__restrict__ mats, f3 o, f3 d, f3 ob, f3 inv,
 					     float &tl, uint32_t emit_obj, f3 &li, ShadowCount &sc)
 {
-	/* visit order of hit children: plain slot order (0), front to back from the shade point (1), or
-	 * front to back from the light (2) */
-	constexpr uint32_t K = (OCT == 8 || !RTX_W8_SORDER) ? 0u : RTX_W8_SORDER == 2 ? ((uint32_t)OCT & 7u) : (~(uint32_t)OCT & 7u);
 	/* the ray in the tree's 16-bit frame: ob / inv are its origin and inverse direction in the
 	 * tree's rotated frame (shadow_query), o / d the world ray the primitives are tested with */
 	const f3 invq = mk3(inv.x * Q.qsi.x, inv.y * Q.qsi.y, inv.z * Q.qsi.z);
 	const f3 oq = mk3((ob.x - Q.qo.x) * Q.qs.x, (ob.y - Q.qo.y) * Q.qs.y, (ob.z - Q.qo.z) * Q.qs.z);
 	const f3 oi = mul3v(oq, invq);
-	lds_u32 *stk = Q.stk, *tq = Q.tq;
-	uint32_t node = tl >= 0.f ? 0u : RTX_NONE, grp = 0, sp = 0, tgrp = 0, tn = 0;
-	uint32_t nbox = 0, ntri = 0, nsph = 0, nstep = 0, nlr = 0, nun = 0;
+	W8Walk w = { tl >= 0.f ? 0u : RTX_NONE, 0u, 0u, 0u, 0u };
+	W8Ctr c = { 0u, 0u, 0u, 0u, 0u, 0u };
 	for (;;) {
-		const u64 walking = ballot(node != RTX_NONE);
-		const u64 holding = ballot(tgrp != 0);
+		const u64 walking = ballot(w.node != RTX_NONE);
+		const u64 holding = ballot(w.tgrp != 0);
 		if (!(walking | holding))
 			break;
-		if (!walking || popc64(holding) >= RTX_W8_DEFER || ballot(tn == RTX_W8_TQ)) {
-			/* a round of deferred transparent-leaf tests */
-			if (COUNT)
-				nlr++;
-			if (tgrp) {
-				const char *pr = (const char *)(Q.w8 + (tgrp >> 8) + (__builtin_ctz(tgrp) ^ K));
-				tgrp &= tgrp - 1;
-				if (!(tgrp & 0xFFu))
-					tgrp = tn ? tq[--tn * WAVE] : 0u;
-				w8_defer_test<COUNT>(pr, o, d, tl, li, ntri, nsph);
-			}
-			continue;
-		}
-		uint32_t lm = 0, base = 0; /* this step's opaque leaf hits (visit order) and their block */
-		if (node != RTX_NONE) {
-			const uint32_t un = uni(node);
-			W8Visit v;
-			if (!ballot(node != un)) {
-				/* every walking lane is at one node: its scalar-path copy through the scalar cache,
-				 * the planes as SGPR float operands (no vector-memory address / data cycles) */
-				v = w8_visit_s<OCT, K>(Q.w8s + (size_t)un, invq, oi, tl);
-			} else {
-				uint32_t w[16];
-				if (node < Q.nt8) { /* a top-level node: the workgroup's LDS copy (no texture-path traffic) */
-#pragma unroll
-					for (int k = 0; k < 4; k++) {
-						const uint4 x = lds4u(Q.t8 + 4 * node + k);
-						w[4 * k] = x.x;
-						w[4 * k + 1] = x.y;
-						w[4 * k + 2] = x.z;
-						w[4 * k + 3] = x.w;
-					}
-				} else {
-					const DW8 *N = Q.w8 + (size_t)node;
-#pragma unroll
-					for (int k = 0; k < 4; k++) {
-						const uint4 x = ldg4u((const uint32_t *)N + 4 * k);
-						w[4 * k] = x.x;
-						w[4 * k + 1] = x.y;
-						w[4 * k + 2] = x.z;
-						w[4 * k + 3] = x.w;
-					}
-				}
-				v = w8_visit<OCT, K, false>(w, invq, oi, tl);
-			}
-			const uint32_t hm = v.hm;
-			base = v.base;
-			lm = hm & ~v.io & ~v.to;
-			uint32_t im = hm & v.io;
-			const uint32_t dm = hm & v.to;
-			if (COUNT) {
-				nstep++;
-				nbox += popc64(v.nv);
-				nun += ballot(node != uni(node)) ? 0u : 1u;
-			}
-			if (dm) { /* transparent leaves: deferred */
-				const uint32_t g = (base << 8) | dm;
-				if (tgrp)
-					tq[tn++ * WAVE] = g;
-				else
-					tgrp = g;
-			}
-			/* the next node (a lane the opaque leaves below block drops it again) */
-			if (im) {
-				node = base + (__builtin_ctz(im) ^ K);
-				im &= im - 1;
-				if (im) {
-					if (grp) {
-						if (sp < Q.lstk)
-							stk[sp * WAVE] = grp;
-						else
-							gptrw(Q.spill)[(size_t)(sp - Q.lstk) * Q.spill_stride] = grp;
-						sp++;
-					}
-					grp = (base << 8) | im;
-				}
-			} else if (grp) {
-				node = (grp >> 8) + (__builtin_ctz(grp) ^ K);
-				grp &= grp - 1;
-				if (!(grp & 0xFFu)) {
-					grp = 0;
-					if (sp) {
-						sp--;
-						grp = sp < Q.lstk ? stk[sp * WAVE] : gptr(Q.spill)[(size_t)(sp - Q.lstk) * Q.spill_stride];
-					}
-				}
-			} else {
-				node = RTX_NONE;
-			}
-		}
-		/* opaque leaves, at once (an opaque hit ends the ray): the tree marks every leaf slot (built
-		 * from the primitive records, emitters left out), each lane tests its own.  (Dealing the
-		 * wave's tests over its lanes with ds_permute, one round for all, measured slower on scene6:
-		 * 2834 vs 2806 ms, every dealt job tested without the early break) */
-		if (!ballot(lm != 0))
-			continue;
-		if (COUNT) {
-			uint32_t r = 0;
-			for (uint32_t m = lm;; m &= m - 1) {
-				if (!ballot(m != 0))
-					break;
-				r++;
-			}
-			nlr += r;
-		}
-		bool blocked = false;
-		while (lm) {
-			const uint32_t p = __builtin_ctz(lm);
-			lm &= lm - 1;
-			if (w8_opaque_test<COUNT>((const char *)(Q.w8 + base + (p ^ K)), o, d, tl, ntri, nsph)) {
-				blocked = true;
-				break;
-			}
-		}
-		if (blocked) { /* the queue too: a full queue left behind would keep the wave in deferred rounds */
-			tl = -1.f;
-			node = RTX_NONE;
-			tgrp = 0;
-			tn = 0;
-		}
+		w8_iter<COUNT, OCT>(Q, o, d, invq, oi, tl, li, w, c, walking, holding);
 	}
-	if (COUNT) {
-		uint32_t a = nbox, bb = ntri, c = nsph;
-#pragma unroll
-		for (int k = 32; k > 0; k >>= 1) {
-			a += __shfl_xor(a, k, WAVE);
-			bb += __shfl_xor(bb, k, WAVE);
-			c += __shfl_xor(c, k, WAVE);
-			nstep = max(nstep, (uint32_t)__shfl_xor(nstep, k, WAVE));
-			nun = max(nun, (uint32_t)__shfl_xor(nun, k, WAVE));
-			nlr = max(nlr, (uint32_t)__shfl_xor(nlr, k, WAVE));
-		}
-		sc.boxes += uni(a);
-		sc.gboxes += uni(a);
-		sc.lrounds += uni(nlr);
-		sc.unif += uni(nun);
-		sc.tris += uni(bb);
-		sc.sph += uni(c);
-		sc.steps += uni(nstep);
-		sc.walks++;
-	}
+	w8_count<COUNT>(c, sc, 1u);
 }
 
 /* is_light_blocked (render.c:126-134): planes first (unbound_objects_is_light_blocked,
@@ -749,6 +781,44 @@ __device__ __forceinline__ void emitter_sample(const KShadow &ks, const DEmitter
 	li = ld3(E.li);
 }
 
+/* an emitter record read through the scalar cache (every lane reads the same one) */
+__device__ __forceinline__ DEmitter emitter_uni(const DEmitter *e)
+{
+	uint32_t w[sizeof(DEmitter) / 4];
+	const auto *W = cptr((const uint32_t *)e);
+#pragma unroll
+	for (int i = 0; i < (int)(sizeof(DEmitter) / 4); i++)
+		w[i] = W[i];
+	DEmitter E;
+	__builtin_memcpy(&E, w, sizeof(E));
+	return E;
+}
+
+/* the shadow walks' view of the trees (QBvh) from the kernel arguments and the workgroup's LDS */
+template <int WALK>
+__device__ __forceinline__ QBvh make_qbvh(const KShadow &ks, const uint4 *top_q, const uint32_t *top_e, lds_u32 *stk,
+					  const uint4 *t8)
+{
+	QBvh Q;
+	Q.q = unip(ks.qnodes);
+	Q.qo = mk3(ks.qo[0], ks.qo[1], ks.qo[2]);
+	Q.qs = mk3(ks.qs[0], ks.qs[1], ks.qs[2]);
+	Q.qsi = mk3(ks.qsi[0], ks.qsi[1], ks.qsi[2]);
+	Q.top = top_q;
+	Q.tend = top_e;
+	Q.nt = uni(ks.ntop);
+	Q.w8 = WALK == WALK_W8 ? unip(ks.w8) : nullptr;
+	Q.w8s = WALK == WALK_W8 ? unip(ks.w8s) : nullptr;
+	Q.t8 = t8;
+	Q.nt8 = (WALK == WALK_W8 && RTX_W8_TOP) ? min(uni(ks.w8top), (uint32_t)RTX_W8_TOP_MAX) : 0u;
+	Q.spill_stride = gridDim.x * blockDim.x;
+	Q.spill = WALK == WALK_W8 ? unip(ks.w8spill) + blockIdx.x * blockDim.x + threadIdx.x : nullptr;
+	Q.lstk = uni(ks.w8lstk);
+	Q.stk = stk;
+	Q.tq = stk + RTX_W8_STACK * WAVE;
+	return Q;
+}
+
 /* one light sample per lane of the shade point `rec` (render.c:170-229): the light point of
  * sample idx (emitters in scene order, the hit object skipped), its shadow ray, attenuation
  * and Phong / Blinn.  Argument-block fields are read from LDS behind reread barriers. */
@@ -784,13 +854,7 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	float ldist, dsq;
 	uint32_t eobj;
 	if (!ballot(act && e != lead)) {
-		uint32_t w[sizeof(DEmitter) / 4];
-		const auto *W = (const __attribute__((address_space(4))) uint32_t *)(EM + lead);
-#pragma unroll
-		for (int i = 0; i < (int)(sizeof(DEmitter) / 4); i++)
-			w[i] = W[i];
-		DEmitter Eu;
-		__builtin_memcpy(&Eu, w, sizeof(Eu));
+		const DEmitter Eu = emitter_uni(emitters + lead);
 		emitter_sample(ks, Eu, lead, j, __float_as_uint(q4.y), __float_as_uint(q4.z), p, ldir, ldist, dsq, li);
 		eobj = Eu.obj;
 	} else {
@@ -798,24 +862,8 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 		emitter_sample(ks, E, e, j, __float_as_uint(q4.y), __float_as_uint(q4.z), p, ldir, ldist, dsq, li);
 		eobj = E.obj;
 	}
-	QBvh Q;
-	Q.q = unip(ks.qnodes);
-	Q.qo = mk3(ks.qo[0], ks.qo[1], ks.qo[2]);
-	Q.qs = mk3(ks.qs[0], ks.qs[1], ks.qs[2]);
-	Q.qsi = mk3(ks.qsi[0], ks.qsi[1], ks.qsi[2]);
-	Q.top = top_q;
-	Q.tend = top_e;
-	Q.nt = uni(ks.ntop);
+	const QBvh Q = make_qbvh<WALK>(ks, top_q, top_e, stk, t8);
 	const bool have_tree = uni(ks.have_tree) != 0 && !RTX_DEBUG_NOWALK;
-	Q.w8 = WALK == WALK_W8 ? unip(ks.w8) : nullptr;
-	Q.w8s = WALK == WALK_W8 ? unip(ks.w8s) : nullptr;
-	Q.t8 = t8;
-	Q.nt8 = (WALK == WALK_W8 && RTX_W8_TOP) ? min(uni(ks.w8top), (uint32_t)RTX_W8_TOP_MAX) : 0u;
-	Q.spill_stride = gridDim.x * blockDim.x;
-	Q.spill = WALK == WALK_W8 ? unip(ks.w8spill) + blockIdx.x * blockDim.x + threadIdx.x : nullptr;
-	Q.lstk = uni(ks.w8lstk);
-	Q.stk = stk;
-	Q.tq = stk + RTX_W8_STACK * WAVE;
 	const bool blocked = shadow_query<COUNT, WALK>(Q, unip(ks.recs), unip(ks.mats), unip(ks.planes), uni(ks.num_planes),
 						 unip(ks.lin), uni(ks.num_lin), have_tree, ks.tf, act, p, ldir, ldist, eobj, li, sc);
 	reread_barrier();
@@ -823,6 +871,155 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	if (act && !blocked)
 		contribution = shade_light<UNI && RTX_SH_SPUNI>(ks, rec, ldir, li, ldist, dsq);
 	return contribution;
+}
+
+#ifndef RTX_SH_REFILL
+#define RTX_SH_REFILL 0 /* one emitter, >= 64 lights: a lane whose walk has ended takes the point's next light
+                         * sample once this many lanes have (point_refill); 0: 64-sample packets.  Measured
+                         * on the bench frame (profiles/r05/refill_*): k_shadow 568.9 ms with packets,
+                         * 599.1 / 592.3 / 608.5 ms refilling at 8 / 16 / 32 idle lanes */
+#endif
+/* All nl light samples of one shade point on the wave, lanes refilled (RTX_SH_REFILL).  Lane l
+ * starts with sample l; a lane whose walk has ended (no node work, no deferred leaf tests) waits
+ * until RTX_SH_REFILL lanes have, then each of them adds its sample's term (render.c:199-228) to
+ * its sum and takes the next unassigned sample, in lane order.  The packets of 64 samples the
+ * other path walks in lockstep wait for their longest ray; here a lane waits at most for
+ * RTX_SH_REFILL - 1 others.  Every sample's ray shares the direction octant OCT (the caller
+ * bounds the light's extent) and the emitter E (the scene's only one).  Which lane takes which
+ * sample depends only on this point's walks, so its sum is deterministic.  p: the point (wave-
+ * uniform); oq: its frame origin in the tree's 16-bit frame.  The scene tables a refill reads
+ * (emitter, planes, frame) are re-read from the workgroup's argument copy at each refill, so no
+ * scalar register holds them across the walk (the walk's own state fills the register budget). */
+template <bool COUNT, int OCT>
+__device__ __forceinline__ f3 point_refill(const KShadow &ks, const float4 *rec, uint32_t nl, uint32_t ka, uint32_t kb, f3 p,
+					   f3 oq, const QBvh &Q, ShadowCount &sc)
+{
+	f3 acc = mk3(0.f, 0.f, 0.f);
+	uint32_t next = WAVE; /* the next unassigned sample (wave-uniform) */
+	uint32_t my = lane_id();
+	bool have = my < nl;
+	f3 d = mk3(0.f, 0.f, 1.f), li = mk3(0.f, 0.f, 0.f), invq = mk3(0.f, 0.f, 0.f), oi = mk3(0.f, 0.f, 0.f);
+	float ldist = 0.f, dsq = 0.f, tl = -1.f;
+	W8Walk w = { RTX_NONE, 0u, 0u, 0u, 0u };
+	W8Ctr c = { 0u, 0u, 0u, 0u, 0u, 0u };
+	/* sample `my`: its light point and ray, the planes and the objects tested one by one
+	 * (shadow_query), the ray in the tree's frame, the walk at the root */
+	auto start = [&]() {
+		reread_barrier();
+		const DEmitter E = emitter_uni(unip(ks.emitters));
+		const DPlane *planes = unip(ks.planes);
+		const uint32_t num_planes = uni(ks.num_planes);
+		const DEmitter *lin = unip(ks.lin);
+		const uint32_t num_lin = uni(ks.num_lin);
+		emitter_sample(ks, E, 0u, my, ka, kb, p, d, ldist, dsq, li);
+		tl = ldist;
+		for (uint32_t i = 0; i < num_planes; i++) {
+			const auto *pl = cptr(planes) + i;
+			float t;
+			const bool h = hit_plane(mk3(pl->n[0], pl->n[1], pl->n[2]), pl->d, p, d, pl->eps, t) && t < ldist && tl >= 0.f;
+			if (pl->transparent) {
+				if (h)
+					li = mul3v(li, mk3(pl->kt[0], pl->kt[1], pl->kt[2]));
+			} else if (h) {
+				tl = -1.f;
+			}
+		}
+		for (uint32_t i = 0; i < num_lin; i++) {
+			const auto *e = cptr(lin) + i;
+			if (e->obj == E.obj || !(tl >= 0.f))
+				continue;
+			bool h;
+			if (e->type == RTX_SPHERE) {
+				float t = 0.f;
+				h = hit_sphere(mk3(e->p0[0], e->p0[1], e->p0[2]), e->radius, p, d, e->eps, t) && t < tl;
+			} else {
+				h = any_tri(mk3(e->p0[0], e->p0[1], e->p0[2]), mk3(e->e1[0], e->e1[1], e->e1[2]),
+					    mk3(e->e2[0], e->e2[1], e->e2[2]), p, d, e->eps, tl);
+			}
+			if (h) {
+				if (e->transparent)
+					li = mul3v(li, mk3(e->kt[0], e->kt[1], e->kt[2]));
+				else
+					tl = -1.f;
+			}
+		}
+		f3 db = d;
+		if (uni(ks.tf.rotated)) {
+			float r[3][3];
+#pragma unroll
+			for (int i = 0; i < 3; i++)
+#pragma unroll
+				for (int j = 0; j < 3; j++)
+					r[i][j] = __uint_as_float(uni(__float_as_uint(ks.tf.r[i][j])));
+			db = tf_dir(r, d);
+		}
+		const f3 inv = safe_inv_fast(db);
+		invq = mk3(inv.x * ks.qsi[0], inv.y * ks.qsi[1], inv.z * ks.qsi[2]);
+		oi = mul3v(oq, invq);
+		w = { tl >= 0.f ? 0u : RTX_NONE, 0u, 0u, 0u, 0u };
+	};
+	if (have)
+		start();
+	for (;;) {
+		const u64 walking = ballot(w.node != RTX_NONE);
+		const u64 holding = ballot(w.tgrp != 0);
+		const bool fin = have && w.node == RTX_NONE && w.tgrp == 0;
+		const u64 fm = ballot(fin);
+		if (!(walking | holding) || (popc64(fm) >= RTX_SH_REFILL && next < nl)) {
+			/* a refill round: the lanes whose walk has ended add their term, take the next samples */
+			if (fin) {
+				if (tl >= 0.f)
+					acc = add3(acc, shade_light<RTX_SH_SPUNI>(ks, rec, d, li, ldist, dsq));
+				my = next + mbcnt(fm);
+				have = my < nl;
+				if (have)
+					start();
+			}
+			next += popc64(fm);
+			if (!ballot(have))
+				break;
+			continue;
+		}
+		/* lanes whose node walk has ended but whose deferred transparent-leaf tests remain would
+		 * wait for a round (RTX_W8_DEFER: all 64 lanes holding) that walking refilled lanes delay:
+		 * once they and the finished lanes make up a refill, run rounds until they finish */
+		const u64 idle_hold = ballot(have && w.node == RTX_NONE && w.tgrp != 0);
+		w8_iter<COUNT, OCT>(Q, p, d, invq, oi, tl, li, w, c,
+				    (idle_hold && popc64(fm | idle_hold) >= RTX_SH_REFILL) ? 0ull : walking, holding);
+	}
+	w8_count<COUNT>(c, sc, (nl + WAVE - 1) / WAVE);
+	if (COUNT)
+		sc.pln += (u64)nl * uni(ks.num_planes);
+	return acc;
+}
+
+/* the octant every shadow ray from p to the emitter E shares in the tree's frame (bit a: the + side
+ * of axis a, as shadow_query's), or 8 when the light's extent straddles an axis plane: the
+ * sphere's centre offset against its radius, or the triangle's three corners, with a margin for
+ * light_point_sh's rounding */
+__device__ __forceinline__ uint32_t light_octant(const DEmitter &E, f3 p, const float (&r)[3][3], bool rot)
+{
+	uint32_t pos = 0, neg = 0;
+	if (E.type == RTX_SPHERE) {
+		const f3 v0 = sub3(ld3(E.p0), p);
+		const f3 v = rot ? tf_dir(r, v0) : v0;
+		const float m = E.radius * 1.001f + 1e-5f * mag3(v);
+		pos = (v.x > m ? 1u : 0u) | (v.y > m ? 2u : 0u) | (v.z > m ? 4u : 0u);
+		neg = (v.x < -m ? 1u : 0u) | (v.y < -m ? 2u : 0u) | (v.z < -m ? 4u : 0u);
+	} else {
+		uint32_t ap = 7u, an = 7u;
+		const f3 c0 = sub3(ld3(E.p0), p);
+		for (int k = 0; k < 3; k++) {
+			const f3 v0 = k == 0 ? c0 : add3(c0, k == 1 ? ld3(E.e1) : ld3(E.e2));
+			const f3 v = rot ? tf_dir(r, v0) : v0;
+			const float m = 1e-5f * mag3(v) + 1e-30f;
+			ap &= (v.x > m ? 1u : 0u) | (v.y > m ? 2u : 0u) | (v.z > m ? 4u : 0u);
+			an &= (v.x < -m ? 1u : 0u) | (v.y < -m ? 2u : 0u) | (v.z < -m ? 4u : 0u);
+		}
+		pos = ap;
+		neg = an;
+	}
+	return (pos | neg) == 7u ? pos : 8u;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -903,7 +1100,44 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 				const uint32_t nl = uni(nls[k]);
 				const float4 *rec = unip(ks.sp) + (size_t)uni(sid[k]) * SPREC;
 				f3 acc = mk3(0.f, 0.f, 0.f);
-				for (uint32_t base = 0; base < nl; base += WAVE) {
+				bool refilled = false;
+				if (WALK == WALK_W8 && RTX_SH_REFILL && !RTX_DEBUG_NOWALK && nl > WAVE && uni(ks.num_emitters) == 1 &&
+				    uni(ks.have_tree)) {
+					/* one emitter whose extent keeps every ray of the point in one octant, the point
+					 * not far from the tree's frame: the refilled lanes (point_refill) */
+					const float4 q0 = sp_field<RTX_SH_SPUNI>(rec, 0), q4 = sp_field<RTX_SH_SPUNI>(rec, 4);
+					const f3 p = mk3(q0.x, q0.y, q0.z);
+					const DEmitter E = emitter_uni(unip(ks.emitters));
+					const bool rot = uni(ks.tf.rotated) != 0;
+					float r[3][3], c[3];
+#pragma unroll
+					for (int i = 0; i < 3; i++) {
+						c[i] = __uint_as_float(uni(__float_as_uint(ks.tf.c[i])));
+#pragma unroll
+						for (int jj = 0; jj < 3; jj++)
+							r[i][jj] = __uint_as_float(uni(__float_as_uint(ks.tf.r[i][jj])));
+					}
+					const f3 ob = rot ? tf_point(r, c, p) : p;
+					const uint32_t oct = (rot && tf_far(ob, __uint_as_float(uni(__float_as_uint(ks.tf.rad)))))
+								     ? 8u
+								     : light_octant(E, p, r, rot);
+					if (oct < 8u && E.obj != __float_as_uint(q4.x)) {
+						const QBvh Q = make_qbvh<WALK>(ks, top_q, top_e, stk, t8);
+						const f3 oq = mk3((ob.x - Q.qo.x) * Q.qs.x, (ob.y - Q.qo.y) * Q.qs.y, (ob.z - Q.qo.z) * Q.qs.z);
+						const uint32_t ka = __float_as_uint(q4.y), kb = __float_as_uint(q4.z);
+						switch (oct) {
+#define RTX_REFILL(K)                                                                            \
+	case K:                                                                                          \
+		acc = point_refill<COUNT, (RTX_SH_OCT ? K : 8)>(ks, rec, nl, ka, kb, p, oq, Q, sc); \
+		break;
+							RTX_REFILL(0) RTX_REFILL(1) RTX_REFILL(2) RTX_REFILL(3) RTX_REFILL(4) RTX_REFILL(5)
+							RTX_REFILL(6) RTX_REFILL(7)
+#undef RTX_REFILL
+						}
+						refilled = true;
+					}
+				}
+				for (uint32_t base = 0; !refilled && base < nl; base += WAVE) {
 					const uint32_t idx = base + lane_id();
 					acc = add3(acc, light_sample<COUNT, WALK, true>(ks, rec, idx, idx < nl, sc, top_q, top_e, stk, t8));
 				}

@@ -198,8 +198,13 @@ def far_camera_scene(tmp_path, dist):
 def test_gpu_rotated_trees_far_camera(renderer, tmp_path, dist, walks):
     """rays from far outside the trees' frame (a distant camera, points far out on the
     back plane): the frame origin of a far ray is formed in double near the frame's centre
-    (rtx_math.h tf_shift / tf_point_at), so the rotated trees' boxes stay conservative and the
-    frame is the world trees' bit for bit, z-buffer and colours, at 3, 60 and 2000 scene radii"""
+    (rtx_math.h tf_shift / tf_point_at), so the rotated trees' boxes stay conservative.  At 3 and
+    60 scene radii the frame is the world trees' bit for bit, z-buffer and colours.  At 2000 radii
+    the world trees themselves stop being conservative: their box test (lo - o) * inv rounds at
+    2^-24 * 2000 radii, far above their padding of 2e-6 * |coordinate| near the world origin, so
+    they may cull a box whose triangle the (world-space) intersector hits.  There the rotated
+    frame must find every hit the world trees find, at a distance no greater (a conservative walk
+    only adds hits), with the pixels it does not change bit-identical."""
     scene = far_camera_scene(tmp_path, dist)
     frame = scene.frame(96, 96)
     params = rtxpy.params_from_args([], seed=1)
@@ -209,5 +214,13 @@ def test_gpu_rotated_trees_far_camera(renderer, tmp_path, dist, walks):
     assert sa.tree_rotated == 1 and sb.tree_rotated == 0 and sa.trace_walk == walks[1]
     sponge = (za > 0) & (za < dist + 3.0)  # the back plane lies 5.6 beyond the sponge's centre
     assert 0.2 < sponge.mean() < 0.95, sponge.mean()  # the sponge fills the frame, the plane around it
-    assert np.array_equal(za, zb), (dist, int((za != zb).sum()))
-    assert np.array_equal(a, b), (dist, int((a != b).any(axis=2).sum()))
+    if dist <= 60.0:
+        assert np.array_equal(za, zb), (dist, int((za != zb).sum()))
+        assert np.array_equal(a, b), (dist, int((a != b).any(axis=2).sum()))
+        return
+    diff = za != zb
+    assert diff.mean() < 0.05, diff.mean()
+    assert np.all(za[zb > 0] > 0), "a hit of the world trees missed by the rotated frame"
+    assert np.all(za[diff & (zb > 0)] <= zb[diff & (zb > 0)]), "the rotated frame's hit lies beyond the world trees'"
+    same = ~diff
+    assert np.array_equal(a[same], b[same])
