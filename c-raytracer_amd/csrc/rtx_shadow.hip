@@ -873,155 +873,6 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	return contribution;
 }
 
-#ifndef RTX_SH_REFILL
-#define RTX_SH_REFILL 0 /* one emitter, >= 64 lights: a lane whose walk has ended takes the point's next light
-                         * sample once this many lanes have (point_refill); 0: 64-sample packets.  Measured
-                         * on the bench frame (profiles/r05/refill_*): k_shadow 568.9 ms with packets,
-                         * 599.1 / 592.3 / 608.5 ms refilling at 8 / 16 / 32 idle lanes */
-#endif
-/* All nl light samples of one shade point on the wave, lanes refilled (RTX_SH_REFILL).  Lane l
- * starts with sample l; a lane whose walk has ended (no node work, no deferred leaf tests) waits
- * until RTX_SH_REFILL lanes have, then each of them adds its sample's term (render.c:199-228) to
- * its sum and takes the next unassigned sample, in lane order.  The packets of 64 samples the
- * other path walks in lockstep wait for their longest ray; here a lane waits at most for
- * RTX_SH_REFILL - 1 others.  Every sample's ray shares the direction octant OCT (the caller
- * bounds the light's extent) and the emitter E (the scene's only one).  Which lane takes which
- * sample depends only on this point's walks, so its sum is deterministic.  p: the point (wave-
- * uniform); oq: its frame origin in the tree's 16-bit frame.  The scene tables a refill reads
- * (emitter, planes, frame) are re-read from the workgroup's argument copy at each refill, so no
- * scalar register holds them across the walk (the walk's own state fills the register budget). */
-template <bool COUNT, int OCT>
-__device__ __forceinline__ f3 point_refill(const KShadow &ks, const float4 *rec, uint32_t nl, uint32_t ka, uint32_t kb, f3 p,
-					   f3 oq, const QBvh &Q, ShadowCount &sc)
-{
-	f3 acc = mk3(0.f, 0.f, 0.f);
-	uint32_t next = WAVE; /* the next unassigned sample (wave-uniform) */
-	uint32_t my = lane_id();
-	bool have = my < nl;
-	f3 d = mk3(0.f, 0.f, 1.f), li = mk3(0.f, 0.f, 0.f), invq = mk3(0.f, 0.f, 0.f), oi = mk3(0.f, 0.f, 0.f);
-	float ldist = 0.f, dsq = 0.f, tl = -1.f;
-	W8Walk w = { RTX_NONE, 0u, 0u, 0u, 0u };
-	W8Ctr c = { 0u, 0u, 0u, 0u, 0u, 0u };
-	/* sample `my`: its light point and ray, the planes and the objects tested one by one
-	 * (shadow_query), the ray in the tree's frame, the walk at the root */
-	auto start = [&]() {
-		reread_barrier();
-		const DEmitter E = emitter_uni(unip(ks.emitters));
-		const DPlane *planes = unip(ks.planes);
-		const uint32_t num_planes = uni(ks.num_planes);
-		const DEmitter *lin = unip(ks.lin);
-		const uint32_t num_lin = uni(ks.num_lin);
-		emitter_sample(ks, E, 0u, my, ka, kb, p, d, ldist, dsq, li);
-		tl = ldist;
-		for (uint32_t i = 0; i < num_planes; i++) {
-			const auto *pl = cptr(planes) + i;
-			float t;
-			const bool h = hit_plane(mk3(pl->n[0], pl->n[1], pl->n[2]), pl->d, p, d, pl->eps, t) && t < ldist && tl >= 0.f;
-			if (pl->transparent) {
-				if (h)
-					li = mul3v(li, mk3(pl->kt[0], pl->kt[1], pl->kt[2]));
-			} else if (h) {
-				tl = -1.f;
-			}
-		}
-		for (uint32_t i = 0; i < num_lin; i++) {
-			const auto *e = cptr(lin) + i;
-			if (e->obj == E.obj || !(tl >= 0.f))
-				continue;
-			bool h;
-			if (e->type == RTX_SPHERE) {
-				float t = 0.f;
-				h = hit_sphere(mk3(e->p0[0], e->p0[1], e->p0[2]), e->radius, p, d, e->eps, t) && t < tl;
-			} else {
-				h = any_tri(mk3(e->p0[0], e->p0[1], e->p0[2]), mk3(e->e1[0], e->e1[1], e->e1[2]),
-					    mk3(e->e2[0], e->e2[1], e->e2[2]), p, d, e->eps, tl);
-			}
-			if (h) {
-				if (e->transparent)
-					li = mul3v(li, mk3(e->kt[0], e->kt[1], e->kt[2]));
-				else
-					tl = -1.f;
-			}
-		}
-		f3 db = d;
-		if (uni(ks.tf.rotated)) {
-			float r[3][3];
-#pragma unroll
-			for (int i = 0; i < 3; i++)
-#pragma unroll
-				for (int j = 0; j < 3; j++)
-					r[i][j] = __uint_as_float(uni(__float_as_uint(ks.tf.r[i][j])));
-			db = tf_dir(r, d);
-		}
-		const f3 inv = safe_inv_fast(db);
-		invq = mk3(inv.x * ks.qsi[0], inv.y * ks.qsi[1], inv.z * ks.qsi[2]);
-		oi = mul3v(oq, invq);
-		w = { tl >= 0.f ? 0u : RTX_NONE, 0u, 0u, 0u, 0u };
-	};
-	if (have)
-		start();
-	for (;;) {
-		const u64 walking = ballot(w.node != RTX_NONE);
-		const u64 holding = ballot(w.tgrp != 0);
-		const bool fin = have && w.node == RTX_NONE && w.tgrp == 0;
-		const u64 fm = ballot(fin);
-		if (!(walking | holding) || (popc64(fm) >= RTX_SH_REFILL && next < nl)) {
-			/* a refill round: the lanes whose walk has ended add their term, take the next samples */
-			if (fin) {
-				if (tl >= 0.f)
-					acc = add3(acc, shade_light<RTX_SH_SPUNI>(ks, rec, d, li, ldist, dsq));
-				my = next + mbcnt(fm);
-				have = my < nl;
-				if (have)
-					start();
-			}
-			next += popc64(fm);
-			if (!ballot(have))
-				break;
-			continue;
-		}
-		/* lanes whose node walk has ended but whose deferred transparent-leaf tests remain would
-		 * wait for a round (RTX_W8_DEFER: all 64 lanes holding) that walking refilled lanes delay:
-		 * once they and the finished lanes make up a refill, run rounds until they finish */
-		const u64 idle_hold = ballot(have && w.node == RTX_NONE && w.tgrp != 0);
-		w8_iter<COUNT, OCT>(Q, p, d, invq, oi, tl, li, w, c,
-				    (idle_hold && popc64(fm | idle_hold) >= RTX_SH_REFILL) ? 0ull : walking, holding);
-	}
-	w8_count<COUNT>(c, sc, (nl + WAVE - 1) / WAVE);
-	if (COUNT)
-		sc.pln += (u64)nl * uni(ks.num_planes);
-	return acc;
-}
-
-/* the octant every shadow ray from p to the emitter E shares in the tree's frame (bit a: the + side
- * of axis a, as shadow_query's), or 8 when the light's extent straddles an axis plane: the
- * sphere's centre offset against its radius, or the triangle's three corners, with a margin for
- * light_point_sh's rounding */
-__device__ __forceinline__ uint32_t light_octant(const DEmitter &E, f3 p, const float (&r)[3][3], bool rot)
-{
-	uint32_t pos = 0, neg = 0;
-	if (E.type == RTX_SPHERE) {
-		const f3 v0 = sub3(ld3(E.p0), p);
-		const f3 v = rot ? tf_dir(r, v0) : v0;
-		const float m = E.radius * 1.001f + 1e-5f * mag3(v);
-		pos = (v.x > m ? 1u : 0u) | (v.y > m ? 2u : 0u) | (v.z > m ? 4u : 0u);
-		neg = (v.x < -m ? 1u : 0u) | (v.y < -m ? 2u : 0u) | (v.z < -m ? 4u : 0u);
-	} else {
-		uint32_t ap = 7u, an = 7u;
-		const f3 c0 = sub3(ld3(E.p0), p);
-		for (int k = 0; k < 3; k++) {
-			const f3 v0 = k == 0 ? c0 : add3(c0, k == 1 ? ld3(E.e1) : ld3(E.e2));
-			const f3 v = rot ? tf_dir(r, v0) : v0;
-			const float m = 1e-5f * mag3(v) + 1e-30f;
-			ap &= (v.x > m ? 1u : 0u) | (v.y > m ? 2u : 0u) | (v.z > m ? 4u : 0u);
-			an &= (v.x < -m ? 1u : 0u) | (v.y < -m ? 2u : 0u) | (v.z < -m ? 4u : 0u);
-		}
-		pos = ap;
-		neg = an;
-	}
-	return (pos | neg) == 7u ? pos : 8u;
-}
-
 /* ------------------------------------------------------------------------ */
 /* the kernel                                                               */
 /* ------------------------------------------------------------------------ */
@@ -1100,44 +951,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 				const uint32_t nl = uni(nls[k]);
 				const float4 *rec = unip(ks.sp) + (size_t)uni(sid[k]) * SPREC;
 				f3 acc = mk3(0.f, 0.f, 0.f);
-				bool refilled = false;
-				if (WALK == WALK_W8 && RTX_SH_REFILL && !RTX_DEBUG_NOWALK && nl > WAVE && uni(ks.num_emitters) == 1 &&
-				    uni(ks.have_tree)) {
-					/* one emitter whose extent keeps every ray of the point in one octant, the point
-					 * not far from the tree's frame: the refilled lanes (point_refill) */
-					const float4 q0 = sp_field<RTX_SH_SPUNI>(rec, 0), q4 = sp_field<RTX_SH_SPUNI>(rec, 4);
-					const f3 p = mk3(q0.x, q0.y, q0.z);
-					const DEmitter E = emitter_uni(unip(ks.emitters));
-					const bool rot = uni(ks.tf.rotated) != 0;
-					float r[3][3], c[3];
-#pragma unroll
-					for (int i = 0; i < 3; i++) {
-						c[i] = __uint_as_float(uni(__float_as_uint(ks.tf.c[i])));
-#pragma unroll
-						for (int jj = 0; jj < 3; jj++)
-							r[i][jj] = __uint_as_float(uni(__float_as_uint(ks.tf.r[i][jj])));
-					}
-					const f3 ob = rot ? tf_point(r, c, p) : p;
-					const uint32_t oct = (rot && tf_far(ob, __uint_as_float(uni(__float_as_uint(ks.tf.rad)))))
-								     ? 8u
-								     : light_octant(E, p, r, rot);
-					if (oct < 8u && E.obj != __float_as_uint(q4.x)) {
-						const QBvh Q = make_qbvh<WALK>(ks, top_q, top_e, stk, t8);
-						const f3 oq = mk3((ob.x - Q.qo.x) * Q.qs.x, (ob.y - Q.qo.y) * Q.qs.y, (ob.z - Q.qo.z) * Q.qs.z);
-						const uint32_t ka = __float_as_uint(q4.y), kb = __float_as_uint(q4.z);
-						switch (oct) {
-#define RTX_REFILL(K)                                                                            \
-	case K:                                                                                          \
-		acc = point_refill<COUNT, (RTX_SH_OCT ? K : 8)>(ks, rec, nl, ka, kb, p, oq, Q, sc); \
-		break;
-							RTX_REFILL(0) RTX_REFILL(1) RTX_REFILL(2) RTX_REFILL(3) RTX_REFILL(4) RTX_REFILL(5)
-							RTX_REFILL(6) RTX_REFILL(7)
-#undef RTX_REFILL
-						}
-						refilled = true;
-					}
-				}
-				for (uint32_t base = 0; !refilled && base < nl; base += WAVE) {
+				for (uint32_t base = 0; base < nl; base += WAVE) {
 					const uint32_t idx = base + lane_id();
 					acc = add3(acc, light_sample<COUNT, WALK, true>(ks, rec, idx, idx < nl, sc, top_q, top_e, stk, t8));
 				}
