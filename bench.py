@@ -83,6 +83,9 @@ def parse():
     ap.add_argument("--no-post", action="store_true", help="skip the postprocess (DoF + mist) side leg")
     ap.add_argument("--cpu-target-s", type=float, default=12.0)
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--loopback", action="store_true",
+                    help="--gpus N > 1 as N shards on device 0 (rtx_group_open_loopback: the device group's own path "
+                         "with a device-to-device copy for the RCCL gather); a one-GPU rehearsal, never a scaling number")
     ap.add_argument("--dry-run", action="store_true",
                     help="rank bring-up only (gloo, no GPU): print the ranks' world and exit (tests)")
     return ap.parse_args()
@@ -702,7 +705,8 @@ def group_line(a, n, scene_name, objects, elapsed, rays, closest, per_dev, gathe
     kms = [d["kernel_ms"] for d in per_dev if d["kernel_ms"] is not None]
     value = rays / elapsed / 1e6 if elapsed else None
     frame_rays = rays // steps if rays is not None else None
-    return {"metric": METRIC, "value": round(value, 2) if value is not None else None, "unit": "Mrays/s", "n_gpus": n,
+    return {"metric": METRIC, "value": round(value, 2) if value is not None else None, "unit": "Mrays/s",
+            "n_gpus": 1 if getattr(a, "loopback", False) else n, "shards": n,
             "steps": steps, "warmup": a.warmup,
             "ms_per_step": round(elapsed / steps * 1e3, 3) if elapsed else None,
             "closest_mrays": round(closest / elapsed / 1e6, 2) if elapsed else None,
@@ -713,7 +717,9 @@ def group_line(a, n, scene_name, objects, elapsed, rays, closest, per_dev, gathe
                        "rng": "counter, i.i.d. light samples (RTX_RNG_COUNTER, the library default)",
                        "step": "rtx_group_render: shards on every device, RCCL send/recv to device 0, unpack, copy to "
                                "pinned host memory (SURVEY 8(d) window)"},
-            "group": {"rtx_group_size": n, "rccl_devices": n if n > 1 else 0,
+            "group": {"rtx_group_size": n, "rccl_devices": n if n > 1 and not a.loopback else 0,
+                      "transport": ("loopback (n shards on device 0, device-to-device copy; a rehearsal of the "
+                                    "group path, not a multi-GPU measurement)") if a.loopback else "rccl",
                       "devices": per_dev,
                       "device_kernel_ms_max": max(kms) if kms else None,
                       "device_kernel_ms_min": min(kms) if kms else None,
@@ -755,7 +761,7 @@ def main_group(a):
     flags = flags_for(a.scene, a.spp)
     params = rtxpy.params_from_args(flags, seed=1)
     params.rng = abi.RTX_RNG_COUNTER  # the reference's i.i.d. light samples
-    g = rtxpy.Group(list(range(a.gpus)))
+    g = rtxpy.Group([0], loopback=a.gpus) if a.loopback else rtxpy.Group(list(range(a.gpus)))
     n = g.size()
     g.set_option(abi.RTX_OPT_SHADOW_WALK, WALKS[a.walk])
     g.set_option(abi.RTX_OPT_TRACE_WALK, WALKS[a.trace_walk])

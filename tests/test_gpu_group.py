@@ -20,6 +20,8 @@ loopback group above, the record layout on the host (tests/test_gather.py), the 
 gathered over torch.distributed with gloo (tests/test_distributed.py), and the group line's
 schema (tests/test_bench_cli.py).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -147,3 +149,25 @@ def test_gpu_loopback_group_sharding_of_a_tall_ragged_frame():
         b, zb = g.render(frame, params)
         g.close()
         assert np.array_equal(a, b) and np.array_equal(za, zb), n
+
+
+def test_gpu_bench_group_line_on_the_loopback_group(tmp_path):
+    """bench.py's device-group mode (main_group: --gpus N without torchrun) run end to end on the
+    one-GPU box through the loopback group: the line's per-device rays add up to the frame's, every
+    shard has kernel times, and it reports one GPU with N shards (a rehearsal, not a scaling line)"""
+    import json
+    import subprocess
+    import sys
+    cmd = [sys.executable, os.path.join(C.ROOT, "bench.py"), "--gpus", "3", "--loopback", "--scene", "scene3",
+           "--width", "192", "--height", "108", "--spp", "2", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+    p = subprocess.run(cmd, cwd=C.ROOT, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["n_gpus"] == 1 and out["shards"] == 3 and out["value"] > 0
+    g = out["group"]
+    assert g["rtx_group_size"] == 3 and g["rccl_devices"] == 0 and g["transport"].startswith("loopback")
+    assert [d["device"] for d in g["devices"]] == [0, 1, 2]
+    assert sum(d["rays"] for d in g["devices"]) == out["config"]["rays_per_frame"]
+    assert all(d["kernel_ms"] > 0 for d in g["devices"]) and g["gather_ms"] > 0
+    assert g["upload"]["peer_copy_ms"][0] == 0.0 and min(g["upload"]["peer_copy_ms"][1:]) > 0
+    assert out["roofline"]["kernel"] == "k_shadow" and out["roofline"]["device"] == 0
