@@ -955,12 +955,16 @@ int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, floa
 	sp_key.set = 1;
 	if (c->sp_tile_key == sp_key && c->sp_tile_seen > 0.0)
 		avg_tile = std::min<uint64_t>(avg_tile, (uint64_t)(c->sp_tile_seen * 1.25) + 64);
+	if (c->opt_sp_tile) /* RTX_OPT_SP_PER_TILE: tests drive the overflow path with a low figure */
+		avg_tile = c->opt_sp_tile;
 	size_t free_b = 0, total_b = 0;
 	HIP_TRY(hipMemGetInfo(&free_b, &total_b));
 	/* shade points of a chunk: up to a third of free HBM (96 GB cap; 288 GB per MI355X) */
 	const uint64_t budget = std::min<uint64_t>(96ull << 30, free_b / 3);
 	/* 128 B per shade point: its record (96), its light term (16) and its sort keys / values (16) */
-	const uint32_t chunk_cap = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(P.ntiles, budget / (avg_tile * 128)));
+	uint32_t chunk_cap = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(P.ntiles, budget / (avg_tile * 128)));
+	if (c->opt_chunk) /* RTX_OPT_CHUNK_TILES */
+		chunk_cap = std::min(chunk_cap, c->opt_chunk);
 	uint32_t chunk_tiles = chunk_cap;
 
 	auto grow = [](auto *&ptr, size_t &have, size_t need) -> hipError_t {
@@ -1289,6 +1293,16 @@ extern "C" int rtx_set_option(rtx_ctx *c, int option, int64_t value)
 		if (value < 1 || value > (1 << 24))
 			return fail(RTX_ERR_ARG, "shadow grab %lld outside 1..2^24", (long long)value);
 		c->opt_grab = (uint32_t)value;
+		return RTX_OK;
+	case RTX_OPT_CHUNK_TILES:
+		if (value < 0 || value > 0xFFFFFFFFll)
+			return fail(RTX_ERR_ARG, "chunk tiles %lld outside 0..2^32-1", (long long)value);
+		c->opt_chunk = (uint32_t)value;
+		return RTX_OK;
+	case RTX_OPT_SP_PER_TILE:
+		if (value < 0 || value > (1 << 20))
+			return fail(RTX_ERR_ARG, "shade points per tile %lld outside 0..2^20", (long long)value);
+		c->opt_sp_tile = (uint32_t)value;
 		return RTX_OK;
 	}
 	return fail(RTX_ERR_ARG, "unknown option %d", option);

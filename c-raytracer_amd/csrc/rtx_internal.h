@@ -128,6 +128,8 @@ struct rtx_ctx {
 	uint32_t opt_lstk = RTX_W8_STACK;
 	int opt_trace_walk = RTX_WALK_AUTO;
 	int opt_frame = RTX_FRAME_AUTO;
+	uint32_t opt_chunk = 0;   /* most tiles per chunk (0: as many as the shade-point budget allows) */
+	uint32_t opt_sp_tile = 0; /* shade points per tile a chunk is sized for (0: the estimate / last render's count) */
 };
 
 struct QFrame {

@@ -285,7 +285,12 @@ enum rtx_option {
 	                               * ones spill to HBM (tests use 1 to exercise the spill on any tree) */
 	RTX_OPT_TRACE_WALK = 7,       /* closest hits (k_trace): RTX_WALK_AUTO (the 8-wide tree when built,
 	                               * default), RTX_WALK_W8 or RTX_WALK_BVH2 (the float BVH2) */
-	RTX_OPT_TREE_FRAME = 8        /* RTX_FRAME_* (build; default RTX_FRAME_AUTO) */
+	RTX_OPT_TREE_FRAME = 8,       /* RTX_FRAME_* (build; default RTX_FRAME_AUTO) */
+	RTX_OPT_CHUNK_TILES = 9,      /* most 8x8 tiles per chunk of a render (0 = as many as the shade-point budget,
+	                               * a third of free HBM, allows; default 0) */
+	RTX_OPT_SP_PER_TILE = 10      /* shade points per tile a chunk is sized for (0 = automatic, default): a
+	                               * chunk that overflows is halved and retried, so any value gives the same
+	                               * image (tests drive the overflow path with a low one) */
 };
 int rtx_set_option(rtx_ctx *ctx, int option, int64_t value);
 /* The frame rtx_upload_scene builds the scene's BVHs in under RTX_FRAME_AUTO (a diagnostic; no
