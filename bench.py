@@ -646,13 +646,20 @@ def main():
         except Exception as e:  # never let the side leg kill the measurement
             log(f"postprocess leg failed: {e}")
 
+    if world > 1:
+        # the GPU work is done: every rank leaves the process group, and rank 0 alone times the
+        # reference CPU leg below (the other ranks exit, leaving the host cores to it)
+        r.close()
+        r = None
+        torch.distributed.destroy_process_group()
     cpu = port = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and not a.no_cpu_baseline:
         try:
             cpu = cpu_reference(path, flags, a.width, a.height, a.cpu_target_s, log)
         except Exception as e:  # never let the baseline kill the measurement
             log(f"reference baseline failed: {e}")
-        port = cpu_port(scene, frame, params, a.cpu_target_s / 2, log)
+        if world == 1:
+            port = cpu_port(scene, frame, params, a.cpu_target_s / 2, log)
         if cpu is None:
             cpu = port
             port = None
@@ -691,9 +698,8 @@ def main():
         if build:
             out["bvh_build"] = build
         print(json.dumps(out), flush=True)
-    r.close()
-    if world > 1:
-        torch.distributed.destroy_process_group()
+    if r is not None:
+        r.close()
 
 
 def group_line(a, n, scene_name, objects, elapsed, rays, closest, per_dev, gather_ms, roofline, cpu=None,
