@@ -874,6 +874,9 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	return contribution;
 }
 
+#ifndef RTX_SH_SORT_DRY
+#define RTX_SH_SORT_DRY 0 /* measurement: compute the order but walk in index order */
+#endif
 #ifndef RTX_SH_SORT
 #define RTX_SH_SORT 1 /* one emitter, i.i.d. draws, 64 < lights <= RTX_SH_SORT_MAX: walk a point's samples in the
                        * order of their first draw's bucket (sample_order; at run time RTX_OPT_SHADOW_SORT) */
@@ -925,7 +928,7 @@ __device__ __forceinline__ void sample_order(uint64_t key, uint32_t nl, uint16_t
 				break;
 			const u64 m = ballot(b[r] == (uint32_t)g);
 			if (b[r] == (uint32_t)g)
-				pw[run[g] + mbcnt(m)] = (uint16_t)j;
+				gptrw(pw)[run[g] + mbcnt(m)] = (uint16_t)j;
 			run[g] += popc64(m);
 		}
 	}
@@ -1016,11 +1019,11 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 					uint16_t *pw = unip(ks.sperm) + (size_t)(blockIdx.x * RTX_SH_NW + wv) * RTX_SH_SORT_MAX;
 					const float4 q4 = sp_field<RTX_SH_SPUNI>(rec, 4);
 					sample_order(key_of(__float_as_uint(q4.y), __float_as_uint(q4.z)), nl, pw);
-					order = pw;
+					order = RTX_SH_SORT_DRY ? nullptr : pw;
 				}
 				for (uint32_t base = 0; base < nl; base += WAVE) {
 					const uint32_t idx = base + lane_id();
-					const uint32_t j = (order && idx < nl) ? (uint32_t)order[idx] : idx;
+					const uint32_t j = (order && idx < nl) ? (uint32_t)gptr(order)[idx] : idx;
 					acc = add3(acc, light_sample<COUNT, WALK, true>(ks, rec, j, idx < nl, sc, top_q, top_e, stk, t8));
 				}
 				const float sx = wave_sum(acc.x), sy = wave_sum(acc.y), sz = wave_sum(acc.z);

@@ -551,6 +551,7 @@ int main(int argc, char **argv)
 	};
 	const bool occ_sim = getenv("W8SIM_OCC") && atoi(getenv("W8SIM_OCC"));
 	const int order = getenv("W8SIM_ORDER") ? atoi(getenv("W8SIM_ORDER")) : 0;
+	const bool sort_samples = getenv("W8SIM_SORT") && atoi(getenv("W8SIM_SORT"));
 	const bool strat = getenv("W8SIM_STRAT") && atoi(getenv("W8SIM_STRAT")); /* RTX_RNG_STRAT light samples */
 	uint32_t prev_lane_blk[64];
 	for (int l = 0; l < 64; l++)
@@ -570,6 +571,23 @@ int main(int argc, char **argv)
 		}
 		/* packets of 64 light samples */
 		std::vector<std::vector<uint32_t>> allseq; /* every sample's node visits (immediate-test walk) */
+		/* the point's light samples: i.i.d. (or stratified) draws, walked in index order or, with
+		 * W8SIM_SORT=1, in the order of their first draw's bucket among ceil(nl / 64) (k_shadow's
+		 * sample_order) */
+		std::vector<float> su1(nl), su2(nl);
+		for (uint32_t j = 0; j < nl; j++) {
+			su1[j] = strat ? ((float)j + U(rng)) / (float)nl : U(rng);
+			su2[j] = U(rng);
+		}
+		std::vector<uint32_t> sord(nl);
+		for (uint32_t j = 0; j < nl; j++)
+			sord[j] = j;
+		if (sort_samples && nl > 64) {
+			const uint32_t G = (nl + 63) / 64;
+			std::stable_sort(sord.begin(), sord.end(), [&](uint32_t a, uint32_t b) {
+				return (uint32_t)(su1[a] * G) < (uint32_t)(su1[b] * G);
+			});
+		}
 		for (uint32_t b0 = 0; b0 < nl; b0 += 64) {
 			std::vector<uint32_t> visits_lane, leaf_at; /* per-lane per-visit leaf hits */
 			std::vector<std::vector<uint32_t>> leaves(64), seq(64);
@@ -580,7 +598,7 @@ int main(int argc, char **argv)
 			uint32_t maxv = 0, imm_len[64] = {};
 			for (uint32_t l = 0; l < 64 && b0 + l < nl; l++) {
 				const uint32_t j = b0 + l;
-				float u1 = strat ? ((float)j + U(rng)) / (float)nl : U(rng), u2 = U(rng);
+				float u1 = su1[sord[j]], u2 = su2[sord[j]];
 				float Lp[3];
 				if (E.type == RTX_SPHERE) {
 					const float inc = u1 * 2.f * 3.1415927f, az = u2 * 2.f * 3.1415927f;
