@@ -170,8 +170,6 @@ extern "C" void rtx_close(rtx_ctx *c)
 	c->ostk_bytes = 0;
 	dfree(c->d_w8spill);
 	c->w8spill_bytes = 0;
-	dfree(c->d_sperm);
-	c->sperm_bytes = 0;
 	dfree(c->d_sortbuf);
 	dfree(c->d_sorttmp);
 	dfree(c->d_post_rad);
@@ -986,18 +984,6 @@ int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, floa
 	c->scene.ostk = c->d_ostk;
 	c->scene.w8spill = nullptr;
 	c->scene.w8spill_lanes = 0;
-	c->scene.sperm = nullptr;
-	c->scene.sperm_waves = 0;
-	if (c->scene.w8 && P.rng == RTX_RNG_COUNTER && c->opt_sort) {
-		/* k_shadow orders a point's i.i.d. light samples by their first draw (rtx_shadow.hip
-		 * RTX_SH_SORT): one order buffer per wave of the largest grid */
-		uint32_t lanes = 0;
-		HIP_TRY(rtx_shadow_grid_lanes((uint32_t)c->cus, &lanes));
-		const uint32_t waves = lanes / 64;
-		HIP_TRY(grow(c->d_sperm, c->sperm_bytes, (size_t)waves * RTX_SH_SORT_MAX * sizeof(uint16_t)));
-		c->scene.sperm = c->d_sperm;
-		c->scene.sperm_waves = waves;
-	}
 	c->scene.trace_w8 = (c->scene.w8 && c->opt_trace_walk != RTX_WALK_BVH2) ? 1u : 0u;
 	c->stats.trace_walk = c->scene.trace_w8 ? RTX_WALK_W8 : RTX_WALK_BVH2;
 	c->scene.w8lstk = c->opt_lstk;
@@ -1312,11 +1298,6 @@ extern "C" int rtx_set_option(rtx_ctx *c, int option, int64_t value)
 		if (value < 0 || value > 0xFFFFFFFFll)
 			return fail(RTX_ERR_ARG, "chunk tiles %lld outside 0..2^32-1", (long long)value);
 		c->opt_chunk = (uint32_t)value;
-		return RTX_OK;
-	case RTX_OPT_SHADOW_SORT:
-		if (value != 0 && value != 1)
-			return fail(RTX_ERR_ARG, "RTX_OPT_SHADOW_SORT takes 0 or 1, not %lld", (long long)value);
-		c->opt_sort = value != 0;
 		return RTX_OK;
 	case RTX_OPT_SP_PER_TILE:
 		if (value < 0 || value > (1 << 20))

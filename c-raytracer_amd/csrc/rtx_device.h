@@ -152,7 +152,6 @@ typedef struct DTreeFrame {
 #define RTX_W8_STACK 8     /* k_shadow lane-stack entries in LDS; deeper ones spill to HBM (DScene.w8spill) */
 #endif
 #define RTX_W8_MAX_ENTRIES (1u << 24)
-#define RTX_SH_SORT_MAX 512 /* k_shadow sorts the light samples of points with up to this many (DScene.sperm) */
 #define RTX_W8_TOP_LEVELS 3 /* levels of the 8-wide tree k_shadow serves from LDS (root, 8, 64 nodes) */
 #define RTX_W8_TOP_MAX 80   /* entries of them at most: 2 + 8 + 64 */
 typedef struct __attribute__((aligned(64))) DW8 {
@@ -234,8 +233,6 @@ typedef struct DScene {
 	uint32_t num_lin;
 	uint32_t *w8spill;      /* k_shadow lane-stack entries from RTX_W8_STACK on, [entry][grid lane] */
 	uint32_t w8spill_lanes; /* grid lanes the spill area was sized for (0: no spill area) */
-	uint16_t *sperm;        /* k_shadow: each wave's light-sample order of its current shade point (RTX_SH_SORT_MAX entries per wave) */
-	uint32_t sperm_waves;   /* waves it was sized for (0: none) */
 	uint32_t w8lstk;        /* lane-stack entries k_shadow keeps in LDS (<= RTX_W8_STACK) */
 	uint32_t root_ref;
 	uint32_t num_nodes;    /* prims == (const DPrim *)(nodes + num_nodes) */

@@ -85,8 +85,6 @@ struct rtx_ctx {
 	DW8S *d_w8s = nullptr;
 	uint32_t *d_w8spill = nullptr; /* k_shadow lane-stack spill of deep 8-wide trees (DScene.w8spill) */
 	size_t w8spill_bytes = 0;
-	uint16_t *d_sperm = nullptr;   /* k_shadow's per-wave light-sample order (DScene.sperm) */
-	size_t sperm_bytes = 0;
 	DScene scene{};
 	bool have_scene = false;
 	/* work buffers (grow-only) */
@@ -132,7 +130,6 @@ struct rtx_ctx {
 	int opt_frame = RTX_FRAME_AUTO;
 	uint32_t opt_chunk = 0;   /* most tiles per chunk (0: as many as the shade-point budget allows) */
 	uint32_t opt_sp_tile = 0; /* shade points per tile a chunk is sized for (0: the estimate / last render's count) */
-	bool opt_sort = true;     /* k_shadow walks a point's i.i.d. light samples in the order of their first draw */
 };
 
 struct QFrame {

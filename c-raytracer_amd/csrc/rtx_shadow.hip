@@ -647,7 +647,6 @@ struct KShadow {
 const DW8 *w8;        /* 8-wide compressed BVH (WALK_W8 instances; qo / qs / qsi are then its frame) */
 	const DW8S *w8s;      /* its nodes' scalar-path copies */
 	uint32_t *w8spill;    /* lane-stack spill area, [entry][grid lane] */
-	uint16_t *sperm;      /* per-wave light-sample order (RTX_SH_SORT), or null */
 	uint32_t w8lstk;      /* lane-stack entries in LDS */
 	uint32_t w8top;       /* entries of the 8-wide tree's top levels, copied to LDS per workgroup (DScene.w8top) */
 	const DEmitter *lin;  /* objects shadow_query tests one by one: the emitters the 8-wide tree leaves out,
@@ -874,67 +873,6 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	return contribution;
 }
 
-#ifndef RTX_SH_SORT_DRY
-#define RTX_SH_SORT_DRY 0 /* measurement: compute the order but walk in index order */
-#endif
-#ifndef RTX_SH_SORT
-#define RTX_SH_SORT 1 /* one emitter, i.i.d. draws, 64 < lights <= RTX_SH_SORT_MAX: walk a point's samples in the
-                       * order of their first draw's bucket (sample_order; at run time RTX_OPT_SHADOW_SORT) */
-#endif
-/* The order in which the wave walks the nl light samples of one shade point (RTX_SH_SORT; one
- * emitter, i.i.d. draws, 64 < nl <= RTX_SH_SORT_MAX): the samples by the bucket of their first
- * draw among G = ceil(nl / 64) equal buckets of [0, 1) (the sphere light's inclination band, the
- * triangle's first coordinate), in sample-index order within a bucket: a counting sort, written to
- * the wave's order buffer pw.  A 64-sample packet then takes about one band of the light, so its
- * rays stay closer together in the tree.  Every sample keeps its own draws (rtx_draw2 of its
- * index) and its own term; only which lane evaluates it changes, and with that the order of the
- * point's float sum.  So the estimator is the reference's i.i.d. one (object.c:298-299), sample for
- * sample, unlike RTX_RNG_STRAT.  The order depends only on the point's key: deterministic. */
-__device__ __forceinline__ void sample_order(uint64_t key, uint32_t nl, uint16_t *pw)
-{
-	constexpr int RMAX = RTX_SH_SORT_MAX / WAVE;
-	const uint32_t G = (nl + WAVE - 1) / WAVE; /* buckets = packets, 2..RMAX */
-	const uint64_t s = rtx_draw_stream(key, 0u); /* the one emitter's stream (emitter_sample: e = 0) */
-	uint32_t b[RMAX], cnt[RMAX];
-#pragma unroll
-	for (int g = 0; g < RMAX; g++)
-		cnt[g] = 0;
-#pragma unroll
-	for (int r = 0; r < RMAX; r++) {
-		const uint32_t j = (uint32_t)r * WAVE + lane_id();
-		b[r] = ((uint32_t)r < G && j < nl) ? (rtx_draw_u1_bits(s, j) * G) >> 24 : (uint32_t)RMAX;
-		if ((uint32_t)r < G) {
-#pragma unroll
-			for (int g = 0; g < RMAX; g++)
-				if ((uint32_t)g < G)
-					cnt[g] += popc64(ballot(b[r] == (uint32_t)g));
-		}
-	}
-	uint32_t run[RMAX]; /* each bucket's next position */
-	uint32_t at = 0;
-#pragma unroll
-	for (int g = 0; g < RMAX; g++) {
-		run[g] = at;
-		at += cnt[g];
-	}
-#pragma unroll
-	for (int r = 0; r < RMAX; r++) {
-		if ((uint32_t)r >= G)
-			break;
-		const uint32_t j = (uint32_t)r * WAVE + lane_id();
-#pragma unroll
-		for (int g = 0; g < RMAX; g++) {
-			if ((uint32_t)g >= G)
-				break;
-			const u64 m = ballot(b[r] == (uint32_t)g);
-			if (b[r] == (uint32_t)g)
-				gptrw(pw)[run[g] + mbcnt(m)] = (uint16_t)j;
-			run[g] += popc64(m);
-		}
-	}
-	__threadfence_block(); /* the order is read back by other lanes of the wave */
-}
-
 /* ------------------------------------------------------------------------ */
 /* the kernel                                                               */
 /* ------------------------------------------------------------------------ */
@@ -1013,18 +951,9 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 				const uint32_t nl = uni(nls[k]);
 				const float4 *rec = unip(ks.sp) + (size_t)uni(sid[k]) * SPREC;
 				f3 acc = mk3(0.f, 0.f, 0.f);
-				const uint16_t *order = nullptr; /* RTX_SH_SORT: the samples' walk order */
-				if (RTX_SH_SORT && WALK == WALK_W8 && nl > WAVE && nl <= RTX_SH_SORT_MAX && uni(ks.num_emitters) == 1 &&
-				    (int32_t)uni((uint32_t)ks.rng) == RTX_RNG_COUNTER && ks.sperm) {
-					uint16_t *pw = unip(ks.sperm) + (size_t)(blockIdx.x * RTX_SH_NW + wv) * RTX_SH_SORT_MAX;
-					const float4 q4 = sp_field<RTX_SH_SPUNI>(rec, 4);
-					sample_order(key_of(__float_as_uint(q4.y), __float_as_uint(q4.z)), nl, pw);
-					order = RTX_SH_SORT_DRY ? nullptr : pw;
-				}
 				for (uint32_t base = 0; base < nl; base += WAVE) {
 					const uint32_t idx = base + lane_id();
-					const uint32_t j = (order && idx < nl) ? (uint32_t)gptr(order)[idx] : idx;
-					acc = add3(acc, light_sample<COUNT, WALK, true>(ks, rec, j, idx < nl, sc, top_q, top_e, stk, t8));
+					acc = add3(acc, light_sample<COUNT, WALK, true>(ks, rec, idx, idx < nl, sc, top_q, top_e, stk, t8));
 				}
 				const float sx = wave_sum(acc.x), sy = wave_sum(acc.y), sz = wave_sum(acc.z);
 				if (lane_id() == 0) {
@@ -1384,15 +1313,6 @@ for (int a = 0; a < 3; a++) {
 	ka.w8 = S->w8;
 	ka.w8s = S->w8s;
 	ka.w8spill = S->w8spill;
-	ka.sperm = nullptr;
-	if (walk == WALK_W8 && S->sperm) { /* one order buffer per wave of this launch's grid */
-		uint32_t lanes = 0;
-		hipError_t e = rtx_shadow_grid_lanes(cus, &lanes);
-		if (e != hipSuccess)
-			return e;
-		if (S->sperm_waves >= lanes / WAVE)
-			ka.sperm = S->sperm;
-	}
 	ka.w8lstk = S->w8lstk;
 	ka.w8top = S->w8top;
 	ka.lin = S->lin; /* a tiny scene: every bounded object, no walk */

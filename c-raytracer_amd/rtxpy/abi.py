@@ -86,7 +86,7 @@ RTX_SHADOW_LINEAR_MAX = 8
 RTX_FRAME_AUTO, RTX_FRAME_WORLD = 0, 1
 RTX_OPT_SHADOW_WALK, RTX_OPT_BVH_LEAF, RTX_OPT_SPSORT, RTX_OPT_SHADOW_SLOT, RTX_OPT_SHADOW_GRAB, \
     RTX_OPT_SHADOW_LDS_STACK, RTX_OPT_TRACE_WALK, RTX_OPT_TREE_FRAME, RTX_OPT_CHUNK_TILES, \
-    RTX_OPT_SP_PER_TILE, RTX_OPT_SHADOW_SORT = 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11
+    RTX_OPT_SP_PER_TILE = 1, 2, 3, 4, 5, 6, 7, 8, 9, 10
 RTX_DOF_NONE, RTX_DOF_SCALE_BIAS, RTX_DOF_CAMERA = 0, 1, 2
 RTX_FALLOFF_QUAD, RTX_FALLOFF_LIN, RTX_FALLOFF_INV_QUAD = 0, 1, 2
 

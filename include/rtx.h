@@ -288,13 +288,9 @@ enum rtx_option {
 	RTX_OPT_TREE_FRAME = 8,       /* RTX_FRAME_* (build; default RTX_FRAME_AUTO) */
 	RTX_OPT_CHUNK_TILES = 9,      /* most 8x8 tiles per chunk of a render (0 = as many as the shade-point budget,
 	                               * a third of free HBM, allows; default 0) */
-	RTX_OPT_SP_PER_TILE = 10,     /* shade points per tile a chunk is sized for (0 = automatic, default): a
+	RTX_OPT_SP_PER_TILE = 10      /* shade points per tile a chunk is sized for (0 = automatic, default): a
 	                               * chunk that overflows is halved and retried, so any value gives the same
 	                               * image (tests drive the overflow path with a low one) */
-	RTX_OPT_SHADOW_SORT = 11      /* 1 (default): k_shadow walks the i.i.d. light samples of a point of one
-	                               * emitter (64 < lights <= 512) in the order of their first draw, so each
-	                               * 64-sample packet covers about one band of the light; the same samples,
-	                               * only their lanes and the float sum's order change.  0: index order */
 };
 int rtx_set_option(rtx_ctx *ctx, int option, int64_t value);
 /* The frame rtx_upload_scene builds the scene's BVHs in under RTX_FRAME_AUTO (a diagnostic; no

@@ -73,11 +73,4 @@ RTX_HD void rtx_draw2(uint64_t key, uint32_t stream, uint32_t index, float *u1, 
 	*u2 = (float)(b >> 8) * (1.0f / 16777216.0f);
 }
 
-/* rtx_draw2's first number as its 24 bits (*u1 = bits * 2^-24), from the (key, stream) part
- * s = rtx_draw_stream(key, stream), which is the same for every index */
-RTX_HD uint64_t rtx_draw_stream(uint64_t key, uint32_t stream)
-{
-	return rtx_mix64(key ^ ((uint64_t)stream + 1u) * 0xd1b54a32d192ed03ull);
-}
-RTX_HD uint32_t rtx_draw_u1_bits(uint64_t s, uint32_t index) { return rtx_hash32((uint32_t)s ^ index) >> 8; }
 #endif

@@ -54,32 +54,3 @@ def test_gpu_chunk_options_reject_bad_values():
     finally:
         r.close()
 
-
-@pytest.mark.parametrize("name", ["s5_path2", "s5_amb"])
-def test_gpu_sample_order_keeps_the_samples(name):
-    """RTX_OPT_SHADOW_SORT (rtx_shadow.hip sample_order): a point's i.i.d. light samples (scene5:
-    300 of one sphere light) are walked in the order of their first draw instead of their index.
-    The samples and their terms are the same, only the lane that evaluates each one and the order
-    of the float sum change: the frame agrees with the index-order frame to float rounding of the
-    sums (a sample lost or doubled would move a pixel by ~1/300 of its light), with equal ray and
-    shade-point counts, and the sorted frame is deterministic."""
-    scene, frame, params, _ = C.load_config(name)
-    params.rng = abi.RTX_RNG_COUNTER
-    params.seed = 7
-    r = rtxpy.Renderer(0)
-    try:
-        r.upload(scene)
-        a, za = r.render(frame, params)
-        sa = r.stats()
-        a2, _ = r.render(frame, params)
-        r.set_option(abi.RTX_OPT_SHADOW_SORT, 0)
-        b, zb = r.render(frame, params)
-        sb = r.stats()
-    finally:
-        r.close()
-    assert np.array_equal(a, a2)
-    assert np.array_equal(za, zb)
-    assert (sa.closest_rays, sa.shadow_rays, sa.shade_points) == (sb.closest_rays, sb.shadow_rays, sb.shade_points)
-    scale = float(np.abs(b).max())
-    assert np.abs(a - b).max() <= 1e-5 * scale, float(np.abs(a - b).max() / scale)
-    assert float(np.abs(a - b).sum() / np.abs(b).sum()) <= 1e-6
