@@ -124,3 +124,33 @@ def test_cpu_config_sample_indices():
         a = set(sample_index(w, h, off, ostride).tolist())
         b = set(sample_index(w, h, off, stride).tolist())
         assert a and a <= b, cfg
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,shards", [("k4_scene5_1080p_n256_shard0of8", 8), ("k5_scene6_2160p_n128", 8)])
+def test_gpu_eight_gpu_configs_through_the_group_path(renderer, cfg, shards):
+    """configs[3] (scene5 1080p -n 256) and configs[4] (scene6 2160p -n 128) are quoted for 8 GPUs:
+    their whole frame through the device group's path at 8 shards (the loopback transport:
+    scene copies, one host thread per shard, tile pack / unpack, statistics; RCCL aside) is the
+    one-device frame bit for bit, with the shards' ray counts summing to its counts"""
+    scene_name, w, h, spp, _, _ = CONFIGS[cfg]
+    scene = load(scene_name)
+    frame = scene.frame(w, h)
+    p = params_for(spp)
+    renderer.upload(scene)
+    a, za = renderer.render(frame, p)
+    sa = renderer.stats()
+    g = rtxpy.Group([0], loopback=shards)
+    try:
+        g.upload(scene)
+        b, zb = g.render(frame, p)
+        sb = g.stats()
+        per = [g.device_stats(k) for k in range(shards)]
+    finally:
+        g.close()
+    assert np.array_equal(a, b) and np.array_equal(za, zb), cfg
+    assert (sb.closest_rays, sb.shadow_rays) == (sa.closest_rays, sa.shadow_rays)
+    assert sum(s.shadow_rays for s in per) == sa.shadow_rays
+    # the interleaved tile deal balances the shards (DESIGN §6): every shard's rays within 10 % of the mean
+    rays = np.array([s.closest_rays + s.shadow_rays for s in per], np.float64)
+    assert rays.max() <= 1.1 * rays.mean() and rays.min() >= 0.9 * rays.mean(), rays / rays.mean()
