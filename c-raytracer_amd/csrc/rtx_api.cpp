@@ -959,8 +959,9 @@ int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, floa
 		avg_tile = c->opt_sp_tile;
 	size_t free_b = 0, total_b = 0;
 	HIP_TRY(hipMemGetInfo(&free_b, &total_b));
-	/* shade points of a chunk: up to a third of free HBM (96 GB cap; 288 GB per MI355X) */
-	const uint64_t budget = std::min<uint64_t>(96ull << 30, free_b / 3);
+	/* shade points of a chunk: up to a third of free HBM (96 GB cap; 288 GB per MI355X), shared
+	 * out among the contexts rendering on this device at once (rtx_group_open_loopback) */
+	const uint64_t budget = std::min<uint64_t>(96ull << 30, free_b / 3) / std::max<uint32_t>(c->mem_share, 1u);
 	/* 128 B per shade point: its record (96), its light term (16) and its sort keys / values (16) */
 	uint32_t chunk_cap = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(P.ntiles, budget / (avg_tile * 128)));
 	if (c->opt_chunk) /* RTX_OPT_CHUNK_TILES */

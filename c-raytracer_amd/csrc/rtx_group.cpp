@@ -173,6 +173,7 @@ extern "C" int rtx_group_open_loopback(int n, int device, rtx_group **out)
 		}
 		g->ctx[r]->stats.transport = n > 1 ? RTX_TRANSPORT_LOOPBACK : RTX_TRANSPORT_NONE;
 		g->ctx[r]->stats.peer_access = 1u;
+		g->ctx[r]->mem_share = (uint32_t)n; /* the n contexts render on this one device at once */
 	}
 	*out = g;
 	return RTX_OK;

@@ -130,6 +130,8 @@ struct rtx_ctx {
 	int opt_frame = RTX_FRAME_AUTO;
 	uint32_t opt_chunk = 0;   /* most tiles per chunk (0: as many as the shade-point budget allows) */
 	uint32_t opt_sp_tile = 0; /* shade points per tile a chunk is sized for (0: the estimate / last render's count) */
+	uint32_t mem_share = 1;   /* contexts sharing this device's HBM at once (a loopback group's n): the shade-point
+	                           * budget of a render is a third of the free HBM divided by it */
 };
 
 struct QFrame {
