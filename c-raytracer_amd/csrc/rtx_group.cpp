@@ -214,7 +214,8 @@ template <class T> static int peer_copy(T *&out, int dst, const T *src, int sd, 
 		return RTX_OK;
 	HIP_TRY(hipSetDevice(dst));
 	HIP_TRY(hipMalloc(&out, bytes));
-	hipError_t e = hipMemcpyPeerAsync(out, dst, src, sd, bytes, s);
+	hipError_t e = sd == dst ? hipMemcpyAsync(out, src, bytes, hipMemcpyDeviceToDevice, s)
+				 : hipMemcpyPeerAsync(out, dst, src, sd, bytes, s);
 	if (e != hipSuccess) {
 		dfree(out);
 		return fail(RTX_ERR_HIP, "peer copy of %zu bytes from device %d to %d failed: %s", bytes, sd, dst, hipGetErrorString(e));
