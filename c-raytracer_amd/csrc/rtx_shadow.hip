@@ -39,6 +39,9 @@
 #ifndef RTX_DEBUG_NOWALK
 #define RTX_DEBUG_NOWALK 0 /* measurement only: skip the BVH walk (everything else in k_shadow stays) */
 #endif
+#ifndef RTX_DEBUG_NOLEAF
+#define RTX_DEBUG_NOLEAF 0 /* measurement only: the walk tests no leaf (wrong images; the cost of the leaf tests) */
+#endif
 #ifndef RTX_SH_OCT
 #define RTX_SH_OCT 1 /* walks specialised on a wave-uniform direction octant */
 #endif
@@ -420,9 +423,9 @@ __device__ __forceinline__ void w8_iter(const QBvh &Q, f3 o, f3 d, f3 invq, f3 o
 		}
 		const uint32_t hm = v.hm;
 		base = v.base;
-		lm = hm & ~v.io & ~v.to;
+		lm = RTX_DEBUG_NOLEAF ? 0u : hm & ~v.io & ~v.to;
 		uint32_t im = hm & v.io;
-		const uint32_t dm = hm & v.to;
+		const uint32_t dm = RTX_DEBUG_NOLEAF ? 0u : hm & v.to;
 		if (COUNT) {
 			c.nstep++;
 			c.nbox += popc64(v.nv);
