@@ -33,6 +33,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # MI355X_MICROARCH.md: 256 CUs x 4 SIMDs, 2.4 GHz max clock, one wave64 VALU instruction per SIMD
 # every 2 cycles -> peak VALU issue in wave-instructions per second
 VALU_PEAK_GINST = 256 * 4 * 2.4e9 / 2 / 1e9
+VALU_SIMDS, VALU_CLOCK_GHZ = 256 * 4, 2.4
+# that peak holds only for the forms gfx950 dual-issues; measured (tools/dev/valu_rates.hip,
+# profiles/r05/valu_rates_r05r.log) every other VALU form (min/max, conversions, compares,
+# cndmask, perm, fma_mix, any operand in an SGPR) issues at half of it: roofline["issue_slots"]
 # useful VALU per operation of k_shadow (the minimal instruction count of the arithmetic the
 # reference's algorithm needs, per lane): box_hit_q octant form 17 (6 cvt, 6 fma,
 # max/max3/min3/min, cmp), any_tri 39, a plane test 12, and per light sample 100 (counter RNG,
@@ -365,6 +369,18 @@ def shadow_roofline_of(c, shadow_ms, a, world):
             out["issued_frac"] = round(issued / VALU_PEAK_GINST, 4)
             out["useful_over_issued"] = round(useful / valu, 4)
             out["issued_valu_per_shadow_ray"] = round(valu * 64 / max(1, c.shadow_rays), 1)
+            if "sq_active_inst_valu2" in rec:
+                # issue slots: gfx950 issues the full-rate VALU forms (f32 add/mul/fma on VGPR or
+                # literal operands, mov, and/or/xor, u32 add/sub, lshrrev) two per quad-cycle and
+                # every other form one per quad-cycle (tools/dev/valu_rates.hip);
+                # SQ_ACTIVE_INST_VALU2 counts the quad-cycles that issued two
+                dual = rec.get("sq_active_inst_valu2_frame", nl * rec["sq_active_inst_valu2"])
+                used = valu - dual
+                avail = dur * VALU_CLOCK_GHZ * 1e9 / 4.0 * VALU_SIMDS
+                out["issue_slots"] = {"used_quad_cycles": int(used), "available_quad_cycles": int(avail),
+                                      "frac": round(used / avail, 4), "dual_issued_frac": round(2 * dual / valu, 4),
+                                      "note": "VALU issue quad-cycles the kernel used (SQ_INSTS_VALU - "
+                                              "SQ_ACTIVE_INST_VALU2) over the chip's (1024 SIMDs x 2.4 GHz / 4)"}
         if "ta_busy_frac" in rec:
             out["vmem"] = {"ta_busy_frac": rec["ta_busy_frac"], "td_busy_frac": rec.get("td_busy_frac"),
                            "note": "PMC TA_TA_BUSY / TD_TD_BUSY per CU cycle: the vector-memory address / data "

@@ -112,6 +112,30 @@ __device__ __forceinline__ bool w8_slab(float lx, float hx, float ly, float hy, 
 	asm("v_min_f32 %0, %0, %1" : "+v"(tf) : "v"(tl));
 	return tn <= tf;
 }
+/* The same test (OCT < 8) as a word whose sign bit says "miss": with A the entry (max of the near
+ * planes) and C the exit clipped to tl (min of the far planes and tl), the box is hit when
+ * A <= C and C >= 0, i.e. when neither C - A nor C is negative.  Two full-rate VALU operations
+ * (v_sub_f32, v_or_b32, which gfx950 dual-issues) replace v_max(0), v_cmp and v_cndmask, which it
+ * does not (tools/dev/valu_rates.hip).  The two tests differ only where C or C - A is -0, a box
+ * the ray touches at t = 0 alone, which holds no hit beyond the primitives' epsilon. */
+template <int OCT>
+__device__ __forceinline__ uint32_t w8_slab_miss(float lx, float hx, float ly, float hy, float lz, float hz, float tl)
+{
+	static_assert(OCT < 8, "octant-specialised only");
+	const float nx = (OCT & 1) ? lx : hx, fx = (OCT & 1) ? hx : lx;
+	const float ny = (OCT & 2) ? ly : hy, fy = (OCT & 2) ? hy : ly;
+	const float nz = (OCT & 4) ? lz : hz, fz = (OCT & 4) ? hz : lz;
+	const float a = fmaxf(fmaxf(nx, ny), nz);
+	float c = fminf(fminf(fx, fy), fz);
+	asm("v_min_f32 %0, %0, %1" : "+v"(c) : "v"(tl));
+	return __float_as_uint(c - a) | __float_as_uint(c);
+}
+/* bit P of the miss word's sign (P < 8): v_lshrrev_b32 + v_and_b32, both dual-issued */
+template <int P> __device__ __forceinline__ uint32_t w8_miss_bit(uint32_t m)
+{
+	return (m >> (31 - P)) & (1u << P);
+}
+
 template <int OCT, int C>
 __device__ __forceinline__ bool w8_child(const uint32_t (&w)[16], f3 s, f3 b, float tl)
 {
@@ -143,10 +167,32 @@ __device__ __forceinline__ void w8_frame(const uint32_t (&w)[16], f3 invq, f3 oi
 		fmaf((float)(w[1] & 0xFFFFu), invq.z, -oi.z));
 }
 
+template <int OCT, int C>
+__device__ __forceinline__ uint32_t w8_child_miss(const uint32_t (&w)[16], f3 s, f3 b, float tl)
+{
+	constexpr int W = C >> 2, B = C & 3;
+	return w8_slab_miss<OCT>(fmaf(ubyte<B>(w[4 + W]), s.x, b.x), fmaf(ubyte<B>(w[6 + W]), s.x, b.x),
+				 fmaf(ubyte<B>(w[8 + W]), s.y, b.y), fmaf(ubyte<B>(w[10 + W]), s.y, b.y),
+				 fmaf(ubyte<B>(w[12 + W]), s.z, b.z), fmaf(ubyte<B>(w[14 + W]), s.z, b.z), tl);
+}
+#ifndef RTX_W8_SIGN
+#define RTX_W8_SIGN 1 /* k_shadow's octant-specialised box tests through miss words (w8_slab_miss) */
+#endif
 /* hit mask of an 8-wide node's children in visit order: bit p for slot p ^ K */
 template <int OCT, uint32_t K>
 __device__ __forceinline__ uint32_t w8_hits(const uint32_t (&w)[16], f3 s, f3 b, float tl)
 {
+	if constexpr (OCT < 8 && RTX_W8_SIGN) {
+		uint32_t m = w8_miss_bit<0 ^ K>(w8_child_miss<OCT, 0>(w, s, b, tl));
+		m |= w8_miss_bit<1 ^ K>(w8_child_miss<OCT, 1>(w, s, b, tl));
+		m |= w8_miss_bit<2 ^ K>(w8_child_miss<OCT, 2>(w, s, b, tl));
+		m |= w8_miss_bit<3 ^ K>(w8_child_miss<OCT, 3>(w, s, b, tl));
+		m |= w8_miss_bit<4 ^ K>(w8_child_miss<OCT, 4>(w, s, b, tl));
+		m |= w8_miss_bit<5 ^ K>(w8_child_miss<OCT, 5>(w, s, b, tl));
+		m |= w8_miss_bit<6 ^ K>(w8_child_miss<OCT, 6>(w, s, b, tl));
+		m |= w8_miss_bit<7 ^ K>(w8_child_miss<OCT, 7>(w, s, b, tl));
+		return m ^ 0xFFu;
+	}
 	uint32_t hm = 0;
 	hm |= w8_child<OCT, 0>(w, s, b, tl) ? 1u << (0 ^ K) : 0u;
 	hm |= w8_child<OCT, 1>(w, s, b, tl) ? 1u << (1 ^ K) : 0u;
@@ -168,6 +214,15 @@ __device__ __forceinline__ uint32_t w8_hit_s(const uint32_t (&q)[24], uint32_t w
 {
 	if (RTX_W8_SKIP && !((w3 >> C) & 1u))
 		return 0u;
+	if constexpr (OCT < 8 && RTX_W8_SIGN) { /* the divergent path's miss-word form: the same bits */
+		auto h = [&](int k) -> float {
+			const uint32_t v = q[4 * k + (C >> 1)];
+			return (float)__builtin_bit_cast(_Float16, (uint16_t)((C & 1) ? (v >> 16) : (v & 0xFFFFu)));
+		};
+		const uint32_t m = w8_slab_miss<OCT>(fmaf(h(0), s.x, b.x), fmaf(h(1), s.x, b.x), fmaf(h(2), s.y, b.y),
+						     fmaf(h(3), s.y, b.y), fmaf(h(4), s.z, b.z), fmaf(h(5), s.z, b.z), tl);
+		return w8_miss_bit<C ^ K>(m) ^ (1u << (C ^ K));
+	}
 	return w8_child_s<OCT, C>(q, s, b, tl) ? 1u << (C ^ K) : 0u;
 }
 template <int OCT, uint32_t K>

@@ -24,6 +24,7 @@ for s in $STEPS; do
   case $s in
     smoke) run smoke 240 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) run tests 1500 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
+    ptests) run ptests 900 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     testsall) run testsall 1500 python3 -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) run bench 900 python3 bench.py --verbose ;;
     benchq) run benchq 600 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --verbose ;;
@@ -60,10 +61,16 @@ for s in $STEPS; do
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-count --no-post ${PMCARGS:-} ;;
     pmcf) run pmcf 900 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post ${PMCARGS:-} ;;
     pmcw) run pmcw 900 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post ${PMCARGS:-} ;;
-    pmcv) run pmcv 900 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$OUT/pmc_valu" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post ${PMCARGS:-} ;;
-    pmcvars) for v in ${VARS:-$(ls c-raytracer_amd/lib/var)}; do RTX_LIBRTX=$PWD/c-raytracer_amd/lib/var/$v/librtx.so run pmcv_$v 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$OUT/pmcv_$v" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post; done ;;
+    pmcv) run pmcv 900 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU2 SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$OUT/pmc_valu" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post ${PMCARGS:-} ;;
+    pmcvars) for v in ${VARS:-$(ls c-raytracer_amd/lib/var)}; do RTX_LIBRTX=$PWD/c-raytracer_amd/lib/var/$v/librtx.so run pmcv_$v 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU2 SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$OUT/pmcv_$v" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post; done ;;
     envsweep) for kv in ${SWEEP}; do env $kv timeout -k 10 300 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-count --no-post > "$OUT/env_$kv.log" 2>&1; rc=$?; echo "$kv rc=$rc $(grep -o '"shadow_ms": [0-9.]*' "$OUT/env_$kv.log")" | tee -a "$OUT/steps.log"; if [ $rc -ge 124 ] || [ $rc -gt 128 ]; then exit $rc; fi; done ;;
     pmcivars) for v in ${VARS:-$(ls c-raytracer_amd/lib/var)}; do RTX_LIBRTX=$PWD/c-raytracer_amd/lib/var/$v/librtx.so run pmci_$v 600 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS -d "$OUT/pmci_$v" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post; done ;;
+    pmcvalu) run pmcvalu 600 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU SQ_BUSY_CU_CYCLES SQ_INSTS_VALU_CVT SQ_INSTS_VALU_FMA_F32 SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -d "$OUT/pmc_valu2" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post ${PMCARGS:-} ;;
+    pmcrates) run pmcrates 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU SQ_BUSY_CU_CYCLES SQ_INSTS_VALU_CVT SQ_INSTS_VALU_FMA_F32 SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -d "$OUT/pmc_rates" -o run --output-format csv -- ./tools/dev/valu_rates ;;
+    pmcmem) B="python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post ${PMCARGS:-}"
+      run pmcm1 600 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE -d "$OUT/pmc_m1" -o run --output-format csv -- $B &&
+      run pmcm2 600 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCR_TCP_STALL_CYCLES_sum TCP_UTCL1_STALL_MULTI_MISS_sum TD_TD_BUSY_sum TD_TC_STALL_sum TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TD_CYCLES_sum GRBM_GUI_ACTIVE -d "$OUT/pmc_m2" -o run --output-format csv -- $B &&
+      run pmcm3 600 rocprofv3 --pmc TD_LOAD_WAVEFRONT_sum TD_SPI_STALL_sum TA_FLAT_READ_WAVEFRONTS_sum TA_DATA_STALLED_BY_TC_CYCLES_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum TCP_TD_TCP_STALL_CYCLES_sum TCP_READ_TAGCONFLICT_STALL_CYCLES_sum TCP_TCC_RW_READ_REQ_sum GRBM_GUI_ACTIVE -d "$OUT/pmc_m3" -o run --output-format csv -- $B ;;
     pmcta) run pmcta 600 rocprofv3 --pmc TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum TCP_READ_TAGCONFLICT_STALL_CYCLES_sum GRBM_GUI_ACTIVE GRBM_COUNT -d "$OUT/pmc_ta" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post ${PMCARGS:-} ;;
     varcount) for v in ${VARS:-$(ls c-raytracer_amd/lib/var)}; do RTX_LIBRTX=$PWD/c-raytracer_amd/lib/var/$v/librtx.so run varcount_$v 600 python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-post --verbose; done ;;
     s6sweep) for kv in ${SWEEP}; do env $kv timeout -k 10 300 python3 bench.py --scene scene6 --width 3840 --height 2160 --spp 128 --steps 1 --warmup 1 --no-cpu-baseline --no-count --no-post > "$OUT/s6_$kv.log" 2>&1; rc=$?; echo "$kv rc=$rc $(grep -o '"shadow_ms": [0-9.]*' "$OUT/s6_$kv.log")" | tee -a "$OUT/steps.log"; if [ $rc -ge 124 ] || [ $rc -gt 128 ]; then exit $rc; fi; done ;;

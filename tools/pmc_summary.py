@@ -75,6 +75,8 @@ def main():
                     "Infinity-Cache hits included)"}
     for k, v in sq.items():
         e[k.lower()] = v
+    if "SQ_ACTIVE_INST_VALU2" in sf:  # dual-issue quad-cycles (bench.py roofline issue_slots)
+        e["sq_active_inst_valu2_frame"] = sf["SQ_ACTIVE_INST_VALU2"]
     if tdir:
         ta, nt = per_launch(tdir, kern)
         cyc = ta["GRBM_GUI_ACTIVE"] / 8.0  # summed over the 8 XCDs
