@@ -501,13 +501,25 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RTX_BENCH_REHEARSE=gloo: the torchrun ranks' whole path (tile shards, gather to rank 0, the
+    # max-over-ranks clock, the JSON line) on however many GPUs the box has, ranks sharing them,
+    # over gloo with host staging; a rehearsal of the code, never a scaling number (the driver's
+    # launch uses RCCL, one GPU per rank)
+    rehearse = world > 1 and os.environ.get("RTX_BENCH_REHEARSE") == "gloo"
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            local = local % torch.cuda.device_count()
+            torch.cuda.set_device(local)
+            torch.distributed.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # small all-reduces (the clock, the ray counts): gloo reduces host tensors
+    red_dev = torch.device("cpu") if rehearse else dev
 
     def log(msg):
         if a.verbose or rank == 0:
@@ -542,7 +554,7 @@ def main():
     npx = a.width * a.height
     d_rgb = torch.zeros((npx, 3), dtype=torch.float32, device=dev)
     d_z = torch.zeros((npx,), dtype=torch.float32, device=dev)
-    gat = Gatherer(a.width, a.height, rank, world, dev) if world > 1 else None
+    gat = Gatherer(a.width, a.height, rank, world, dev, host_staging=rehearse) if world > 1 else None
     stream = torch.cuda.current_stream(dev)
     # the render window runs up to the framebuffer on the host (rank 0, pinned)
     h_rgb = torch.empty((npx, 3), dtype=torch.float32, pin_memory=True) if rank == 0 else None
@@ -588,10 +600,10 @@ def main():
              "shade_points": int(s.shade_points), "chunks": int(s.chunks)}
 
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
-        rr = torch.tensor([rays, closest], dtype=torch.float64, device=dev)
+        rr = torch.tensor([rays, closest], dtype=torch.float64, device=red_dev)
         torch.distributed.all_reduce(rr)
         rays, closest = int(rr[0].item()), int(rr[1].item())
 
@@ -688,7 +700,8 @@ def main():
                "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": data_label(a),
                "config": {"workload": workload(a),
                           "scene": os.path.basename(path), "width": a.width, "height": a.height, "spp": a.spp,
-                          "objects": int(scene.num_objects), "rays_per_frame_rank0": stats_closest + stats_shadow,
+                          "objects": int(scene.num_objects), "rays_per_frame": rays // max(1, a.steps),
+                          "rays_per_frame_rank0": stats_closest + stats_shadow,
                           "closest_rays_rank0": stats_closest, "shadow_rays_rank0": stats_shadow,
                           "parallelism": f"tiles{world}", "launch": "torchrun" if world > 1 else "single",
                           "kernel_ms_rank0": round(kernel_ms, 3), "kernels_rank0": split,
@@ -703,6 +716,11 @@ def main():
                "roofline": roofline, "cpu_baseline": cpu}
         if gat is not None:
             out["config"]["gather_message_bytes_per_rank"] = gat.message_bytes
+        if rehearse:
+            out["n_gpus"] = min(world, torch.cuda.device_count())
+            out["ranks"] = world
+            out["rehearsal"] = ("RTX_BENCH_REHEARSE=gloo: torchrun ranks sharing the box's GPUs, gathered over gloo "
+                                "through host memory; the code path of the RCCL launch, not a scaling number")
         if strat:
             out["rng_strat_frame"] = strat
         if cpu:

@@ -40,9 +40,12 @@ def tile_pixel_index(width, height, tiles):
 class Gatherer:
     """Packs / gathers (to rank 0) / unpacks one rank's tiles.  Works on any device torch supports."""
 
-    def __init__(self, width, height, rank, world, device):
+    def __init__(self, width, height, rank, world, device, host_staging=False):
+        """host_staging: the process group's backend reduces host tensors only (gloo with ranks
+        on GPUs, bench.py's RTX_BENCH_REHEARSE): the packed tiles are gathered through host memory"""
         self.w, self.h, self.rank, self.world = width, height, rank, world
         self.device = device
+        self.host_staging = host_staging
         counts = [len(rank_tiles(width, height, r, world)) for r in range(world)]
         self.max_tiles = max(counts) if counts else 0
         idx = np.full((self.max_tiles, 64), -1, np.int64)
@@ -77,6 +80,13 @@ class Gatherer:
         packed = self.pack(rgb_flat, z_flat)
         if self.world == 1:
             self.gathered.copy_(packed)
+        elif self.host_staging:
+            h = packed.cpu()
+            parts = [torch.empty_like(h) for _ in range(self.world)] if self.rank == 0 else None
+            torch.distributed.gather(h, parts, dst=0, group=group)
+            if self.rank != 0:
+                return None
+            self.gathered.copy_(torch.cat(parts))
         else:
             torch.distributed.gather(packed, self.parts if self.rank == 0 else None, dst=0, group=group)
             if self.rank != 0:

@@ -19,7 +19,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, host_staging=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import sys
@@ -33,7 +33,7 @@ def _worker(rank, world, port, out_dir):
     scene, frame, params, _ = C.load_config("s3_amb")
     params.tile_offset, params.tile_stride = rank, world
     rgb, z, counts = oracle.render(scene, frame, params, threads=1)
-    g = Gatherer(frame.width, frame.height, rank, world, torch.device("cpu"))
+    g = Gatherer(frame.width, frame.height, rank, world, torch.device("cpu"), host_staging=host_staging)
     out = g.gather(torch.from_numpy(rgb.reshape(-1, 3)), torch.from_numpy(z.reshape(-1)))
     assert (out is None) == (rank != 0)  # gathered to rank 0 only
     c = torch.tensor(counts, dtype=torch.int64)
@@ -44,9 +44,10 @@ def _worker(rank, world, port, out_dir):
     torch.distributed.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_tile_gather_bit_exact(tmp_path, world):
-    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+@pytest.mark.parametrize("world,host_staging", [(2, False), (3, False), (2, True)])
+def test_gloo_tile_gather_bit_exact(tmp_path, world, host_staging):
+    """host_staging: the gather through host tensors (bench.py RTX_BENCH_REHEARSE=gloo)"""
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), host_staging), nprocs=world, join=True,
                        start_method="spawn")
     import conftest as C
     from rtxpy import oracle

@@ -75,6 +75,22 @@
 #define OP_k_maxu(x) asm volatile("v_max_u32_e32 %0, %1, %0" : "+v"(x) : "v"(a));
 #define OP_k_minmix(x) asm volatile("v_min_f32_e32 %0, %1, %0\n v_add_f32_e32 v2, v3, v2" : "+v"(x) : "v"(a) : "v2", "v3");
 
+#define OP_k_mullo(x) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(x) : "v"(a));
+#define OP_k_mulhi(x) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(x) : "v"(a));
+#define OP_k_mad64(x) asm volatile("v_mad_u64_u32 v[0:1], s[0:1], %0, %1, v[2:3]" : : "v"(x), "v"(a) : "v0", "v1", "s0", "s1");
+#define OP_k_alignbit(x) asm volatile("v_alignbit_b32 %0, %0, %0, 13" : "+v"(x));
+#define OP_k_add3(x) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(x) : "v"(a), "v"(b));
+#define OP_k_xad(x) asm volatile("v_xad_u32 %0, %0, %1, %2" : "+v"(x) : "v"(a), "v"(b));
+#define OP_k_sqrt(x) asm volatile("v_sqrt_f32_e32 %0, %0" : "+v"(x));
+#define OP_k_sin(x) asm volatile("v_sin_f32_e32 %0, %0" : "+v"(x));
+#define OP_k_divfmas(x) asm volatile("v_div_fmas_f32 %0, %0, %1, %2" : "+v"(x) : "v"(a), "v"(b) : "vcc");
+#define OP_k_rndne(x) asm volatile("v_rndne_f32_e32 %0, %0" : "+v"(x));
+#define OP_k_mbcnt(x) asm volatile("v_mbcnt_lo_u32_b32 %0, -1, %0" : "+v"(x));
+#define OP_k_movsgpr(x) asm volatile("v_mov_b32_e32 %0, %1" : "=v"(x) : "s"(sel));
+#define OP_k_mul64(x) asm volatile("v_lshrrev_b64 v[0:1], 7, v[0:1]" ::: "v0", "v1");
+
+#define LIST3(X) X(k_mullo) X(k_mulhi) X(k_mad64) X(k_alignbit) X(k_add3) X(k_xad) X(k_sqrt) X(k_sin) X(k_divfmas) X(k_rndne) X(k_mbcnt) X(k_movsgpr) X(k_mul64)
+
 #define LIST2(X) X(k_cmp32) X(k_cnd32) X(k_or) X(k_xor) X(k_lshl) X(k_max) X(k_subu) X(k_andlit) X(k_addsgpr) \
 	X(k_mullit) X(k_orsdwa) X(k_cvtsdwa) X(k_bfi) X(k_lshlor) X(k_fmaak) X(k_mulu24) X(k_cvtpkbf) X(k_maxu) X(k_minmix)
 
@@ -87,6 +103,7 @@
 #define DEF(N) KERNEL(N, 0)
 LIST(DEF)
 LIST2(DEF)
+LIST3(DEF)
 
 typedef void (*kfn)(float *, float, float, uint32_t);
 static void run(const char *name, kfn f, float *out, int blocks, double clk_ghz, int cus)
@@ -120,6 +137,7 @@ int main()
 #define RUN(N) run(#N, N, out, blocks, 2.4, p.multiProcessorCount);
 	LIST(RUN)
 	LIST2(RUN)
+	LIST3(RUN)
 	hipFree(out);
 	return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
 }
