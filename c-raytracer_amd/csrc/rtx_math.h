@@ -148,12 +148,14 @@ __device__ __forceinline__ f3 safe_inv(f3 d)
 		   fabsf(d.z) > 1e-30f ? 1.f / d.z : copysignf(1e30f, d.z));
 }
 
-/* the same with v_rcp_f32 (1 ulp) for the shadow walk's culling-only box tests */
+/* the same with v_rcp_f32 (1 ulp) for the walks' culling-only box tests: 1/d clamped to
+ * [-1e30, 1e30] by one v_med3_f32 (1/(+-0) = +-inf lands on +-1e30, the sign of a zero kept as
+ * copysign keeps it) instead of a compare, a select and a copysign per component */
 __device__ __forceinline__ f3 safe_inv_fast(f3 d)
 {
-	return mk3(fabsf(d.x) > 1e-30f ? __builtin_amdgcn_rcpf(d.x) : copysignf(1e30f, d.x),
-		   fabsf(d.y) > 1e-30f ? __builtin_amdgcn_rcpf(d.y) : copysignf(1e30f, d.y),
-		   fabsf(d.z) > 1e-30f ? __builtin_amdgcn_rcpf(d.z) : copysignf(1e30f, d.z));
+	return mk3(__builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(d.x), -1e30f, 1e30f),
+		   __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(d.y), -1e30f, 1e30f),
+		   __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(d.z), -1e30f, 1e30f));
 }
 
 /* a point / direction in the trees' frame (rtx_device.h DTreeFrame): x' = R (x - c), d' = R d.

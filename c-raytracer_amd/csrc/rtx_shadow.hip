@@ -42,6 +42,9 @@
 #ifndef RTX_DEBUG_NOLEAF
 #define RTX_DEBUG_NOLEAF 0 /* measurement only: the walk tests no leaf (wrong images; the cost of the leaf tests) */
 #endif
+#ifndef RTX_SH_FASTSQRT
+#define RTX_SH_FASTSQRT 1 /* the shadow ray's length from v_sqrt_f32 (1 ulp) instead of the correctly rounded sequence */
+#endif
 #ifndef RTX_SH_OCT
 #define RTX_SH_OCT 1 /* walks specialised on a wave-uniform direction octant */
 #endif
@@ -778,8 +781,8 @@ __device__ __forceinline__ void emitter_sample(const KShadow &ks, const DEmitter
 		u1 = ((float)j + u1) / (float)E.num_lights;
 	const f3 lp = light_point_sh(E, p, u1, u2);
 	const f3 dv = sub3(lp, p);
-	ldist = mag3(dv);
 	dsq = magsqr3(dv);
+	ldist = RTX_SH_FASTSQRT ? __builtin_amdgcn_sqrtf(dsq) : sqrtf(dsq); /* mag3(dv) */
 	ldir = mul3s(dv, sh_rcp(ldist));
 	li = ld3(E.li);
 }
