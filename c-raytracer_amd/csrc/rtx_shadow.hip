@@ -550,6 +550,25 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 /* is_light_blocked (render.c:126-134): planes first (unbound_objects_is_light_blocked,
  * object.c:183-197), then the BVH walk, specialised on the direction octant when every live
  * lane shares it.  Returns the lane's blocked flag; li carries the transmittance product. */
+/* hit_plane(...) && t < dist (object.c:473-488 and is_light_blocked's plane test) with the
+ * quotient t = num / a as num * v_rcp_f32(a) (within 2 ulp of the IEEE quotient, like the
+ * light points of RTX_SH_FASTTRIG): the decisions differ from the IEEE test only for a t within
+ * 2 ulp of the plane's epsilon or of the light sample's distance */
+#ifndef RTX_SH_PLANE_RCP
+#define RTX_SH_PLANE_RCP 1
+#endif
+__device__ __forceinline__ bool plane_blocks(f3 n, float dd, f3 o, f3 d, float eps, float dist)
+{
+	float t;
+	if (!RTX_SH_PLANE_RCP)
+		return hit_plane(n, dd, o, d, eps, t) && t < dist;
+	const float a = dot3(n, d);
+	if (!(fabsf(a) >= eps)) /* hit_plane's fabsf(a) < eps (a NaN misses there too) */
+		return false;
+	t = (dd - dot3(n, o)) * __builtin_amdgcn_rcpf(a);
+	return t > eps && t < dist;
+}
+
 template <bool COUNT, int WALK>
 __device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restrict__ recs, const DMaterial *__restrict__ mats,
 					     const DPlane *__restrict__ planes, uint32_t num_planes, const DEmitter *__restrict__ lin,
@@ -559,8 +578,7 @@ __device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restri
 	float tl = act ? dist : -1.f;
 	for (uint32_t i = 0; i < num_planes; i++) { /* plane records are wave-uniform: s_load */
 		const auto *pl = cptr(planes) + i;
-		float t;
-		const bool h = hit_plane(mk3(pl->n[0], pl->n[1], pl->n[2]), pl->d, o, d, pl->eps, t) && t < dist && tl >= 0.f;
+		const bool h = plane_blocks(mk3(pl->n[0], pl->n[1], pl->n[2]), pl->d, o, d, pl->eps, dist) && tl >= 0.f;
 		if (pl->transparent) {
 			if (h)
 				li = mul3v(li, mk3(pl->kt[0], pl->kt[1], pl->kt[2]));
