@@ -159,17 +159,18 @@ typedef struct __attribute__((aligned(64))) DW8 {
 } DW8;
 
 /* The scalar-path copy of an 8-wide node (DScene.w8s, indexed like the entries; only node
- * entries are filled): when every walking lane of a wave is at one node, k_shadow reads it with
- * two s_load_dwordx16 and takes the 8-bit plane offsets as ready half floats (SGPR operands of
- * v_fma_mix_f32) instead of converting 48 bytes per lane.  The halves are the bytes' exact
+ * entries are filled): when every walking lane of a wave is at one node, the walks read it
+ * through the scalar cache (the header with one s_load_dwordx8, each child's planes with one
+ * more) and take the 8-bit plane offsets as ready floats, an axis's two planes as one SGPR pair
+ * of a v_pk_fma_f32, instead of converting 48 bytes per lane.  The floats are the bytes' exact
  * values, so both paths compute bit-identical box tests.
- *   w = the node's w0..w3;  org = its origin as floats;  q[k][c] = byte c of plane k (lo_x, hi_x,
- *   lo_y, hi_y, lo_z, hi_z) as an IEEE half */
-typedef struct __attribute__((aligned(128))) DW8S {
+ *   w = the node's w0..w3;  org = its origin as floats;  q[c] = child c's plane offsets lo_x,
+ *   hi_x, lo_y, hi_y, lo_z, hi_z (bytes c & 3 of w4 + (c >> 2) ... as floats), then two zeros */
+typedef struct __attribute__((aligned(32))) DW8S {
 	uint32_t w[4];
 	float org[3];
 	uint32_t pad;
-	uint16_t q[6][8];
+	float q[8][8];
 } DW8S;
 
 typedef struct DPlane {

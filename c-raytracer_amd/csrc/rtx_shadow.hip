@@ -370,12 +370,12 @@ struct W8Ctr {
 };
 
 /* One iteration of the 8-wide any-hit walk for the wave: a round of deferred transparent-leaf
- * tests, or one node step with its opaque leaf tests (see shadow_walk8).  walking / holding: the
- * lanes with node work / deferred tests; at least one lane has one or the other.  o / d: the
+ * tests, or one node step with its opaque leaf tests (see shadow_walk8).  wk / hd: this lane has
+ * node work / deferred tests; walking / holding: their ballots (at least one lane has one).  o / d: the
  * world ray; invq / oi: its inverse direction and origin term in the tree's 16-bit frame. */
 template <bool COUNT, int OCT>
 __device__ __forceinline__ void w8_iter(const QBvh &Q, f3 o, f3 d, f3 invq, f3 oi, float &tl, f3 &li, W8Walk &w, W8Ctr &c,
-					u64 walking, u64 holding)
+					bool wk, bool hd, u64 walking, u64 holding)
 {
 	constexpr uint32_t K = w8_sorder<OCT>();
 	lds_u32 *stk = Q.stk, *tq = Q.tq;
@@ -383,7 +383,7 @@ __device__ __forceinline__ void w8_iter(const QBvh &Q, f3 o, f3 d, f3 invq, f3 o
 		/* a round of deferred transparent-leaf tests */
 		if (COUNT)
 			c.nlr++;
-		if (w.tgrp) {
+		if (hd) {
 			const char *pr = (const char *)(Q.w8 + (w.tgrp >> 8) + (__builtin_ctz(w.tgrp) ^ K));
 			w.tgrp &= w.tgrp - 1;
 			if (!(w.tgrp & 0xFFu))
@@ -393,7 +393,7 @@ __device__ __forceinline__ void w8_iter(const QBvh &Q, f3 o, f3 d, f3 invq, f3 o
 		return;
 	}
 	uint32_t lm = 0, base = 0; /* this step's opaque leaf hits (visit order) and their block */
-	if (w.node != RTX_NONE) {
+	if (wk) {
 		const uint32_t un = uni(w.node);
 		W8Visit v;
 		if (!ballot(w.node != un)) {
@@ -538,11 +538,13 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 	W8Walk w = { tl >= 0.f ? 0u : RTX_NONE, 0u, 0u, 0u, 0u };
 	W8Ctr c = { 0u, 0u, 0u, 0u, 0u, 0u };
 	for (;;) {
-		const u64 walking = ballot(w.node != RTX_NONE);
-		const u64 holding = ballot(w.tgrp != 0);
+		/* the lane's two conditions once, as lane masks the branches below reuse */
+		const bool wk = w.node != RTX_NONE, hd = w.tgrp != 0;
+		const u64 walking = ballot(wk);
+		const u64 holding = ballot(hd);
 		if (!(walking | holding))
 			break;
-		w8_iter<COUNT, OCT>(Q, o, d, invq, oi, tl, li, w, c, walking, holding);
+		w8_iter<COUNT, OCT>(Q, o, d, invq, oi, tl, li, w, c, wk, hd, walking, holding);
 	}
 	w8_count<COUNT>(c, sc, 1u);
 }

@@ -171,6 +171,9 @@ __device__ void trace_closest_bvh2(const DScene &S, uint32_t *stk, bool act, f3 
  * groups on the lane's stack (LDS, deeper entries in HBM), and every node's boxes are tested
  * against the current closest t.  The emitters the tree leaves out (DScene.w8noemit) are
  * tested before the walk.  Strict < everywhere: the first hit found at the least t wins. */
+#ifndef RTX_TRACE_SCALAR
+#define RTX_TRACE_SCALAR 1 /* a step where every lane is at one node reads its scalar-path copy (rtx_device.h DW8S) */
+#endif
 #ifndef RTX_TRACE_NEAR
 #define RTX_TRACE_NEAR 1 /* closest hits: visit the nearest hit inner child first (scene6 k_trace 605 -> 417 ms) */
 #endif
@@ -213,7 +216,7 @@ __device__ __forceinline__ void closest_walk8(const DScene &S, lds_u32 *stk, uin
 		uint32_t nearp = 8;
 		float tin = INFINITY;
 		const uint32_t un = uni(node);
-		if (!ballot(node != un)) {
+		if (RTX_TRACE_SCALAR && !ballot(node != un)) {
 			if (T) {
 				const W8VisitT r = w8_visit_st<OCT, K>(S.w8s + (size_t)un, invq, oi, tbest - t0);
 				v = r.v;

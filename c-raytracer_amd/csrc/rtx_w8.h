@@ -144,18 +144,26 @@ __device__ __forceinline__ bool w8_child(const uint32_t (&w)[16], f3 s, f3 b, fl
 			    fmaf(ubyte<B>(w[8 + W]), s.y, b.y), fmaf(ubyte<B>(w[10 + W]), s.y, b.y),
 			    fmaf(ubyte<B>(w[12 + W]), s.z, b.z), fmaf(ubyte<B>(w[14 + W]), s.z, b.z), tl);
 }
-/* the same child test on the scalar-path copy (rtx_device.h DW8S): the plane offsets are ready
- * floats, the same values the conversions above produce, so the results are bit-identical */
-template <int OCT, int C>
-__device__ __forceinline__ bool w8_child_s(const uint32_t (&q)[24], f3 s, f3 b, float tl)
+/* the scalar-path copy (rtx_device.h DW8S): child C's plane offsets, ready floats (the same
+ * values the conversions above produce, so the results are bit-identical), one s_load_dwordx8 */
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float f8v __attribute__((ext_vector_type(8)));
+template <int C> __device__ __forceinline__ f8v w8s_planes(const DW8S *n)
 {
-	/* plane k's offset of child C: the half in word 4k + C/2, half C & 1 (v_fma_mix_f32 op_sel) */
-	auto h = [&](int k) -> float {
-		const uint32_t v = q[4 * k + (C >> 1)];
-		return (float)__builtin_bit_cast(_Float16, (uint16_t)((C & 1) ? (v >> 16) : (v & 0xFFFFu)));
-	};
-	return w8_slab<OCT>(fmaf(h(0), s.x, b.x), fmaf(h(1), s.x, b.x), fmaf(h(2), s.y, b.y), fmaf(h(3), s.y, b.y),
-			    fmaf(h(4), s.z, b.z), fmaf(h(5), s.z, b.z), tl);
+	return *(const __attribute__((address_space(4))) f8v *)&n->q[C][0];
+}
+/* one axis's two plane distances q * s + b: the SGPR pair in one v_pk_fma_f32 */
+__device__ __forceinline__ f2v w8s_axis(float lo, float hi, float s, float b)
+{
+	const f2v q = { lo, hi }, sv = { s, s }, bv = { b, b };
+	return __builtin_elementwise_fma(q, sv, bv);
+}
+template <int OCT, int C>
+__device__ __forceinline__ bool w8_child_s(const DW8S *n, f3 s, f3 b, float tl)
+{
+	const f8v p = w8s_planes<C>(n);
+	const f2v tx = w8s_axis(p[0], p[1], s.x, b.x), ty = w8s_axis(p[2], p[3], s.y, b.y), tz = w8s_axis(p[4], p[5], s.z, b.z);
+	return w8_slab<OCT>(tx.x, tx.y, ty.x, ty.y, tz.x, tz.y, tl);
 }
 
 /* the node frame of an 8-wide node: per-axis scale s = invq * 2^e and offset b = o * invq - oi */
@@ -210,23 +218,20 @@ __device__ __forceinline__ uint32_t w8_hits(const uint32_t (&w)[16], f3 s, f3 b,
 #define RTX_W8_SKIP 1 /* scalar path: branch over the empty slots (the slot mask is wave-uniform): scene5 k_shadow 557 -> 548 ms, scene6 2739 -> 2721 ms */
 #endif
 template <int OCT, uint32_t K, int C>
-__device__ __forceinline__ uint32_t w8_hit_s(const uint32_t (&q)[24], uint32_t w3, f3 s, f3 b, float tl)
+__device__ __forceinline__ uint32_t w8_hit_s(const DW8S *n, uint32_t w3, f3 s, f3 b, float tl)
 {
 	if (RTX_W8_SKIP && !((w3 >> C) & 1u))
 		return 0u;
 	if constexpr (OCT < 8 && RTX_W8_SIGN) { /* the divergent path's miss-word form: the same bits */
-		auto h = [&](int k) -> float {
-			const uint32_t v = q[4 * k + (C >> 1)];
-			return (float)__builtin_bit_cast(_Float16, (uint16_t)((C & 1) ? (v >> 16) : (v & 0xFFFFu)));
-		};
-		const uint32_t m = w8_slab_miss<OCT>(fmaf(h(0), s.x, b.x), fmaf(h(1), s.x, b.x), fmaf(h(2), s.y, b.y),
-						     fmaf(h(3), s.y, b.y), fmaf(h(4), s.z, b.z), fmaf(h(5), s.z, b.z), tl);
+		const f8v p = w8s_planes<C>(n);
+		const f2v tx = w8s_axis(p[0], p[1], s.x, b.x), ty = w8s_axis(p[2], p[3], s.y, b.y), tz = w8s_axis(p[4], p[5], s.z, b.z);
+		const uint32_t m = w8_slab_miss<OCT>(tx.x, tx.y, ty.x, ty.y, tz.x, tz.y, tl);
 		return w8_miss_bit<C ^ K>(m) ^ (1u << (C ^ K));
 	}
-	return w8_child_s<OCT, C>(q, s, b, tl) ? 1u << (C ^ K) : 0u;
+	return w8_child_s<OCT, C>(n, s, b, tl) ? 1u << (C ^ K) : 0u;
 }
 template <int OCT, uint32_t K>
-__device__ __forceinline__ uint32_t w8_hits_s(const uint32_t (&q)[24], uint32_t w3, f3 s, f3 b, float tl)
+__device__ __forceinline__ uint32_t w8_hits_s(const DW8S *q, uint32_t w3, f3 s, f3 b, float tl)
 {
 	uint32_t hm = 0;
 	hm |= w8_hit_s<OCT, K, 0>(q, w3, s, b, tl);
@@ -273,23 +278,15 @@ __device__ __forceinline__ W8Visit w8_visit(const uint32_t (&w)[16], f3 invq, f3
 template <int OCT, uint32_t K>
 __device__ __forceinline__ W8Visit w8_visit_s(const DW8S *n, f3 invq, f3 oi, float tl)
 {
-	typedef uint32_t u16v __attribute__((ext_vector_type(16)));
-	const auto *U = (const __attribute__((address_space(4))) u16v *)n;
-	const u16v p0 = U[0], p1 = U[1];
-	uint32_t q[24];
-#pragma unroll
-	for (int k = 0; k < 8; k++)
-		q[k] = p0[8 + k];
-#pragma unroll
-	for (int k = 0; k < 16; k++)
-		q[8 + k] = p1[k];
+	typedef uint32_t u8v __attribute__((ext_vector_type(8)));
+	const u8v p0 = *(const __attribute__((address_space(4))) u8v *)n; /* w0..w3, org */
 	const uint32_t w1 = p0[1], w2 = p0[2], w3 = p0[3];
 	const float org0 = __uint_as_float(p0[4]), org1 = __uint_as_float(p0[5]), org2 = __uint_as_float(p0[6]);
 	const f3 s = mk3(ldexpf(invq.x, (int)((w1 >> 16) & 15u)), ldexpf(invq.y, (int)((w1 >> 20) & 15u)),
 			 ldexpf(invq.z, (int)((w1 >> 24) & 15u)));
 	const f3 b = mk3(fmaf(org0, invq.x, -oi.x), fmaf(org1, invq.y, -oi.y), fmaf(org2, invq.z, -oi.z));
 	W8Visit v;
-	v.hm = w8_hits_s<OCT, K>(q, w3, s, b, tl);
+	v.hm = w8_hits_s<OCT, K>(n, w3, s, b, tl);
 	v.base = w2 >> 8;
 	v.io = perm_xor<K>(w2 & 0xFFu);
 	v.to = perm_xor<K>((w3 >> 8) & 0xFFu);
@@ -312,23 +309,19 @@ __device__ __forceinline__ void w8_child_t(const uint32_t *w, f3 s, f3 b, float 
 {
 	if (SC && RTX_W8_SKIP && !(((io >> 8) >> C) & 1u)) /* an empty slot (wave-uniform on the scalar path) */
 		return;
-	float l[6];
-	if (SC) {
-#pragma unroll
-		for (int k = 0; k < 6; k++) {
-			const uint32_t x = w[4 * k + (C >> 1)];
-			l[k] = (float)__builtin_bit_cast(_Float16, (uint16_t)((C & 1) ? (x >> 16) : (x & 0xFFFFu)));
-		}
+	float t[6];
+	if (SC) { /* w: the scalar-path copy (DW8S) */
+		const f8v p = w8s_planes<C>((const DW8S *)w);
+		const f2v tx = w8s_axis(p[0], p[1], s.x, b.x), ty = w8s_axis(p[2], p[3], s.y, b.y), tz = w8s_axis(p[4], p[5], s.z, b.z);
+		t[0] = tx.x, t[1] = tx.y, t[2] = ty.x, t[3] = ty.y, t[4] = tz.x, t[5] = tz.y;
 	} else {
 		constexpr int W = C >> 2, B = C & 3;
-#pragma unroll
-		for (int k = 0; k < 6; k++)
-			l[k] = ubyte<B>(w[4 + 2 * k + W]);
+		t[0] = fmaf(ubyte<B>(w[4 + W]), s.x, b.x), t[1] = fmaf(ubyte<B>(w[6 + W]), s.x, b.x);
+		t[2] = fmaf(ubyte<B>(w[8 + W]), s.y, b.y), t[3] = fmaf(ubyte<B>(w[10 + W]), s.y, b.y);
+		t[4] = fmaf(ubyte<B>(w[12 + W]), s.z, b.z), t[5] = fmaf(ubyte<B>(w[14 + W]), s.z, b.z);
 	}
 	float tn;
-	const bool h = w8_slab_tn<OCT>(fmaf(l[0], s.x, b.x), fmaf(l[1], s.x, b.x), fmaf(l[2], s.y, b.y), fmaf(l[3], s.y, b.y),
-				       fmaf(l[4], s.z, b.z), fmaf(l[5], s.z, b.z), tl, tn) &&
-		       (OCT != 8 || ((io >> 8) >> C) & 1u);
+	const bool h = w8_slab_tn<OCT>(t[0], t[1], t[2], t[3], t[4], t[5], tl, tn) && (OCT != 8 || ((io >> 8) >> C) & 1u);
 	hm |= h ? 1u << (C ^ K) : 0u;
 	const bool in = h && ((io >> C) & 1u);
 	near = (in && tn < tin) ? (uint32_t)(C ^ K) : near;
@@ -368,23 +361,15 @@ __device__ __forceinline__ W8VisitT w8_visit_t(const uint32_t (&w)[16], f3 invq,
 template <int OCT, uint32_t K>
 __device__ __forceinline__ W8VisitT w8_visit_st(const DW8S *n, f3 invq, f3 oi, float tl)
 {
-	typedef uint32_t u16v __attribute__((ext_vector_type(16)));
-	const auto *U = (const __attribute__((address_space(4))) u16v *)n;
-	const u16v p0 = U[0], p1 = U[1];
-	uint32_t q[24];
-#pragma unroll
-	for (int k = 0; k < 8; k++)
-		q[k] = p0[8 + k];
-#pragma unroll
-	for (int k = 0; k < 16; k++)
-		q[8 + k] = p1[k];
+	typedef uint32_t u8v __attribute__((ext_vector_type(8)));
+	const u8v p0 = *(const __attribute__((address_space(4))) u8v *)n; /* w0..w3, org */
 	const uint32_t w1 = p0[1], w2 = p0[2], w3 = p0[3];
 	const f3 s = mk3(ldexpf(invq.x, (int)((w1 >> 16) & 15u)), ldexpf(invq.y, (int)((w1 >> 20) & 15u)),
 			 ldexpf(invq.z, (int)((w1 >> 24) & 15u)));
 	const f3 b = mk3(fmaf(__uint_as_float(p0[4]), invq.x, -oi.x), fmaf(__uint_as_float(p0[5]), invq.y, -oi.y),
 			 fmaf(__uint_as_float(p0[6]), invq.z, -oi.z));
 	W8VisitT r;
-	w8_hits_t<OCT, K, true>(q, s, b, tl, (w2 & 0xFFu) | ((w3 & 0xFFu) << 8), r);
+	w8_hits_t<OCT, K, true>((const uint32_t *)n, s, b, tl, (w2 & 0xFFu) | ((w3 & 0xFFu) << 8), r);
 	r.v.base = w2 >> 8;
 	r.v.io = perm_xor<K>(w2 & 0xFFu);
 	r.v.to = perm_xor<K>((w3 >> 8) & 0xFFu);

@@ -403,7 +403,7 @@ __global__ __launch_bounds__(W8D_T) void k_w8d_next(uint32_t m, uint32_t blk, co
 	}
 }
 
-/* the scalar-path copies of the inner entries (rtx_device.h DW8S; planes as exact halves) */
+/* the scalar-path copies of the inner entries (rtx_device.h DW8S; planes as exact floats) */
 __global__ __launch_bounds__(W8D_T) void k_w8d_scalar(uint32_t n, const DW8 *__restrict__ w8, const uint32_t *__restrict__ leafmap,
 						      DW8S *__restrict__ w8s)
 {
@@ -420,10 +420,8 @@ __global__ __launch_bounds__(W8D_T) void k_w8d_scalar(uint32_t n, const DW8 *__r
 		f.org[1] = (float)(nd.w[0] >> 16);
 		f.org[2] = (float)(nd.w[1] & 0xFFFFu);
 		for (int k = 0; k < 6; k++)
-			for (int ch = 0; ch < 8; ch++) {
-				const uint32_t q = (nd.w[4 + 2 * k + (ch >> 2)] >> (8 * (ch & 3))) & 0xFFu;
-				f.q[k][ch] = __builtin_bit_cast(uint16_t, (_Float16)(float)q); /* exact: q <= 255 */
-			}
+			for (int ch = 0; ch < 8; ch++)
+				f.q[ch][k] = (float)((nd.w[4 + 2 * k + (ch >> 2)] >> (8 * (ch & 3))) & 0xFFu);
 	}
 	w8s[i] = f;
 }
