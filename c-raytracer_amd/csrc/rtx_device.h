@@ -125,7 +125,7 @@ typedef struct DTreeFrame {
 
 /* 8-wide compressed BVH for the shadow walk (rtx_shadow.hip shadow_walk8), in the style of
  * Ylitie et al.'s compressed wide BVH: an array of 64-byte entries (one 64-byte half line, four
- * global_load_dwordx4 or one s_load_dwordx16).  A node entry:
+ * global_load_dwordx4; the scalar path reads the DW8S copy below).  A node entry:
  *   w0 = ox | oy << 16, w1 = oz | ex << 16 | ey << 20 | ez << 24
  *        the node's frame on the 16-bit grid of DQNode: origin o (grid units) and a per-axis step
  *        of 2^e grid units (e <= 9)

@@ -290,7 +290,7 @@ __device__ __forceinline__ void shadow_walk(const QBvh &Q, const char *__restric
 }
 
 /* is_light_blocked's BVH part (accel.c:360-387) over the 8-wide BVH (rtx_device.h DW8): one
- * 64-byte node per step (four 16-byte loads, or one s_load_dwordx16 when every live lane is at
+ * 64-byte node per step (four 16-byte loads, or its DW8S copy through scalar loads when every live lane is at
  * the node), eight box tests.  Hit children are taken in the octant's visit order (slot p ^ K):
  *  - opaque leaf slots are tested at once (an opaque hit ends the ray);
  *  - transparent leaf slots (tmask) can only multiply the transmittance, so their tests are
