@@ -101,3 +101,34 @@ def test_pmc_summary_sums_a_chunked_frame(tmp_path, monkeypatch):
     assert n == 2 and mean["SQ_INSTS_VALU"] == 1166.0
     assert m.per_frame(str(d), "k_shadow", 1)["SQ_INSTS_VALU"] == 2332.0
     assert m.per_frame(str(d), "k_shadow", 2)["SQ_INSTS_VALU"] == 1166.0
+
+
+def test_roofline_issue_slots(tmp_path, monkeypatch):
+    """bench.py's roofline: the VALU issue slots the kernel used (SQ_INSTS_VALU minus the
+    quad-cycles that issued two, SQ_ACTIVE_INST_VALU2) over the chip's in the kernel's time, from a
+    PMC summary whose source hash matches the kernel."""
+    import types
+    import bench
+    (tmp_path / "profiles").mkdir()
+    key = "scene5_1920x1080_n64_g1"
+    rec = {key: {"kernel_src_sha": bench.shadow_src_sha(), "sq_insts_valu": 4.0e11, "sq_insts_valu_frame": 4.0e11,
+                 "sq_active_inst_valu2": 1.0e11, "sq_active_inst_valu2_frame": 1.0e11,
+                 "hbm_bytes_per_launch": 1e11, "hbm_bytes_per_frame": 1e11}}
+    with open(tmp_path / "profiles" / "pmc_k_shadow.json", "w") as fh:
+        json.dump(rec, fh)
+    sha = bench.shadow_src_sha()
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    monkeypatch.setattr(bench, "shadow_src_sha", lambda: sha)
+    n = dict(shade_points=7e7, shadow_tri_tests=1.8e10, shadow_sphere_tests=0, shadow_global_box_tests=5e11,
+             shadow_box_tests=5.2e11, shadow_plane_tests=2.1e10, shadow_rays=2.1e10, shadow_wave_steps=1.6e9,
+             shadow_wave_walks=3.5e8, shadow_leaf_rounds=7.6e8, shadow_uniform_steps=6.4e8, closest_rays=1.35e8,
+             node_visits=6e9, shadow_node_visits=5e9, tri_tests=2e10, sphere_tests=0, wide_nodes=63578, wide_depth=8,
+             chunks=1)
+    c = types.SimpleNamespace(**n)
+    a = types.SimpleNamespace(scene="scene5", width=1920, height=1080, spp=64)
+    out = bench.shadow_roofline_of(c, 500.0, a, 1)
+    assert out["pmc"]["matches_this_kernel"]
+    s = out["issue_slots"]
+    avail = 0.5 * 2.4e9 / 4 * 1024
+    assert s["used_quad_cycles"] == int(3.0e11) and abs(s["frac"] - 3.0e11 / avail) < 1e-4
+    assert s["dual_issued_frac"] == 0.5
