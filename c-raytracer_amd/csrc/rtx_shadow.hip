@@ -302,6 +302,12 @@ __device__ __forceinline__ void shadow_walk(const QBvh &Q, const char *__restric
  *    register, the older groups in the lane's LDS stack (entries from Q.lstk on in HBM,
  *    Q.spill), at most one per level, so any depth walks.
  * tl < 0 on entry: inactive lane.  On an opaque hit tl becomes -1. */
+#ifndef RTX_SH_OWNINC
+#define RTX_SH_OWNINC 1 /* a slot's point found from the lane's previous one (off[] is nondecreasing) */
+#endif
+#ifndef RTX_SH_SLOTFOLD
+#define RTX_SH_SLOTFOLD 1 /* slot sums folded by lane 0 from LDS (k_shadow's several-points-per-packet path) */
+#endif
 #ifndef RTX_W8_TOP
 #define RTX_W8_TOP 1 /* divergent steps read the tree's top levels (DScene.w8top entries) from an LDS copy */
 #endif
@@ -992,13 +998,24 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 		} else {
 			/* several points share a packet: each point's samples fill consecutive slots of B
 			 * (power of two) lanes, B = slot_b; a point may straddle packets */
+			uint32_t kp = 0; /* this lane's point in the previous packet (its slots only move forward) */
 			for (uint32_t base = 0;;) {
 				reread_barrier();
 				const uint32_t tot = uni(off[WAVE]), slot_b = uni(ks.slot_b), slot_lg = uni(ks.slot_lg);
 				if (base >= tot)
 					break;
 				const uint32_t slot = base + (lane_id() >> slot_lg);
-				const uint32_t k = slot < tot ? owner_of(off, slot) : 0u;
+				uint32_t k = 0;
+				if (slot < tot) {
+					if (RTX_SH_OWNINC) { /* owner_of from the previous packet's owner: a step or two, not six */
+						k = kp;
+						while (off[k + 1] <= slot)
+							k++;
+						kp = k;
+					} else {
+						k = owner_of(off, slot);
+					}
+				}
 				const uint32_t idx = ((slot - off[k]) << slot_lg) + (lane_id() & (slot_b - 1));
 				const bool act = slot < tot && idx < nls[k];
 				const float4 *rec = unip(ks.sp) + (size_t)sid[k] * SPREC;
@@ -1007,7 +1024,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 				 * then the slot sums are added to their point's total one slot at a time in slot order, so a
 				 * point whose slots straddle packets gets the same sum whatever its neighbours (with one slot
 				 * per point this is the 64-lane butterfly over zeros and one slot it replaced, bit for bit) */
-				const uint32_t t2 = uni(off[WAVE]), sb = uni(ks.slot_b), spp = WAVE / sb;
+				const uint32_t t2 = uni(off[WAVE]), sb = uni(ks.slot_b), lg = uni(ks.slot_lg), spp = WAVE >> lg;
 				f3 v = act ? contribution : mk3(0.f, 0.f, 0.f);
 				if (sb > 16) {
 					v.x += lane_xor_f<16>(v.x);
@@ -1035,6 +1052,42 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 					v.z += lane_xor_f<1>(v.z);
 				}
 				const uint32_t ns = min(t2 - base, spp);
+				if (WALK == WALK_W8 && RTX_SH_SLOTFOLD) {
+					/* the same fold with the slot sums handed over in LDS instead of v_readlane (four
+					 * single-issue reads and three adds on SGPR operands per slot): each slot's first
+					 * lane stores (sum, point) in the wave's lane-stack area, empty between walks, and
+					 * lane 0 folds them in slot order (an LDS read, a compare and three adds per slot) */
+					float4 *sl = (float4 *)&wstk[wv][0][0];
+					if (!(lane_id() & (sb - 1)) && (lane_id() >> lg) < ns)
+						sl[lane_id() >> lg] = make_float4(v.x, v.y, v.z, __uint_as_float(k));
+					lds_sync();
+					if (lane_id() == 0) {
+						uint32_t kc = __float_as_uint(sl[0].w);
+						float rx = Ls[0][kc], ry = Ls[1][kc], rz = Ls[2][kc];
+						for (uint32_t j = 0; j < ns; j++) {
+							const float4 q = sl[j];
+							const uint32_t kj = __float_as_uint(q.w);
+							if (kj != kc) {
+								Ls[0][kc] = rx;
+								Ls[1][kc] = ry;
+								Ls[2][kc] = rz;
+								kc = kj;
+								rx = Ls[0][kc];
+								ry = Ls[1][kc];
+								rz = Ls[2][kc];
+							}
+							rx += q.x;
+							ry += q.y;
+							rz += q.z;
+						}
+						Ls[0][kc] = rx;
+						Ls[1][kc] = ry;
+						Ls[2][kc] = rz;
+					}
+					lds_sync();
+					base += spp;
+					continue;
+				}
 				uint32_t kc = readlane(k, 0);
 				float rx = Ls[0][kc], ry = Ls[1][kc], rz = Ls[2][kc];
 				for (uint32_t j = 0; j < ns; j++) {
