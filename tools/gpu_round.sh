@@ -64,7 +64,7 @@ for s in $STEPS; do
     pmcf) run pmcf 900 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post ${PMCARGS:-} ;;
     pmcw) run pmcw 900 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post ${PMCARGS:-} ;;
     pmcv) run pmcv 900 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU2 SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$OUT/pmc_valu" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post ${PMCARGS:-} ;;
-    pmcvars) for v in ${VARS:-$(ls c-raytracer_amd/lib/var)}; do RTX_LIBRTX=$PWD/c-raytracer_amd/lib/var/$v/librtx.so run pmcv_$v 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU2 SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$OUT/pmcv_$v" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post; done ;;
+    pmcvars) for v in ${VARS:-$(ls c-raytracer_amd/lib/var)}; do RTX_LIBRTX=$PWD/c-raytracer_amd/lib/var/$v/librtx.so run pmcv_$v 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU2 SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$OUT/pmcv_$v" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post ${PMCARGS:-}; done ;;
     envsweep) for kv in ${SWEEP}; do env $kv timeout -k 10 300 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-count --no-post > "$OUT/env_$kv.log" 2>&1; rc=$?; echo "$kv rc=$rc $(grep -o '"shadow_ms": [0-9.]*' "$OUT/env_$kv.log")" | tee -a "$OUT/steps.log"; if [ $rc -ge 124 ] || [ $rc -gt 128 ]; then exit $rc; fi; done ;;
     pmcivars) for v in ${VARS:-$(ls c-raytracer_amd/lib/var)}; do RTX_LIBRTX=$PWD/c-raytracer_amd/lib/var/$v/librtx.so run pmci_$v 600 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS -d "$OUT/pmci_$v" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post; done ;;
     pmcvalu) run pmcvalu 600 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU SQ_BUSY_CU_CYCLES SQ_INSTS_VALU_CVT SQ_INSTS_VALU_FMA_F32 SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -d "$OUT/pmc_valu2" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post ${PMCARGS:-} ;;
