@@ -47,6 +47,7 @@ for s in $STEPS; do
     treediff) run treediff 600 python3 -u -m pytest tests/test_gpu_build.py -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "collapse_equals or builds_the_host" ;;
     grabs) for g in ${GRABS:-2048 8192}; do run grab_$g 600 python3 bench.py --shadow-grab $g --steps 2 --warmup 1 --no-cpu-baseline --no-count --no-post; done ;;
     loopback) for n in ${LOOPN:-2 8}; do run loopback_$n 600 python3 bench.py --gpus $n --loopback --steps 3 --warmup 1 --no-cpu-baseline ${LOOPARGS:-}; done ;;
+    slottests) run slottests 600 python3 -u -m pytest tests/test_gpu_slots.py -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     trtests) run trtests 600 python3 -u -m pytest tests/test_gpu_torchrun.py -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     trbench) RTX_BENCH_REHEARSE=gloo run trbench 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node=${TRN:-2} --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus ${TRN:-2} --steps 2 --warmup 1 --cpu-target-s 4 ;;
     frametests) run frametests 900 python3 -u -m pytest tests/test_gpu_frame.py -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
