@@ -688,6 +688,15 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 	}
 	if (hs.w8.empty() && !hs.w8_on_device)
 		hs.w8depth = 0;
+	/* does the 8-wide tree hold spheres?  (the emitters it leaves out do not count) */
+	if (hs.w8depth) {
+		std::vector<char> is_emit(sc->num_objects, 0);
+		for (const DEmitter &e : emit)
+			is_emit[e.obj] = 1;
+		hs.w8sph = false;
+		for (uint32_t k = 0; k < nb && !hs.w8sph; k++)
+			hs.w8sph = sc->objects[bounded[k]].type == RTX_SPHERE && !(hs.w8noemit && is_emit[bounded[k]]);
+	}
 	if (linear) {
 		for (uint32_t k = 0; k < nb; k++) {
 			const rtx_object &o = sc->objects[bounded[k]];
@@ -835,6 +844,7 @@ int rtx_upload_built(rtx_ctx *c, const HostScene &hs, DevTree *take)
 	memcpy(S.w8qo, hs.w8f.qo, 12);
 	memcpy(S.w8qs, hs.w8f.qs, 12);
 	S.w8noemit = hs.w8noemit ? 1u : 0u;
+	S.w8sph = hs.w8sph ? 1u : 0u;
 	S.w8s = have_w8 ? c->d_w8s : nullptr;
 	S.root_ref = hs.root_ref;
 	S.num_prims = hs.nb;

@@ -229,6 +229,7 @@ typedef struct DScene {
 	const DW8S *w8s;        /* scalar-path copies of its nodes (num_w8 slots, node entries filled) */
 	uint32_t trace_w8;      /* k_trace walks the 8-wide tree for closest hits (else the float BVH2) */
 	uint32_t w8noemit;      /* the emitters are not in it (k_shadow tests them linearly) */
+	uint32_t w8sph;         /* it holds spheres (else k_shadow's leaf tests are the triangle's alone) */
 	const DEmitter *lin;    /* tiny scenes (RTX_WALK_LINEAR): every bounded object as a record k_shadow tests
 	                         * one by one like the planes (object order), no walk; null otherwise */
 	uint32_t num_lin;

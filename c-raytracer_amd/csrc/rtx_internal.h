@@ -163,6 +163,7 @@ struct HostScene {
 	uint32_t *dev_w8leaf = nullptr;
 	uint32_t w8_entries = 0, w8_wide = 0;
 	uint32_t w8top = 0; /* entries of the 8-wide tree's top levels (rtx_device.h DScene.w8top) */
+	bool w8sph = true;  /* the 8-wide tree holds spheres (DScene.w8sph) */
 	std::vector<DPlane> planes;
 	std::vector<DMaterial> mats;
 	std::vector<DEmitter> emit;

@@ -213,6 +213,7 @@ struct QBvh {
 	uint32_t lstk;        /* lane-stack entries in LDS (<= RTX_W8_STACK) */
 	lds_u32 *stk;         /* this lane's LDS stack of sibling groups: entry k at stk[k * WAVE] */
 	lds_u32 *tq;          /* WALK_W8: this lane's LDS queue of deferred leaf groups, entry k at tq[k * WAVE] */
+	bool sph;             /* WALK_W8: the tree holds spheres (DScene.w8sph) */
 };
 
 /* the shadow walks k_shadow instantiates */
@@ -314,18 +315,21 @@ __device__ __forceinline__ void shadow_walk(const QBvh &Q, const char *__restric
 #ifndef RTX_W8_TQ
 #define RTX_W8_TQ 4 /* deferred leaf groups per lane in LDS (besides the one in a register) */
 #endif
+#ifndef RTX_W8_TRIONLY
+#define RTX_W8_TRIONLY 1 /* leaf tests of a tree without spheres skip the sphere case (DScene.w8sph) */
+#endif
 #ifndef RTX_W8_DEFER
 #define RTX_W8_DEFER 64 /* lanes holding deferred leaf tests that trigger a round of them (16 / 32 / 48 / 64: 613 / 601 / 598 / 594 ms) */
 #endif
 /* a deferred leaf test: the transparent primitive at entry pr (rtx_device.h DW8 leaf entry,
  * whose 4th float4 holds its material's kt) against this lane's shadow ray; a hit multiplies
  * the transmittance (accel.c:370-377) */
-template <bool COUNT>
+template <bool COUNT, bool SPH>
 __device__ __forceinline__ void w8_defer_test(const char *pr, f3 o, f3 d, float tl, f3 &li, uint32_t &ntri, uint32_t &nsph)
 {
 	const float4 a = ldg4(pr, 0), b = ldg4(pr, 16), c = ldg4(pr, 32);
 	bool h;
-	if ((__float_as_uint(c.w) >> 24) == RTX_SPHERE) {
+	if (SPH && (__float_as_uint(c.w) >> 24) == RTX_SPHERE) {
 		if (COUNT)
 			nsph++;
 		float t = 0.f;
@@ -342,12 +346,13 @@ __device__ __forceinline__ void w8_defer_test(const char *pr, f3 o, f3 d, float 
 }
 
 /* an opaque leaf test: does the primitive at entry pr block this lane's shadow ray?  (no
- * emitter or transparency cases: the 8-wide tree marks its leaves when built from host records) */
-template <bool COUNT>
+ * emitter or transparency cases: the 8-wide tree marks its leaves when built from host records).
+ * SPH false: the tree holds no spheres (DScene.w8sph), the test is the triangle's alone */
+template <bool COUNT, bool SPH>
 __device__ __forceinline__ bool w8_opaque_test(const char *pr, f3 o, f3 d, float tl, uint32_t &ntri, uint32_t &nsph)
 {
 	const float4 a = ldg4(pr, 0), b = ldg4(pr, 16), c = ldg4(pr, 32);
-	if ((__float_as_uint(c.w) >> 24) == RTX_SPHERE) {
+	if (SPH && (__float_as_uint(c.w) >> 24) == RTX_SPHERE) {
 		if (COUNT)
 			nsph++;
 		float t = 0.f;
@@ -375,6 +380,20 @@ struct W8Ctr {
 	uint32_t nbox, ntri, nsph, nstep, nlr, nun;
 };
 
+/* this lane's opaque leaf hits lm (visit order) in the block at base, tested in turn: does one
+ * block the ray?  (the wave's lanes in step, a lane leaving at its first blocking hit) */
+template <bool COUNT, bool SPH, uint32_t K>
+__device__ __forceinline__ bool w8_opaque_leaves(const DW8 *w8, uint32_t lm, uint32_t base, f3 o, f3 d, float tl, W8Ctr &c)
+{
+	while (lm) {
+		const uint32_t p = __builtin_ctz(lm);
+		lm &= lm - 1;
+		if (w8_opaque_test<COUNT, SPH>((const char *)(w8 + base + (p ^ K)), o, d, tl, c.ntri, c.nsph))
+			return true;
+	}
+	return false;
+}
+
 /* One iteration of the 8-wide any-hit walk for the wave: a round of deferred transparent-leaf
  * tests, or one node step with its opaque leaf tests (see shadow_walk8).  wk / hd: this lane has
  * node work / deferred tests; walking / holding: their ballots (at least one lane has one).  o / d: the
@@ -394,7 +413,10 @@ __device__ __forceinline__ void w8_iter(const QBvh &Q, f3 o, f3 d, f3 invq, f3 o
 			w.tgrp &= w.tgrp - 1;
 			if (!(w.tgrp & 0xFFu))
 				w.tgrp = w.tn ? tq[--w.tn * WAVE] : 0u;
-			w8_defer_test<COUNT>(pr, o, d, tl, li, c.ntri, c.nsph);
+			if (!RTX_W8_TRIONLY || Q.sph)
+			w8_defer_test<COUNT, true>(pr, o, d, tl, li, c.ntri, c.nsph);
+		else
+			w8_defer_test<COUNT, false>(pr, o, d, tl, li, c.ntri, c.nsph);
 		}
 		return;
 	}
@@ -490,15 +512,8 @@ __device__ __forceinline__ void w8_iter(const QBvh &Q, f3 o, f3 d, f3 invq, f3 o
 		}
 		c.nlr += r;
 	}
-	bool blocked = false;
-	while (lm) {
-		const uint32_t p = __builtin_ctz(lm);
-		lm &= lm - 1;
-		if (w8_opaque_test<COUNT>((const char *)(Q.w8 + base + (p ^ K)), o, d, tl, c.ntri, c.nsph)) {
-			blocked = true;
-			break;
-		}
-	}
+	const bool blocked = (!RTX_W8_TRIONLY || Q.sph) ? w8_opaque_leaves<COUNT, true, K>(Q.w8, lm, base, o, d, tl, c)
+							  : w8_opaque_leaves<COUNT, false, K>(Q.w8, lm, base, o, d, tl, c);
 	if (blocked) { /* the queue too: a full queue left behind would keep the wave in deferred rounds */
 		tl = -1.f;
 		w.node = RTX_NONE;
@@ -681,6 +696,7 @@ const DW8 *w8;        /* 8-wide compressed BVH (WALK_W8 instances; qo / qs / qsi
 	uint32_t *w8spill;    /* lane-stack spill area, [entry][grid lane] */
 	uint32_t w8lstk;      /* lane-stack entries in LDS */
 	uint32_t w8top;       /* entries of the 8-wide tree's top levels, copied to LDS per workgroup (DScene.w8top) */
+	uint32_t w8sph;       /* the 8-wide tree holds spheres (DScene.w8sph) */
 	const DEmitter *lin;  /* objects shadow_query tests one by one: the emitters the 8-wide tree leaves out,
 	                       * or every bounded object of a tiny scene (no tree walk) */
 	uint32_t num_lin;
@@ -846,6 +862,7 @@ __device__ __forceinline__ QBvh make_qbvh(const KShadow &ks, const uint4 *top_q,
 	Q.spill_stride = gridDim.x * blockDim.x;
 	Q.spill = WALK == WALK_W8 ? unip(ks.w8spill) + blockIdx.x * blockDim.x + threadIdx.x : nullptr;
 	Q.lstk = uni(ks.w8lstk);
+	Q.sph = uni(ks.w8sph) != 0;
 	Q.stk = stk;
 	Q.tq = stk + RTX_W8_STACK * WAVE;
 	return Q;
@@ -1394,6 +1411,7 @@ for (int a = 0; a < 3; a++) {
 	ka.w8spill = S->w8spill;
 	ka.w8lstk = S->w8lstk;
 	ka.w8top = S->w8top;
+	ka.w8sph = S->w8sph;
 	ka.lin = S->lin; /* a tiny scene: every bounded object, no walk */
 	ka.num_lin = S->lin ? S->num_lin : 0u;
 	if (walk == WALK_W8) { /* the 8-wide tree's own frame; the emitters it leaves out are tested linearly */
