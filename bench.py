@@ -42,6 +42,12 @@ VALU_SIMDS, VALU_CLOCK_GHZ = 256 * 4, 2.4
 # max/max3/min3/min, cmp), any_tri 39, a plane test 12, and per light sample 100 (counter RNG,
 # light point, direction, attenuation, Phong/Blinn incl. powf)
 USEFUL_VALU = {"box": 17, "tri": 39, "sphere": 25, "plane": 12, "sample": 100}
+# SURVEY 8(d)'s other two bases for the same kernel: FLOPs (~12 per AABB test with a precomputed
+# 1/d, ~27 per Moller-Trumbore test) against the FP32 vector peak, and the algorithmic byte model
+# B_ray = 64 per node fetch + 48 per triangle + 32 per sphere + 16 per plane test + 48 per ray
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector
+FLOP_MODEL = {"box": 12, "tri": 27}
+BYTE_MODEL = {"node": 64, "tri": 48, "sphere": 32, "plane": 16, "ray": 48}
 SHADOW_SRCS = ["c-raytracer_amd/csrc/rtx_shadow.hip", "c-raytracer_amd/csrc/rtx_w8.h", "c-raytracer_amd/csrc/rtx_wave.h",
                "c-raytracer_amd/csrc/rtx_math.h", "c-raytracer_amd/csrc/rtx_device.h", "include/rtx_rng.h"]
 
@@ -134,17 +140,22 @@ def dry_run(a, mode):
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    backend, ws, seen = None, 1, [rank]
     if world > 1:
         torch.distributed.init_process_group("gloo")
         t = torch.ones(1)
         torch.distributed.all_reduce(t)
         ranks = int(t.item())
+        backend, ws = torch.distributed.get_backend(), torch.distributed.get_world_size()
+        seen = [None] * ws
+        torch.distributed.all_gather_object(seen, rank)
         torch.distributed.destroy_process_group()
     else:
         ranks = 1
     if rank == 0:
         print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_joined": ranks, "gpus_flag": a.gpus,
-                          "launch": "torchrun" if world > 1 else "single"}), flush=True)
+                          "launch": "torchrun" if world > 1 else "single", "backend": backend, "world_size": ws,
+                          "ranks_seen": sorted(seen)}), flush=True)
 
 
 def scene_path(which):
@@ -285,6 +296,73 @@ def cpu_reference(scene_file, flags, width, height, target_s, log):
     return None
 
 
+def frame_hash(rgb, z):
+    """sha256 (16 hex digits) of a frame's float32 rgb and z buffers, row-major"""
+    import hashlib
+    import numpy as np
+    h = hashlib.sha256()
+    h.update(np.ascontiguousarray(rgb, dtype=np.float32).tobytes())
+    h.update(np.ascontiguousarray(z, dtype=np.float32).tobytes())
+    return h.hexdigest()[:16]
+
+
+def _device_ids(dev):
+    """what torch reports about a device: name, PCI bus / device / domain ids and UUID where the
+    build exposes them"""
+    import torch
+    p = torch.cuda.get_device_properties(dev)
+    out = {"name": p.name}
+    for k in ("pci_bus_id", "pci_device_id", "pci_domain_id", "uuid"):
+        v = getattr(p, k, None)
+        if v is not None:
+            out[k] = str(v)
+    return out
+
+
+def rank_validation(a, rank, local, world, dev, rehearse, r, frame, params, d_rgb, d_z, stream, h_rgb, h_z, per_frame):
+    """what the N > 1 torchrun line can show about itself.  Every rank reports what
+    torch.distributed and the runtime see (world size, backend, rank, device ids) and its shard's rays
+    per frame (all_gather_object, one small collective after the timed steps); rank 0 then renders
+    the whole frame alone (the N = 1 frame: tile stride 1 on its own device) and checks that the
+    shards' rays add up to that frame's exactly and that the gathered image is that frame bit for
+    bit (the counter RNG makes the image independent of the sharding).
+    Returns the line's `validation` object on rank 0 (None elsewhere)."""
+    import numpy as np
+    import torch
+    import rtxpy
+    from rtxpy import abi
+    ws = torch.distributed.get_world_size()
+    me = {"rank": rank, "local_rank": local, "device": local, "ids": _device_ids(dev),
+          "closest_rays": int(per_frame[0]), "shadow_rays": int(per_frame[1])}
+    ranks = [None] * ws
+    torch.distributed.all_gather_object(ranks, me)
+    if rank != 0:
+        return None
+    p1 = rtxpy.default_params(**{f: getattr(params, f) for f, _ in abi.Params._fields_})
+    p1.tile_offset, p1.tile_stride = 0, 1
+    r.render_device(frame, p1, d_rgb.data_ptr(), d_z.data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    s1 = r.stats()
+    full_hash = frame_hash(d_rgb.cpu().numpy(), d_z.cpu().numpy())
+    gathered_hash = frame_hash(h_rgb.numpy(), h_z.numpy())
+    sum_c = sum(x["closest_rays"] for x in ranks)
+    sum_s = sum(x["shadow_rays"] for x in ranks)
+    devs = {(x["ids"].get("pci_domain_id"), x["ids"].get("pci_bus_id"), x["ids"].get("uuid"), x["local_rank"])
+            for x in ranks}
+    checks = {"world_size_is_gpus": ws == a.gpus,
+              "ranks_joined": sorted(x["rank"] for x in ranks) == list(range(ws)),
+              "distinct_devices": rehearse or len(devs) == ws,
+              "rays_sum_to_one_gpu_frame": (sum_c, sum_s) == (int(s1.closest_rays), int(s1.shadow_rays)),
+              "gathered_frame_is_one_gpu_frame": gathered_hash == full_hash}
+    return {"backend": torch.distributed.get_backend(), "world_size": ws, "ranks": ranks,
+            "rays_per_frame_sum": [sum_c, sum_s],
+            "one_gpu_frame_rays": [int(s1.closest_rays), int(s1.shadow_rays)],
+            "gathered_frame_sha256_16": gathered_hash, "one_gpu_frame_sha256_16": full_hash,
+            "checks": checks, "ok": all(checks.values()),
+            "note": "rank 0 rendered the whole frame alone after the timed steps (the N = 1 frame) to check the "
+                    "sharded run against it; bench.py exits non-zero after printing when ok is false"}
+
+
 def shadow_roofline(r, frame, params, d_rgb, d_z, stream, shadow_ms, a, world):
     """the counting pass (count_traversal) of the same frame on renderer r, then shadow_roofline_of"""
     from rtxpy import abi
@@ -340,6 +418,28 @@ def shadow_roofline_of(c, shadow_ms, a, world):
                        "GBs": round(algo_bytes / dur / 1e9, 1),
                        "note": "bytes of the records the lanes read (served by L1 / L2 / Infinity Cache, so no HBM "
                                "fraction); HBM-side bytes: traffic"}}
+    # the same launch on SURVEY 8(d)'s FLOP and byte bases: a node fetch is one 64-byte
+    # 8-wide node (8 box tests) on the 8-wide walk, one 16-byte threaded record per box test otherwise
+    w8 = int(c.wide_nodes) > 0
+    node_bytes = BYTE_MODEL["node"] * c.shadow_box_tests / 8 if w8 else 16 * c.shadow_box_tests
+    model_bytes = (node_bytes + BYTE_MODEL["tri"] * c.shadow_tri_tests + BYTE_MODEL["sphere"] * c.shadow_sphere_tests
+                   + BYTE_MODEL["plane"] * c.shadow_plane_tests + BYTE_MODEL["ray"] * c.shadow_rays)
+    flops = FLOP_MODEL["box"] * c.shadow_box_tests + FLOP_MODEL["tri"] * c.shadow_tri_tests
+    out["bases"] = {
+        "valu_useful": {"frac": out["frac"], "note": "useful VALU wave-instructions over the all-dual-issue peak (the "
+                                                      "line's roofline.frac)"},
+        "flop": {"achieved": round(flops / dur / 1e12, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                 "frac": round(flops / dur / 1e12 / FP32_PEAK_TFLOPS, 4), "flop_per_launch": int(flops),
+                 "model": "SURVEY 8(d): 12 FLOP per box test, 27 per triangle test"},
+        "bytes_model": {"bytes_per_launch": int(model_bytes), "achieved": round(model_bytes / dur / 1e12, 2),
+                        "unit": "TB/s", "peak_hbm": HBM_PEAK_GBS / 1e3,
+                        "x_hbm_peak": round(model_bytes / dur / 1e9 / HBM_PEAK_GBS, 3),
+                        "model": "SURVEY 8(d) B_ray: 64 B per node fetch (one 64-B 8-wide node per 8 box tests), 48 per "
+                                 "triangle, 32 per sphere, 16 per plane test, 48 per ray",
+                        "note": "above HBM peak: the tree is served from L2 and the Infinity Cache, so north_star's "
+                                "HBM-bound roofline cannot bind this walk; the PMC HBM bytes are hbm.frac"},
+        "binding": "VALU issue slots (roofline.issue_slots.frac) with the texture-data path beside it "
+                   "(roofline.vmem.td_busy_frac); DESIGN.md section 5"}
     if out["frac"] > 1.0:  # the useful-instruction model overestimates: report, never abort the bench
         print(f"warning: VALU roofline fraction {out['frac']} > 1 (USEFUL_VALU model too high)", file=sys.stderr)
     pmc = os.path.join(ROOT, "profiles", "pmc_k_shadow.json")
@@ -357,6 +457,7 @@ def shadow_roofline_of(c, shadow_ms, a, world):
                       "matches_this_kernel": rec.get("kernel_src_sha") == shadow_src_sha(), "launches_per_frame": nl}
         if "hbm_bytes_per_launch" in rec:
             hbm = rec.get("hbm_bytes_per_frame", nl * rec["hbm_bytes_per_launch"])
+            out["bases"]["hbm_pmc"] = {"frac": round(hbm / dur / 1e9 / HBM_PEAK_GBS, 4)}
             out["traffic"] = int(hbm)
             out["hbm"] = {"bytes_per_launch": int(hbm),
                           "achieved": round(hbm / dur / 1e9, 1), "peak": HBM_PEAK_GBS,
@@ -381,6 +482,7 @@ def shadow_roofline_of(c, shadow_ms, a, world):
                                       "frac": round(used / avail, 4), "dual_issued_frac": round(2 * dual / valu, 4),
                                       "note": "VALU issue quad-cycles the kernel used (SQ_INSTS_VALU - "
                                               "SQ_ACTIVE_INST_VALU2) over the chip's (1024 SIMDs x 2.4 GHz / 4)"}
+                out["bases"]["valu_issue_slots"] = {"frac": out["issue_slots"]["frac"]}
         if "ta_busy_frac" in rec:
             out["vmem"] = {"ta_busy_frac": rec["ta_busy_frac"], "td_busy_frac": rec.get("td_busy_frac"),
                            "note": "PMC TA_TA_BUSY / TD_TD_BUSY per CU cycle: the vector-memory address / data "
@@ -609,6 +711,10 @@ def main():
 
     kernel_ms = float(np.mean(kms))
     shadow_ms = float(np.mean(sms))
+    validation = None
+    if world > 1:
+        validation = rank_validation(a, rank, local, world, dev, rehearse, r, frame, params, d_rgb, d_z, stream,
+                                     h_rgb, h_z, (stats_closest, stats_shadow))
     roofline = None
     if not a.no_count:
         roofline = shadow_roofline(r, frame, params, d_rgb, d_z, stream, shadow_ms, a, world)
@@ -716,6 +822,8 @@ def main():
                "roofline": roofline, "cpu_baseline": cpu}
         if gat is not None:
             out["config"]["gather_message_bytes_per_rank"] = gat.message_bytes
+        if validation is not None:
+            out["validation"] = validation
         if rehearse:
             out["n_gpus"] = min(world, torch.cuda.device_count())
             out["ranks"] = world
@@ -732,6 +840,9 @@ def main():
         if build:
             out["bvh_build"] = build
         print(json.dumps(out), flush=True)
+        if validation is not None and not validation["ok"]:
+            print(f"bench.py: the {world}-rank run failed its own checks: {validation['checks']}", file=sys.stderr)
+            sys.exit(3)
     if r is not None:
         r.close()
 
@@ -772,6 +883,47 @@ def group_line(a, n, scene_name, objects, elapsed, rays, closest, per_dev, gathe
                                  "(the same measurement as the N=1 line's)"}
 
 
+def group_validation(a, g, n, scene, frame, params, h_rgb, h_z, frame_rays, log):
+    """VERDICT r05 #5 for the device group: the members as the runtime reports them (every RCCL
+    communicator's count, rank and device read back, peer access both ways per pair with device 0,
+    PCI bus ids), and the last timed frame against the whole frame rendered by one context on
+    device 0 alone (the N = 1 frame): the shards' rays must add up to its rays exactly and the
+    gathered image must be it bit for bit."""
+    import rtxpy
+    from rtxpy import abi
+    members = [g.member(r) for r in range(n)]
+    single = rtxpy.Renderer(g.devices[0])
+    try:
+        single.set_option(abi.RTX_OPT_SHADOW_WALK, WALKS[a.walk])
+        single.set_option(abi.RTX_OPT_TRACE_WALK, WALKS[a.trace_walk])
+        single.set_option(abi.RTX_OPT_SHADOW_SLOT, a.shadow_slot)
+        single.set_option(abi.RTX_OPT_TREE_FRAME, FRAMES[a.frame])
+        single.upload(scene)
+        rgb1, z1 = single.render(frame, params)
+        s1 = single.stats()
+    finally:
+        single.close()
+    one_hash, gathered_hash = frame_hash(rgb1, z1), frame_hash(h_rgb, h_z)
+    rccl = n > 1 and not a.loopback
+    checks = {"members_are_gpus": len(members) == a.gpus,
+              "distinct_devices": a.loopback or len({m["pci_bus_id"] for m in members}) == n,
+              "rays_sum_to_one_gpu_frame": (int(frame_rays[0]), int(frame_rays[1])) == (int(s1.closest_rays),
+                                                                                        int(s1.shadow_rays)),
+              "gathered_frame_is_one_gpu_frame": gathered_hash == one_hash}
+    if rccl:
+        checks["rccl_comms_count_n"] = all(m["comm_count"] == n for m in members)
+        checks["rccl_ranks_distinct"] = sorted(m["comm_rank"] for m in members) == list(range(n))
+        checks["rccl_comm_on_member_device"] = all(m["comm_device"] == m["device"] for m in members)
+    log(f"validation: {checks}")
+    return {"members": members, "rays_per_frame": [int(frame_rays[0]), int(frame_rays[1])],
+            "one_gpu_frame_rays": [int(s1.closest_rays), int(s1.shadow_rays)],
+            "gathered_frame_sha256_16": gathered_hash, "one_gpu_frame_sha256_16": one_hash,
+            "checks": checks, "ok": all(checks.values()),
+            "note": "members from rtx_group_member_info (ncclCommCount / ncclCommUserRank / ncclCommCuDevice, "
+                    "hipDeviceCanAccessPeer both ways with device 0, hipDeviceGetPCIBusId); the N = 1 frame from one "
+                    "context on device 0 after the timed steps; bench.py exits non-zero after printing when ok is false"}
+
+
 def main_group(a):
     """--gpus N > 1 in one process: the C-ABI device group (rtx_group_*), the path engine --gpus N
     ships.  A step is rtx_group_render: every device renders its tile shard on its own host
@@ -794,6 +946,15 @@ def main_group(a):
                          {"bound": "valu", "achieved": None, "peak": VALU_PEAK_GINST, "unit": "Ginst/s", "frac": None,
                           "traffic": None, "kernel": "k_shadow", "device": 0})
         out["dry_run"] = True
+        mkeys = ("device", "comm_count", "comm_rank", "comm_device", "can_access_peer0", "peer0_can_access",
+                 "peer_enabled", "transport", "pci_bus_id")
+        out["validation"] = {"members": [dict.fromkeys(mkeys) for _ in range(a.gpus)], "rays_per_frame": None,
+                             "one_gpu_frame_rays": None, "gathered_frame_sha256_16": None,
+                             "one_gpu_frame_sha256_16": None,
+                             "checks": dict.fromkeys(("members_are_gpus", "distinct_devices", "rays_sum_to_one_gpu_frame",
+                                                      "gathered_frame_is_one_gpu_frame", "rccl_comms_count_n",
+                                                      "rccl_ranks_distinct", "rccl_comm_on_member_device")),
+                             "ok": None}
         print(json.dumps(out), flush=True)
         return
     import torch
@@ -840,6 +1001,7 @@ def main_group(a):
         m = np.array(dev[r], dtype=np.float64).mean(0)
         per_dev.append({"device": r, "kernel_ms": round(m[0], 3), "trace_ms": round(m[1], 3), "shadow_ms": round(m[2], 3),
                         "rays": int(m[3])})
+    validation = group_validation(a, g, n, scene, frame, params, h_rgb, h_z, (s.closest_rays, s.shadow_rays), log)
     roofline = None
     if not a.no_count:
         p2 = rtxpy.default_params(**{f: getattr(params, f) for f, _ in abi.Params._fields_})
@@ -859,9 +1021,13 @@ def main_group(a):
             log(f"reference baseline failed: {e}")
     out = group_line(a, n, os.path.basename(path), int(scene.num_objects), elapsed, rays, closest, per_dev,
                      round(float(np.mean(gms)), 3), roofline, cpu, upload)
+    out["validation"] = validation
     if cpu and out["value"]:
         out["config"]["gpu_over_cpu"] = round(out["value"] / cpu["value"], 1)
     print(json.dumps(out), flush=True)
+    if not validation["ok"]:
+        print(f"bench.py: the {n}-device group failed its own checks: {validation['checks']}", file=sys.stderr)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

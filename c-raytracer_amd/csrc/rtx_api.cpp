@@ -445,10 +445,10 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 	float tlo[3], thi[3]; /* the bounded objects' box in the trees' frame */
 	memcpy(tlo, c->bound_lo, 12);
 	memcpy(thi, c->bound_hi, 12);
+	/* the objects' centre and radius for the far-origin test (rtx_math.h tf_far), in every frame */
+	rtx_frame_far(c->bound_lo, c->bound_hi, tf);
 	if (tf.rotated) {
-		const double rad = rtx_frame_radius(c->bound_lo, c->bound_hi, tf);
-		tf.rad = std::nextafter((float)rad, FLT_MAX); /* rounded up (rtx_math.h tf_far) */
-		const double pad = hs.frame_pad = rtx_frame_pad(rad);
+		const double pad = hs.frame_pad = rtx_frame_pad(rtx_frame_radius(c->bound_lo, c->bound_hi, tf));
 		rtx_frame_boxes(sc, bounded, tf, pad, lo.data(), hi.data(), tlo, thi);
 	}
 	hs.frame_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf0).count();
@@ -509,6 +509,7 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 		e.prim = RTX_NONE;
 		e.transparent = (mats[o.material].flags & RTX_MF_TRANSPARENT) ? 1u : 0u;
 		memcpy(e.kt, mats[o.material].kt, 12);
+		rtx_world_box(o, e.wlo, e.whi);
 	}
 
 	const auto tb0 = std::chrono::steady_clock::now();
@@ -714,6 +715,7 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 			e.transparent = (mats[o.material].flags & RTX_MF_TRANSPARENT) ? 1u : 0u;
 			memcpy(e.kt, mats[o.material].kt, 12);
 			e.prim = RTX_NONE;
+			rtx_world_box(o, e.wlo, e.whi);
 			hs.lin.push_back(e);
 		}
 	} else if (!hs.w8depth) {
@@ -1135,6 +1137,8 @@ int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, floa
 	st.shadow_wave_walks = ctr[RTX_C_SWALKS];
 	st.shadow_leaf_rounds = ctr[RTX_C_SLEAFR];
 	st.shadow_uniform_steps = ctr[RTX_C_SUNIF];
+	st.far_closest_rays = ctr[RTX_C_FARC];
+	st.far_shadow_rays = ctr[RTX_C_FARS];
 	st.node_visits = ctr[RTX_C_NODES] + st.shadow_node_visits;
 	st.tri_tests = ctr[RTX_C_TRIS] + ctr[RTX_C_STRIS];
 	st.sphere_tests = ctr[RTX_C_SPHERES] + ctr[RTX_C_SSPHERES];

@@ -41,6 +41,8 @@
 #define RTX_REF_CNT 15u
 #define RTX_REF_OFF (~63u)
 #define RTX_PLANE_BIT 0x80000000u
+#define RTX_SP_FAR 0x80000000u    /* shade-point record, object word: the point is far from the bounded
+                                   * objects (rtx_math.h tf_far), k_shadow walks from the light end */
 #define RTX_NONE 0xFFFFFFFFu
 #define RTX_EMPTY_REF 0xFFFFFFFFu /* BVH with no bounded objects */
 #define RTX_MAX_LEAF 16
@@ -117,10 +119,13 @@ typedef struct DTreeFrame {
 	float r[3][3];
 	float c[3];
 	uint32_t rotated;
-	float rad; /* the largest |x - c| component over the bounded objects' world box (rtx_frame_radius):
-	            * ray origins farther than RTX_FRAME_FAR * rad from c are handled by tf_shift /
-	            * tf_far_end (rtx_math.h), as the boxes' padding covers the transform's rounding only
-	            * near c */
+	float rad;   /* the largest |x - centre| component over the bounded objects' world box
+	              * (rtx_frame_radius), the centre being c + cf: ray origins farther than
+	              * RTX_FRAME_FAR * rad from it (in the frame's max-norm, rtx_math.h tf_far) are
+	              * handled by tf_shift / tf_point_at, as the boxes' padding covers the slab test's
+	              * rounding only for origins near the objects */
+	float cf[3]; /* that centre in the frame's coordinates: 0 for a rotated frame (c is the centre),
+	              * the world box's centre for the world frame (c = 0) */
 } DTreeFrame;
 
 /* 8-wide compressed BVH for the shadow walk (rtx_shadow.hip shadow_walk8), in the style of
@@ -206,6 +211,9 @@ typedef struct DEmitter {
 	uint32_t transparent;
 	float kt[3];
 	uint32_t prim;      /* its primitive record index (closest hits of the 8-wide walk) */
+	float wlo[3], whi[3]; /* its padded world box (rtx_world_box): tested before the object by rays from
+	                       * far origins, whose intersector arithmetic is not to be trusted far off it
+	                       * (the reference's own tree culls by this box before object_intersects) */
 } DEmitter;
 
 #define RTX_MAX_EMITTERS 64
@@ -309,6 +317,8 @@ enum {
 	RTX_C_SWALKS,       /* ... wave walks (64 shadow rays each) */
 	RTX_C_SLEAFR,       /* ... 8-wide walk: wave iterations of the leaf loops (rounds of primitive fetches) */
 	RTX_C_SUNIF,        /* ... 8-wide walk: wave steps whose active lanes were all at one node */
+	RTX_C_FARC,         /* count mode: closest-hit rays whose origin was far (rtx_math.h tf_far: tf_shift) */
+	RTX_C_FARS,         /* count mode: shadow rays from far shade points (walked from the light end) */
 	RTX_C_N
 };
 

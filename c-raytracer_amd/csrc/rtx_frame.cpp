@@ -284,12 +284,25 @@ static float up(double x)
 
 double rtx_frame_radius(const float world_lo[3], const float world_hi[3], const DTreeFrame &F)
 {
-	/* the largest |x - c| component over the bounded objects' world box: it holds every vertex and
-	 * every sphere with its radius */
+	/* the largest |x - centre| component over the bounded objects' world box (centre c + cf): it
+	 * holds every vertex and every sphere with its radius */
 	double rad = 0;
-	for (int i = 0; i < 3; i++)
-		rad = std::max(rad, std::max(fabs((double)world_lo[i] - F.c[i]), fabs((double)world_hi[i] - F.c[i])));
+	for (int i = 0; i < 3; i++) {
+		const double ce = (double)F.c[i] + F.cf[i];
+		rad = std::max(rad, std::max(fabs((double)world_lo[i] - ce), fabs((double)world_hi[i] - ce)));
+	}
 	return rad;
+}
+
+void rtx_frame_far(const float world_lo[3], const float world_hi[3], DTreeFrame &F)
+{
+	/* a rotated frame is centred on the objects (c); the world frame keeps c = 0 (its boxes are the
+	 * world boxes) and names their centre in cf */
+	for (int i = 0; i < 3; i++)
+		F.cf[i] = F.rotated ? 0.f : 0.5f * world_lo[i] + 0.5f * world_hi[i];
+	/* rounded up; a scene without bounded objects (an empty box, lo > hi) keeps rad 0 */
+	const double rad = rtx_frame_radius(world_lo, world_hi, F);
+	F.rad = std::isfinite(rad) ? std::nextafter((float)rad, FLT_MAX) : FLT_MAX;
 }
 
 void rtx_frame_box(const rtx_object &o, const DTreeFrame &F, double pad, float lo[3], float hi[3])

@@ -27,6 +27,8 @@ double rtx_frame_choose(const rtx_scene_desc *sc, const std::vector<uint32_t> &b
 /* the largest |x - c| component over the bounded objects' world box world_lo / world_hi (every
  * vertex, every sphere with its radius) */
 double rtx_frame_radius(const float world_lo[3], const float world_hi[3], const DTreeFrame &F);
+/* F.cf and F.rad for the far-origin test (rtx_math.h tf_far), in either frame */
+void rtx_frame_far(const float world_lo[3], const float world_hi[3], DTreeFrame &F);
 /* the transform's leaf-box padding for a scene of that radius */
 double rtx_frame_pad(double radius);
 /* object o's box in frame F (F.rotated), rounded outward and padded by pad plus the relative

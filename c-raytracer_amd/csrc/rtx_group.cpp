@@ -101,6 +101,18 @@ static bool enable_peer(int dev, int peer)
 	return e == hipSuccess;
 }
 
+/* the caller's current device, restored on every way out of rtx_group_open (enable_peer and the
+ * contexts' set-up switch devices) */
+struct DeviceGuard {
+	int dev = -1;
+	DeviceGuard() { (void)hipGetDevice(&dev); }
+	~DeviceGuard()
+	{
+		if (dev >= 0)
+			(void)hipSetDevice(dev);
+	}
+};
+
 extern "C" int rtx_group_open(int n, const int *devices, rtx_group **out)
 {
 	if (!out)
@@ -108,6 +120,7 @@ extern "C" int rtx_group_open(int n, const int *devices, rtx_group **out)
 	*out = nullptr;
 	if (n < 1 || n > 64)
 		return fail(RTX_ERR_ARG, "group of %d devices (1..64)", n);
+	DeviceGuard keep;
 	std::vector<int> dev(n);
 	for (int r = 0; r < n; r++) {
 		dev[r] = devices ? devices[r] : r;
@@ -156,6 +169,7 @@ extern "C" int rtx_group_open_loopback(int n, int device, rtx_group **out)
 	*out = nullptr;
 	if (n < 1 || n > 64)
 		return fail(RTX_ERR_ARG, "loopback group of %d shards (1..64)", n);
+	DeviceGuard keep;
 	rtx_group *g = new rtx_group();
 	g->n = n;
 	g->loopback = true;
@@ -180,6 +194,36 @@ extern "C" int rtx_group_open_loopback(int n, int device, rtx_group **out)
 }
 
 extern "C" int rtx_group_size(const rtx_group *g) { return g ? g->n : 0; }
+
+extern "C" int rtx_group_member_info(const rtx_group *g, int r, rtx_group_member *out)
+{
+	if (!g || !out)
+		return fail(RTX_ERR_ARG, "null argument");
+	if (r < 0 || r >= g->n)
+		return fail(RTX_ERR_ARG, "member %d of a group of %d", r, g->n);
+	memset(out, 0, sizeof(*out));
+	const int dev = g->ctx[r]->device, dev0 = g->ctx[0]->device;
+	out->device = dev;
+	out->comm_rank = out->comm_device = -1;
+	if (r < (int)g->comm.size() && g->comm[r]) {
+		NCCL_TRY(ncclCommCount(g->comm[r], &out->comm_count));
+		NCCL_TRY(ncclCommUserRank(g->comm[r], &out->comm_rank));
+		NCCL_TRY(ncclCommCuDevice(g->comm[r], &out->comm_device));
+	}
+	int can = 0;
+	if (dev == dev0) {
+		out->can_access_peer0 = out->peer0_can_access = 1u;
+	} else {
+		HIP_TRY(hipDeviceCanAccessPeer(&can, dev, dev0));
+		out->can_access_peer0 = can ? 1u : 0u;
+		HIP_TRY(hipDeviceCanAccessPeer(&can, dev0, dev));
+		out->peer0_can_access = can ? 1u : 0u;
+	}
+	out->peer_enabled = g->peer[r];
+	out->transport = g->ctx[r]->stats.transport;
+	HIP_TRY(hipDeviceGetPCIBusId(out->pci_bus_id, (int)sizeof(out->pci_bus_id), dev));
+	return RTX_OK;
+}
 
 extern "C" int rtx_group_set_builder(rtx_group *g, int builder)
 {
@@ -439,6 +483,8 @@ extern "C" int rtx_group_render(rtx_group *g, const rtx_frame *fr, const rtx_par
 		s.shadow_wave_walks += o.shadow_wave_walks;
 		s.shadow_leaf_rounds += o.shadow_leaf_rounds;
 		s.shadow_uniform_steps += o.shadow_uniform_steps;
+		s.far_closest_rays += o.far_closest_rays;
+		s.far_shadow_rays += o.far_shadow_rays;
 		s.waves += o.waves;
 		s.chunks += o.chunks;
 		s.kernel_ms = std::max(s.kernel_ms, o.kernel_ms);

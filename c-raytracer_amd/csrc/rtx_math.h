@@ -170,15 +170,18 @@ __device__ __forceinline__ f3 tf_point(const float (&r)[3][3], const float (&c)[
 	return tf_dir(r, mk3(x.x - c[0], x.y - c[1], x.z - c[2]));
 }
 
-/* Ray origins far from the trees' frame centre.  The transform's rounding grows with |x - c|
- * (about 3 * 2^-24 (|x - c| + t)), and the leaf boxes are padded for origins within a few radii
- * of c (rtx_frame.cpp).  An origin beyond RTX_FRAME_FAR radii (|x'| max-norm) gets a frame origin
- * near c computed in double, so the box tests stay conservative for any origin; the world ray
- * the primitives are tested with is untouched, so no hit changes. */
+/* Ray origins far from the bounded objects.  The slab test's rounding grows with the origin's
+ * distance (the transform's about 3 * 2^-24 (|x - c| + t), the world trees' (lo - o) * inv about
+ * 2^-24 |o|), and the leaf boxes are padded for origins within a few radii of the objects
+ * (rtx_frame.cpp; the world trees' 2e-6 relative padding).  An origin beyond RTX_FRAME_FAR radii
+ * of their centre (the frame's max-norm about cf: DTreeFrame.cf, 0 for a rotated frame) gets a
+ * frame origin near the objects computed in double, so the box tests stay conservative for any
+ * origin, in every frame; the world ray the primitives are tested with is untouched, so no hit
+ * changes. */
 #define RTX_FRAME_FAR 4.f
-__device__ __forceinline__ bool tf_far(f3 ob, float rad)
+__device__ __forceinline__ bool tf_far(f3 ob, const float (&cf)[3], float rad)
 {
-	return fmaxf(fabsf(ob.x), fmaxf(fabsf(ob.y), fabsf(ob.z))) > RTX_FRAME_FAR * rad;
+	return fmaxf(fabsf(ob.x - cf[0]), fmaxf(fabsf(ob.y - cf[1]), fabsf(ob.z - cf[2]))) > RTX_FRAME_FAR * rad;
 }
 /* x' = R (x - c) of the world point x + s d, the sum and product formed in double */
 __device__ __forceinline__ f3 tf_point_at(const float (&r)[3][3], const float (&c)[3], f3 x, f3 d, float s)
@@ -188,12 +191,21 @@ __device__ __forceinline__ f3 tf_point_at(const float (&r)[3][3], const float (&
 	return mk3((float)(r[0][0] * v0 + r[0][1] * v1 + r[0][2] * v2), (float)(r[1][0] * v0 + r[1][1] * v1 + r[1][2] * v2),
 		   (float)(r[2][0] * v0 + r[2][1] * v1 + r[2][2] * v2));
 }
+/* the same in the world frame (R = I, c = 0): x + s d rounded once */
+__device__ __forceinline__ f3 tf_world_at(f3 x, f3 d, float s)
+{
+	return mk3((float)((double)x.x + (double)s * d.x), (float)((double)x.y + (double)s * d.y),
+		   (float)((double)x.z + (double)s * d.z));
+}
 /* closest-hit rays (k_trace): the frame origin moved along the ray to t0, 2 radii before its
  * closest approach to c (every bounded object lies within sqrt(3) radii of c, so no hit comes
  * before t0); the walk then tests boxes against tbest - t0.  t0 = 0 for a ray leaving the scene. */
-__device__ __forceinline__ f3 tf_shift(const float (&r)[3][3], const float (&c)[3], float rad, f3 o, f3 d, float &t0)
+__device__ __forceinline__ f3 tf_shift(const float (&r)[3][3], const float (&c)[3], const float (&cf)[3], float rad, f3 o,
+				      f3 d, float &t0)
 {
-	const double tca = -(((double)o.x - c[0]) * d.x + ((double)o.y - c[1]) * d.y + ((double)o.z - c[2]) * d.z);
+	/* the objects' world centre is c + cf (one of the two is 0) */
+	const double tca = -(((double)o.x - c[0] - cf[0]) * d.x + ((double)o.y - c[1] - cf[1]) * d.y +
+			     ((double)o.z - c[2] - cf[2]) * d.z);
 	const double ts = tca - 2.0 * (double)rad;
 	t0 = ts > 0.0 ? (float)ts : 0.f;
 	return tf_point_at(r, c, o, d, t0);
@@ -210,6 +222,19 @@ __device__ __forceinline__ bool slab(float lox, float hix, float loy, float hiy,
 	float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlim));
 	tnear = tn;
 	return tn <= tf;
+}
+
+/* A far ray (tf_far) intersects a sphere only when it meets the sphere's world box, tested from
+ * its origin shifted near the objects (oiw = ow * iw, ow formed in double).  The reference tests
+ * every object's own world box before the object (accel.c:112-158, one object per BVH leaf), and
+ * line_intersects_sphere's b*b - c (object.c:306-321) cancels catastrophically from far off
+ * (|o - c|^2 >> r^2): a sphere sharing a multi-primitive leaf, or one whose leaf box is taken in a
+ * rotated frame, could otherwise be "hit" by a far ray that passes well clear of it. */
+__device__ __forceinline__ bool far_sphere_box(f3 c, float r, f3 oiw, f3 iw, float tlim)
+{
+	const float px = r + 2e-6f * (fabsf(c.x) + r), py = r + 2e-6f * (fabsf(c.y) + r), pz = r + 2e-6f * (fabsf(c.z) + r);
+	float tn;
+	return slab(c.x - px, c.x + px, c.y - py, c.y + py, c.z - pz, c.z + pz, oiw, iw, tlim, tn);
 }
 
 /* ---- float -> uint32_t of material.c:164,173 ---- */

@@ -148,6 +148,7 @@ struct ShadowCount {
 	u64 walks;     /* wave walks (64 rays each) */
 	u64 lrounds;   /* 8-wide walk: wave iterations of the leaf loops (immediate and deferred) */
 	u64 unif;      /* 8-wide walk: wave steps with one node for all walking lanes (scalar path) */
+	u64 far;       /* rays from far shade points, walked from the light end (RTX_SP_FAR) */
 };
 
 /* one primitive record (a, b, c = its first 48 bytes) against this lane's shadow ray
@@ -595,8 +596,8 @@ __device__ __forceinline__ bool plane_blocks(f3 n, float dd, f3 o, f3 d, float e
 template <bool COUNT, int WALK>
 __device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restrict__ recs, const DMaterial *__restrict__ mats,
 					     const DPlane *__restrict__ planes, uint32_t num_planes, const DEmitter *__restrict__ lin,
-					     uint32_t num_lin, bool have_tree, const DTreeFrame &tf, bool act, f3 o, f3 d, float dist,
-					     uint32_t emit_obj, f3 &li, ShadowCount &sc)
+					     uint32_t num_lin, bool have_tree, const DTreeFrame &tf, bool act, bool far, f3 o, f3 d,
+					     float dist, uint32_t emit_obj, f3 &li, ShadowCount &sc)
 {
 	float tl = act ? dist : -1.f;
 	for (uint32_t i = 0; i < num_planes; i++) { /* plane records are wave-uniform: s_load */
@@ -616,6 +617,12 @@ __device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restri
 		const auto *e = cptr(lin) + i;
 		if (e->obj == emit_obj || !(tl >= 0.f))
 			continue;
+		if (far) { /* a far shade point: the object's world box first, from the light end (shadow walk) */
+			const f3 ow = tf_world_at(o, d, dist), iw = safe_inv_fast(mk3(-d.x, -d.y, -d.z));
+			float tn;
+			if (!slab(e->wlo[0], e->whi[0], e->wlo[1], e->whi[1], e->wlo[2], e->whi[2], mul3v(ow, iw), iw, dist, tn))
+				continue;
+		}
 		bool h;
 		if (e->type == RTX_SPHERE) {
 			float t = 0.f;
@@ -637,7 +644,12 @@ __device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restri
 	const u64 live = ballot(alive);
 	if (!live || !have_tree)
 		return act && !alive;
-	/* the ray in the trees' frame (rtx_device.h DTreeFrame): origin ob, direction db */
+	/* the ray in the trees' frame (rtx_device.h DTreeFrame): origin ob, direction db.  A shade point
+	 * far from the bounded objects (a plane point far out, rtx_math.h tf_far; k_trace marks its
+	 * record RTX_SP_FAR): the walk runs the segment from its other end, the light point, x' formed
+	 * in double there; the same boxes meet the segment [0, dist] from either end, and the
+	 * primitives are still tested from o along d.  In every frame: the world trees' slab test
+	 * rounds at 2^-24 |o| too. */
 	f3 ob = o, db = d;
 	if (uni(tf.rotated)) {
 		float r[3][3], c[3];
@@ -650,14 +662,16 @@ __device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restri
 		}
 		ob = tf_point(r, c, o);
 		db = tf_dir(r, d);
-		/* a far origin (a plane point far from the bounded objects, rtx_math.h tf_far): the walk runs
-		 * the segment from its other end, x' computed in double there; the same boxes meet the
-		 * segment [0, dist] from either end, and the primitives are still tested from o along d */
-		if (tf_far(ob, __uint_as_float(uni(__float_as_uint(tf.rad))))) {
+		if (far) {
 			ob = tf_point_at(r, c, o, d, dist);
 			db = mk3(-db.x, -db.y, -db.z);
 		}
+	} else if (far) {
+		ob = tf_world_at(o, d, dist);
+		db = mk3(-d.x, -d.y, -d.z);
 	}
+	if (COUNT)
+		sc.far += (u64)popc64(ballot(alive && far));
 	const f3 inv = safe_inv_fast(db); /* boxes are padded 2e-6 relative: a 1-ulp 1/d keeps the test conservative */
 	const uint32_t oct = ((~__float_as_uint(inv.x)) >> 31) | (((~__float_as_uint(inv.y)) >> 31) << 1) |
 			     (((~__float_as_uint(inv.z)) >> 31) << 2);
@@ -878,7 +892,7 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	reread_barrier();
 	const float4 q0 = sp_field<UNI && RTX_SH_SPUNI>(rec, 0), q4 = sp_field<UNI && RTX_SH_SPUNI>(rec, 4);
 	const f3 p = mk3(q0.x, q0.y, q0.z);
-	const uint32_t obj = __float_as_uint(q4.x);
+	const uint32_t obj = __float_as_uint(q4.x) & ~RTX_SP_FAR, far = __float_as_uint(q4.x) & RTX_SP_FAR;
 	const DEmitter *emitters = unip(ks.emitters);
 	const auto *EM = cptr(emitters);
 	const uint32_t num_emitters = uni(ks.num_emitters);
@@ -914,7 +928,8 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	const QBvh Q = make_qbvh<WALK>(ks, top_q, top_e, stk, t8);
 	const bool have_tree = uni(ks.have_tree) != 0 && !RTX_DEBUG_NOWALK;
 	const bool blocked = shadow_query<COUNT, WALK>(Q, unip(ks.recs), unip(ks.mats), unip(ks.planes), uni(ks.num_planes),
-						 unip(ks.lin), uni(ks.num_lin), have_tree, ks.tf, act, p, ldir, ldist, eobj, li, sc);
+						 unip(ks.lin), uni(ks.num_lin), have_tree, ks.tf, act, far != 0, p, ldir, ldist, eobj, li,
+							 sc);
 	reread_barrier();
 	f3 contribution = mk3(0.f, 0.f, 0.f);
 	if (act && !blocked)
@@ -962,7 +977,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 	uint32_t *off = wt_w[wv].off, *nls = wt_w[wv].nls, *sid = wt_w[wv].sid;
 	float(*Ls)[WAVE] = wt_w[wv].Ls;
 	lds_u32 *stk = (lds_u32 *)&wstk[wv][0][lane_id()];
-	ShadowCount sc = { 0, 0, 0, 0, 0, 0, 0, 0, 0 };
+	ShadowCount sc = { 0, 0, 0, 0, 0, 0, 0, 0, 0, 0 };
 	u64 rays_total = 0;
 	for (;;) {
 		reread_barrier();
@@ -1157,6 +1172,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 			atomicAdd(&ctr[RTX_C_SWALKS], sc.walks);
 			atomicAdd(&ctr[RTX_C_SLEAFR], sc.lrounds);
 			atomicAdd(&ctr[RTX_C_SUNIF], sc.unif);
+			atomicAdd(&ctr[RTX_C_FARS], sc.far);
 		}
 	}
 }

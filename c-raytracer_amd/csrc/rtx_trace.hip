@@ -34,7 +34,7 @@
 /* per-lane traversal, stack in LDS laid out [entry][lane]                  */
 /* ------------------------------------------------------------------------ */
 struct TraceCount {
-	uint32_t nodes, tris, sph, pln;
+	uint32_t nodes, tris, sph, pln, far;
 };
 
 template <bool COUNT>
@@ -84,9 +84,14 @@ __device__ void trace_closest_bvh2(const DScene &S, uint32_t *stk, bool act, f3 
 		const f3 inv = safe_inv(db);
 		float t0 = 0.f;
 		f3 ob = S.tf.rotated ? tf_point(S.tf.r, S.tf.c, o) : o;
-		if (S.tf.rotated && tf_far(ob, S.tf.rad))
-			ob = tf_shift(S.tf.r, S.tf.c, S.tf.rad, o, d, t0);
+		const bool far = tf_far(ob, S.tf.cf, S.tf.rad);
+		if (far) {
+			ob = tf_shift(S.tf.r, S.tf.c, S.tf.cf, S.tf.rad, o, d, t0);
+			if (COUNT)
+				tc.far++;
+		}
 		const f3 oi = mul3v(ob, inv);
+		const f3 iw = safe_inv(d), oiw = mul3v(far ? tf_world_at(o, d, t0) : o, iw); /* far_sphere_box */
 		uint32_t ref = S.root_ref;
 		uint32_t sp = 0;
 		/* entries from RTX_TRACE_LSTK on live in HBM, [entry][grid lane]; lane addresses formed at
@@ -117,7 +122,8 @@ __device__ void trace_closest_bvh2(const DScene &S, uint32_t *stk, bool act, f3 
 					if ((__float_as_uint(c.w) >> 24) == RTX_SPHERE) {
 						if (COUNT)
 							tc.sph++;
-						h = hit_sphere(mk3(a.x, a.y, a.z), b.x, o, d, a.w, t);
+						h = (!far || far_sphere_box(mk3(a.x, a.y, a.z), b.x, oiw, iw, tbest - t0)) &&
+						    hit_sphere(mk3(a.x, a.y, a.z), b.x, o, d, a.w, t);
 					} else {
 						if (COUNT)
 							tc.tris++;
@@ -185,7 +191,8 @@ __device__ void trace_closest_bvh2(const DScene &S, uint32_t *stk, bool act, f3 
 #endif
 template <bool COUNT, int OCT>
 __device__ __forceinline__ void closest_walk8(const DScene &S, lds_u32 *stk, uint32_t *ostk, size_t ostride, f3 o, f3 d,
-					      f3 ob, f3 inv, float t0, float &tbest, uint32_t &hid, TraceCount &tc)
+					      f3 ob, f3 inv, float t0, bool far, float &tbest, uint32_t &hid,
+					      TraceCount &tc)
 {
 	/* the lane stack: stk / ostk are the wave's bases (LDS, then HBM [entry][grid lane]); a lane's
 	 * address is formed at each use (lane_id), none kept live across the walk */
@@ -258,7 +265,13 @@ __device__ __forceinline__ void closest_walk8(const DScene &S, lds_u32 *stk, uin
 			if ((__float_as_uint(c.w) >> 24) == RTX_SPHERE) {
 				if (COUNT)
 					tc.sph++;
-				h = hit_sphere(mk3(a.x, a.y, a.z), b.x, o, d, a.w, t);
+				if (far) { /* rtx_math.h far_sphere_box */
+					const f3 iw = safe_inv_fast(d);
+					h = far_sphere_box(mk3(a.x, a.y, a.z), b.x, mul3v(tf_world_at(o, d, t0), iw), iw, tbest - t0) &&
+					    hit_sphere(mk3(a.x, a.y, a.z), b.x, o, d, a.w, t);
+				} else {
+					h = hit_sphere(mk3(a.x, a.y, a.z), b.x, o, d, a.w, t);
+				}
 			} else {
 				if (COUNT)
 					tc.tris++;
@@ -339,10 +352,29 @@ __device__ void trace_closest_w8(const DScene &S, uint32_t *stk, bool act, f3 o,
 				hid = RTX_PLANE_BIT | i;
 			}
 		}
-		if (S.w8noemit)
+	}
+	const u64 live = ballot(act);
+	if (live) {
+		/* the ray in the trees' frame (rtx_device.h DTreeFrame) for the box tests */
+		const bool rot = S.tf.rotated != 0;
+		float t0 = 0.f;
+		f3 ob = rot ? tf_point(S.tf.r, S.tf.c, o) : o;
+		const bool far = act && tf_far(ob, S.tf.cf, S.tf.rad);
+		if (far) { /* a far origin (tf_shift), in any frame */
+			ob = tf_shift(S.tf.r, S.tf.c, S.tf.cf, S.tf.rad, o, d, t0);
+			if (COUNT)
+				tc.far++;
+		}
+		const f3 inv = safe_inv_fast(rot ? tf_dir(S.tf.r, d) : d);
+		/* the emitters the tree leaves out, one by one (as the reference's tree holds them, a far
+		 * ray meets an emitter's box first: its world box from the origin shifted to t0 in double) */
+		if (act && S.w8noemit) {
+			const f3 ow = tf_world_at(o, d, t0), iw = safe_inv_fast(d), oiw = mul3v(ow, iw);
 			for (uint32_t i = 0; i < S.num_emitters; i++) {
 				const DEmitter &e = S.emitters[i];
-				float t = 0.f;
+				float t = 0.f, tn;
+				if (far && !slab(e.wlo[0], e.whi[0], e.wlo[1], e.whi[1], e.wlo[2], e.whi[2], oiw, iw, tbest - t0, tn))
+					continue;
 				bool h;
 				if (e.type == RTX_SPHERE)
 					h = hit_sphere(ld3(e.p0), e.radius, o, d, e.eps, t);
@@ -353,16 +385,7 @@ __device__ void trace_closest_w8(const DScene &S, uint32_t *stk, bool act, f3 o,
 					hid = e.prim;
 				}
 			}
-	}
-	const u64 live = ballot(act);
-	if (live) {
-		/* the ray in the trees' frame (rtx_device.h DTreeFrame) for the box tests */
-		const bool rot = S.tf.rotated != 0;
-		float t0 = 0.f;
-		f3 ob = rot ? tf_point(S.tf.r, S.tf.c, o) : o;
-		if (rot && tf_far(ob, S.tf.rad)) /* a far origin (tf_shift) */
-			ob = tf_shift(S.tf.r, S.tf.c, S.tf.rad, o, d, t0);
-		const f3 inv = safe_inv_fast(rot ? tf_dir(S.tf.r, d) : d);
+		}
 		lds_u32 *ls = (lds_u32 *)stk;
 		uint32_t *ostk = S.ostk + (size_t)blockIdx.x * WAVE;
 		const size_t ostride = (size_t)gridDim.x * WAVE;
@@ -374,13 +397,13 @@ __device__ void trace_closest_w8(const DScene &S, uint32_t *stk, bool act, f3 o,
 			switch (sel) {
 #define RTX_CWALK(K)                                                                    \
 	case K:                                                                             \
-		closest_walk8<COUNT, K>(S, ls, ostk, ostride, o, d, ob, inv, t0, tbest, hid, tc); \
+		closest_walk8<COUNT, K>(S, ls, ostk, ostride, o, d, ob, inv, t0, far, tbest, hid, tc); \
 		break;
 				RTX_CWALK(0) RTX_CWALK(1) RTX_CWALK(2) RTX_CWALK(3) RTX_CWALK(4) RTX_CWALK(5) RTX_CWALK(6)
 				RTX_CWALK(7)
 #undef RTX_CWALK
 			default:
-				closest_walk8<COUNT, 8>(S, ls, ostk, ostride, o, d, ob, inv, t0, tbest, hid, tc);
+				closest_walk8<COUNT, 8>(S, ls, ostk, ostride, o, d, ob, inv, t0, far, tbest, hid, tc);
 				break;
 			}
 		}
@@ -487,6 +510,15 @@ struct ShadePt {
 	uint32_t mat, obj, key_lo, key_hi, nl, slot;
 };
 
+/* RTX_SP_FAR for a shade point far from the bounded objects (rtx_math.h tf_far), whose shadow
+ * rays k_shadow then walks from the light end; the test k_shadow made per ray before round 6,
+ * made once per point, in any frame */
+__device__ __forceinline__ uint32_t sp_far(const DTreeFrame &tf, f3 p)
+{
+	const f3 ob = tf.rotated ? tf_point(tf.r, tf.c, p) : p;
+	return tf_far(ob, tf.cf, tf.rad) ? RTX_SP_FAR : 0u;
+}
+
 __device__ __forceinline__ void spr_store(float4 *rec, const ShadePt &s)
 {
 	rec[0] = make_float4(s.p.x, s.p.y, s.p.z, s.w.x);
@@ -571,7 +603,7 @@ __device__ __forceinline__ void gi_batch(const DScene &S, const DParams &P, uint
 			cs.d = dir;
 			cs.w = w;
 			cs.mat = hi.mat;
-			cs.obj = hi.obj;
+			cs.obj = hi.obj | (has ? sp_far(S.tf, hi.p) : 0u);
 			cs.slot = par.slot;
 			cs.tex = has ? texture_color(m, hi.p, P.u32conv) : mk3(0.f, 0.f, 0.f);
 			cs.key_lo = (uint32_t)ckey;
@@ -602,7 +634,7 @@ __global__ __launch_bounds__(WAVE, RTX_TRACE_OCC) void k_trace(DScene S, DFrame 
 	for (uint32_t e = 0; e < S.num_emitters; e++)
 		total_lights += S.emitters[e].num_lights;
 	u64 n_closest = 0;
-	TraceCount tc = { 0, 0, 0, 0 };
+	TraceCount tc = { 0, 0, 0, 0, 0 };
 	DTask *my_tasks = tasks + (size_t)blockIdx.x * task_cap;
 	TraceOut T;
 	T.staging = staging + (size_t)blockIdx.x * staging_cap * SPREC;
@@ -686,7 +718,7 @@ __global__ __launch_bounds__(WAVE, RTX_TRACE_OCC) void k_trace(DScene S, DFrame 
 				sp.d = d;
 				sp.w = w;
 				sp.mat = h.mat;
-				sp.obj = h.obj;
+				sp.obj = h.obj | (has ? sp_far(S.tf, h.p) : 0u);
 				sp.slot = slot;
 				sp.tex = has ? texture_color(m, h.p, P.u32conv) : mk3(0.f, 0.f, 0.f);
 				sp.key_lo = (uint32_t)key;
@@ -802,19 +834,21 @@ __global__ __launch_bounds__(WAVE, RTX_TRACE_OCC) void k_trace(DScene S, DFrame 
 			tile_rec[tile - tile_begin] = make_uint2(start, n);
 	}
 	if (COUNT) {
-		u64 a = tc.nodes, b = tc.tris, c = tc.sph, d2 = tc.pln;
+		u64 a = tc.nodes, b = tc.tris, c = tc.sph, d2 = tc.pln, f = tc.far;
 #pragma unroll
 		for (int o2 = 32; o2 > 0; o2 >>= 1) {
 			a += __shfl_xor(a, o2, WAVE);
 			b += __shfl_xor(b, o2, WAVE);
 			c += __shfl_xor(c, o2, WAVE);
 			d2 += __shfl_xor(d2, o2, WAVE);
+			f += __shfl_xor(f, o2, WAVE);
 		}
 		if (lane_id() == 0) {
 			atomicAdd(&ctr[RTX_C_NODES], a);
 			atomicAdd(&ctr[RTX_C_TRIS], b);
 			atomicAdd(&ctr[RTX_C_SPHERES], c);
 			atomicAdd(&ctr[RTX_C_PLANES], d2);
+			atomicAdd(&ctr[RTX_C_FARC], f);
 		}
 	}
 	if (lane_id() == 0) {

@@ -350,6 +350,15 @@ class Group:
         _check(self.lib.rtx_group_device_stats(self._g, r, C.byref(s)))
         return s
 
+    def member(self, r):
+        """what the runtime reports about member r (rtx_group_member_info): its device, its RCCL
+        communicator's count / rank / device, peer access to and from member 0, PCI bus id"""
+        m = abi.GroupMember()
+        _check(self.lib.rtx_group_member_info(self._g, r, C.byref(m)))
+        return {"device": m.device, "comm_count": m.comm_count, "comm_rank": m.comm_rank, "comm_device": m.comm_device,
+                "can_access_peer0": m.can_access_peer0, "peer0_can_access": m.peer0_can_access,
+                "peer_enabled": m.peer_enabled, "transport": m.transport, "pci_bus_id": m.pci_bus_id.decode()}
+
     def close(self):
         if self._g:
             self.lib.rtx_group_close(self._g)

@@ -73,10 +73,17 @@ class Stats(C.Structure):
                 ("shadow_uniform_steps", C.c_uint64), ("shadow_walk", C.c_uint32), ("wide_entries", C.c_uint32),
                 ("trace_walk", C.c_uint32), ("pad2_", C.c_uint32), ("tree_rotated", C.c_uint32),
                 ("pad3_", C.c_uint32), ("frame_cost", C.c_double), ("frame_ms", C.c_double),
-                ("upload_copy_ms", C.c_double), ("transport", C.c_uint32), ("peer_access", C.c_uint32)]
+                ("upload_copy_ms", C.c_double), ("transport", C.c_uint32), ("peer_access", C.c_uint32),
+                ("far_closest_rays", C.c_uint64), ("far_shadow_rays", C.c_uint64)]
 
 
 RTX_TRANSPORT_NONE, RTX_TRANSPORT_RCCL, RTX_TRANSPORT_LOOPBACK = 0, 1, 2
+
+
+class GroupMember(C.Structure):
+    _fields_ = [("device", C.c_int32), ("comm_count", C.c_int32), ("comm_rank", C.c_int32), ("comm_device", C.c_int32),
+                ("can_access_peer0", C.c_uint32), ("peer0_can_access", C.c_uint32), ("peer_enabled", C.c_uint32),
+                ("transport", C.c_uint32), ("pci_bus_id", C.c_char * 32)]
 
 
 RTX_BUILD_SAH_HOST, RTX_BUILD_LBVH_GPU, RTX_BUILD_PLOC_GPU, RTX_BUILD_SAH_GPU = 0, 1, 2, 3
@@ -113,7 +120,7 @@ RTX_SYMBOLS = ["rtx_params_default", "rtx_device_count", "rtx_open", "rtx_upload
                "rtx_render_device", "rtx_get_stats", "rtx_close", "rtx_last_error", "rtx_kat", "rtx_postprocess",
                "rtx_postprocess_device", "rtx_set_builder", "rtx_set_option", "rtx_group_open", "rtx_group_open_loopback", "rtx_group_size", "rtx_read_wide_tree",
                "rtx_group_set_builder", "rtx_group_set_option", "rtx_group_upload_scene", "rtx_group_render", "rtx_group_get_stats", "rtx_group_device_stats",
-               "rtx_group_close", "rtx_tile_pack_count", "rtx_tile_pack_host", "rtx_tile_unpack_host",
+               "rtx_group_member_info", "rtx_group_close", "rtx_tile_pack_count", "rtx_tile_pack_host", "rtx_tile_unpack_host",
                "rtx_tile_pack_device", "rtx_tile_unpack_device", "rtx_tree_frame"]
 RTX_SCENE_SYMBOLS = ["rtx_scene_load", "rtx_scene_parse", "rtx_scene_desc_of", "rtx_scene_num_json_objects",
                      "rtx_scene_free", "rtx_scene_last_error", "rtx_frame_setup", "rtx_tiff_write", "rtx_hash_djb",
@@ -205,6 +212,8 @@ def declare_rtx(lib):
     lib.rtx_group_get_stats.restype = C.c_int
     lib.rtx_group_device_stats.argtypes = [C.c_void_p, C.c_int, C.POINTER(Stats)]
     lib.rtx_group_device_stats.restype = C.c_int
+    lib.rtx_group_member_info.argtypes = [C.c_void_p, C.c_int, C.POINTER(GroupMember)]
+    lib.rtx_group_member_info.restype = C.c_int
     lib.rtx_group_close.argtypes = [C.c_void_p]
     lib.rtx_group_close.restype = None
     lib.rtx_tile_pack_count.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]

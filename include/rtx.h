@@ -228,6 +228,10 @@ typedef struct rtx_stats {
 	uint32_t transport;               /* device groups: RTX_TRANSPORT_* of the shard gather */
 	uint32_t peer_access;             /* device groups: this device and device 0 have peer access enabled
 	                                   * (hipDeviceEnablePeerAccess both ways; 1 on device 0 itself) */
+	/* only with count_traversal: rays whose origin lies more than 4 scene radii from the bounded
+	 * objects, whose box tests start from a point formed in double near them (any tree frame) */
+	uint64_t far_closest_rays;        /* closest-hit rays (the frame origin moved along the ray) */
+	uint64_t far_shadow_rays;         /* shadow rays from far shade points (walked from the light end) */
 } rtx_stats;
 
 typedef struct rtx_ctx rtx_ctx;
@@ -339,6 +343,20 @@ int rtx_group_render(rtx_group *g, const rtx_frame *frame, const rtx_params *par
 int rtx_group_get_stats(const rtx_group *g, rtx_stats *out);
 /* the statistics of device r (0 <= r < rtx_group_size) for the last frame */
 int rtx_group_device_stats(const rtx_group *g, int r, rtx_stats *out);
+/* What the runtime reports about member r, read back rather than assumed (a line that claims N
+ * devices can show that N communicators of one clique formed on N distinct devices) */
+typedef struct rtx_group_member {
+	int32_t device;           /* the HIP device ordinal of member r */
+	int32_t comm_count;       /* ncclCommCount of its RCCL communicator (0: none, n = 1 or loopback) */
+	int32_t comm_rank;        /* ncclCommUserRank (-1: none) */
+	int32_t comm_device;      /* ncclCommCuDevice (-1: none) */
+	uint32_t can_access_peer0; /* hipDeviceCanAccessPeer(device, device of member 0) */
+	uint32_t peer0_can_access; /* hipDeviceCanAccessPeer(device of member 0, device) */
+	uint32_t peer_enabled;    /* peer access enabled both ways at rtx_group_open (1 for member 0) */
+	uint32_t transport;       /* RTX_TRANSPORT_* */
+	char pci_bus_id[32];      /* hipDeviceGetPCIBusId */
+} rtx_group_member;
+int rtx_group_member_info(const rtx_group *g, int r, rtx_group_member *out);
 void rtx_group_close(rtx_group *g);
 
 /* The gather's tile records (rtx_tiles.h): shard `offset` of `stride` of a W x H frame packs

@@ -61,7 +61,7 @@ def test_struct_sizes_match_c():
     assert ctypes.sizeof(abi.Object) == 4 * (4 + 18 + 2)
     assert ctypes.sizeof(abi.Frame) == 4 * (2 + 12)
     assert ctypes.sizeof(abi.Params) == 56
-    assert ctypes.sizeof(abi.Stats) == 11 * 8 + 6 * 8 + 6 * 4 + 4 * 8 + 2 * 4 + 8 + 8 + 2 * 4 + 8 + 2 * 4 + 2 * 4 + 2 * 4 + 2 * 8 + 8 + 2 * 4
+    assert ctypes.sizeof(abi.Stats) == 11 * 8 + 6 * 8 + 6 * 4 + 4 * 8 + 2 * 4 + 8 + 8 + 2 * 4 + 8 + 2 * 4 + 2 * 4 + 2 * 4 + 2 * 8 + 8 + 2 * 4 + 2 * 8
 
 
 def test_struct_layouts_match_compiled_header(tmp_path):
@@ -71,7 +71,8 @@ def test_struct_layouts_match_compiled_header(tmp_path):
     if not shutil.which("gcc"):
         pytest.skip("gcc not available")
     structs = {"rtx_material": abi.Material, "rtx_object": abi.Object, "rtx_frame": abi.Frame,
-               "rtx_params": abi.Params, "rtx_stats": abi.Stats, "rtx_post": abi.Post}
+               "rtx_params": abi.Params, "rtx_stats": abi.Stats, "rtx_post": abi.Post,
+               "rtx_group_member": abi.GroupMember}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "rtx.h"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')

@@ -21,6 +21,7 @@ def test_gpus_flag_launches_that_many_ranks():
     line = [l for l in p.stdout.splitlines() if l.startswith("{")][-1]
     out = json.loads(line)
     assert out["n_gpus"] == 2 and out["ranks_joined"] == 2 and out["launch"] == "torchrun"
+    assert out["world_size"] == 2 and out["ranks_seen"] == [0, 1] and out["backend"] == "gloo"
 
 
 def test_gpus_flag_without_torchrun_drives_the_device_group():
@@ -52,6 +53,13 @@ def test_group_line_schema():
     assert "cpu_baseline_note" in out  # the same reference CPU leg as the N=1 line, after the GPU steps
     rl = out["roofline"]
     assert rl["kernel"] == "k_shadow" and rl["device"] == 0 and {"bound", "achieved", "peak", "unit", "frac", "traffic"} <= set(rl)
+    # the line validates itself (members read back from RCCL / HIP, the N = 1 frame)
+    v = out["validation"]
+    assert len(v["members"]) == 8 and {"comm_count", "comm_rank", "comm_device", "can_access_peer0",
+                                       "peer0_can_access", "pci_bus_id"} <= set(v["members"][0])
+    assert {"rays_sum_to_one_gpu_frame", "gathered_frame_is_one_gpu_frame", "rccl_comms_count_n",
+            "rccl_ranks_distinct", "distinct_devices"} <= set(v["checks"])
+    assert {"one_gpu_frame_rays", "gathered_frame_sha256_16", "one_gpu_frame_sha256_16", "ok"} <= set(v)
 
 
 def test_workload_labels_name_the_baseline_config():
@@ -132,3 +140,12 @@ def test_roofline_issue_slots(tmp_path, monkeypatch):
     avail = 0.5 * 2.4e9 / 4 * 1024
     assert s["used_quad_cycles"] == int(3.0e11) and abs(s["frac"] - 3.0e11 / avail) < 1e-4
     assert s["dual_issued_frac"] == 0.5
+    # the same launch on SURVEY 8(d)'s FLOP and byte-model bases beside the VALU ones
+    b = out["bases"]
+    flop = 12 * 5.2e11 + 27 * 1.8e10
+    assert abs(b["flop"]["frac"] - flop / 0.5 / 1e12 / 157.3) < 1e-4
+    model = 64 * 5.2e11 / 8 + 48 * 1.8e10 + 16 * 2.1e10 + 48 * 2.1e10
+    assert b["bytes_model"]["bytes_per_launch"] == int(model)
+    assert abs(b["bytes_model"]["x_hbm_peak"] - model / 0.5 / 8e12) < 1e-3
+    assert b["valu_useful"]["frac"] == out["frac"] and b["valu_issue_slots"]["frac"] == s["frac"]
+    assert abs(b["hbm_pmc"]["frac"] - 1e11 / 0.5 / 8e12) < 1e-4 and "binding" in b

@@ -171,3 +171,11 @@ def test_gpu_bench_group_line_on_the_loopback_group(tmp_path):
     assert all(d["kernel_ms"] > 0 for d in g["devices"]) and g["gather_ms"] > 0
     assert g["upload"]["peer_copy_ms"][0] == 0.0 and min(g["upload"]["peer_copy_ms"][1:]) > 0
     assert out["roofline"]["kernel"] == "k_shadow" and out["roofline"]["device"] == 0
+    # the line validates itself: members read back, the one-context frame equal to
+    # the gathered one in rays and bits
+    v = out["validation"]
+    assert v["ok"], v["checks"]
+    assert [m["device"] for m in v["members"]] == [0, 0, 0] and all(m["comm_count"] == 0 for m in v["members"])
+    assert all(m["transport"] == 2 and m["pci_bus_id"] for m in v["members"])
+    assert v["rays_per_frame"] == v["one_gpu_frame_rays"] and sum(v["rays_per_frame"]) == out["config"]["rays_per_frame"]
+    assert v["gathered_frame_sha256_16"] == v["one_gpu_frame_sha256_16"]

@@ -47,3 +47,10 @@ def test_gpu_torchrun_ranks_rehearsal(ranks):
     assert multi["config"]["rays_per_frame"] == one["config"]["rays_per_frame"] == one["config"]["rays_per_frame_rank0"]
     assert 0 < multi["config"]["rays_per_frame_rank0"] < multi["config"]["rays_per_frame"]
     assert multi["value"] > 0 and multi["config"]["gather_message_bytes_per_rank"] > 0
+    # the line validates itself: torch.distributed's own world size and backend,
+    # every rank reporting, and rank 0's one-GPU frame equal to the gathered one in rays and bits
+    v = multi["validation"]
+    assert v["ok"] and v["world_size"] == ranks and v["backend"] == "gloo", v["checks"]
+    assert [x["rank"] for x in v["ranks"]] == list(range(ranks))
+    assert v["rays_per_frame_sum"] == v["one_gpu_frame_rays"] and sum(v["rays_per_frame_sum"]) == one["config"]["rays_per_frame"]
+    assert v["gathered_frame_sha256_16"] == v["one_gpu_frame_sha256_16"]
