@@ -47,8 +47,8 @@ extern "C" hipError_t rtx_sah_build(uint32_t n, const float *d_lo, const float *
 				    uint32_t *levels_out, hipStream_t st);
 extern "C" hipError_t rtx_w8_collapse_device(const DNode *recs, uint32_t nnodes, uint32_t nb, const uint32_t *skip_obj,
 					     uint32_t num_objects, DW8 **w8_out, DW8S **w8s_out, uint32_t **leafmap_out,
-					     uint32_t *entries_out, uint32_t *depth_out, uint32_t *wide_out, uint32_t *top_out,
-					     float qo[3], float qs[3], hipStream_t st);
+					     uint32_t *entries_out, uint32_t *scalar_entries_out, uint32_t *depth_out,
+					     uint32_t *wide_out, uint32_t *top_out, float qo[3], float qs[3], hipStream_t st);
 extern "C" hipError_t rtx_launch_w8_scalar(uint32_t n, const DW8 *w8, const uint32_t *leafmap, DW8S *w8s, hipStream_t st);
 extern "C" hipError_t rtx_lbvh_build(uint32_t n, const float *d_lo, const float *d_hi, const DPrim *d_prims_in,
 				     const float blo[3], const float bhi[3], uint32_t max_leaf, DNode **recs_out,
@@ -580,7 +580,7 @@ int rtx_build_scene(rtx_ctx *c, const rtx_scene_desc *sc, HostScene &hs)
 				return rc;
 			uint32_t ent = 0, dep = 0, wide = 0, top = 0;
 			e = rtx_w8_collapse_device(recs, nnodes, nb, d_skip, sc->num_objects, &hs.dev_w8, &hs.dev_w8s, &hs.dev_w8leaf, &ent,
-						   &dep, &wide, &top, hs.w8f.qo, hs.w8f.qs, c->stream);
+						   &hs.w8s_entries, &dep, &wide, &top, hs.w8f.qo, hs.w8f.qs, c->stream);
 			dfree(d_skip);
 			if (e != hipSuccess)
 				return fail(RTX_ERR_HIP, "8-wide BVH collapse on the device failed: %s", hipGetErrorString(e));
@@ -1139,6 +1139,7 @@ int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, floa
 	st.shadow_uniform_steps = ctr[RTX_C_SUNIF];
 	st.far_closest_rays = ctr[RTX_C_FARC];
 	st.far_shadow_rays = ctr[RTX_C_FARS];
+	st.shadow_stack_spills = ctr[RTX_C_SSPILL];
 	st.node_visits = ctr[RTX_C_NODES] + st.shadow_node_visits;
 	st.tri_tests = ctr[RTX_C_TRIS] + ctr[RTX_C_STRIS];
 	st.sphere_tests = ctr[RTX_C_SPHERES] + ctr[RTX_C_SSPHERES];

@@ -319,6 +319,7 @@ enum {
 	RTX_C_SUNIF,        /* ... 8-wide walk: wave steps whose active lanes were all at one node */
 	RTX_C_FARC,         /* count mode: closest-hit rays whose origin was far (rtx_math.h tf_far: tf_shift) */
 	RTX_C_FARS,         /* count mode: shadow rays from far shade points (walked from the light end) */
+	RTX_C_SSPILL,       /* count mode, 8-wide walk: lane-stack pushes beyond the LDS entries (HBM) */
 	RTX_C_N
 };
 

@@ -283,7 +283,7 @@ static int upload_copy(rtx_group *g, int r, const HostScene &hs, const DevTree &
 	int rc = RTX_OK;
 	if ((!hs.recs_on_device || !(rc = peer_copy(c->d_nodes, c->device, c0->d_nodes, c0->device, rec_bytes, c->stream))) &&
 	    !(rc = peer_copy(t.w8, c->device, src.w8, src.device, ent * sizeof(DW8), c->stream)) &&
-	    !(rc = peer_copy(t.w8s, c->device, src.w8s, src.device, ent * sizeof(DW8S), c->stream)) &&
+	    !(rc = peer_copy(t.w8s, c->device, src.w8s, src.device, (ent ? hs.w8s_entries : 0) * sizeof(DW8S), c->stream)) &&
 	    !(rc = peer_copy(t.leaf, c->device, src.leaf, src.device, ent * sizeof(uint32_t), c->stream))) {
 		hipError_t e = hipStreamSynchronize(c->stream);
 		if (e != hipSuccess)
@@ -485,6 +485,7 @@ extern "C" int rtx_group_render(rtx_group *g, const rtx_frame *fr, const rtx_par
 		s.shadow_uniform_steps += o.shadow_uniform_steps;
 		s.far_closest_rays += o.far_closest_rays;
 		s.far_shadow_rays += o.far_shadow_rays;
+		s.shadow_stack_spills += o.shadow_stack_spills;
 		s.waves += o.waves;
 		s.chunks += o.chunks;
 		s.kernel_ms = std::max(s.kernel_ms, o.kernel_ms);

@@ -162,6 +162,7 @@ struct HostScene {
 	DW8S *dev_w8s = nullptr;
 	uint32_t *dev_w8leaf = nullptr;
 	uint32_t w8_entries = 0, w8_wide = 0;
+	uint32_t w8s_entries = 0; /* device collapse: scalar-path copies allocated (entries below the last node entry) */
 	uint32_t w8top = 0; /* entries of the 8-wide tree's top levels (rtx_device.h DScene.w8top) */
 	bool w8sph = true;  /* the 8-wide tree holds spheres (DScene.w8sph) */
 	std::vector<DPlane> planes;

@@ -230,11 +230,23 @@ __device__ __forceinline__ bool slab(float lox, float hix, float loy, float hiy,
  * line_intersects_sphere's b*b - c (object.c:306-321) cancels catastrophically from far off
  * (|o - c|^2 >> r^2): a sphere sharing a multi-primitive leaf, or one whose leaf box is taken in a
  * rotated frame, could otherwise be "hit" by a far ray that passes well clear of it. */
-__device__ __forceinline__ bool far_sphere_box(f3 c, float r, f3 oiw, f3 iw, float tlim)
+/* does the ray x(t) = o + (s + sgn t) d, t in [0, tlim], meet the world box [lo, hi]?  Its origin
+ * o + s d is formed in double.  Far rays only: the empty asm keeps the compiler from hoisting this
+ * set-up (double-precision FMAs, three v_rcp) out of the branch that needs it, so a near ray
+ * pays nothing and the registers of the hot loops around it stay free. */
+__device__ __forceinline__ bool world_box_at(float lx, float hx, float ly, float hy, float lz, float hz, f3 o, f3 d,
+					     float s, float sgn, float tlim)
+{
+	f3 dd = d;
+	asm volatile("" : "+v"(dd.x), "+v"(dd.y), "+v"(dd.z));
+	const f3 iw = safe_inv_fast(mk3(sgn * dd.x, sgn * dd.y, sgn * dd.z));
+	float tn;
+	return slab(lx, hx, ly, hy, lz, hz, mul3v(tf_world_at(o, dd, s), iw), iw, tlim, tn);
+}
+__device__ __forceinline__ bool far_sphere_box(f3 c, float r, f3 o, f3 d, float t0, float tlim)
 {
 	const float px = r + 2e-6f * (fabsf(c.x) + r), py = r + 2e-6f * (fabsf(c.y) + r), pz = r + 2e-6f * (fabsf(c.z) + r);
-	float tn;
-	return slab(c.x - px, c.x + px, c.y - py, c.y + py, c.z - pz, c.z + pz, oiw, iw, tlim, tn);
+	return world_box_at(c.x - px, c.x + px, c.y - py, c.y + py, c.z - pz, c.z + pz, o, d, t0, 1.f, tlim);
 }
 
 /* ---- float -> uint32_t of material.c:164,173 ---- */

@@ -51,6 +51,12 @@
 #ifndef RTX_SH_FASTPOW
 #define RTX_SH_FASTPOW 1 /* specular powf from v_log_f32 / v_exp_f32 (sh_pow) */
 #endif
+#ifndef RTX_SH_FARLIN
+#define RTX_SH_FARLIN 1 /* far shade points: objects tested one by one are culled by their world boxes first */
+#endif
+#ifndef RTX_SH_SPILL_UNI
+#define RTX_SH_SPILL_UNI 1 /* the lane-stack spill area addressed from a wave-uniform base */
+#endif
 #ifndef RTX_SH_SPUNI
 #define RTX_SH_SPUNI 1 /* >= 64 lights: the shade-point record through scalar loads */
 #endif
@@ -149,6 +155,7 @@ struct ShadowCount {
 	u64 lrounds;   /* 8-wide walk: wave iterations of the leaf loops (immediate and deferred) */
 	u64 unif;      /* 8-wide walk: wave steps with one node for all walking lanes (scalar path) */
 	u64 far;       /* rays from far shade points, walked from the light end (RTX_SP_FAR) */
+	u64 spills;    /* 8-wide walk: lane-stack pushes beyond the LDS entries (to DScene.w8spill in HBM) */
 };
 
 /* one primitive record (a, b, c = its first 48 bytes) against this lane's shadow ray
@@ -209,8 +216,10 @@ struct QBvh {
 	const DW8S *w8s;      /* ... its nodes' scalar-path copies */
 	const uint4 *t8;      /* the workgroup's LDS copy of its entries [0, nt8) (top levels) */
 	uint32_t nt8;
-	uint32_t *spill;      /* this lane's stack entries from lstk on: entry k at spill[(k - lstk) * spill_stride] */
-	uint32_t spill_stride;
+	uint32_t *spill;      /* the wave's lane-stack entries from lstk on: lane l's entry k at
+	                       * spill[(k - lstk) * spill_stride + spill_lane0 + l] (a wave-uniform base and a
+	                       * lane index formed at each use, no per-lane 64-bit pointer kept live) */
+	uint32_t spill_stride, spill_lane0;
 	uint32_t lstk;        /* lane-stack entries in LDS (<= RTX_W8_STACK) */
 	lds_u32 *stk;         /* this lane's LDS stack of sibling groups: entry k at stk[k * WAVE] */
 	lds_u32 *tq;          /* WALK_W8: this lane's LDS queue of deferred leaf groups, entry k at tq[k * WAVE] */
@@ -319,6 +328,12 @@ __device__ __forceinline__ void shadow_walk(const QBvh &Q, const char *__restric
 #ifndef RTX_W8_TRIONLY
 #define RTX_W8_TRIONLY 1 /* leaf tests of a tree without spheres skip the sphere case (DScene.w8sph) */
 #endif
+#ifndef RTX_W8_LEAF2
+#define RTX_W8_LEAF2 1 /* a round of opaque leaf tests takes two of a lane's hit leaf slots */
+#endif
+#ifndef RTX_W8_DEFER2
+#define RTX_W8_DEFER2 1 /* a round of deferred transparent-leaf tests takes two of a lane's queued leaves */
+#endif
 #ifndef RTX_W8_DEFER
 #define RTX_W8_DEFER 64 /* lanes holding deferred leaf tests that trigger a round of them (16 / 32 / 48 / 64: 613 / 601 / 598 / 594 ms) */
 #endif
@@ -378,7 +393,7 @@ struct W8Walk {
 };
 /* the walk's counters (COUNT instances) */
 struct W8Ctr {
-	uint32_t nbox, ntri, nsph, nstep, nlr, nun;
+	uint32_t nbox, ntri, nsph, nstep, nlr, nun, nspill;
 };
 
 /* this lane's opaque leaf hits lm (visit order) in the block at base, tested in turn: does one
@@ -389,6 +404,19 @@ __device__ __forceinline__ bool w8_opaque_leaves(const DW8 *w8, uint32_t lm, uin
 	while (lm) {
 		const uint32_t p = __builtin_ctz(lm);
 		lm &= lm - 1;
+		if (RTX_W8_LEAF2) {
+			/* two of the lane's hit leaves per round (the same tests in the same order, half the
+			 * rounds: a Menger face's two triangles share a box in the rotated frame, so a lane that
+			 * meets one meets both) */
+			const bool two = lm != 0;
+			const uint32_t q = two ? __builtin_ctz(lm) : p;
+			lm &= lm - 1;
+			if (w8_opaque_test<COUNT, SPH>((const char *)(w8 + base + (p ^ K)), o, d, tl, c.ntri, c.nsph))
+				return true;
+			if (two && w8_opaque_test<COUNT, SPH>((const char *)(w8 + base + (q ^ K)), o, d, tl, c.ntri, c.nsph))
+				return true;
+			continue;
+		}
 		if (w8_opaque_test<COUNT, SPH>((const char *)(w8 + base + (p ^ K)), o, d, tl, c.ntri, c.nsph))
 			return true;
 	}
@@ -414,10 +442,24 @@ __device__ __forceinline__ void w8_iter(const QBvh &Q, f3 o, f3 d, f3 invq, f3 o
 			w.tgrp &= w.tgrp - 1;
 			if (!(w.tgrp & 0xFFu))
 				w.tgrp = w.tn ? tq[--w.tn * WAVE] : 0u;
-			if (!RTX_W8_TRIONLY || Q.sph)
-			w8_defer_test<COUNT, true>(pr, o, d, tl, li, c.ntri, c.nsph);
-		else
-			w8_defer_test<COUNT, false>(pr, o, d, tl, li, c.ntri, c.nsph);
+			/* RTX_W8_DEFER2: the lane's next queued leaf in the same round (the transmittance
+			 * products in the same order) */
+			const char *pr2 = nullptr;
+			if (RTX_W8_DEFER2 && w.tgrp) {
+				pr2 = (const char *)(Q.w8 + (w.tgrp >> 8) + (__builtin_ctz(w.tgrp) ^ K));
+				w.tgrp &= w.tgrp - 1;
+				if (!(w.tgrp & 0xFFu))
+					w.tgrp = w.tn ? tq[--w.tn * WAVE] : 0u;
+			}
+			if (!RTX_W8_TRIONLY || Q.sph) {
+				w8_defer_test<COUNT, true>(pr, o, d, tl, li, c.ntri, c.nsph);
+				if (RTX_W8_DEFER2 && pr2)
+					w8_defer_test<COUNT, true>(pr2, o, d, tl, li, c.ntri, c.nsph);
+			} else {
+				w8_defer_test<COUNT, false>(pr, o, d, tl, li, c.ntri, c.nsph);
+				if (RTX_W8_DEFER2 && pr2)
+					w8_defer_test<COUNT, false>(pr2, o, d, tl, li, c.ntri, c.nsph);
+			}
 		}
 		return;
 	}
@@ -478,8 +520,12 @@ __device__ __forceinline__ void w8_iter(const QBvh &Q, f3 o, f3 d, f3 invq, f3 o
 				if (w.grp) {
 					if (w.sp < Q.lstk)
 						stk[w.sp * WAVE] = w.grp;
-					else
-						gptrw(Q.spill)[(size_t)(w.sp - Q.lstk) * Q.spill_stride] = w.grp;
+					else {
+						gptrw(Q.spill)[(size_t)(w.sp - Q.lstk) * Q.spill_stride + Q.spill_lane0 +
+							       (RTX_SH_SPILL_UNI ? lane_id() : 0u)] = w.grp;
+						if (COUNT)
+							c.nspill++;
+					}
 					w.sp++;
 				}
 				w.grp = (base << 8) | im;
@@ -491,7 +537,9 @@ __device__ __forceinline__ void w8_iter(const QBvh &Q, f3 o, f3 d, f3 invq, f3 o
 				w.grp = 0;
 				if (w.sp) {
 					w.sp--;
-					w.grp = w.sp < Q.lstk ? stk[w.sp * WAVE] : gptr(Q.spill)[(size_t)(w.sp - Q.lstk) * Q.spill_stride];
+					w.grp = w.sp < Q.lstk ? stk[w.sp * WAVE]
+							      : gptr(Q.spill)[(size_t)(w.sp - Q.lstk) * Q.spill_stride + Q.spill_lane0 +
+									       (RTX_SH_SPILL_UNI ? lane_id() : 0u)];
 				}
 			}
 		} else {
@@ -509,6 +557,8 @@ __device__ __forceinline__ void w8_iter(const QBvh &Q, f3 o, f3 d, f3 invq, f3 o
 		for (uint32_t m = lm;; m &= m - 1) {
 			if (!ballot(m != 0))
 				break;
+			if (RTX_W8_LEAF2)
+				m &= m - 1;
 			r++;
 		}
 		c.nlr += r;
@@ -528,10 +578,11 @@ template <bool COUNT> __device__ __forceinline__ void w8_count(W8Ctr c, ShadowCo
 {
 	if (!COUNT)
 		return;
-	uint32_t a = c.nbox, bb = c.ntri, cc = c.nsph, nstep = c.nstep, nun = c.nun, nlr = c.nlr;
+	uint32_t a = c.nbox, bb = c.ntri, cc = c.nsph, nstep = c.nstep, nun = c.nun, nlr = c.nlr, nsp = c.nspill;
 #pragma unroll
 	for (int k = 32; k > 0; k >>= 1) {
 		a += __shfl_xor(a, k, WAVE);
+		nsp += __shfl_xor(nsp, k, WAVE);
 		bb += __shfl_xor(bb, k, WAVE);
 		cc += __shfl_xor(cc, k, WAVE);
 		nstep = max(nstep, (uint32_t)__shfl_xor(nstep, k, WAVE));
@@ -542,6 +593,7 @@ template <bool COUNT> __device__ __forceinline__ void w8_count(W8Ctr c, ShadowCo
 	sc.gboxes += uni(a);
 	sc.lrounds += uni(nlr);
 	sc.unif += uni(nun);
+	sc.spills += uni(nsp);
 	sc.tris += uni(bb);
 	sc.sph += uni(cc);
 	sc.steps += uni(nstep);
@@ -558,7 +610,7 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 	const f3 oq = mk3((ob.x - Q.qo.x) * Q.qs.x, (ob.y - Q.qo.y) * Q.qs.y, (ob.z - Q.qo.z) * Q.qs.z);
 	const f3 oi = mul3v(oq, invq);
 	W8Walk w = { tl >= 0.f ? 0u : RTX_NONE, 0u, 0u, 0u, 0u };
-	W8Ctr c = { 0u, 0u, 0u, 0u, 0u, 0u };
+	W8Ctr c = { 0u, 0u, 0u, 0u, 0u, 0u, 0u };
 	for (;;) {
 		/* the lane's two conditions once, as lane masks the branches below reuse */
 		const bool wk = w.node != RTX_NONE, hd = w.tgrp != 0;
@@ -617,16 +669,16 @@ __device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restri
 		const auto *e = cptr(lin) + i;
 		if (e->obj == emit_obj || !(tl >= 0.f))
 			continue;
-		if (far) { /* a far shade point: the object's world box first, from the light end (shadow walk) */
-			const f3 ow = tf_world_at(o, d, dist), iw = safe_inv_fast(mk3(-d.x, -d.y, -d.z));
-			float tn;
-			if (!slab(e->wlo[0], e->whi[0], e->wlo[1], e->whi[1], e->wlo[2], e->whi[2], mul3v(ow, iw), iw, dist, tn))
-				continue;
-		}
+		/* a far shade point: the object's world box first, from the light end like the walk */
+		if (RTX_SH_FARLIN == 1 && far &&
+		    !world_box_at(e->wlo[0], e->whi[0], e->wlo[1], e->whi[1], e->wlo[2], e->whi[2], o, d, dist, -1.f, dist))
+			continue;
 		bool h;
 		if (e->type == RTX_SPHERE) {
 			float t = 0.f;
-			h = hit_sphere(mk3(e->p0[0], e->p0[1], e->p0[2]), e->radius, o, d, e->eps, t) && t < tl;
+			h = (RTX_SH_FARLIN != 2 || !far ||
+			     world_box_at(e->wlo[0], e->whi[0], e->wlo[1], e->whi[1], e->wlo[2], e->whi[2], o, d, 0.f, 1.f, dist)) &&
+			    hit_sphere(mk3(e->p0[0], e->p0[1], e->p0[2]), e->radius, o, d, e->eps, t) && t < tl;
 		} else {
 			h = any_tri(mk3(e->p0[0], e->p0[1], e->p0[2]), mk3(e->e1[0], e->e1[1], e->e1[2]),
 				    mk3(e->e2[0], e->e2[1], e->e2[2]), o, d, e->eps, tl);
@@ -874,7 +926,8 @@ __device__ __forceinline__ QBvh make_qbvh(const KShadow &ks, const uint4 *top_q,
 	Q.t8 = t8;
 	Q.nt8 = (WALK == WALK_W8 && RTX_W8_TOP) ? min(uni(ks.w8top), (uint32_t)RTX_W8_TOP_MAX) : 0u;
 	Q.spill_stride = gridDim.x * blockDim.x;
-	Q.spill = WALK == WALK_W8 ? unip(ks.w8spill) + blockIdx.x * blockDim.x + threadIdx.x : nullptr;
+	Q.spill = WALK == WALK_W8 ? unip(ks.w8spill) : nullptr;
+	Q.spill_lane0 = blockIdx.x * blockDim.x + (RTX_SH_SPILL_UNI ? uni(threadIdx.x / WAVE) * WAVE : threadIdx.x);
 	Q.lstk = uni(ks.w8lstk);
 	Q.sph = uni(ks.w8sph) != 0;
 	Q.stk = stk;
@@ -949,7 +1002,11 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 	constexpr bool TOP = WALK == WALK_BVH2;
 	__shared__ uint4 top_q[TOP ? RTX_TOP_MAX : 1];    /* the top records (rtx_device.h RTX_QTOP_CUT) */
 	__shared__ uint32_t top_e[TOP ? RTX_TOP_MAX : 1]; /* cut records: the DQNode index after the subtree */
-	/* the wide walks' lane stacks */	__shared__ uint32_t wstk[RTX_SH_NW][WALK == WALK_W8 ? RTX_W8_STACK + RTX_W8_TQ : 1][WAVE];
+	/* the wide walks' lane stacks (16-byte aligned: the slot fold below reuses a wave's stack area as
+	 * float4 records, RTX_SH_SLOTFOLD) */
+	__shared__ __attribute__((aligned(16))) uint32_t wstk[RTX_SH_NW][WALK == WALK_W8 ? RTX_W8_STACK + RTX_W8_TQ : 1][WAVE];
+	static_assert(WALK != WALK_W8 || (RTX_W8_STACK + RTX_W8_TQ) * WAVE * sizeof(uint32_t) >= WAVE * sizeof(float4),
+		      "a wave's lane-stack area must hold one float4 per lane for the slot fold");
 	__shared__ KShadow ks_s; /* the arguments, one copy for the workgroup */
 	/* WALK_W8: the 8-wide tree's top levels (RTX_W8_TOP_LEVELS), read by divergent steps from LDS */
 	__shared__ uint4 t8[WALK == WALK_W8 && RTX_W8_TOP ? RTX_W8_TOP_MAX * 4 : 1];
@@ -977,7 +1034,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 	uint32_t *off = wt_w[wv].off, *nls = wt_w[wv].nls, *sid = wt_w[wv].sid;
 	float(*Ls)[WAVE] = wt_w[wv].Ls;
 	lds_u32 *stk = (lds_u32 *)&wstk[wv][0][lane_id()];
-	ShadowCount sc = { 0, 0, 0, 0, 0, 0, 0, 0, 0, 0 };
+	ShadowCount sc = { 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0 };
 	u64 rays_total = 0;
 	for (;;) {
 		reread_barrier();
@@ -1173,6 +1230,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 			atomicAdd(&ctr[RTX_C_SLEAFR], sc.lrounds);
 			atomicAdd(&ctr[RTX_C_SUNIF], sc.unif);
 			atomicAdd(&ctr[RTX_C_FARS], sc.far);
+			atomicAdd(&ctr[RTX_C_SSPILL], sc.spills);
 		}
 	}
 }

@@ -91,7 +91,6 @@ __device__ void trace_closest_bvh2(const DScene &S, uint32_t *stk, bool act, f3 
 				tc.far++;
 		}
 		const f3 oi = mul3v(ob, inv);
-		const f3 iw = safe_inv(d), oiw = mul3v(far ? tf_world_at(o, d, t0) : o, iw); /* far_sphere_box */
 		uint32_t ref = S.root_ref;
 		uint32_t sp = 0;
 		/* entries from RTX_TRACE_LSTK on live in HBM, [entry][grid lane]; lane addresses formed at
@@ -122,7 +121,7 @@ __device__ void trace_closest_bvh2(const DScene &S, uint32_t *stk, bool act, f3 
 					if ((__float_as_uint(c.w) >> 24) == RTX_SPHERE) {
 						if (COUNT)
 							tc.sph++;
-						h = (!far || far_sphere_box(mk3(a.x, a.y, a.z), b.x, oiw, iw, tbest - t0)) &&
+						h = (!far || far_sphere_box(mk3(a.x, a.y, a.z), b.x, o, d, t0, tbest - t0)) &&
 						    hit_sphere(mk3(a.x, a.y, a.z), b.x, o, d, a.w, t);
 					} else {
 						if (COUNT)
@@ -265,13 +264,8 @@ __device__ __forceinline__ void closest_walk8(const DScene &S, lds_u32 *stk, uin
 			if ((__float_as_uint(c.w) >> 24) == RTX_SPHERE) {
 				if (COUNT)
 					tc.sph++;
-				if (far) { /* rtx_math.h far_sphere_box */
-					const f3 iw = safe_inv_fast(d);
-					h = far_sphere_box(mk3(a.x, a.y, a.z), b.x, mul3v(tf_world_at(o, d, t0), iw), iw, tbest - t0) &&
-					    hit_sphere(mk3(a.x, a.y, a.z), b.x, o, d, a.w, t);
-				} else {
-					h = hit_sphere(mk3(a.x, a.y, a.z), b.x, o, d, a.w, t);
-				}
+				h = (!far || far_sphere_box(mk3(a.x, a.y, a.z), b.x, o, d, t0, tbest - t0)) && /* rtx_math.h */
+				    hit_sphere(mk3(a.x, a.y, a.z), b.x, o, d, a.w, t);
 			} else {
 				if (COUNT)
 					tc.tris++;
@@ -369,11 +363,10 @@ __device__ void trace_closest_w8(const DScene &S, uint32_t *stk, bool act, f3 o,
 		/* the emitters the tree leaves out, one by one (as the reference's tree holds them, a far
 		 * ray meets an emitter's box first: its world box from the origin shifted to t0 in double) */
 		if (act && S.w8noemit) {
-			const f3 ow = tf_world_at(o, d, t0), iw = safe_inv_fast(d), oiw = mul3v(ow, iw);
 			for (uint32_t i = 0; i < S.num_emitters; i++) {
 				const DEmitter &e = S.emitters[i];
-				float t = 0.f, tn;
-				if (far && !slab(e.wlo[0], e.whi[0], e.wlo[1], e.whi[1], e.wlo[2], e.whi[2], oiw, iw, tbest - t0, tn))
+				float t = 0.f;
+				if (far && !world_box_at(e.wlo[0], e.whi[0], e.wlo[1], e.whi[1], e.wlo[2], e.whi[2], o, d, t0, 1.f, tbest - t0))
 					continue;
 				bool h;
 				if (e.type == RTX_SPHERE)

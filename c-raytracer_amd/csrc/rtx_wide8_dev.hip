@@ -442,8 +442,8 @@ extern "C" hipError_t rtx_launch_w8_scalar(uint32_t n, const DW8 *w8, const uint
  * *depth_out = 0 when nothing is left or the tree exceeds RTX_W8_MAX_ENTRIES. */
 extern "C" hipError_t rtx_w8_collapse_device(const DNode *recs, uint32_t nnodes, uint32_t nb, const uint32_t *skip_obj,
 					     uint32_t num_objects, DW8 **w8_out, DW8S **w8s_out, uint32_t **leafmap_out,
-					     uint32_t *entries_out, uint32_t *depth_out, uint32_t *wide_out, uint32_t *top_out,
-					     float qo[3], float qs[3], hipStream_t st)
+					     uint32_t *entries_out, uint32_t *scalar_entries_out, uint32_t *depth_out,
+					     uint32_t *wide_out, uint32_t *top_out, float qo[3], float qs[3], hipStream_t st)
 {
 	hipError_t e = hipSuccess;
 	*w8_out = nullptr;
@@ -550,6 +550,7 @@ extern "C" hipError_t rtx_w8_collapse_device(const DNode *recs, uint32_t nnodes,
 		hst[2] = 0;
 		TRY(hipMemcpyAsync(items, &hst[1], 8, hipMemcpyHostToDevice, st));
 		uint32_t m = 1, blk = 2, depth = 0, wide = 0, top = 0;
+		uint32_t last = 2; /* where the last level's children start: every node entry lies below it */
 		while (m) {
 			if (blk + 8 * (size_t)m > RTX_W8_MAX_ENTRIES || blk + 8 * (size_t)m > cap) {
 				depth = 0;
@@ -567,6 +568,7 @@ extern "C" hipError_t rtx_w8_collapse_device(const DNode *recs, uint32_t nnodes,
 			TRY(hipStreamSynchronize(st));
 			wide += m;
 			depth++;
+			last = blk;
 			blk += 8 * m;
 			if (depth == RTX_W8_TOP_LEVELS - 1) /* every entry of levels 0 .. RTX_W8_TOP_LEVELS-1 */
 				top = blk;
@@ -578,10 +580,12 @@ extern "C" hipError_t rtx_w8_collapse_device(const DNode *recs, uint32_t nnodes,
 		/* exact-size buffers */
 		TRY(hipMalloc(&w8f, (size_t)blk * sizeof(DW8)));
 		TRY(hipMalloc(&lmf, (size_t)blk * 4));
-		TRY(hipMalloc(&w8s, (size_t)blk * sizeof(DW8S)));
+		/* the scalar copies only up to the last node entry: the deepest level's entries are leaves
+		 * (children of the last level's nodes), never read through the scalar path */
+		TRY(hipMalloc(&w8s, (size_t)last * sizeof(DW8S)));
 		TRY(hipMemcpyAsync(w8f, w8, (size_t)blk * sizeof(DW8), hipMemcpyDeviceToDevice, st));
 		TRY(hipMemcpyAsync(lmf, lm, (size_t)blk * 4, hipMemcpyDeviceToDevice, st));
-		hipLaunchKernelGGL(k_w8d_scalar, dim3((blk + W8D_T - 1) / W8D_T), dim3(W8D_T), 0, st, blk, w8f, lmf, w8s);
+		hipLaunchKernelGGL(k_w8d_scalar, dim3((last + W8D_T - 1) / W8D_T), dim3(W8D_T), 0, st, last, w8f, lmf, w8s);
 		TRY(hipGetLastError());
 		TRY(hipStreamSynchronize(st));
 		*w8_out = w8f;
@@ -591,6 +595,7 @@ extern "C" hipError_t rtx_w8_collapse_device(const DNode *recs, uint32_t nnodes,
 		w8s = nullptr;
 		lmf = nullptr;
 		*entries_out = blk;
+		*scalar_entries_out = last;
 		*top_out = std::min<uint32_t>(top ? top : blk, RTX_W8_TOP_MAX);
 		*depth_out = depth;
 		*wide_out = wide;

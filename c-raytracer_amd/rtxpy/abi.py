@@ -74,7 +74,8 @@ class Stats(C.Structure):
                 ("trace_walk", C.c_uint32), ("pad2_", C.c_uint32), ("tree_rotated", C.c_uint32),
                 ("pad3_", C.c_uint32), ("frame_cost", C.c_double), ("frame_ms", C.c_double),
                 ("upload_copy_ms", C.c_double), ("transport", C.c_uint32), ("peer_access", C.c_uint32),
-                ("far_closest_rays", C.c_uint64), ("far_shadow_rays", C.c_uint64)]
+                ("far_closest_rays", C.c_uint64), ("far_shadow_rays", C.c_uint64),
+                ("shadow_stack_spills", C.c_uint64)]
 
 
 RTX_TRANSPORT_NONE, RTX_TRANSPORT_RCCL, RTX_TRANSPORT_LOOPBACK = 0, 1, 2
@@ -243,3 +244,5 @@ def declare_oracle(lib):
     lib.rtx_oracle_render.restype = C.c_int
     lib.rtx_oracle_kat.argtypes = [C.c_int, C.c_uint32, C.c_void_p, C.c_void_p, C.POINTER(Params)]
     lib.rtx_oracle_kat.restype = C.c_int
+    lib.rtx_oracle_primary.argtypes = [C.POINTER(SceneDesc), C.POINTER(Frame), C.c_void_p, C.c_void_p, C.c_int]
+    lib.rtx_oracle_primary.restype = C.c_int

@@ -40,6 +40,18 @@ def render(scene, frame, params=None, threads=0):
     return rgb, z, (int(counts[0]), int(counts[1]))
 
 
+def primary(scene, frame, threads=0):
+    """the primary hits alone (rtx_oracle_primary): z as render() writes it for -b >= 1, and the hit
+    object's index (-1 on a miss); independent of the light samples"""
+    w, h = frame.width, frame.height
+    z = np.zeros((h, w), np.float32)
+    obj = np.zeros((h, w), np.int32)
+    rc = lib().rtx_oracle_primary(C.byref(scene.desc), C.byref(frame), z.ctypes.data, obj.ctypes.data, threads)
+    if rc != 0:
+        raise RtxError(rc, "oracle primary failed")
+    return z, obj
+
+
 def kat(kind, records, params=None):
     records = np.ascontiguousarray(records, dtype=np.float32).reshape(-1, abi.KAT_IN[kind])
     out = np.zeros((records.shape[0], abi.KAT_OUT[kind]), np.float32)

@@ -232,6 +232,8 @@ typedef struct rtx_stats {
 	 * objects, whose box tests start from a point formed in double near them (any tree frame) */
 	uint64_t far_closest_rays;        /* closest-hit rays (the frame origin moved along the ray) */
 	uint64_t far_shadow_rays;         /* shadow rays from far shade points (walked from the light end) */
+	uint64_t shadow_stack_spills;     /* only with count_traversal, 8-wide walk: lane-stack entries pushed beyond
+	                                   * the LDS ones (to HBM, DScene.w8spill) */
 } rtx_stats;
 
 typedef struct rtx_ctx rtx_ctx;

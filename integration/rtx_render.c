@@ -113,11 +113,27 @@ void accel_init(void)
 		error("%s", rtx_last_error());
 }
 
-/* render_init (render.c:61-116): the same flags into rtx_params */
+/* render_init (render.c:61-116): the same flags into rtx_params, plus the drop-in's own
+ * --rng const|counter|strat (the library's light-sample streams; const = every rand_flt() draw
+ * 0.5, the reference built with a constant rand()) and --seed N */
 void render_init(void)
 {
 	rtx_params_default(&params);
 	rtx_params_from_argv(myargc, myargv, &params);
+	int i = argv_check_with_args("--rng", 1);
+	if (i) {
+		if (!strcmp(myargv[i + 1], "const"))
+			params.rng = RTX_RNG_CONST;
+		else if (!strcmp(myargv[i + 1], "counter"))
+			params.rng = RTX_RNG_COUNTER;
+		else if (!strcmp(myargv[i + 1], "strat"))
+			params.rng = RTX_RNG_STRAT;
+		else
+			error("--rng %s: expected const, counter or strat.", myargv[i + 1]);
+	}
+	i = argv_check_with_args("--seed", 1);
+	if (i)
+		params.seed = strtoull(myargv[i + 1], NULL, 10);
 }
 
 /* render (render.c:345-368): the frame image_init (image.c:34-56) set up, into image.raster and

@@ -910,6 +910,49 @@ int rtx_oracle_render(const rtx_scene_desc *sc, const rtx_frame *fr, const rtx_p
 	return RTX_OK;
 }
 
+/*
+ * The primary hits alone (render.c:353-363's rays, get_closest_intersection render.c:118-124): the
+ * z-buffer render() writes for a frame with -b >= 1 (cast_ray returns the primary hit distance,
+ * render.c:342; 0 on a miss), and the hit object's index (-1 on a miss).  Independent of the
+ * light-sample stream, so a whole BASELINE frame's depth and hit mask can be checked at any spp.
+ */
+int rtx_oracle_primary(const rtx_scene_desc *sc, const rtx_frame *fr, float *z, int32_t *obj, int threads)
+{
+	if (!sc || !fr || !fr->width || !fr->height || !z)
+		return RTX_ERR_ARG;
+	oscene s;
+	int rc = build_scene(&s, sc);
+	if (rc) {
+		free_scene(&s);
+		return rc;
+	}
+	const uint32_t W = fr->width, H = fr->height;
+	const int nt = threads > 0 ? threads : omp_get_max_threads();
+#pragma omp parallel for num_threads(nt) schedule(dynamic, 4)
+	for (int64_t row = 0; row < (int64_t)H; row++) {
+		v3 pp;
+		mul3s(fr->step_y, (float)row, pp);
+		add3v(pp, fr->corner, pp);
+		for (uint32_t col = 0; col < W; col++) {
+			add3v(pp, fr->step_x, pp);
+			ray_t r;
+			assign3(r.point, fr->origin);
+			sub3v(pp, fr->origin, r.dir);
+			norm3(r.dir);
+			int32_t o = -1;
+			v3 n;
+			float t = FLT_MAX;
+			closest(&s, &r, &o, n, &t);
+			const size_t px = (size_t)row * W + col;
+			z[px] = o >= 0 ? t : 0.f;
+			if (obj)
+				obj[px] = o;
+		}
+	}
+	free_scene(&s);
+	return RTX_OK;
+}
+
 /* Per-function known answers (record layouts in rtx_kat.h). */
 int rtx_oracle_kat(int kind, uint32_t n, const float *in, float *out, const rtx_params *p)
 {

@@ -30,10 +30,11 @@ from rtxpy.dist import rank_tiles, tile_pixel_index
 
 CONFIGS = {
     # name: (scene, width, height, spp, oracle tile stride, GPU shard (offset, stride) or None)
-    "k2_scene3_1080p_n16": ("scene3", 1920, 1080, 16, 131, None),
-    "k3_scene5_1080p_n64": ("scene5", 1920, 1080, 64, 263, None),
+    # strides: 1 tile in 53 / 47 / 1048 (of the shard's, 1 in 131) / 199
+    "k2_scene3_1080p_n16": ("scene3", 1920, 1080, 16, 53, None),
+    "k3_scene5_1080p_n64": ("scene5", 1920, 1080, 64, 47, None),
     "k4_scene5_1080p_n256_shard0of8": ("scene5", 1920, 1080, 256, 8 * 131, (0, 8)),
-    "k5_scene6_2160p_n128": ("scene6", 3840, 2160, 128, 2003, None),
+    "k5_scene6_2160p_n128": ("scene6", 3840, 2160, 128, 199, None),
 }
 
 
@@ -89,6 +90,17 @@ def test_gpu_baseline_config_vs_oracle(renderer, cfg):
     info["sample_px"] = int(idx.size)
     print(cfg, info, "gpu rays", full.closest_rays, full.shadow_rays, "ms", round(full.kernel_ms, 1))
     assert ok, info
+    # the whole frame's (or shard's) depth and hit mask against the oracle's primary hits: z does not
+    # depend on the light samples (render.c:342, 364), so every pixel is checked at full size
+    pz, _ = oracle.primary(scene, frame)
+    sidx = sample_index(w, h, off, stride)
+    gz, oz = z.reshape(-1)[sidx], pz.reshape(-1)[sidx]
+    hit_mismatch = float(((gz > 0) != (oz > 0)).mean())
+    both = (gz > 0) & (oz > 0)
+    z_ok = float((np.abs(gz[both] - oz[both]) / np.maximum(oz[both], 1.0) <= 1e-4).mean())
+    print(cfg, "frame-wide", {"px": int(sidx.size), "hit_mismatch": hit_mismatch, "z_ok": z_ok,
+                              "z_equal": float((gz == oz).mean())})
+    assert hit_mismatch <= 1e-4 + 1.0 / sidx.size and z_ok >= 0.999, (hit_mismatch, z_ok)
     # the sharded render of exactly the oracle's tiles: bit-identical pixels, exact ray counts
     s_rgb, s_z = renderer.render(frame, params_for(spp, off, ostride))
     st = renderer.stats()

@@ -33,6 +33,11 @@ def renderer():
     r.close()
 
 
+def max_lights(scene):
+    """the most light samples one shade point can cast (the largest emitter's lights)"""
+    return max([int(o.num_lights) for o in scene.objects()] + [0])
+
+
 def render(renderer, scene, frame, params):
     renderer.upload(scene)
     rgb, z = renderer.render(frame, params)
@@ -196,8 +201,13 @@ def test_gpu_frame_vs_reference_ieee(renderer, name):
     ref_rgb, ref_z = C.golden_frame(name + "_o2")
     ok, info = C.compare_const(rgb, z, ref_rgb, ref_z)
     assert ok, info
-    assert abs(st.closest_rays - m["closest_rays_o2"]) <= 0.005 * m["closest_rays_o2"] + 16
-    assert abs(st.shadow_rays - m["shadow_rays_o2"]) <= 0.005 * m["shadow_rays_o2"] + 600
+    # the ray counts are the reference's (measured: equal on 17 of 18 frames).  The one mechanism
+    # that moves them: the reference's slab test (accel.c:112-158) is not conservative and ours is,
+    # so a ray grazing a leaf box's edge can find a primitive the reference's tree culls; each such
+    # ray adds or drops one cast_ray and its shade point's light samples (s5_amb: -1 and -300)
+    dc = st.closest_rays - m["closest_rays_o2"]
+    assert abs(dc) <= 1, dc
+    assert abs(st.shadow_rays - m["shadow_rays_o2"]) <= max_lights(scene) * abs(dc), (dc, st.shadow_rays)
 
 
 @pytest.mark.parametrize("name", CONST)
@@ -223,8 +233,8 @@ def test_gpu_vs_oracle_counter_rng(renderer, name, rng):
     o_rgb, o_z, (nc, ns) = oracle.render(scene, frame, params)
     ok, info = C.compare_const(rgb, z, o_rgb, o_z)
     assert ok, info
-    assert abs(st.closest_rays - nc) <= 0.005 * nc + 16
-    assert abs(st.shadow_rays - ns) <= 0.005 * ns + 600
+    # exact (measured on all 12 cases): the same stream on both sides, path-GI directions included
+    assert (st.closest_rays, st.shadow_rays) == (nc, ns)
 
 
 SEEDSETS = sorted(C.seed_manifest())
@@ -343,8 +353,15 @@ def test_gpu_edge_scene(renderer, args):
     o_rgb, o_z, (nc, ns) = oracle.render(scene, frame, params)
     ok, info = C.compare_const(rgb, z, o_rgb, o_z)
     assert ok, info
-    assert abs(st.closest_rays - nc) <= 0.005 * nc + 4
-    assert abs(st.shadow_rays - ns) <= 0.005 * ns + 100
+    # measured: +1 / +2 cast_rays and +37 light samples (one shade point under the 37-light
+    # triangle emitter) on three of the four flag sets; the mechanism of the frame tests above (a
+    # grazing ray the reference's non-conservative slab test culls and ours does not)
+    dc = st.closest_rays - nc
+    assert 0 <= dc <= 2, dc
+    if dc:
+        assert abs(st.shadow_rays - ns) <= max_lights(scene) * dc, (dc, st.shadow_rays, ns)
+    else:
+        assert st.shadow_rays == ns
 
 
 ONE_OBJECT_SCENE = """{
@@ -385,7 +402,8 @@ def test_gpu_one_bounded_object(renderer, builder, walk, args):
     ok, info = C.compare_const(rgb, z, o_rgb, o_z)
     assert ok, info
     assert st.bvh_nodes == 0 and st.bvh_prims == 1
-    assert ns > 0 and abs(st.shadow_rays - ns) <= 0.005 * ns + 100
+    dc = st.closest_rays - nc  # the frame tests' one mechanism (a grazing ray), at most one ray here
+    assert ns > 0 and abs(dc) <= 1 and abs(st.shadow_rays - ns) <= max_lights(scene) * abs(dc), (dc, st.shadow_rays, ns)
 
 
 def test_gpu_errors():

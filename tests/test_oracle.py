@@ -118,6 +118,17 @@ def test_frame_vs_reference_ofast(name):
     assert abs(ns - m["shadow_rays"]) <= 0.005 * m["shadow_rays"] + 600
 
 
+@pytest.mark.parametrize("name", [k for k in CONST if "_b0" not in k])
+def test_primary_mode_is_the_reference_z(name):
+    """rtx_oracle_primary (the primary hits alone, used for the frame-wide depth checks of the
+    BASELINE configs) writes exactly the z-buffer of the reference built at -O2"""
+    scene, frame, params, m = C.load_config(name)
+    z, obj = oracle.primary(scene, frame)
+    ref_rgb, ref_z = C.golden_frame(name + "_o2")
+    assert np.array_equal(z, ref_z)
+    assert np.array_equal(obj >= 0, ref_z > 0)
+
+
 def test_frame_b0_has_zero_z():
     # -b 0: the primary call itself has no bounces left, so every z is 0 (SURVEY Appendix A.4)
     scene, frame, params, m = C.load_config("s1_b0")

@@ -6,7 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=$1; shift
 OUT=gpurun_out/$TAG; mkdir -p "$OUT"; export TMPDIR=/tmp
-python3 tools/standins.py scene5 > /dev/null
+python3 tools/standins.py scene5 scene6 > /dev/null
 SETS=${SETS:-"sq:SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS"}
 for v in "$@"; do
   if [ "$v" = main ]; then lib=""; else lib=$PWD/c-raytracer_amd/lib/var/$v/librtx.so; fi
@@ -15,7 +15,7 @@ for v in "$@"; do
     name=${s%%:*}; ctrs=${s#*:}
     echo "=== $v $name ($(date +%T))"
     RTX_LIBRTX=$lib timeout -k 10 600 rocprofv3 --pmc $ctrs -d "$OUT/${v}_$name" -o run --output-format csv -- \
-      python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post > "$OUT/${v}_$name.log" 2>&1
+      python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-count --no-post ${PMCARGS:-} > "$OUT/${v}_$name.log" 2>&1
     rc=$?; echo "=== rc=$rc"; tail -2 "$OUT/${v}_$name.log"
     if [ $rc -ge 124 ]; then exit $rc; fi
   done
