@@ -52,7 +52,7 @@
 #define RTX_SH_FASTPOW 1 /* specular powf from v_log_f32 / v_exp_f32 (sh_pow) */
 #endif
 #ifndef RTX_SH_FARLIN
-#define RTX_SH_FARLIN 1 /* far shade points: objects tested one by one are culled by their world boxes first */
+#define RTX_SH_FARLIN 0 /* far shade points: objects tested one by one are culled by their world boxes first */
 #endif
 #ifndef RTX_SH_SPILL_UNI
 #define RTX_SH_SPILL_UNI 1 /* the lane-stack spill area addressed from a wave-uniform base */
@@ -216,13 +216,12 @@ struct QBvh {
 	const DW8S *w8s;      /* ... its nodes' scalar-path copies */
 	const uint4 *t8;      /* the workgroup's LDS copy of its entries [0, nt8) (top levels) */
 	uint32_t nt8;
-	uint32_t *spill;      /* the wave's lane-stack entries from lstk on: lane l's entry k at
-	                       * spill[(k - lstk) * spill_stride + spill_lane0 + l] (a wave-uniform base and a
-	                       * lane index formed at each use, no per-lane 64-bit pointer kept live) */
-	uint32_t spill_stride, spill_lane0;
+	uint32_t *spill;      /* the lane-stack entries from lstk on, [entry][grid lane] (w8_spill_at) */
+	uint32_t wv;          /* this wave's index in its workgroup */
 	uint32_t lstk;        /* lane-stack entries in LDS (<= RTX_W8_STACK) */
-	lds_u32 *stk;         /* this lane's LDS stack of sibling groups: entry k at stk[k * WAVE] */
-	lds_u32 *tq;          /* WALK_W8: this lane's LDS queue of deferred leaf groups, entry k at tq[k * WAVE] */
+	lds_u32 *stk;         /* the wave's LDS stacks of sibling groups: lane l's entry k at stk[k * WAVE + l]
+	                       * (RTX_W8_LANEADDR 0: this lane's, entry k at stk[k * WAVE]) */
+	lds_u32 *tq;          /* WALK_W8: the LDS queues of deferred leaf groups, likewise */
 	bool sph;             /* WALK_W8: the tree holds spheres (DScene.w8sph) */
 };
 
@@ -328,6 +327,11 @@ __device__ __forceinline__ void shadow_walk(const QBvh &Q, const char *__restric
 #ifndef RTX_W8_TRIONLY
 #define RTX_W8_TRIONLY 1 /* leaf tests of a tree without spheres skip the sphere case (DScene.w8sph) */
 #endif
+#ifndef RTX_W8_LANEADDR
+#define RTX_W8_LANEADDR 0 /* the lane-stack / queue LDS addresses formed from lane_id() at each access (no per-lane
+                           * address register live across the walk, which the allocator spilled to scratch) */
+#endif
+#define W8_LN (RTX_W8_LANEADDR ? lane_id() : 0u)
 #ifndef RTX_W8_LEAF2
 #define RTX_W8_LEAF2 1 /* a round of opaque leaf tests takes two of a lane's hit leaf slots */
 #endif
@@ -377,6 +381,17 @@ __device__ __forceinline__ bool w8_opaque_test(const char *pr, f3 o, f3 d, float
 	if (COUNT)
 		ntri++;
 	return any_tri(mk3(a.x, a.y, a.z), mk3(b.x, b.y, b.z), mk3(c.x, c.y, c.z), o, d, a.w, tl);
+}
+
+/* lane-stack entry k (>= Q.lstk) of this lane in HBM, [entry][grid lane]: its address formed where
+ * it is used, from the launch's constant block size, the workgroup's and wave's indices and
+ * lane_id() (volatile asm, so nothing of it is hoisted into the packet's set-up: round 5's
+ * per-lane spill pointer and round 6's first stride / lane-offset pair were computed per packet
+ * and spilled to scratch there, one 12-byte scratch store per lane and packet) */
+__device__ __forceinline__ uint32_t *w8_spill_at(const QBvh &Q, uint32_t k)
+{
+	constexpr uint32_t B = WAVE * RTX_SH_NW; /* k_shadow's block size (rtx_launch_shadow) */
+	return Q.spill + ((size_t)(k - Q.lstk) * ((size_t)gridDim.x * B) + (size_t)blockIdx.x * B + Q.wv * WAVE + lane_id());
 }
 
 /* the visit order of hit children: plain slot order (RTX_W8_SORDER 0), front to back from the
@@ -441,7 +456,7 @@ __device__ __forceinline__ void w8_iter(const QBvh &Q, f3 o, f3 d, f3 invq, f3 o
 			const char *pr = (const char *)(Q.w8 + (w.tgrp >> 8) + (__builtin_ctz(w.tgrp) ^ K));
 			w.tgrp &= w.tgrp - 1;
 			if (!(w.tgrp & 0xFFu))
-				w.tgrp = w.tn ? tq[--w.tn * WAVE] : 0u;
+				w.tgrp = w.tn ? tq[--w.tn * WAVE + W8_LN] : 0u;
 			/* RTX_W8_DEFER2: the lane's next queued leaf in the same round (the transmittance
 			 * products in the same order) */
 			const char *pr2 = nullptr;
@@ -449,7 +464,7 @@ __device__ __forceinline__ void w8_iter(const QBvh &Q, f3 o, f3 d, f3 invq, f3 o
 				pr2 = (const char *)(Q.w8 + (w.tgrp >> 8) + (__builtin_ctz(w.tgrp) ^ K));
 				w.tgrp &= w.tgrp - 1;
 				if (!(w.tgrp & 0xFFu))
-					w.tgrp = w.tn ? tq[--w.tn * WAVE] : 0u;
+					w.tgrp = w.tn ? tq[--w.tn * WAVE + W8_LN] : 0u;
 			}
 			if (!RTX_W8_TRIONLY || Q.sph) {
 				w8_defer_test<COUNT, true>(pr, o, d, tl, li, c.ntri, c.nsph);
@@ -508,7 +523,7 @@ __device__ __forceinline__ void w8_iter(const QBvh &Q, f3 o, f3 d, f3 invq, f3 o
 		if (dm) { /* transparent leaves: deferred */
 			const uint32_t g = (base << 8) | dm;
 			if (w.tgrp)
-				tq[w.tn++ * WAVE] = g;
+				tq[w.tn++ * WAVE + W8_LN] = g;
 			else
 				w.tgrp = g;
 		}
@@ -519,10 +534,9 @@ __device__ __forceinline__ void w8_iter(const QBvh &Q, f3 o, f3 d, f3 invq, f3 o
 			if (im) {
 				if (w.grp) {
 					if (w.sp < Q.lstk)
-						stk[w.sp * WAVE] = w.grp;
+						stk[w.sp * WAVE + W8_LN] = w.grp;
 					else {
-						gptrw(Q.spill)[(size_t)(w.sp - Q.lstk) * Q.spill_stride + Q.spill_lane0 +
-							       (RTX_SH_SPILL_UNI ? lane_id() : 0u)] = w.grp;
+						*w8_spill_at(Q, w.sp) = w.grp;
 						if (COUNT)
 							c.nspill++;
 					}
@@ -537,9 +551,8 @@ __device__ __forceinline__ void w8_iter(const QBvh &Q, f3 o, f3 d, f3 invq, f3 o
 				w.grp = 0;
 				if (w.sp) {
 					w.sp--;
-					w.grp = w.sp < Q.lstk ? stk[w.sp * WAVE]
-							      : gptr(Q.spill)[(size_t)(w.sp - Q.lstk) * Q.spill_stride + Q.spill_lane0 +
-									       (RTX_SH_SPILL_UNI ? lane_id() : 0u)];
+					w.grp = w.sp < Q.lstk ? stk[w.sp * WAVE + W8_LN]
+							      : *w8_spill_at(Q, w.sp);
 				}
 			}
 		} else {
@@ -844,18 +857,28 @@ __device__ __forceinline__ float sh_pow(float x, float y)
 	return rintf(h) != h ? -r : r;
 }
 
+/* the attenuation factor of a light sample at distance ldist (render.c:217-222), formed before
+ * the walk so one float, not ldist and dsq, lives across it (the product with the transmittance
+ * after the walk is the same operation in the same order) */
+__device__ __forceinline__ float sample_att(const KShadow &ks, float ldist, float dsq)
+{
+	const int32_t att = (int32_t)uni((uint32_t)ks.attenuation);
+	if (att == RTX_ATT_LIN)
+		return sh_rcp(ks.att_offset + ldist);
+	if (att == RTX_ATT_SQR)
+		return sh_rcp(ks.att_offset + dsq);
+	return 1.f;
+}
+
 /* direct-lighting terms of one unblocked light sample (render.c:199-228), read after the walk */
 template <bool UNI>
-__device__ __forceinline__ f3 shade_light(const KShadow &ks, const float4 *rec, f3 ldir, f3 li, float ldist, float dsq)
+__device__ __forceinline__ f3 shade_light(const KShadow &ks, const float4 *rec, f3 ldir, f3 li, float attf)
 {
 	const float4 q1 = sp_field<UNI>(rec, 1), q2 = sp_field<UNI>(rec, 2), q3 = sp_field<UNI>(rec, 3);
 	const f3 n = mk3(q1.x, q1.y, q1.z), dir = mk3(q2.x, q2.y, q2.z);
 	const float a = dot3(ldir, n);
-	const int32_t att = (int32_t)uni((uint32_t)ks.attenuation);
-	if (att == RTX_ATT_LIN)
-		li = mul3s(li, sh_rcp(ks.att_offset + ldist));
-	else if (att == RTX_ATT_SQR)
-		li = mul3s(li, sh_rcp(ks.att_offset + dsq));
+	if ((int32_t)uni((uint32_t)ks.attenuation) != RTX_ATT_NONE)
+		li = mul3s(li, attf);
 	f3 ks3;
 	float shin;
 	if (UNI) { /* the material of a wave-uniform record: scalar reads */
@@ -911,7 +934,7 @@ __device__ __forceinline__ DEmitter emitter_uni(const DEmitter *e)
 /* the shadow walks' view of the trees (QBvh) from the kernel arguments and the workgroup's LDS */
 template <int WALK>
 __device__ __forceinline__ QBvh make_qbvh(const KShadow &ks, const uint4 *top_q, const uint32_t *top_e, lds_u32 *stk,
-					  const uint4 *t8)
+					  const uint4 *t8, uint32_t wv)
 {
 	QBvh Q;
 	Q.q = unip(ks.qnodes);
@@ -925,9 +948,8 @@ __device__ __forceinline__ QBvh make_qbvh(const KShadow &ks, const uint4 *top_q,
 	Q.w8s = WALK == WALK_W8 ? unip(ks.w8s) : nullptr;
 	Q.t8 = t8;
 	Q.nt8 = (WALK == WALK_W8 && RTX_W8_TOP) ? min(uni(ks.w8top), (uint32_t)RTX_W8_TOP_MAX) : 0u;
-	Q.spill_stride = gridDim.x * blockDim.x;
 	Q.spill = WALK == WALK_W8 ? unip(ks.w8spill) : nullptr;
-	Q.spill_lane0 = blockIdx.x * blockDim.x + (RTX_SH_SPILL_UNI ? uni(threadIdx.x / WAVE) * WAVE : threadIdx.x);
+	Q.wv = wv;
 	Q.lstk = uni(ks.w8lstk);
 	Q.sph = uni(ks.w8sph) != 0;
 	Q.stk = stk;
@@ -940,7 +962,7 @@ __device__ __forceinline__ QBvh make_qbvh(const KShadow &ks, const uint4 *top_q,
  * and Phong / Blinn.  Argument-block fields are read from LDS behind reread barriers. */
 template <bool COUNT, int WALK, bool UNI>
 __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec, uint32_t idx, bool act, ShadowCount &sc,
-					   const uint4 *top_q, const uint32_t *top_e, lds_u32 *stk, const uint4 *t8)
+					   const uint4 *top_q, const uint32_t *top_e, lds_u32 *stk, const uint4 *t8, uint32_t wv)
 {
 	reread_barrier();
 	const float4 q0 = sp_field<UNI && RTX_SH_SPUNI>(rec, 0), q4 = sp_field<UNI && RTX_SH_SPUNI>(rec, 4);
@@ -978,7 +1000,8 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 		emitter_sample(ks, E, e, j, __float_as_uint(q4.y), __float_as_uint(q4.z), p, ldir, ldist, dsq, li);
 		eobj = E.obj;
 	}
-	const QBvh Q = make_qbvh<WALK>(ks, top_q, top_e, stk, t8);
+	const float attf = sample_att(ks, ldist, dsq);
+	const QBvh Q = make_qbvh<WALK>(ks, top_q, top_e, stk, t8, wv);
 	const bool have_tree = uni(ks.have_tree) != 0 && !RTX_DEBUG_NOWALK;
 	const bool blocked = shadow_query<COUNT, WALK>(Q, unip(ks.recs), unip(ks.mats), unip(ks.planes), uni(ks.num_planes),
 						 unip(ks.lin), uni(ks.num_lin), have_tree, ks.tf, act, far != 0, p, ldir, ldist, eobj, li,
@@ -986,7 +1009,7 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	reread_barrier();
 	f3 contribution = mk3(0.f, 0.f, 0.f);
 	if (act && !blocked)
-		contribution = shade_light<UNI && RTX_SH_SPUNI>(ks, rec, ldir, li, ldist, dsq);
+		contribution = shade_light<UNI && RTX_SH_SPUNI>(ks, rec, ldir, li, attf);
 	return contribution;
 }
 
@@ -1033,7 +1056,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 	KShadow &ks = ks_s;
 	uint32_t *off = wt_w[wv].off, *nls = wt_w[wv].nls, *sid = wt_w[wv].sid;
 	float(*Ls)[WAVE] = wt_w[wv].Ls;
-	lds_u32 *stk = (lds_u32 *)&wstk[wv][0][lane_id()];
+	lds_u32 *stk = (lds_u32 *)&wstk[wv][0][RTX_W8_LANEADDR ? 0u : lane_id()];
 	ShadowCount sc = { 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0 };
 	u64 rays_total = 0;
 	for (;;) {
@@ -1074,7 +1097,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 				f3 acc = mk3(0.f, 0.f, 0.f);
 				for (uint32_t base = 0; base < nl; base += WAVE) {
 					const uint32_t idx = base + lane_id();
-					acc = add3(acc, light_sample<COUNT, WALK, true>(ks, rec, idx, idx < nl, sc, top_q, top_e, stk, t8));
+					acc = add3(acc, light_sample<COUNT, WALK, true>(ks, rec, idx, idx < nl, sc, top_q, top_e, stk, t8, wv));
 				}
 				const float sx = wave_sum(acc.x), sy = wave_sum(acc.y), sz = wave_sum(acc.z);
 				if (lane_id() == 0) {
@@ -1108,7 +1131,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 				const uint32_t idx = ((slot - off[k]) << slot_lg) + (lane_id() & (slot_b - 1));
 				const bool act = slot < tot && idx < nls[k];
 				const float4 *rec = unip(ks.sp) + (size_t)sid[k] * SPREC;
-				const f3 contribution = light_sample<COUNT, WALK, false>(ks, rec, idx, act, sc, top_q, top_e, stk, t8);
+				const f3 contribution = light_sample<COUNT, WALK, false>(ks, rec, idx, act, sc, top_q, top_e, stk, t8, wv);
 				/* per-shade-point sums.  Each slot's B lanes reduce in a fixed butterfly (masks B/2 .. 1),
 				 * then the slot sums are added to their point's total one slot at a time in slot order, so a
 				 * point whose slots straddle packets gets the same sum whatever its neighbours (with one slot
