@@ -57,6 +57,9 @@
 #ifndef RTX_SH_SPILL_UNI
 #define RTX_SH_SPILL_UNI 1 /* the lane-stack spill area addressed from a wave-uniform base */
 #endif
+#ifndef RTX_SH_RECAFTER
+#define RTX_SH_RECAFTER 1 /* several points per packet: the record address formed again after the walk */
+#endif
 #ifndef RTX_SH_SPUNI
 #define RTX_SH_SPUNI 1 /* >= 64 lights: the shade-point record through scalar loads */
 #endif
@@ -328,10 +331,10 @@ __device__ __forceinline__ void shadow_walk(const QBvh &Q, const char *__restric
 #define RTX_W8_TRIONLY 1 /* leaf tests of a tree without spheres skip the sphere case (DScene.w8sph) */
 #endif
 #ifndef RTX_W8_LANEADDR
-#define RTX_W8_LANEADDR 0 /* the lane-stack / queue LDS addresses formed from lane_id() at each access (no per-lane
+#define RTX_W8_LANEADDR 2 /* the lane-stack / queue LDS addresses formed from lane_id() at each access (no per-lane
                            * address register live across the walk, which the allocator spilled to scratch) */
 #endif
-#define W8_LN (RTX_W8_LANEADDR ? lane_id() : 0u)
+#define W8_LN (LA ? lane_id() : 0u)
 #ifndef RTX_W8_LEAF2
 #define RTX_W8_LEAF2 1 /* a round of opaque leaf tests takes two of a lane's hit leaf slots */
 #endif
@@ -442,7 +445,7 @@ __device__ __forceinline__ bool w8_opaque_leaves(const DW8 *w8, uint32_t lm, uin
  * tests, or one node step with its opaque leaf tests (see shadow_walk8).  wk / hd: this lane has
  * node work / deferred tests; walking / holding: their ballots (at least one lane has one).  o / d: the
  * world ray; invq / oi: its inverse direction and origin term in the tree's 16-bit frame. */
-template <bool COUNT, int OCT>
+template <bool COUNT, int OCT, bool LA>
 __device__ __forceinline__ void w8_iter(const QBvh &Q, f3 o, f3 d, f3 invq, f3 oi, float &tl, f3 &li, W8Walk &w, W8Ctr &c,
 					bool wk, bool hd, u64 walking, u64 holding)
 {
@@ -536,7 +539,7 @@ __device__ __forceinline__ void w8_iter(const QBvh &Q, f3 o, f3 d, f3 invq, f3 o
 					if (w.sp < Q.lstk)
 						stk[w.sp * WAVE + W8_LN] = w.grp;
 					else {
-						*w8_spill_at(Q, w.sp) = w.grp;
+						*gptrw(w8_spill_at(Q, w.sp)) = w.grp;
 						if (COUNT)
 							c.nspill++;
 					}
@@ -552,7 +555,7 @@ __device__ __forceinline__ void w8_iter(const QBvh &Q, f3 o, f3 d, f3 invq, f3 o
 				if (w.sp) {
 					w.sp--;
 					w.grp = w.sp < Q.lstk ? stk[w.sp * WAVE + W8_LN]
-							      : *w8_spill_at(Q, w.sp);
+							      : *gptr(w8_spill_at(Q, w.sp));
 				}
 			}
 		} else {
@@ -613,7 +616,7 @@ template <bool COUNT> __device__ __forceinline__ void w8_count(W8Ctr c, ShadowCo
 	sc.walks += walks;
 }
 
-template <bool COUNT, int OCT>
+template <bool COUNT, int OCT, bool LA>
 __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__restrict__ mats, f3 o, f3 d, f3 ob, f3 inv,
 					     float &tl, uint32_t emit_obj, f3 &li, ShadowCount &sc)
 {
@@ -631,7 +634,7 @@ __device__ __forceinline__ void shadow_walk8(const QBvh &Q, const DMaterial *__r
 		const u64 holding = ballot(hd);
 		if (!(walking | holding))
 			break;
-		w8_iter<COUNT, OCT>(Q, o, d, invq, oi, tl, li, w, c, wk, hd, walking, holding);
+		w8_iter<COUNT, OCT, LA>(Q, o, d, invq, oi, tl, li, w, c, wk, hd, walking, holding);
 	}
 	w8_count<COUNT>(c, sc, 1u);
 }
@@ -658,7 +661,7 @@ __device__ __forceinline__ bool plane_blocks(f3 n, float dd, f3 o, f3 d, float e
 	return t > eps && t < dist;
 }
 
-template <bool COUNT, int WALK>
+template <bool COUNT, int WALK, bool LA>
 __device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restrict__ recs, const DMaterial *__restrict__ mats,
 					     const DPlane *__restrict__ planes, uint32_t num_planes, const DEmitter *__restrict__ lin,
 					     uint32_t num_lin, bool have_tree, const DTreeFrame &tf, bool act, bool far, f3 o, f3 d,
@@ -746,7 +749,7 @@ __device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restri
 #define RTX_WALK(K)                                                                            \
 	case K:                                                                                \
 		if (WALK == WALK_W8)                                                           \
-			shadow_walk8<COUNT, K>(Q, mats, o, d, ob, inv, tl, emit_obj, li, sc);  \
+			shadow_walk8<COUNT, K, LA>(Q, mats, o, d, ob, inv, tl, emit_obj, li, sc); \
 		else                                                                           \
 			shadow_walk<COUNT, K>(Q, recs, mats, o, d, ob, inv, tl, emit_obj, li, sc); \
 		break;
@@ -754,7 +757,7 @@ __device__ __forceinline__ bool shadow_query(const QBvh &Q, const char *__restri
 #undef RTX_WALK
 	default:
 		if (WALK == WALK_W8)
-			shadow_walk8<COUNT, 8>(Q, mats, o, d, ob, inv, tl, emit_obj, li, sc);
+			shadow_walk8<COUNT, 8, LA>(Q, mats, o, d, ob, inv, tl, emit_obj, li, sc);
 		else
 			shadow_walk<COUNT, 8>(Q, recs, mats, o, d, ob, inv, tl, emit_obj, li, sc);
 		break;
@@ -960,11 +963,16 @@ __device__ __forceinline__ QBvh make_qbvh(const KShadow &ks, const uint4 *top_q,
 /* one light sample per lane of the shade point `rec` (render.c:170-229): the light point of
  * sample idx (emitters in scene order, the hit object skipped), its shadow ray, attenuation
  * and Phong / Blinn.  Argument-block fields are read from LDS behind reread barriers. */
-template <bool COUNT, int WALK, bool UNI>
-__device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec, uint32_t idx, bool act, ShadowCount &sc,
+template <bool COUNT, int WALK, bool UNI, bool LA>
+__device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec_uni, uint32_t sidv, uint32_t idx, bool act, ShadowCount &sc,
 					   const uint4 *top_q, const uint32_t *top_e, lds_u32 *stk, const uint4 *t8, uint32_t wv)
 {
 	reread_barrier();
+	/* the shade point's record: wave-uniform (UNI), or this lane's record sidv, whose address is
+	 * formed again after the walk (the asm below) so only the 32-bit index lives across it: the
+	 * 64-bit address did, and the allocator spilled it to scratch around the generic-octant walk,
+	 * one store per packet (scene6: 43 GB of WRITE_SIZE per frame) */
+	const float4 *rec = UNI ? rec_uni : unip(ks.sp) + (size_t)sidv * SPREC;
 	const float4 q0 = sp_field<UNI && RTX_SH_SPUNI>(rec, 0), q4 = sp_field<UNI && RTX_SH_SPUNI>(rec, 4);
 	const f3 p = mk3(q0.x, q0.y, q0.z);
 	const uint32_t obj = __float_as_uint(q4.x) & ~RTX_SP_FAR, far = __float_as_uint(q4.x) & RTX_SP_FAR;
@@ -1003,10 +1011,14 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 	const float attf = sample_att(ks, ldist, dsq);
 	const QBvh Q = make_qbvh<WALK>(ks, top_q, top_e, stk, t8, wv);
 	const bool have_tree = uni(ks.have_tree) != 0 && !RTX_DEBUG_NOWALK;
-	const bool blocked = shadow_query<COUNT, WALK>(Q, unip(ks.recs), unip(ks.mats), unip(ks.planes), uni(ks.num_planes),
+	const bool blocked = shadow_query<COUNT, WALK, LA>(Q, unip(ks.recs), unip(ks.mats), unip(ks.planes), uni(ks.num_planes),
 						 unip(ks.lin), uni(ks.num_lin), have_tree, ks.tf, act, far != 0, p, ldir, ldist, eobj, li,
 							 sc);
 	reread_barrier();
+	if (!UNI && RTX_SH_RECAFTER) {
+		asm volatile("" : "+v"(sidv));
+		rec = unip(ks.sp) + (size_t)sidv * SPREC;
+	}
 	f3 contribution = mk3(0.f, 0.f, 0.f);
 	if (act && !blocked)
 		contribution = shade_light<UNI && RTX_SH_SPUNI>(ks, rec, ldir, li, attf);
@@ -1019,7 +1031,11 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec,
 /* Persistent workgroups of RTX_SH_NW waves.  A workgroup copies the threaded BVH's top levels
  * to LDS once; then each wave takes per_wave shade points at a time from a global queue
  * (RTX_C_SPQUEUE), in processing (Morton) order, until the points run out. */
-template <bool COUNT, int OCC, int WALK>
+/* PATH: 0 both packet layouts (a runtime branch on slot_b: the counting instances), 1 only the
+ * wave-uniform packets (slot_b = 64), 2 only the lane slots (slot_b < 64).  The product launches a
+ * kernel of one layout, so each gets a register allocation of its own: with both in one kernel a
+ * change to the slot loop moved the uniform loop's spills into its walk */
+template <bool COUNT, int OCC, int WALK, int PATH>
 __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 {
 	constexpr bool TOP = WALK == WALK_BVH2;
@@ -1056,7 +1072,11 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 	KShadow &ks = ks_s;
 	uint32_t *off = wt_w[wv].off, *nls = wt_w[wv].nls, *sid = wt_w[wv].sid;
 	float(*Ls)[WAVE] = wt_w[wv].Ls;
-	lds_u32 *stk = (lds_u32 *)&wstk[wv][0][RTX_W8_LANEADDR ? 0u : lane_id()];
+	/* the lane-stack addresses: per lane, or formed from lane_id() at each access (RTX_W8_LANEADDR; 2:
+	 * the lane-slot kernel only, whose allocation spilled the per-lane address and reloaded it at
+	 * every push and pop) */
+	constexpr bool LA = RTX_W8_LANEADDR == 2 ? PATH == 2 : RTX_W8_LANEADDR != 0;
+	lds_u32 *stk = (lds_u32 *)&wstk[wv][0][LA ? 0u : lane_id()];
 	ShadowCount sc = { 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0 };
 	u64 rays_total = 0;
 	for (;;) {
@@ -1086,7 +1106,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 		if (lane_id() == 0)
 			off[WAVE] = total;
 		lds_sync();
-		if (uni(ks.slot_b) == WAVE) {
+		if (PATH == 1 || (PATH == 0 && uni(ks.slot_b) == WAVE)) {
 			/* >= 64 lights: every packet is 64 samples of ONE shade point.  The point is wave-uniform
 			 * (its record is read once per packet through one address, no owner search), each lane
 			 * sums its samples over the point's packets, and one butterfly per point reduces them. */
@@ -1097,7 +1117,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 				f3 acc = mk3(0.f, 0.f, 0.f);
 				for (uint32_t base = 0; base < nl; base += WAVE) {
 					const uint32_t idx = base + lane_id();
-					acc = add3(acc, light_sample<COUNT, WALK, true>(ks, rec, idx, idx < nl, sc, top_q, top_e, stk, t8, wv));
+					acc = add3(acc, light_sample<COUNT, WALK, true, LA>(ks, rec, 0u, idx, idx < nl, sc, top_q, top_e, stk, t8, wv));
 				}
 				const float sx = wave_sum(acc.x), sy = wave_sum(acc.y), sz = wave_sum(acc.z);
 				if (lane_id() == 0) {
@@ -1130,8 +1150,8 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 				}
 				const uint32_t idx = ((slot - off[k]) << slot_lg) + (lane_id() & (slot_b - 1));
 				const bool act = slot < tot && idx < nls[k];
-				const float4 *rec = unip(ks.sp) + (size_t)sid[k] * SPREC;
-				const f3 contribution = light_sample<COUNT, WALK, false>(ks, rec, idx, act, sc, top_q, top_e, stk, t8, wv);
+				const f3 contribution = light_sample<COUNT, WALK, false, LA>(ks, nullptr, sid[k], idx, act, sc, top_q, top_e, stk,
+											 t8, wv);
 				/* per-shade-point sums.  Each slot's B lanes reduce in a fixed butterfly (masks B/2 .. 1),
 				 * then the slot sums are added to their point's total one slot at a time in slot order, so a
 				 * point whose slots straddle packets gets the same sum whatever its neighbours (with one slot
@@ -1395,10 +1415,10 @@ extern "C" hipError_t rtx_launch_kat_shadow(int kind, uint32_t n, const float *i
 /* ------------------------------------------------------------------------ */
 /* launcher (called from rtx_api.cpp)                                       */
 /* ------------------------------------------------------------------------ */
-template <bool C, int O, int W> static hipError_t shadow_slots(uint32_t cus, uint32_t *slots)
+template <bool C, int O, int W, int P> static hipError_t shadow_slots(uint32_t cus, uint32_t *slots)
 {
 	int per_cu = 0;
-	hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(&k_shadow<C, O, W>),
+	hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(&k_shadow<C, O, W, P>),
 								   WAVE * RTX_SH_NW, 0);
 	*slots = per_cu > 0 && cus > 0 ? (uint32_t)per_cu * cus : 1024u;
 	return e;
@@ -1406,15 +1426,26 @@ template <bool C, int O, int W> static hipError_t shadow_slots(uint32_t cus, uin
 
 /* the persistent grid: as many workgroups as are resident on the device at once (no more than
  * the work needs); the waves then share the shade points through RTX_C_SPQUEUE */
-template <bool C, int O, int W> static hipError_t launch_shadow(const KShadow &ka, uint32_t nw, uint32_t cus, hipStream_t stream)
+template <bool C, int O, int W, int P> static hipError_t launch_shadow_p(const KShadow &ka, uint32_t nw, uint32_t cus, hipStream_t stream)
 {
 	uint32_t slots = 0;
-	hipError_t e = shadow_slots<C, O, W>(cus, &slots);
+	hipError_t e = shadow_slots<C, O, W, P>(cus, &slots);
 	if (e != hipSuccess)
 		return e;
 	const uint32_t need = (nw + RTX_SH_NW - 1) / RTX_SH_NW;
-	hipLaunchKernelGGL((k_shadow<C, O, W>), dim3(need < slots ? need : slots), dim3(WAVE * RTX_SH_NW), 0, stream, ka);
+	hipLaunchKernelGGL((k_shadow<C, O, W, P>), dim3(need < slots ? need : slots), dim3(WAVE * RTX_SH_NW), 0, stream, ka);
 	return hipGetLastError();
+}
+/* the counting instances keep both layouts in one kernel; the product picks the layout's own */
+template <bool C, int O, int W> static hipError_t launch_shadow(const KShadow &ka, uint32_t nw, uint32_t cus, hipStream_t stream)
+{
+	if constexpr (C) {
+		return launch_shadow_p<C, O, W, 0>(ka, nw, cus, stream);
+	} else {
+		if (ka.slot_b == WAVE)
+			return launch_shadow_p<C, O, W, 1>(ka, nw, cus, stream);
+		return launch_shadow_p<C, O, W, 2>(ka, nw, cus, stream);
+	}
 }
 
 template <int W> static hipError_t launch_walk(const KShadow &ka, uint32_t nw, uint32_t cus, int count, hipStream_t stream)
@@ -1436,14 +1467,20 @@ static int walk_of(const DScene *S) { return S->w8 ? WALK_W8 : WALK_BVH2; }
 /* grid lanes of the largest k_shadow launch on `cus` CUs (sizes the 8-wide walk's spill area) */
 extern "C" hipError_t rtx_shadow_grid_lanes(uint32_t cus, uint32_t *lanes)
 {
-	uint32_t a = 0, b = 0;
-	hipError_t e = shadow_slots<false, RTX_SHADOW_OCC_DEFAULT, WALK_W8>(cus, &a);
+	uint32_t a = 0, b = 0, a2 = 0;
+	hipError_t e = shadow_slots<false, RTX_SHADOW_OCC_DEFAULT, WALK_W8, 1>(cus, &a);
 	if (e == hipSuccess)
-		e = shadow_slots<true, 1, WALK_W8>(cus, &b);
+		e = shadow_slots<false, RTX_SHADOW_OCC_DEFAULT, WALK_W8, 2>(cus, &a2);
+	a = a > a2 ? a : a2;
+	if (e == hipSuccess)
+		e = shadow_slots<true, 1, WALK_W8, 0>(cus, &b);
 #if RTX_MEASURE
-	uint32_t c = 0;
+	uint32_t c = 0, c2 = 0;
 	if (e == hipSuccess)
-		e = shadow_slots<false, 1, WALK_W8>(cus, &c);
+		e = shadow_slots<false, 1, WALK_W8, 1>(cus, &c);
+	if (e == hipSuccess)
+		e = shadow_slots<false, 1, WALK_W8, 2>(cus, &c2);
+	c = c > c2 ? c : c2;
 	b = b > c ? b : c;
 #endif
 	*lanes = (a > b ? a : b) * WAVE * RTX_SH_NW;
