@@ -22,6 +22,12 @@
  * rtx_group_open_loopback: n shards as n contexts on one device, the gather a device-to-device
  * copy instead of RCCL; the rest of the path is the one above (tests/test_gpu_group.py runs it
  * at n = 2, 3, 8 on a one-GPU box against rtx_render).
+ *
+ * rtx_group_open_rccl_self: the other half a one-GPU box can check, the RCCL calls themselves.
+ * One device with a one-rank communicator (ncclCommInitAll); the gather packs shard 0 too and
+ * moves it through the same grouped ncclSend / ncclRecv (rank 0 to itself) into a receive buffer
+ * filled with NaN bytes beforehand, then unpacks it over the frame, so the image is the
+ * one-device image only if RCCL delivered every record.
  */
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -50,11 +56,12 @@ extern "C" hipError_t rtx_launch_tile_unpack(const float4 *in, uint32_t w, uint3
 struct rtx_group {
 	int n = 0;
 	bool loopback = false;         /* rtx_group_open_loopback: every context on one device */
+	bool rccl_self = false;        /* rtx_group_open_rccl_self: shard 0 sent to itself over RCCL */
 	std::vector<uint32_t> peer;    /* peer access between device r and device 0 enabled */
 	std::vector<rtx_ctx *> ctx;
-	std::vector<ncclComm_t> comm;  /* n > 1: one per device, rank r = ctx[r] */
-	std::vector<float4 *> d_buf;   /* r > 0: shard r's packed records on device r */
-	std::vector<float4 *> d_recv;  /* r > 0: shard r's records received on device 0 */
+	std::vector<ncclComm_t> comm;  /* n > 1 or rccl_self: one per device, rank r = ctx[r] */
+	std::vector<float4 *> d_buf;   /* r > 0 (rccl_self: r = 0): shard r's packed records on device r */
+	std::vector<float4 *> d_recv;  /* the same shards' records received on device 0 */
 	std::vector<size_t> buf_cap;   /* capacity of d_buf[r] in records */
 	std::vector<size_t> recv_cap;  /* capacity of d_recv[r] in records */
 	rtx_stats stats{};
@@ -190,6 +197,26 @@ extern "C" int rtx_group_open_loopback(int n, int device, rtx_group **out)
 		g->ctx[r]->mem_share = (uint32_t)n; /* the n contexts render on this one device at once */
 	}
 	*out = g;
+	return RTX_OK;
+}
+
+extern "C" int rtx_group_open_rccl_self(int device, rtx_group **out)
+{
+	int rc = rtx_group_open(1, &device, out);
+	if (rc)
+		return rc;
+	rtx_group *g = *out;
+	DeviceGuard keep;
+	g->comm.assign(1, nullptr);
+	ncclResult_t e = ncclCommInitAll(g->comm.data(), 1, &device);
+	if (e != ncclSuccess) {
+		g->comm.assign(1, nullptr);
+		rtx_group_close(g);
+		*out = nullptr;
+		return fail(RTX_ERR_HIP, "ncclCommInitAll on device %d failed: %s", device, ncclGetErrorString(e));
+	}
+	g->rccl_self = true;
+	g->ctx[0]->stats.transport = RTX_TRANSPORT_RCCL_SELF;
 	return RTX_OK;
 }
 
@@ -408,9 +435,10 @@ extern "C" int rtx_group_render(rtx_group *g, const rtx_frame *fr, const rtx_par
 
 	const auto tg0 = std::chrono::steady_clock::now();
 	rtx_ctx *c0 = g->ctx[0];
-	if (n > 1) {
+	const int r0 = g->rccl_self ? 0 : 1; /* the first shard that travels */
+	if (n > 1 || g->rccl_self) {
 		/* pack on every shard device, then one grouped send/recv to device 0 */
-		for (int r = 1; r < n; r++) {
+		for (int r = r0; r < n; r++) {
 			rtx_ctx *c = g->ctx[r];
 			const size_t recs = rtx_tile_pack_count(w, h, (uint32_t)r, (uint32_t)n);
 			/* each buffer keeps its own capacity, so a failed allocation (capacity 0, null
@@ -435,8 +463,12 @@ extern "C" int rtx_group_render(rtx_group *g, const rtx_frame *fr, const rtx_par
 				HIP_TRY(hipStreamSynchronize(g->ctx[r]->stream));
 			}
 		} else {
+			if (g->rccl_self) { /* what RCCL does not deliver stays NaN and fails the comparison */
+				HIP_TRY(hipSetDevice(c0->device));
+				HIP_TRY(hipMemsetAsync(g->d_recv[0], 0xFF, rtx_tile_pack_count(w, h, 0, 1) * sizeof(float4), c0->stream));
+			}
 			NCCL_TRY(ncclGroupStart());
-			for (int r = 1; r < n; r++) {
+			for (int r = r0; r < n; r++) {
 				const size_t floats = rtx_tile_pack_count(w, h, (uint32_t)r, (uint32_t)n) * 4;
 				if (!floats)
 					continue;
@@ -446,7 +478,7 @@ extern "C" int rtx_group_render(rtx_group *g, const rtx_frame *fr, const rtx_par
 			NCCL_TRY(ncclGroupEnd());
 		}
 		HIP_TRY(hipSetDevice(c0->device));
-		for (int r = 1; r < n; r++)
+		for (int r = r0; r < n; r++)
 			HIP_TRY(rtx_launch_tile_unpack(g->d_recv[r], w, h, (uint32_t)r, (uint32_t)n, c0->d_rgb, c0->d_z, c0->stream));
 		for (int r = 1; r < n; r++) {
 			HIP_TRY(hipSetDevice(g->ctx[r]->device));
@@ -496,7 +528,7 @@ extern "C" int rtx_group_render(rtx_group *g, const rtx_frame *fr, const rtx_par
 		s.upload_copy_ms = std::max(s.upload_copy_ms, o.upload_copy_ms);
 		s.peer_access = s.peer_access && o.peer_access;
 	}
-	s.gather_ms = n > 1 ? gather_ms : 0.0;
+	s.gather_ms = n > 1 || g->rccl_self ? gather_ms : 0.0;
 	s.devices = (uint32_t)n;
 	g->stats = s;
 	return RTX_OK;

@@ -66,6 +66,9 @@
 #ifndef RTX_SHADOW_OCC_DEFAULT
 #define RTX_SHADOW_OCC_DEFAULT 8 /* waves per SIMD the walk is register-capped for */
 #endif
+#ifndef RTX_SHADOW_OCC_SLOT
+#define RTX_SHADOW_OCC_SLOT RTX_SHADOW_OCC_DEFAULT /* the same for the lane-slot kernel */
+#endif
 /* light_point (object.c:293-304) in k_shadow: a sphere light's inclination and azimuth are
  * u * 2pi, so their sines and cosines come from the revolution-scaled v_sin_f32 / v_cos_f32
  * instead of OCML's range-reduced sinf / cosf.  KAT: RTX_KAT_SPH_LIGHT_SH, <= 4e-6 of the
@@ -1444,7 +1447,7 @@ template <bool C, int O, int W> static hipError_t launch_shadow(const KShadow &k
 	} else {
 		if (ka.slot_b == WAVE)
 			return launch_shadow_p<C, O, W, 1>(ka, nw, cus, stream);
-		return launch_shadow_p<C, O, W, 2>(ka, nw, cus, stream);
+		return launch_shadow_p<C, O == RTX_SHADOW_OCC_DEFAULT ? RTX_SHADOW_OCC_SLOT : O, W, 2>(ka, nw, cus, stream);
 	}
 }
 
@@ -1470,7 +1473,7 @@ extern "C" hipError_t rtx_shadow_grid_lanes(uint32_t cus, uint32_t *lanes)
 	uint32_t a = 0, b = 0, a2 = 0;
 	hipError_t e = shadow_slots<false, RTX_SHADOW_OCC_DEFAULT, WALK_W8, 1>(cus, &a);
 	if (e == hipSuccess)
-		e = shadow_slots<false, RTX_SHADOW_OCC_DEFAULT, WALK_W8, 2>(cus, &a2);
+		e = shadow_slots<false, RTX_SHADOW_OCC_SLOT, WALK_W8, 2>(cus, &a2);
 	a = a > a2 ? a : a2;
 	if (e == hipSuccess)
 		e = shadow_slots<true, 1, WALK_W8, 0>(cus, &b);

@@ -302,12 +302,16 @@ def gpu_kat(kind, records, params=None):
 class Group:
     """Several HIP devices rendering one frame (rtx_group_open .. rtx_group_close): tiles dealt
     round-robin over the devices, gathered to the first one over RCCL.  loopback=n: n shards as
-    n contexts on device devices[0] (rtx_group_open_loopback, the test transport)."""
+    n contexts on device devices[0] (rtx_group_open_loopback, the test transport).  rccl_self:
+    one device whose shard still travels through RCCL, to itself (rtx_group_open_rccl_self)."""
 
-    def __init__(self, devices, loopback=None):
+    def __init__(self, devices, loopback=None, rccl_self=False):
         self.lib = rtx_lib()
         self._g = C.c_void_p()
-        if loopback:
+        if rccl_self:
+            _check(self.lib.rtx_group_open_rccl_self(int(devices[0]), C.byref(self._g)))
+            self.devices = [devices[0]]
+        elif loopback:
             _check(self.lib.rtx_group_open_loopback(int(loopback), int(devices[0]), C.byref(self._g)))
             self.devices = [devices[0]] * int(loopback)
         else:

@@ -78,7 +78,7 @@ class Stats(C.Structure):
                 ("shadow_stack_spills", C.c_uint64)]
 
 
-RTX_TRANSPORT_NONE, RTX_TRANSPORT_RCCL, RTX_TRANSPORT_LOOPBACK = 0, 1, 2
+RTX_TRANSPORT_NONE, RTX_TRANSPORT_RCCL, RTX_TRANSPORT_LOOPBACK, RTX_TRANSPORT_RCCL_SELF = 0, 1, 2, 3
 
 
 class GroupMember(C.Structure):
@@ -119,7 +119,7 @@ KAT_NAMES = ["moller", "sphere", "plane", "slab", "noise", "texture", "sph_light
 # symbols include/rtx.h declares (checked by tests/test_abi.py)
 RTX_SYMBOLS = ["rtx_params_default", "rtx_device_count", "rtx_open", "rtx_upload_scene", "rtx_render",
                "rtx_render_device", "rtx_get_stats", "rtx_close", "rtx_last_error", "rtx_kat", "rtx_postprocess",
-               "rtx_postprocess_device", "rtx_set_builder", "rtx_set_option", "rtx_group_open", "rtx_group_open_loopback", "rtx_group_size", "rtx_read_wide_tree",
+               "rtx_postprocess_device", "rtx_set_builder", "rtx_set_option", "rtx_group_open", "rtx_group_open_loopback", "rtx_group_open_rccl_self", "rtx_group_size", "rtx_read_wide_tree",
                "rtx_group_set_builder", "rtx_group_set_option", "rtx_group_upload_scene", "rtx_group_render", "rtx_group_get_stats", "rtx_group_device_stats",
                "rtx_group_member_info", "rtx_group_close", "rtx_tile_pack_count", "rtx_tile_pack_host", "rtx_tile_unpack_host",
                "rtx_tile_pack_device", "rtx_tile_unpack_device", "rtx_tree_frame"]
@@ -201,6 +201,8 @@ def declare_rtx(lib):
     lib.rtx_read_wide_tree.restype = C.c_int
     lib.rtx_group_open_loopback.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_void_p)]
     lib.rtx_group_open_loopback.restype = C.c_int
+    lib.rtx_group_open_rccl_self.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+    lib.rtx_group_open_rccl_self.restype = C.c_int
     lib.rtx_group_size.argtypes = [C.c_void_p]
     lib.rtx_group_size.restype = C.c_int
     lib.rtx_group_set_builder.argtypes = [C.c_void_p, C.c_int]

@@ -324,7 +324,7 @@ int rtx_read_wide_tree(rtx_ctx *ctx, void *entries, uint32_t capacity, uint32_t 
  * host thread calls the group; it must not be shared.
  */
 typedef struct rtx_group rtx_group;
-enum { RTX_TRANSPORT_NONE = 0, RTX_TRANSPORT_RCCL = 1, RTX_TRANSPORT_LOOPBACK = 2 };
+enum { RTX_TRANSPORT_NONE = 0, RTX_TRANSPORT_RCCL = 1, RTX_TRANSPORT_LOOPBACK = 2, RTX_TRANSPORT_RCCL_SELF = 3 };
 
 /* n devices: devices[0..n-1], or 0..n-1 when devices is NULL (each must be gfx950, distinct) */
 int rtx_group_open(int n, const int *devices, rtx_group **out);
@@ -333,6 +333,11 @@ int rtx_group_open(int n, const int *devices, rtx_group **out);
  * thread per shard, tile pack, unpack, statistics) except the gather, which is a device-to-device
  * copy in place of RCCL send/recv.  Lets a one-GPU machine check rtx_group_render at any n. */
 int rtx_group_open_loopback(int n, int device, rtx_group **out);
+/* Test transport: a group of ONE device whose gather still runs the RCCL calls: a one-rank
+ * communicator (ncclCommInitAll), shard 0 packed, sent to itself with the grouped ncclSend /
+ * ncclRecv of rtx_group_render into a NaN-filled buffer and unpacked over the frame.  Lets a
+ * one-GPU machine execute the group's RCCL code; the image must equal rtx_render's. */
+int rtx_group_open_rccl_self(int device, rtx_group **out);
 int rtx_group_size(const rtx_group *g);
 int rtx_group_set_builder(rtx_group *g, int builder);
 int rtx_group_set_option(rtx_group *g, int option, int64_t value); /* rtx_set_option on every device */

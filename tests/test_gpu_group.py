@@ -14,9 +14,13 @@ summed over the shards; only the transport differs (a device-to-device copy inst
 RCCL ncclSend / ncclRecv).  The frame must equal rtx_render's bit for bit, with equal summed ray
 counts (render.c:349-352 is the parallel point the shards replace).
 
-NOT exercised here: RCCL itself and peer copies between distinct devices (this box has one GPU,
-and the driver's 8-GPU runs have been skipped for want of a node).  What stands in for them: the
-loopback group above, the record layout on the host (tests/test_gather.py), the same records
+The RCCL calls themselves run through rtx_group_open_rccl_self: one device with a one-rank
+communicator, whose whole frame is packed, sent to itself by the group's grouped ncclSend /
+ncclRecv into a NaN-filled buffer and unpacked.
+
+NOT exercised here: RCCL between distinct devices and peer copies (this box has one GPU, and the
+driver's 8-GPU runs have been skipped for want of a node).  What stands in for them: the two
+transports above, the record layout on the host (tests/test_gather.py), the same records
 gathered over torch.distributed with gloo (tests/test_distributed.py), and the group line's
 schema (tests/test_bench_cli.py).
 """
@@ -133,6 +137,34 @@ def test_gpu_loopback_group_matches_render(name, n):
             (sa.wide_nodes, sa.wide_entries, sa.wide_depth, sa.bvh_nodes, sa.tree_rotated, sa.shadow_walk)
         assert (p.upload_copy_ms > 0.0) == (k > 0)
         assert p.closest_rays > 0
+
+
+@pytest.mark.parametrize("name", ["s5_path2", "s3_path2"])
+def test_gpu_rccl_self_group_matches_render(name):
+    """The group's RCCL code on one GPU (rtx_group_open_rccl_self): a one-rank communicator, the
+    whole frame packed, sent to itself by the grouped ncclSend / ncclRecv into a NaN-filled buffer
+    and unpacked over the frame.  The image is rtx_render's bit for bit only if RCCL delivered
+    every record; the member reads its communicator back (count 1, rank 0, its own device)."""
+    scene, frame, params, _ = C.load_config(name)
+    r = rtxpy.Renderer(0)
+    r.upload(scene)
+    a, za = r.render(frame, params)
+    sa = r.stats()
+    r.close()
+    g = rtxpy.Group([0], rccl_self=True)
+    assert g.size() == 1
+    m = g.member(0)
+    assert (m["comm_count"], m["comm_rank"], m["comm_device"], m["device"]) == (1, 0, 0, 0)
+    assert m["transport"] == abi.RTX_TRANSPORT_RCCL_SELF
+    g.upload(scene)
+    b, zb = g.render(frame, params)
+    sb = g.stats()
+    b2, zb2 = g.render(frame, params)
+    g.close()
+    assert np.array_equal(a, b) and np.array_equal(za, zb)
+    assert np.array_equal(b, b2) and np.array_equal(zb, zb2)
+    assert (sb.closest_rays, sb.shadow_rays) == (sa.closest_rays, sa.shadow_rays)
+    assert sb.gather_ms > 0.0 and sb.transport == abi.RTX_TRANSPORT_RCCL_SELF
 
 
 def test_gpu_loopback_group_sharding_of_a_tall_ragged_frame():
