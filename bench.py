@@ -52,6 +52,10 @@ SHADOW_SRCS = ["c-raytracer_amd/csrc/rtx_shadow.hip", "c-raytracer_amd/csrc/rtx_
                "c-raytracer_amd/csrc/rtx_math.h", "c-raytracer_amd/csrc/rtx_device.h", "include/rtx_rng.h"]
 
 
+CPU_AT_N1 = ("cpu_baseline is timed on rank 0 of the N = 1 run only (the same workload on one GPU: "
+             "python bench.py --gpus 1); an N > 1 line leaves it null")
+
+
 def shadow_src_sha():
     """sha1 over k_shadow's sources with comments and blank space stripped: ties a committed PMC
     summary to the kernel code it measured (a comment edit keeps the tie, a code edit breaks it)"""
@@ -782,13 +786,13 @@ def main():
             log(f"postprocess leg failed: {e}")
 
     if world > 1:
-        # the GPU work is done: every rank leaves the process group, and rank 0 alone times the
-        # reference CPU leg below (the other ranks exit, leaving the host cores to it)
+        # the GPU work is done: every rank leaves the process group
         r.close()
         r = None
         torch.distributed.destroy_process_group()
     cpu = port = None
-    if rank == 0 and not a.no_cpu_baseline:
+    # the CPU baseline is timed on rank 0 at N = 1 only; the N > 1 lines point to that line
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
             cpu = cpu_reference(path, flags, a.width, a.height, a.cpu_target_s, log)
         except Exception as e:  # never let the baseline kill the measurement
@@ -823,6 +827,8 @@ def main():
                "roofline": roofline, "cpu_baseline": cpu}
         if gat is not None:
             out["config"]["gather_message_bytes_per_rank"] = gat.message_bytes
+        if world > 1:
+            out["cpu_baseline_note"] = CPU_AT_N1
         if validation is not None:
             out["validation"] = validation
         if rehearse:
@@ -880,8 +886,9 @@ def group_line(a, n, scene_name, objects, elapsed, rays, closest, per_dev, gathe
                       "upload": upload},
             "roofline": roofline,
             "cpu_baseline": cpu,
-            "cpu_baseline_note": "the reference's own CPU path on this box's host cores, timed after the GPU steps "
-                                 "(the same measurement as the N=1 line's)"}
+            "cpu_baseline_note": CPU_AT_N1 if cpu is None else
+                                 "the reference's own CPU path on this box's host cores, timed after the GPU steps "
+                                 "(the loopback rehearsal runs on one GPU, so it carries the N = 1 baseline)"}
 
 
 def group_validation(a, g, n, scene, frame, params, h_rgb, h_z, frame_rays, log):
@@ -1015,7 +1022,7 @@ def main_group(a):
               "peer_copy_ms": [round(g.device_stats(r).upload_copy_ms, 1) for r in range(n)]}
     g.close()
     cpu = None
-    if not a.no_cpu_baseline:
+    if a.loopback and not a.no_cpu_baseline:  # N > 1 devices: the baseline belongs to the N = 1 line
         try:
             cpu = cpu_reference(path, flags, a.width, a.height, a.cpu_target_s, log)
         except Exception as e:  # never let the baseline kill the measurement
