@@ -188,11 +188,16 @@ __device__ void trace_closest_bvh2(const DScene &S, uint32_t *stk, bool act, f3 
 #ifndef RTX_TRACE_EMPTYCOUNT
 #define RTX_TRACE_EMPTYCOUNT 0 /* measurement builds: count only the visits that hit no child */
 #endif
-template <bool COUNT, int OCT>
+/* FAR: some lane of the wave has a far origin (t0 and the per-lane far flag live across the walk);
+ * the other instances take t0 = 0 and no far lane as constants, so the waves of near rays (all of
+ * them in the reference scenes' views) keep those registers for the walk */
+template <bool COUNT, int OCT, bool FAR>
 __device__ __forceinline__ void closest_walk8(const DScene &S, lds_u32 *stk, uint32_t *ostk, size_t ostride, f3 o, f3 d,
-					      f3 ob, f3 inv, float t0, bool far, float &tbest, uint32_t &hid,
+					      f3 ob, f3 inv, float t0_, bool far_, float &tbest, uint32_t &hid,
 					      TraceCount &tc)
 {
+	const float t0 = FAR ? t0_ : 0.f;
+	const bool far = FAR && far_;
 	/* the lane stack: stk / ostk are the wave's bases (LDS, then HBM [entry][grid lane]); a lane's
 	 * address is formed at each use (lane_id), none kept live across the walk */
 	uint32_t sp = 0;
@@ -386,17 +391,20 @@ __device__ void trace_closest_w8(const DScene &S, uint32_t *stk, bool act, f3 o,
 				     (((~__float_as_uint(inv.z)) >> 31) << 2);
 		const uint32_t lead = readlane(oct, (uint32_t)__ffsll((long long)live) - 1);
 		const uint32_t sel = ballot(act & (oct != lead)) ? 8u : lead;
-		if (act) {
+		const bool anyfar = ballot(far) != 0;
+		if (act && anyfar) {
+			closest_walk8<COUNT, 8, true>(S, ls, ostk, ostride, o, d, ob, inv, t0, far, tbest, hid, tc);
+		} else if (act) {
 			switch (sel) {
-#define RTX_CWALK(K)                                                                    \
-	case K:                                                                             \
-		closest_walk8<COUNT, K>(S, ls, ostk, ostride, o, d, ob, inv, t0, far, tbest, hid, tc); \
+#define RTX_CWALK(K)                                                                           \
+	case K:                                                                                    \
+		closest_walk8<COUNT, K, false>(S, ls, ostk, ostride, o, d, ob, inv, t0, far, tbest, hid, tc); \
 		break;
 				RTX_CWALK(0) RTX_CWALK(1) RTX_CWALK(2) RTX_CWALK(3) RTX_CWALK(4) RTX_CWALK(5) RTX_CWALK(6)
 				RTX_CWALK(7)
 #undef RTX_CWALK
 			default:
-				closest_walk8<COUNT, 8>(S, ls, ostk, ostride, o, d, ob, inv, t0, far, tbest, hid, tc);
+				closest_walk8<COUNT, 8, false>(S, ls, ostk, ostride, o, d, ob, inv, t0, far, tbest, hid, tc);
 				break;
 			}
 		}
