@@ -148,6 +148,7 @@ static void free_scene(rtx_ctx *c)
 	dfree(c->d_mats);
 	dfree(c->d_emitters);
 	dfree(c->d_lin);
+	dfree(c->d_cull);
 	dfree(c->d_qnodes);
 	dfree(c->d_top);
 	dfree(c->d_w8);
@@ -758,6 +759,67 @@ int rtx_upload_built(rtx_ctx *c, HostScene &hs)
 	return rc;
 }
 
+/* k_shadow's cone cull (DScene.cull, RTX_OPT_SHADOW_CULL): the bounding spheres of the 8-wide
+ * tree's second level in world coordinates, from the root entry and its child nodes read back from
+ * the device.  Every primitive of the tree lies in one of these boxes (a root slot's children, or
+ * the root slot itself when it is a leaf); the spheres are formed in double from the quantised
+ * boxes (which contain the primitives' float boxes) and padded for the kernel's float test. */
+static int build_cull(rtx_ctx *c, const HostScene &hs, uint32_t num_w8, uint32_t *n_out)
+{
+	*n_out = 0;
+	if (!c->d_w8 || num_w8 < 2)
+		return RTX_OK;
+	DW8 root, kid[8];
+	HIP_TRY(hipMemcpy(&root, c->d_w8, sizeof(DW8), hipMemcpyDeviceToHost));
+	const uint32_t base = root.w[2] >> 8, imask = root.w[2] & 0xFFu, vmask = root.w[3] & 0xFFu;
+	if (!vmask)
+		return RTX_OK;
+	if ((uint64_t)base + 8 > num_w8)
+		return fail(RTX_ERR_STATE, "8-wide root's children at %u beyond %u entries", base, num_w8);
+	HIP_TRY(hipMemcpy(kid, c->d_w8 + base, sizeof(kid), hipMemcpyDeviceToHost));
+	std::vector<float4> sph;
+	auto add_box = [&](const DW8 &N, int slot) {
+		const double org[3] = { (double)(N.w[0] & 0xFFFFu), (double)(N.w[0] >> 16), (double)(N.w[1] & 0xFFFFu) };
+		const int ex[3] = { (int)((N.w[1] >> 16) & 15u), (int)((N.w[1] >> 20) & 15u), (int)((N.w[1] >> 24) & 15u) };
+		double ctr[3], r2 = 0;
+		for (int a = 0; a < 3; a++) {
+			const uint32_t lo8 = (N.w[4 + 4 * a + (slot >> 2)] >> (8 * (slot & 3))) & 0xFFu;
+			const uint32_t hi8 = (N.w[6 + 4 * a + (slot >> 2)] >> (8 * (slot & 3))) & 0xFFu;
+			const double lo = (org[a] + std::ldexp((double)lo8, ex[a])) / (double)hs.w8f.qs[a] + (double)hs.w8f.qo[a];
+			const double hi = (org[a] + std::ldexp((double)hi8, ex[a])) / (double)hs.w8f.qs[a] + (double)hs.w8f.qo[a];
+			ctr[a] = 0.5 * (lo + hi);
+			r2 += 0.25 * (hi - lo) * (hi - lo);
+		}
+		double w[3], m = 0;
+		for (int a = 0; a < 3; a++) /* the frame's x' = R (x - c): x = R^T x' + c */
+			w[a] = hs.tf.rotated ? (double)hs.tf.c[a] + hs.tf.r[0][a] * ctr[0] + hs.tf.r[1][a] * ctr[1] + hs.tf.r[2][a] * ctr[2]
+					      : ctr[a];
+		for (int a = 0; a < 3; a++)
+			m = std::max(m, std::fabs(w[a]));
+		const double r = std::sqrt(r2);
+		sph.push_back(make_float4((float)w[0], (float)w[1], (float)w[2], (float)(r * (1 + 1e-5) + 1e-5 * m + 1e-6)));
+	};
+	for (int s = 0; s < 8; s++) {
+		if (!((vmask >> s) & 1u))
+			continue;
+		if ((imask >> s) & 1u) {
+			const DW8 &K = kid[s];
+			for (int s2 = 0; s2 < 8; s2++)
+				if ((K.w[3] >> s2) & 1u)
+					add_box(K, s2);
+		} else {
+			add_box(root, s);
+		}
+	}
+	if (sph.empty() || sph.size() > RTX_CULL_MAX)
+		return RTX_OK;
+	int rc = upload(c->d_cull, sph, c->stream);
+	if (rc)
+		return rc;
+	*n_out = (uint32_t)sph.size();
+	return RTX_OK;
+}
+
 int rtx_upload_built(rtx_ctx *c, const HostScene &hs, DevTree *take)
 {
 	int rc;
@@ -821,6 +883,9 @@ int rtx_upload_built(rtx_ctx *c, const HostScene &hs, DevTree *take)
 	}
 	dfree(d_map);
 	PHASE(clk, "8-wide leaf fill", c->stream);
+	uint32_t ncull = 0; /* the cone cull needs the emitters out of the tree (else a light's own leaf meets every cone) */
+	if (have_w8 && hs.w8noemit && hs.lin.empty() && (rc = build_cull(c, hs, num_w8, &ncull)))
+		return rc;
 	memcpy(c->bound_lo, hs.bound_lo, 12);
 	memcpy(c->bound_hi, hs.bound_hi, 12);
 	DScene &S = c->scene;
@@ -854,6 +919,8 @@ int rtx_upload_built(rtx_ctx *c, const HostScene &hs, DevTree *take)
 	S.num_emitters = hs.num_emitters;
 	S.stack_size = std::max<uint32_t>(hs.depth + 1, 4);
 	S.tf = hs.tf;
+	S.cull = ncull ? (const float *)c->d_cull : nullptr;
+	S.num_cull = ncull;
 	c->total_lights = 0;
 	for (const DEmitter &e : hs.emit)
 		c->total_lights += e.num_lights;
@@ -1090,7 +1157,10 @@ int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, floa
 						  c->sorttmp_bytes, &perm, stream));
 		}
 		HIP_TRY(hipEventRecord(c->ev[4], stream));
-		HIP_TRY(rtx_launch_shadow(&c->scene, &P, c->d_sp, perm, n_sp, per_wave, slot_b, c->d_contrib, c->d_ctr,
+		DScene Ssh = c->scene; /* RTX_OPT_SHADOW_CULL off: no cull spheres */
+		if (!c->opt_cull)
+			Ssh.num_cull = 0;
+		HIP_TRY(rtx_launch_shadow(&Ssh, &P, c->d_sp, perm, n_sp, per_wave, slot_b, c->d_contrib, c->d_ctr,
 					  p->count_traversal, (uint32_t)c->cus, stream));
 		HIP_TRY(hipEventRecord(c->ev[2], stream));
 		HIP_TRY(rtx_launch_accum(&F, &P, c->d_tile_rec, c->d_contrib, begin, end - begin, d_rgb, stream));
@@ -1140,6 +1210,7 @@ int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, floa
 	st.far_closest_rays = ctr[RTX_C_FARC];
 	st.far_shadow_rays = ctr[RTX_C_FARS];
 	st.shadow_stack_spills = ctr[RTX_C_SSPILL];
+	st.shadow_cone_clear = ctr[RTX_C_SCLEAR];
 	st.node_visits = ctr[RTX_C_NODES] + st.shadow_node_visits;
 	st.tri_tests = ctr[RTX_C_TRIS] + ctr[RTX_C_STRIS];
 	st.sphere_tests = ctr[RTX_C_SPHERES] + ctr[RTX_C_SSPHERES];
@@ -1319,6 +1390,11 @@ extern "C" int rtx_set_option(rtx_ctx *c, int option, int64_t value)
 		if (value < 0 || value > (1 << 20))
 			return fail(RTX_ERR_ARG, "shade points per tile %lld outside 0..2^20", (long long)value);
 		c->opt_sp_tile = (uint32_t)value;
+		return RTX_OK;
+	case RTX_OPT_SHADOW_CULL:
+		if (value != 0 && value != 1)
+			return fail(RTX_ERR_ARG, "shadow cull %lld is not 0 or 1", (long long)value);
+		c->opt_cull = value != 0;
 		return RTX_OK;
 	}
 	return fail(RTX_ERR_ARG, "unknown option %d", option);

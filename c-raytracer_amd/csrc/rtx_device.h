@@ -253,7 +253,13 @@ typedef struct DScene {
 	float ambient[3];
 	uint32_t *ostk;        /* k_trace: lane-stack entries from RTX_TRACE_LSTK on, [entry][grid lane] in HBM */
 	DTreeFrame tf;         /* the frame every tree's boxes are in (identity unless rotated) */
+	const float *cull;     /* k_shadow's cone cull (RTX_OPT_SHADOW_CULL): bounding spheres {world centre,
+	                        * radius} (4 floats each) of the 8-wide tree's second level (a root slot's children, or the
+	                        * slot's own box when it is a leaf), at most RTX_CULL_MAX; every primitive of
+	                        * the tree lies in one.  Null / 0: no cull */
+	uint32_t num_cull;
 } DScene;
+#define RTX_CULL_MAX 64
 
 /* k_trace keeps the first RTX_TRACE_LSTK entries of a lane's closest-hit stack in LDS and the
  * deeper ones (rare) in HBM (DScene.ostk): the LDS per wave, not the tree depth, sets how many
@@ -320,6 +326,7 @@ enum {
 	RTX_C_FARC,         /* count mode: closest-hit rays whose origin was far (rtx_math.h tf_far: tf_shift) */
 	RTX_C_FARS,         /* count mode: shadow rays from far shade points (walked from the light end) */
 	RTX_C_SSPILL,       /* count mode, 8-wide walk: lane-stack pushes beyond the LDS entries (HBM) */
+	RTX_C_SCLEAR,       /* count mode: shadow rays of packets the cone cull let skip the walk */
 	RTX_C_N
 };
 

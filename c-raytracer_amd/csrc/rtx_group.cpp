@@ -518,6 +518,7 @@ extern "C" int rtx_group_render(rtx_group *g, const rtx_frame *fr, const rtx_par
 		s.far_closest_rays += o.far_closest_rays;
 		s.far_shadow_rays += o.far_shadow_rays;
 		s.shadow_stack_spills += o.shadow_stack_spills;
+		s.shadow_cone_clear += o.shadow_cone_clear;
 		s.waves += o.waves;
 		s.chunks += o.chunks;
 		s.kernel_ms = std::max(s.kernel_ms, o.kernel_ms);

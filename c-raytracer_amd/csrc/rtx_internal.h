@@ -84,6 +84,7 @@ struct rtx_ctx {
 	DW8 *d_w8 = nullptr;
 	DW8S *d_w8s = nullptr;
 	uint32_t *d_w8spill = nullptr; /* k_shadow lane-stack spill of deep 8-wide trees (DScene.w8spill) */
+	float4 *d_cull = nullptr;      /* the 8-wide tree's top-level bounding spheres (DScene.cull) */
 	size_t w8spill_bytes = 0;
 	DScene scene{};
 	bool have_scene = false;
@@ -130,6 +131,7 @@ struct rtx_ctx {
 	int opt_frame = RTX_FRAME_AUTO;
 	uint32_t opt_chunk = 0;   /* most tiles per chunk (0: as many as the shade-point budget allows) */
 	uint32_t opt_sp_tile = 0; /* shade points per tile a chunk is sized for (0: the estimate / last render's count) */
+	bool opt_cull = true;     /* RTX_OPT_SHADOW_CULL */
 	uint32_t mem_share = 1;   /* contexts sharing this device's HBM at once (a loopback group's n): the shade-point
 	                           * budget of a render is a third of the free HBM divided by it */
 };

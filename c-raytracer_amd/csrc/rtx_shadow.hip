@@ -162,6 +162,7 @@ struct ShadowCount {
 	u64 unif;      /* 8-wide walk: wave steps with one node for all walking lanes (scalar path) */
 	u64 far;       /* rays from far shade points, walked from the light end (RTX_SP_FAR) */
 	u64 spills;    /* 8-wide walk: lane-stack pushes beyond the LDS entries (to DScene.w8spill in HBM) */
+	u64 clear;     /* rays of packets the cone cull let skip the walk (cone_clear) */
 };
 
 /* one primitive record (a, b, c = its first 48 bytes) against this lane's shadow ray
@@ -800,6 +801,8 @@ const DW8 *w8;        /* 8-wide compressed BVH (WALK_W8 instances; qo / qs / qsi
 	uint32_t n_sp, per_wave, slot_b, slot_lg;
 	int32_t rng, attenuation, reflection;
 	float att_offset;
+	const float4 *cull;   /* DScene.cull: the 8-wide tree's second-level bounding spheres (cone_clear) */
+	uint32_t num_cull;    /* 0: no cull (RTX_OPT_SHADOW_CULL off, or no such tree) */
 };
 
 __device__ __forceinline__ void reread_barrier() { asm volatile("" ::: "memory"); }
@@ -963,12 +966,65 @@ __device__ __forceinline__ QBvh make_qbvh(const KShadow &ks, const uint4 *top_q,
 	return Q;
 }
 
+/* The cone cull of a packet of one shade point's samples of one emitter: every shadow ray of the
+ * packet runs from p to a point of the emitter, so it lies in the cone from p around the emitter's
+ * bounding sphere (centre and half-diagonal of its padded world box DEmitter.wlo / whi), cut at
+ * the sphere's far side.  Lane k tests the bounding sphere k of the 8-wide tree's second level
+ * (DScene.cull, world space): centre distance t along the axis, e off it; the sphere misses the
+ * cone when e cos(a) - t sin(a) > r or it lies wholly before p or beyond the light.  r is padded
+ * by 2e-5 of the coordinates' and distances' magnitudes, far above the rays' float rounding, so a
+ * clear packet is one whose walks could reach no primitive: skipping them changes no bit of the
+ * image (test_gpu_cone_cull_is_invisible).  True when no lane's sphere meets the cone. */
+__device__ __forceinline__ bool cone_clear(const KShadow &ks, const DEmitter &E, f3 p)
+{
+	const uint32_t n = uni(ks.num_cull);
+	if (!n)
+		return false;
+	const f3 lc = mk3(0.5f * (E.wlo[0] + E.whi[0]), 0.5f * (E.wlo[1] + E.whi[1]), 0.5f * (E.wlo[2] + E.whi[2]));
+	const f3 lh = mk3(0.5f * (E.whi[0] - E.wlo[0]), 0.5f * (E.whi[1] - E.wlo[1]), 0.5f * (E.whi[2] - E.wlo[2]));
+	const float lr = sqrtf(magsqr3(lh));
+	const f3 ax0 = sub3(lc, p);
+	const float L = sqrtf(magsqr3(ax0));
+	if (!(L > 1.01f * lr)) /* the point at or inside the light's sphere: no cone */
+		return false;
+	const f3 ax = mul3s(ax0, 1.f / L);
+	const float sn = lr / L, cs = sqrtf(fmaxf(0.f, 1.f - sn * sn));
+	const float mag = fmaxf(fmaxf(fabsf(p.x), fabsf(p.y)), fabsf(p.z)) + fmaxf(fmaxf(fabsf(lc.x), fabsf(lc.y)), fabsf(lc.z));
+	bool meets = false;
+	const uint32_t k = lane_id();
+	if (k < n) {
+		const float4 sp = ldg4((const char *)(unip(ks.cull) + k), 0);
+		const f3 v = sub3(mk3(sp.x, sp.y, sp.z), p);
+		const float vv = magsqr3(v), t = dot3(v, ax);
+		const float e = sqrtf(fmaxf(0.f, vv - t * t));
+		const float br = sp.w + 2e-5f * (mag + sqrtf(vv) + L + lr);
+		meets = vv <= br * br || (t >= -br && t <= L + lr + br && e * cs - t * sn <= br);
+	}
+	return !ballot(meets);
+}
+
+/* the emitters (bit e, e < 64) whose cone from shade point p meets no top-level box of the tree:
+ * formed once per point of the wave-uniform path, before its packets (a far point: none) */
+__device__ __forceinline__ u64 cone_mask(const KShadow &ks, f3 p, bool far)
+{
+	if (!uni(ks.num_cull) || far)
+		return 0ull;
+	const DEmitter *emitters = unip(ks.emitters);
+	const uint32_t ne = min(uni(ks.num_emitters), 64u);
+	u64 m = 0ull;
+	for (uint32_t e = 0; e < ne; e++)
+		if (cone_clear(ks, emitter_uni(emitters + e), p))
+			m |= 1ull << e;
+	return m;
+}
+
 /* one light sample per lane of the shade point `rec` (render.c:170-229): the light point of
  * sample idx (emitters in scene order, the hit object skipped), its shadow ray, attenuation
  * and Phong / Blinn.  Argument-block fields are read from LDS behind reread barriers. */
 template <bool COUNT, int WALK, bool UNI, bool LA>
 __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec_uni, uint32_t sidv, uint32_t idx, bool act, ShadowCount &sc,
-					   const uint4 *top_q, const uint32_t *top_e, lds_u32 *stk, const uint4 *t8, uint32_t wv)
+					   const uint4 *top_q, const uint32_t *top_e, lds_u32 *stk, const uint4 *t8, uint32_t wv,
+					   const uint32_t *cmask)
 {
 	reread_barrier();
 	/* the shade point's record: wave-uniform (UNI), or this lane's record sidv, whose address is
@@ -1002,10 +1058,14 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec_
 	f3 ldir, li;
 	float ldist, dsq;
 	uint32_t eobj;
+	bool clear = false; /* UNI: the packet's cone meets no top-level box of the tree (cone_clear) */
 	if (!ballot(act && e != lead)) {
 		const DEmitter Eu = emitter_uni(emitters + lead);
 		emitter_sample(ks, Eu, lead, j, __float_as_uint(q4.y), __float_as_uint(q4.z), p, ldir, ldist, dsq, li);
 		eobj = Eu.obj;
+		/* the point's cone_mask, kept in the wave's LDS table (a 64-bit mask in SGPRs across the walk
+		 * cost the walk a spilled register) */
+		clear = UNI && WALK == WALK_W8 && ((uni(cmask[lead >> 5]) >> (lead & 31u)) & 1u);
 	} else {
 		const DEmitter &E = emitters[e];
 		emitter_sample(ks, E, e, j, __float_as_uint(q4.y), __float_as_uint(q4.z), p, ldir, ldist, dsq, li);
@@ -1013,7 +1073,9 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec_
 	}
 	const float attf = sample_att(ks, ldist, dsq);
 	const QBvh Q = make_qbvh<WALK>(ks, top_q, top_e, stk, t8, wv);
-	const bool have_tree = uni(ks.have_tree) != 0 && !RTX_DEBUG_NOWALK;
+	const bool have_tree = uni(ks.have_tree) != 0 && !RTX_DEBUG_NOWALK && !clear;
+	if (COUNT && clear)
+		sc.clear += (u64)popc64(ballot(act));
 	const bool blocked = shadow_query<COUNT, WALK, LA>(Q, unip(ks.recs), unip(ks.mats), unip(ks.planes), uni(ks.num_planes),
 						 unip(ks.lin), uni(ks.num_lin), have_tree, ks.tf, act, far != 0, p, ldir, ldist, eobj, li,
 							 sc);
@@ -1058,6 +1120,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 		uint32_t nls[WAVE];     /* shadow rays of each shade point */
 		uint32_t sid[WAVE];     /* each shade point's index in the record array */
 		float Ls[3][WAVE];      /* per shade point light sum, in packet order */
+		uint32_t cm[2];         /* the current point's cone_mask (wave-uniform path) */
 	};
 	__shared__ WaveTables wt_w[RTX_SH_NW];
 	const uint32_t ntop = TOP ? ka.ntop : 0u;
@@ -1080,7 +1143,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 	 * every push and pop) */
 	constexpr bool LA = RTX_W8_LANEADDR == 2 ? PATH == 2 : RTX_W8_LANEADDR != 0;
 	lds_u32 *stk = (lds_u32 *)&wstk[wv][0][LA ? 0u : lane_id()];
-	ShadowCount sc = { 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0 };
+	ShadowCount sc = { 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0 };
 	u64 rays_total = 0;
 	for (;;) {
 		reread_barrier();
@@ -1117,10 +1180,20 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 				reread_barrier();
 				const uint32_t nl = uni(nls[k]);
 				const float4 *rec = unip(ks.sp) + (size_t)uni(sid[k]) * SPREC;
+				if (WALK == WALK_W8) {
+					const float4 q0 = sp_field<RTX_SH_SPUNI>(rec, 0), q4 = sp_field<RTX_SH_SPUNI>(rec, 4);
+					const u64 m = cone_mask(ks, mk3(q0.x, q0.y, q0.z), (__float_as_uint(q4.x) & RTX_SP_FAR) != 0);
+					if (lane_id() == 0) {
+						wt_w[wv].cm[0] = (uint32_t)m;
+						wt_w[wv].cm[1] = (uint32_t)(m >> 32);
+					}
+					lds_sync();
+				}
 				f3 acc = mk3(0.f, 0.f, 0.f);
 				for (uint32_t base = 0; base < nl; base += WAVE) {
 					const uint32_t idx = base + lane_id();
-					acc = add3(acc, light_sample<COUNT, WALK, true, LA>(ks, rec, 0u, idx, idx < nl, sc, top_q, top_e, stk, t8, wv));
+					acc = add3(acc, light_sample<COUNT, WALK, true, LA>(ks, rec, 0u, idx, idx < nl, sc, top_q, top_e, stk, t8, wv,
+											    wt_w[wv].cm));
 				}
 				const float sx = wave_sum(acc.x), sy = wave_sum(acc.y), sz = wave_sum(acc.z);
 				if (lane_id() == 0) {
@@ -1154,7 +1227,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 				const uint32_t idx = ((slot - off[k]) << slot_lg) + (lane_id() & (slot_b - 1));
 				const bool act = slot < tot && idx < nls[k];
 				const f3 contribution = light_sample<COUNT, WALK, false, LA>(ks, nullptr, sid[k], idx, act, sc, top_q, top_e, stk,
-											 t8, wv);
+											 t8, wv, nullptr);
 				/* per-shade-point sums.  Each slot's B lanes reduce in a fixed butterfly (masks B/2 .. 1),
 				 * then the slot sums are added to their point's total one slot at a time in slot order, so a
 				 * point whose slots straddle packets gets the same sum whatever its neighbours (with one slot
@@ -1277,6 +1350,7 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 			atomicAdd(&ctr[RTX_C_SUNIF], sc.unif);
 			atomicAdd(&ctr[RTX_C_FARS], sc.far);
 			atomicAdd(&ctr[RTX_C_SSPILL], sc.spills);
+			atomicAdd(&ctr[RTX_C_SCLEAR], sc.clear);
 		}
 	}
 }
@@ -1550,6 +1624,8 @@ for (int a = 0; a < 3; a++) {
 	ka.w8top = S->w8top;
 	ka.w8sph = S->w8sph;
 	ka.lin = S->lin; /* a tiny scene: every bounded object, no walk */
+	ka.cull = (const float4 *)S->cull;
+	ka.num_cull = (walk == WALK_W8 && S->cull) ? S->num_cull : 0u;
 	ka.num_lin = S->lin ? S->num_lin : 0u;
 	if (walk == WALK_W8) { /* the 8-wide tree's own frame; the emitters it leaves out are tested linearly */
 		for (int a = 0; a < 3; a++) {

@@ -75,7 +75,7 @@ class Stats(C.Structure):
                 ("pad3_", C.c_uint32), ("frame_cost", C.c_double), ("frame_ms", C.c_double),
                 ("upload_copy_ms", C.c_double), ("transport", C.c_uint32), ("peer_access", C.c_uint32),
                 ("far_closest_rays", C.c_uint64), ("far_shadow_rays", C.c_uint64),
-                ("shadow_stack_spills", C.c_uint64)]
+                ("shadow_stack_spills", C.c_uint64), ("shadow_cone_clear", C.c_uint64)]
 
 
 RTX_TRANSPORT_NONE, RTX_TRANSPORT_RCCL, RTX_TRANSPORT_LOOPBACK, RTX_TRANSPORT_RCCL_SELF = 0, 1, 2, 3
@@ -94,7 +94,7 @@ RTX_SHADOW_LINEAR_MAX = 8
 RTX_FRAME_AUTO, RTX_FRAME_WORLD = 0, 1
 RTX_OPT_SHADOW_WALK, RTX_OPT_BVH_LEAF, RTX_OPT_SPSORT, RTX_OPT_SHADOW_SLOT, RTX_OPT_SHADOW_GRAB, \
     RTX_OPT_SHADOW_LDS_STACK, RTX_OPT_TRACE_WALK, RTX_OPT_TREE_FRAME, RTX_OPT_CHUNK_TILES, \
-    RTX_OPT_SP_PER_TILE = 1, 2, 3, 4, 5, 6, 7, 8, 9, 10
+    RTX_OPT_SP_PER_TILE, RTX_OPT_SHADOW_CULL = 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11
 RTX_DOF_NONE, RTX_DOF_SCALE_BIAS, RTX_DOF_CAMERA = 0, 1, 2
 RTX_FALLOFF_QUAD, RTX_FALLOFF_LIN, RTX_FALLOFF_INV_QUAD = 0, 1, 2
 

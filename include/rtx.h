@@ -234,6 +234,9 @@ typedef struct rtx_stats {
 	uint64_t far_shadow_rays;         /* shadow rays from far shade points (walked from the light end) */
 	uint64_t shadow_stack_spills;     /* only with count_traversal, 8-wide walk: lane-stack entries pushed beyond
 	                                   * the LDS ones (to HBM, DScene.w8spill) */
+	uint64_t shadow_cone_clear;       /* only with count_traversal: shadow rays of packets whose light cone met no
+	                                   * box of the 8-wide tree's top levels, so they were not walked
+	                                   * (RTX_OPT_SHADOW_CULL) */
 } rtx_stats;
 
 typedef struct rtx_ctx rtx_ctx;
@@ -294,9 +297,13 @@ enum rtx_option {
 	RTX_OPT_TREE_FRAME = 8,       /* RTX_FRAME_* (build; default RTX_FRAME_AUTO) */
 	RTX_OPT_CHUNK_TILES = 9,      /* most 8x8 tiles per chunk of a render (0 = as many as the shade-point budget,
 	                               * a third of free HBM, allows; default 0) */
-	RTX_OPT_SP_PER_TILE = 10      /* shade points per tile a chunk is sized for (0 = automatic, default): a
+	RTX_OPT_SP_PER_TILE = 10,     /* shade points per tile a chunk is sized for (0 = automatic, default): a
 	                               * chunk that overflows is halved and retried, so any value gives the same
 	                               * image (tests drive the overflow path with a low one) */
+	RTX_OPT_SHADOW_CULL = 11      /* 1 (default): a packet of one shade point's light samples skips the 8-wide
+	                               * walk when the cone from the point around the light's bounding sphere
+	                               * meets no box of the tree's top two levels (the walk would find nothing,
+	                               * so the image is the same); 0: every packet walks */
 };
 int rtx_set_option(rtx_ctx *ctx, int option, int64_t value);
 /* The frame rtx_upload_scene builds the scene's BVHs in under RTX_FRAME_AUTO (a diagnostic; no

@@ -61,7 +61,7 @@ def test_struct_sizes_match_c():
     assert ctypes.sizeof(abi.Object) == 4 * (4 + 18 + 2)
     assert ctypes.sizeof(abi.Frame) == 4 * (2 + 12)
     assert ctypes.sizeof(abi.Params) == 56
-    assert ctypes.sizeof(abi.Stats) == 11 * 8 + 6 * 8 + 6 * 4 + 4 * 8 + 2 * 4 + 8 + 8 + 2 * 4 + 8 + 2 * 4 + 2 * 4 + 2 * 4 + 2 * 8 + 8 + 2 * 4 + 3 * 8
+    assert ctypes.sizeof(abi.Stats) == 11 * 8 + 6 * 8 + 6 * 4 + 4 * 8 + 2 * 4 + 8 + 8 + 2 * 4 + 8 + 2 * 4 + 2 * 4 + 2 * 4 + 2 * 8 + 8 + 2 * 4 + 4 * 8
 
 
 def test_struct_layouts_match_compiled_header(tmp_path):

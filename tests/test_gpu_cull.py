@@ -1,0 +1,85 @@
+"""k_shadow's cone cull (rtx.h RTX_OPT_SHADOW_CULL, rtx_shadow.hip cone_clear, rtx_api.cpp
+build_cull): a packet of one shade point's samples of one emitter skips the 8-wide walk when the
+cone from the point around the emitter's bounding sphere meets none of the bounding spheres of the
+tree's second level.  Every shadow ray of the packet lies in that cone, so a skipped walk is one
+that could reach no primitive: the image, the depth buffer and the ray counts are the same bit for
+bit with the cull on and off (is_light_blocked, render.c:126-134, finds nothing in the tree either
+way).  The counting render reports how many rays skipped their walk (rtx_stats.shadow_cone_clear).
+"""
+import numpy as np
+import pytest
+
+import conftest as C
+import rtxpy
+from rtxpy import abi
+from test_gpu_configs import load
+
+pytestmark = pytest.mark.gpu
+
+
+def render_both(scene, frame, params, slot=0, frame_opt=abi.RTX_FRAME_AUTO):
+    out = {}
+    r = rtxpy.Renderer(0)
+    try:
+        r.set_option(abi.RTX_OPT_TREE_FRAME, frame_opt)
+        r.upload(scene)
+        r.set_option(abi.RTX_OPT_SHADOW_SLOT, slot)
+        for cull in (1, 0):
+            r.set_option(abi.RTX_OPT_SHADOW_CULL, cull)
+            for count in (0, 1):
+                p = rtxpy.default_params(**{f: getattr(params, f) for f, _ in abi.Params._fields_})
+                p.count_traversal = count
+                rgb, z = r.render(frame, p)
+                out[(cull, count)] = (rgb, z, r.stats())
+    finally:
+        r.close()
+    return out
+
+
+def check(out, want_clear):
+    rgb0, z0, s0 = out[(0, 0)]
+    for key, (rgb, z, s) in out.items():
+        assert np.array_equal(rgb, rgb0) and np.array_equal(z, z0), key
+        assert (s.closest_rays, s.shadow_rays, s.shade_points) == (s0.closest_rays, s0.shadow_rays, s0.shade_points), key
+    on, off = out[(1, 1)][2], out[(0, 1)][2]
+    assert off.shadow_cone_clear == 0
+    if want_clear:
+        assert on.shadow_cone_clear > 0
+        # the cleared rays' walks are gone: fewer box tests, no other change in what was tested
+        assert on.shadow_node_visits < off.shadow_node_visits
+    return on.shadow_cone_clear / max(1, on.shadow_rays)
+
+
+@pytest.mark.parametrize("name", ["s5_path2", "s3_path2", "s2_blinn_lin", "s6_amb"])
+def test_gpu_cone_cull_is_invisible(name):
+    scene, frame, params, _ = C.load_config(name)
+    out = render_both(scene, frame, params, slot=64)  # 64-lane packets: one point per packet
+    frac = check(out, want_clear=False)
+    print(name, "cleared", round(frac, 4))
+
+
+def test_gpu_cone_cull_on_the_bench_scene():
+    """scene5 with the dragon stand-in (bench.py's scene, a smaller frame): most floor and wall
+    points see the light past the dragon, so most packets skip the walk; the frame is the same"""
+    scene = load("scene5")
+    frame = scene.frame(320, 180)
+    params = rtxpy.params_from_args(["-g", "path", "-n", "4"], seed=1)
+    params.rng = abi.RTX_RNG_COUNTER
+    out = render_both(scene, frame, params)
+    frac = check(out, want_clear=True)
+    print("scene5 cleared", round(frac, 4))
+    assert frac > 0.3
+
+
+@pytest.mark.parametrize("frame_opt", [abi.RTX_FRAME_AUTO, abi.RTX_FRAME_WORLD])
+def test_gpu_cone_cull_in_the_rotated_frame(frame_opt):
+    """scene6's Menger stand-in builds its trees in a rotated frame: the spheres are formed in it
+    and moved to world space (x = R^T x' + c); with 64-lane packets the cull runs, and the frame is
+    the same as without it in both tree frames"""
+    scene = load("scene6")
+    frame = scene.frame(160, 90)
+    params = rtxpy.params_from_args(["-g", "path", "-n", "2"], seed=1)
+    params.rng = abi.RTX_RNG_COUNTER
+    out = render_both(scene, frame, params, slot=64, frame_opt=frame_opt)
+    frac = check(out, want_clear=False)
+    print("scene6 frame", frame_opt, "cleared", round(frac, 4))

@@ -1,0 +1,13 @@
+# round-6: the shadow cone cull: its GPU tests and the frame suites, then the bench frame and
+# configs[4] with the cull on and off
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+OUT=gpurun_out/r06p; mkdir -p $OUT; export TMPDIR=/tmp
+python3 tools/standins.py scene5 scene6 > /dev/null
+run() { local name=$1 to=$2; shift 2; echo "=== $name"; timeout -k 10 $to "$@" > $OUT/$name.log 2>&1; local rc=$?; echo "=== $name rc=$rc"; tail -3 $OUT/$name.log; if [ $rc -ne 0 ]; then exit $rc; fi; }
+run culltests 600 python3 -u -m pytest tests/test_gpu_cull.py -m gpu -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider
+run ptests 900 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_frame.py -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider
+run bench_cull 600 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-post --verbose
+run bench_nocull 600 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-post --verbose --no-cull
+run s6_cull 600 python3 bench.py --scene scene6 --width 3840 --height 2160 --spp 128 --steps 1 --warmup 1 --no-cpu-baseline --no-post --verbose
+echo done-r06p

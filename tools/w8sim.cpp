@@ -550,6 +550,12 @@ int main(int argc, char **argv)
 		return RTX_NONE;
 	};
 	const bool occ_sim = getenv("W8SIM_OCC") && atoi(getenv("W8SIM_OCC"));
+	/* W8SIM_CONE=1: a per-point cone walk before the packets: the tree's boxes (as bounding spheres)
+	 * against the cone from the shade point around the light's bounding sphere; a point whose cone
+	 * meets no leaf entry needs no walk for any of its samples */
+	const bool cone_sim = getenv("W8SIM_CONE") && atoi(getenv("W8SIM_CONE"));
+	double cone_pts_empty = 0, cone_visits = 0, cone_leaves = 0, ws_empty = 0, lr_empty = 0, pk_empty = 0;
+	std::vector<double> cone_leaf_hist(8, 0.0), cone_depth_hist(16, 0.0), ws_depth(16, 0.0);
 	const int order = getenv("W8SIM_ORDER") ? atoi(getenv("W8SIM_ORDER")) : 0;
 	const bool sort_samples = getenv("W8SIM_SORT") && atoi(getenv("W8SIM_SORT"));
 	const bool strat = getenv("W8SIM_STRAT") && atoi(getenv("W8SIM_STRAT")); /* RTX_RNG_STRAT light samples */
@@ -559,6 +565,98 @@ int main(int argc, char **argv)
 	for (int pi = 0; pi < npts; pi++) {
 		const float P[3] = { pts[pi][0], pts[pi][1], pts[pi][2] };
 		uint32_t probe_occ = RTX_NONE, last_blk = RTX_NONE;
+		bool cone_empty = false;
+		uint32_t cone_maxd = 0;
+		const double ws0 = S.wave_steps, lr0 = S.leaf_rounds, pk0 = S.packets;
+		if (cone_sim) {
+			double Lc[3], lr;
+			if (E.type == RTX_SPHERE) {
+				for (int a = 0; a < 3; a++)
+					Lc[a] = E.p0[a];
+				lr = E.radius;
+			} else {
+				for (int a = 0; a < 3; a++)
+					Lc[a] = E.p0[a] + (E.e1[a] + E.e2[a]) / 3.0;
+				lr = 0;
+				for (int k = 0; k < 3; k++) {
+					double v[3], q = 0;
+					for (int a = 0; a < 3; a++)
+						v[a] = E.p0[a] + (k == 1 ? E.e1[a] : k == 2 ? E.e2[a] : 0.0) - Lc[a];
+					for (int a = 0; a < 3; a++)
+						q += v[a] * v[a];
+					lr = std::max(lr, sqrt(q));
+				}
+			}
+			lr = lr * (1 + 1e-5) + 1e-6;
+			double Pf[3], Cf[3];
+			for (int a = 0; a < 3; a++) {
+				Pf[a] = tf.rotated ? tf.r[a][0] * (P[0] - tf.c[0]) + tf.r[a][1] * (P[1] - tf.c[1]) + tf.r[a][2] * (P[2] - tf.c[2]) : P[a];
+				Cf[a] = tf.rotated ? tf.r[a][0] * (Lc[0] - tf.c[0]) + tf.r[a][1] * (Lc[1] - tf.c[1]) + tf.r[a][2] * (Lc[2] - tf.c[2]) : Lc[a];
+			}
+			double ax[3], L = 0;
+			for (int a = 0; a < 3; a++) {
+				ax[a] = Cf[a] - Pf[a];
+				L += ax[a] * ax[a];
+			}
+			L = sqrt(L);
+			for (int a = 0; a < 3; a++)
+				ax[a] /= L;
+			const double sn = std::min(1.0, lr / L), cs = sqrt(std::max(0.0, 1 - sn * sn));
+			uint32_t nleaves = 0, maxd = 0;
+			std::vector<std::pair<uint32_t, uint32_t>> cst{ { 0u, 1u } };
+			while (!cst.empty()) {
+				const uint32_t node = cst.back().first, dep = cst.back().second;
+				cst.pop_back();
+				maxd = std::max(maxd, dep);
+				const DW8 &N = w8[node];
+				cone_visits++;
+				const double org[3] = { (double)(N.w[0] & 0xFFFF), (double)(N.w[0] >> 16), (double)(N.w[1] & 0xFFFF) };
+				const int ex[3] = { (int)((N.w[1] >> 16) & 15), (int)((N.w[1] >> 20) & 15), (int)((N.w[1] >> 24) & 15) };
+				const uint32_t base = N.w[2] >> 8;
+				for (int c = 0; c < 8; c++) {
+					if (!((N.w[3] >> c) & 1))
+						continue;
+					double bc[3], br = 0;
+					for (int a = 0; a < 3; a++) {
+						const uint8_t *l8 = (const uint8_t *)&N.w[4 + 4 * a], *h8 = (const uint8_t *)&N.w[6 + 4 * a];
+						const double lo = (org[a] + ldexp(l8[c], ex[a])) / F.qs[a] + F.qo[a];
+						const double hi = (org[a] + ldexp(h8[c], ex[a])) / F.qs[a] + F.qo[a];
+						bc[a] = 0.5 * (lo + hi);
+						br += 0.25 * (hi - lo) * (hi - lo);
+					}
+					br = sqrt(br) * (1 + 1e-6) + 1e-6;
+					double v[3], t = 0, vv = 0;
+					for (int a = 0; a < 3; a++) {
+						v[a] = bc[a] - Pf[a];
+						t += v[a] * ax[a];
+						vv += v[a] * v[a];
+					}
+					const double e = sqrt(std::max(0.0, vv - t * t));
+					const bool hit = vv <= br * br || (t >= -br && t <= L + lr + br && e * cs - t * sn <= br);
+					if (!hit)
+						continue;
+					if ((N.w[2] >> c) & 1) {
+						cst.push_back({ base + c, dep + 1 });
+					} else {
+						const DPrim &pp = *(const DPrim *)&w8[base + c];
+						uint32_t obj;
+						memcpy(&obj, &pp.b[3], 4);
+						if (obj != sc->emitters[0])
+							nleaves++;
+					}
+				}
+			}
+			cone_leaves += nleaves;
+			cone_empty = nleaves == 0;
+			cone_pts_empty += cone_empty;
+			cone_maxd = maxd;
+			if (cone_empty)
+				cone_depth_hist[std::min<uint32_t>(maxd, 15)]++;
+			int b = 0;
+			for (uint32_t x = nleaves; x && b < 7; x >>= 3)
+				b++;
+			cone_leaf_hist[b]++;
+		}
 		if (occ_sim) {
 			float Lc[3];
 			for (int a = 0; a < 3; a++)
@@ -974,6 +1072,26 @@ int main(int argc, char **argv)
 		}
 		for (int r = 0; r < 6; r++)
 			refill_sim(allseq, RF_T[r], S.rf_steps[r], S.rf_usteps[r], S.rf_refills[r]);
+		if (cone_sim && cone_empty) {
+			ws_depth[std::min<uint32_t>(cone_maxd, 15)] += S.wave_steps - ws0;
+			ws_empty += S.wave_steps - ws0;
+			lr_empty += S.leaf_rounds - lr0;
+			pk_empty += S.packets - pk0;
+		}
+	}
+	if (cone_sim) {
+		printf("cone walk: %.3f of points meet no leaf entry; %.2f node visits and %.1f leaf entries per point; those points "
+		       "hold %.3f of the packets, %.3f of the wave steps, %.3f of the leaf rounds\n", cone_pts_empty / npts,
+		       cone_visits / npts, cone_leaves / npts, pk_empty / S.packets, ws_empty / S.wave_steps, lr_empty / S.leaf_rounds);
+		printf("  leaf entries per point: 0 %.3f, 1-7 %.3f, 8-63 %.3f, 64-511 %.3f, 512-4095 %.3f, >=4096 %.3f\n",
+		       cone_leaf_hist[0] / npts, cone_leaf_hist[1] / npts, cone_leaf_hist[2] / npts, cone_leaf_hist[3] / npts,
+		       cone_leaf_hist[4] / npts, (cone_leaf_hist[5] + cone_leaf_hist[6] + cone_leaf_hist[7]) / npts);
+		double cp = 0, cw = 0;
+		for (int d = 1; d < 8; d++) {
+			cp += cone_depth_hist[d];
+			cw += ws_depth[d];
+			printf("  proved empty within %d levels: %.3f of points, %.3f of the wave steps\n", d, cp / npts, cw / S.wave_steps);
+		}
 	}
 	printf("lane refill (a finished lane takes the point's next light sample when >= T lanes are idle), per point:\n"
 	       "   T   wave steps (uniform)   refill rounds   cost (178/divergent + 95/uniform step + 220/refill)\n");
