@@ -413,6 +413,7 @@ def shadow_roofline_of(c, shadow_ms, a, world):
            "wave_walks": int(c.shadow_wave_walks), "leaf_rounds": int(c.shadow_leaf_rounds),
            "uniform_steps": int(c.shadow_uniform_steps),
            "stack_spills": int(getattr(c, "shadow_stack_spills", 0)),
+           "cone_clear_rays": int(getattr(c, "shadow_cone_clear", 0)),
            "shadow_rays_per_s": round(c.shadow_rays / dur / 1e9, 3),
            "shadow_rays_per_s_unit": "G/s (tree-independent: the reference's is_light_blocked calls per second)",
            "k_trace": {"closest_rays": int(c.closest_rays),
