@@ -1181,8 +1181,14 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 				const uint32_t nl = uni(nls[k]);
 				const float4 *rec = unip(ks.sp) + (size_t)uni(sid[k]) * SPREC;
 				if (WALK == WALK_W8) {
-					const float4 q0 = sp_field<RTX_SH_SPUNI>(rec, 0), q4 = sp_field<RTX_SH_SPUNI>(rec, 4);
-					const u64 m = cone_mask(ks, mk3(q0.x, q0.y, q0.z), (__float_as_uint(q4.x) & RTX_SP_FAR) != 0);
+					/* the point through vector loads made uniform, not the scalar loads light_sample
+					 * makes: shared with them, the point was live from here and the compiler hoisted
+					 * the far path's double-precision copies of it out of the packet loop and
+					 * spilled them, three stores per point */
+					const float4 q0 = ldg4(rec, 0), q4 = ldg4(rec, 64);
+					const f3 pu = mk3(__uint_as_float(uni(__float_as_uint(q0.x))), __uint_as_float(uni(__float_as_uint(q0.y))),
+							  __uint_as_float(uni(__float_as_uint(q0.z))));
+					const u64 m = cone_mask(ks, pu, (uni(__float_as_uint(q4.x)) & RTX_SP_FAR) != 0);
 					if (lane_id() == 0) {
 						wt_w[wv].cm[0] = (uint32_t)m;
 						wt_w[wv].cm[1] = (uint32_t)(m >> 32);
