@@ -555,6 +555,7 @@ int main(int argc, char **argv)
 	 * meets no leaf entry needs no walk for any of its samples */
 	const bool cone_sim = getenv("W8SIM_CONE") && atoi(getenv("W8SIM_CONE"));
 	double cone_pts_empty = 0, cone_visits = 0, cone_leaves = 0, ws_empty = 0, lr_empty = 0, pk_empty = 0;
+	double nohit_pts = 0, ws_nohit = 0; /* points none of whose sample rays reached a leaf box (any cull's bound) */
 	std::vector<double> cone_leaf_hist(8, 0.0), cone_depth_hist(16, 0.0), ws_depth(16, 0.0);
 	const int order = getenv("W8SIM_ORDER") ? atoi(getenv("W8SIM_ORDER")) : 0;
 	const bool sort_samples = getenv("W8SIM_SORT") && atoi(getenv("W8SIM_SORT"));
@@ -565,7 +566,7 @@ int main(int argc, char **argv)
 	for (int pi = 0; pi < npts; pi++) {
 		const float P[3] = { pts[pi][0], pts[pi][1], pts[pi][2] };
 		uint32_t probe_occ = RTX_NONE, last_blk = RTX_NONE;
-		bool cone_empty = false;
+		bool cone_empty = false, point_leafhit = false;
 		uint32_t cone_maxd = 0;
 		const double ws0 = S.wave_steps, lr0 = S.leaf_rounds, pk0 = S.packets;
 		if (cone_sim) {
@@ -833,6 +834,7 @@ int main(int argc, char **argv)
 						}
 					}
 					leaves[l].push_back(nleaf);
+				point_leafhit |= nleaf > 0;
 					if (im) {
 						const uint32_t p0 = near ? near_p : (uint32_t)__builtin_ctz(im);
 						node = base + (p0 ^ K);
@@ -1072,6 +1074,10 @@ int main(int argc, char **argv)
 		}
 		for (int r = 0; r < 6; r++)
 			refill_sim(allseq, RF_T[r], S.rf_steps[r], S.rf_usteps[r], S.rf_refills[r]);
+		if (cone_sim && !point_leafhit) {
+			nohit_pts++;
+			ws_nohit += S.wave_steps - ws0;
+		}
 		if (cone_sim && cone_empty) {
 			ws_depth[std::min<uint32_t>(cone_maxd, 15)] += S.wave_steps - ws0;
 			ws_empty += S.wave_steps - ws0;
@@ -1086,6 +1092,8 @@ int main(int argc, char **argv)
 		printf("  leaf entries per point: 0 %.3f, 1-7 %.3f, 8-63 %.3f, 64-511 %.3f, 512-4095 %.3f, >=4096 %.3f\n",
 		       cone_leaf_hist[0] / npts, cone_leaf_hist[1] / npts, cone_leaf_hist[2] / npts, cone_leaf_hist[3] / npts,
 		       cone_leaf_hist[4] / npts, (cone_leaf_hist[5] + cone_leaf_hist[6] + cone_leaf_hist[7]) / npts);
+		printf("  bound: %.3f of points had no sample ray reach a leaf box, holding %.3f of the wave steps\n", nohit_pts / npts,
+		       ws_nohit / S.wave_steps);
 		double cp = 0, cw = 0;
 		for (int d = 1; d < 8; d++) {
 			cp += cone_depth_hist[d];
