@@ -6,6 +6,8 @@ that could reach no primitive: the image, the depth buffer and the ray counts ar
 bit with the cull on and off (is_light_blocked, render.c:126-134, finds nothing in the tree either
 way).  The counting render reports how many rays skipped their walk (rtx_stats.shadow_cone_clear).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -83,3 +85,36 @@ def test_gpu_cone_cull_in_the_rotated_frame(frame_opt):
     out = render_both(scene, frame, params, slot=64, frame_opt=frame_opt)
     frac = check(out, want_clear=False)
     print("scene6 frame", frame_opt, "cleared", round(frac, 4))
+
+
+def three_emitter_scene(tmp_path):
+    """the bench scene with two more emitters: a second sphere light and a triangle light (its
+    bounding sphere is its padded world box's), 428 samples per point, so packets of one emitter
+    and packets straddling two (which take the per-lane emitter path and are never culled)"""
+    import json
+    import shutil
+    load("scene5")  # writes the dragon stand-in
+    with open(os.path.join(C.SCENES, "scene5_standin.json")) as fh:
+        d = json.load(fh)
+    os.makedirs(tmp_path / "meshes", exist_ok=True)
+    shutil.copy(os.path.join(C.GOLDEN, "meshes", "dragon_standin.stl"), tmp_path / "meshes" / "dragon_standin.stl")
+    d["Objects"].append({"type": "Sphere", "parameters": {"material": 2, "epsilon": 0.0003, "position": [5.5, -3.5, 1.5],
+                                                          "radius": 0.3, "lights": 64}})
+    d["Objects"].append({"type": "Triangle", "parameters": {"material": 2, "epsilon": 0.0001, "lights": 64,
+                                                            "vertex_1": [-0.4, -4.6, 2.6], "vertex_2": [0.4, -4.6, 2.6],
+                                                            "vertex_3": [0.0, -4.6, 3.3]}})
+    path = tmp_path / "three.json"
+    path.write_text(json.dumps(d))
+    return rtxpy.Scene.load(str(path), base_dir=str(tmp_path))
+
+
+def test_gpu_cone_cull_with_three_emitters(tmp_path):
+    """a point's cone_mask holds one bit per emitter: with three emitters (two spheres, one
+    triangle) the frame is the same with the cull on and off, and some rays are culled"""
+    scene = three_emitter_scene(tmp_path)
+    frame = scene.frame(160, 90)
+    params = rtxpy.params_from_args(["-g", "path", "-n", "2"], seed=3)
+    params.rng = abi.RTX_RNG_COUNTER
+    out = render_both(scene, frame, params)
+    frac = check(out, want_clear=True)
+    print("three emitters cleared", round(frac, 4))
