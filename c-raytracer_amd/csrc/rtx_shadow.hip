@@ -968,8 +968,7 @@ __device__ __forceinline__ QBvh make_qbvh(const KShadow &ks, const uint4 *top_q,
 
 /* The cone cull of a packet of one shade point's samples of one emitter: every shadow ray of the
  * packet runs from p to a point of the emitter, so it lies in the cone from p around the emitter's
- * bounding sphere (centre and half-diagonal of its padded world box DEmitter.wlo / whi), cut at
- * the sphere's far side.  Lane k tests the bounding sphere k of the 8-wide tree's second level
+ * bounding sphere (below), cut at the sphere's far side.  Lane k tests the bounding sphere k of the 8-wide tree's second level
  * (DScene.cull, world space): centre distance t along the axis, e off it; the sphere misses the
  * cone when e cos(a) - t sin(a) > r or it lies wholly before p or beyond the light.  r is padded
  * by 2e-5 of the coordinates' and distances' magnitudes, far above the rays' float rounding, so a
@@ -980,9 +979,20 @@ __device__ __forceinline__ bool cone_clear(const KShadow &ks, const DEmitter &E,
 	const uint32_t n = uni(ks.num_cull);
 	if (!n)
 		return false;
-	const f3 lc = mk3(0.5f * (E.wlo[0] + E.whi[0]), 0.5f * (E.wlo[1] + E.whi[1]), 0.5f * (E.wlo[2] + E.whi[2]));
-	const f3 lh = mk3(0.5f * (E.whi[0] - E.wlo[0]), 0.5f * (E.whi[1] - E.wlo[1]), 0.5f * (E.whi[2] - E.wlo[2]));
-	const float lr = sqrtf(magsqr3(lh));
+	/* the emitter's bounding sphere: a sphere light itself (its light points are c + ld with |ld|
+	 * the radius to a few ulp, light_point_sh), a triangle's circumscribing sphere about its
+	 * centroid (its light points lie in it); padded by 1e-4 of the radius and 1e-6 of |c| */
+	f3 lc;
+	float lr;
+	if (E.type == RTX_SPHERE) {
+		lc = ld3(E.p0);
+		lr = E.radius;
+	} else {
+		const f3 a = ld3(E.p0), b = ld3(E.p1), c = ld3(E.p2);
+		lc = mul3s(add3(add3(a, b), c), 1.f / 3.f);
+		lr = sqrtf(fmaxf(fmaxf(magsqr3(sub3(a, lc)), magsqr3(sub3(b, lc))), magsqr3(sub3(c, lc))));
+	}
+	lr = lr * 1.0001f + 1e-6f * fmaxf(fmaxf(fabsf(lc.x), fabsf(lc.y)), fabsf(lc.z));
 	const f3 ax0 = sub3(lc, p);
 	const float L = sqrtf(magsqr3(ax0));
 	if (!(L > 1.01f * lr)) /* the point at or inside the light's sphere: no cone */
