@@ -770,13 +770,15 @@ static int build_cull(rtx_ctx *c, const HostScene &hs, uint32_t num_w8, uint32_t
 	if (!c->d_w8 || num_w8 < 2)
 		return RTX_OK;
 	DW8 root, kid[8];
-	HIP_TRY(hipMemcpy(&root, c->d_w8, sizeof(DW8), hipMemcpyDeviceToHost));
+	HIP_TRY(hipMemcpyAsync(&root, c->d_w8, sizeof(DW8), hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
 	const uint32_t base = root.w[2] >> 8, imask = root.w[2] & 0xFFu, vmask = root.w[3] & 0xFFu;
 	if (!vmask)
 		return RTX_OK;
 	if ((uint64_t)base + 8 > num_w8)
 		return fail(RTX_ERR_STATE, "8-wide root's children at %u beyond %u entries", base, num_w8);
-	HIP_TRY(hipMemcpy(kid, c->d_w8 + base, sizeof(kid), hipMemcpyDeviceToHost));
+	HIP_TRY(hipMemcpyAsync(kid, c->d_w8 + base, sizeof(kid), hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
 	std::vector<float4> sph;
 	auto add_box = [&](const DW8 &N, int slot) {
 		const double org[3] = { (double)(N.w[0] & 0xFFFFu), (double)(N.w[0] >> 16), (double)(N.w[1] & 0xFFFFu) };
