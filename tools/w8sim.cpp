@@ -556,6 +556,8 @@ int main(int argc, char **argv)
 	const bool cone_sim = getenv("W8SIM_CONE") && atoi(getenv("W8SIM_CONE"));
 	double cone_pts_empty = 0, cone_visits = 0, cone_leaves = 0, ws_empty = 0, lr_empty = 0, pk_empty = 0;
 	double nohit_pts = 0, ws_nohit = 0; /* points none of whose sample rays reached a leaf box (any cull's bound) */
+	/* walking points: steps as packed (index order) against their lanes packed by walk length */
+	double wk_steps = 0, wk_sorted = 0, wk_part = 0, wk_lanes = 0, wk_walkers = 0;
 	std::vector<double> cone_leaf_hist(8, 0.0), cone_depth_hist(16, 0.0), ws_depth(16, 0.0);
 	const int order = getenv("W8SIM_ORDER") ? atoi(getenv("W8SIM_ORDER")) : 0;
 	const bool sort_samples = getenv("W8SIM_SORT") && atoi(getenv("W8SIM_SORT"));
@@ -687,6 +689,7 @@ int main(int argc, char **argv)
 				return (uint32_t)(su1[a] * G) < (uint32_t)(su1[b] * G);
 			});
 		}
+		std::vector<uint32_t> pt_len; /* every sample's walk length (visits) of this point */
 		for (uint32_t b0 = 0; b0 < nl; b0 += 64) {
 			std::vector<uint32_t> visits_lane, leaf_at; /* per-lane per-visit leaf hits */
 			std::vector<std::vector<uint32_t>> leaves(64), seq(64);
@@ -933,6 +936,8 @@ int main(int argc, char **argv)
 				}
 			}
 			S.wave_steps += maxv;
+			for (uint32_t l = 0; l < 64 && b0 + l < nl; l++)
+				pt_len.push_back(imm_len[l]);
 			for (uint32_t i = 0; i < maxv; i++) {
 				std::vector<uint32_t> at(64, ~0u);
 				uint32_t first = ~0u;
@@ -1074,6 +1079,30 @@ int main(int argc, char **argv)
 		}
 		for (int r = 0; r < 6; r++)
 			refill_sim(allseq, RF_T[r], S.rf_steps[r], S.rf_usteps[r], S.rf_refills[r]);
+		if (cone_sim && !cone_empty && !pt_len.empty()) {
+			double st = 0;
+			for (size_t b = 0; b < pt_len.size(); b += 64)
+				st += *std::max_element(pt_len.begin() + b, pt_len.begin() + std::min(pt_len.size(), b + 64));
+			std::vector<uint32_t> srt = pt_len, prt;
+			std::sort(srt.begin(), srt.end(), std::greater<uint32_t>());
+			for (uint32_t v : pt_len)
+				if (v > 1)
+					prt.push_back(v);
+			const size_t nwalk = prt.size();
+			for (uint32_t v : pt_len)
+				if (v <= 1)
+					prt.push_back(v);
+			double ss = 0, sp = 0;
+			for (size_t b = 0; b < srt.size(); b += 64) {
+				ss += *std::max_element(srt.begin() + b, srt.begin() + std::min(srt.size(), b + 64));
+				sp += *std::max_element(prt.begin() + b, prt.begin() + std::min(prt.size(), b + 64));
+			}
+			wk_steps += st;
+			wk_sorted += ss;
+			wk_part += sp;
+			wk_lanes += pt_len.size();
+			wk_walkers += nwalk;
+		}
 		if (cone_sim && !point_leafhit) {
 			nohit_pts++;
 			ws_nohit += S.wave_steps - ws0;
@@ -1094,6 +1123,9 @@ int main(int argc, char **argv)
 		       cone_leaf_hist[4] / npts, (cone_leaf_hist[5] + cone_leaf_hist[6] + cone_leaf_hist[7]) / npts);
 		printf("  bound: %.3f of points had no sample ray reach a leaf box, holding %.3f of the wave steps\n", nohit_pts / npts,
 		       ws_nohit / S.wave_steps);
+		printf("  points the cone does not clear: %.3f of their samples walk past the root; node steps as packed %.0f, "
+		       "packed by walk length %.0f (%.3f), walkers first %.0f (%.3f)\n", wk_walkers / std::max(1.0, wk_lanes),
+		       wk_steps, wk_sorted, wk_sorted / std::max(1.0, wk_steps), wk_part, wk_part / std::max(1.0, wk_steps));
 		double cp = 0, cw = 0;
 		for (int d = 1; d < 8; d++) {
 			cp += cone_depth_hist[d];
