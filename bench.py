@@ -88,6 +88,8 @@ def parse():
                     help="closest-hit BVH layout (rtx_set_option RTX_OPT_TRACE_WALK)")
     ap.add_argument("--no-cull", action="store_true",
                     help="every shadow packet walks the tree (rtx_set_option RTX_OPT_SHADOW_CULL 0; an A/B of the cone cull)")
+    ap.add_argument("--cull-slots", action="store_true",
+                    help="the lane-slot packets cull too (rtx_set_option RTX_OPT_SHADOW_CULL 2)")
     ap.add_argument("--frame", default="auto", choices=["auto", "world"],
                     help="the frame the BVHs are built in (rtx_set_option RTX_OPT_TREE_FRAME; auto = the library default)")
     ap.add_argument("--shadow-slot", type=int, default=0,
@@ -650,7 +652,7 @@ def main():
     r.set_option(abi.RTX_OPT_TRACE_WALK, WALKS[a.trace_walk])
     r.set_option(abi.RTX_OPT_SHADOW_SLOT, a.shadow_slot)
     r.set_option(abi.RTX_OPT_TREE_FRAME, FRAMES[a.frame])
-    r.set_option(abi.RTX_OPT_SHADOW_CULL, 0 if a.no_cull else 1)
+    r.set_option(abi.RTX_OPT_SHADOW_CULL, 0 if a.no_cull else 2 if a.cull_slots else 1)
     if a.shadow_grab:
         r.set_option(abi.RTX_OPT_SHADOW_GRAB, a.shadow_grab)
     t0 = time.perf_counter()
@@ -910,7 +912,7 @@ def group_validation(a, g, n, scene, frame, params, h_rgb, h_z, frame_rays, log)
         single.set_option(abi.RTX_OPT_TRACE_WALK, WALKS[a.trace_walk])
         single.set_option(abi.RTX_OPT_SHADOW_SLOT, a.shadow_slot)
         single.set_option(abi.RTX_OPT_TREE_FRAME, FRAMES[a.frame])
-        single.set_option(abi.RTX_OPT_SHADOW_CULL, 0 if a.no_cull else 1)
+        single.set_option(abi.RTX_OPT_SHADOW_CULL, 0 if a.no_cull else 2 if a.cull_slots else 1)
         single.upload(scene)
         rgb1, z1 = single.render(frame, params)
         s1 = single.stats()
@@ -981,7 +983,7 @@ def main_group(a):
     g.set_option(abi.RTX_OPT_TRACE_WALK, WALKS[a.trace_walk])
     g.set_option(abi.RTX_OPT_SHADOW_SLOT, a.shadow_slot)
     g.set_option(abi.RTX_OPT_TREE_FRAME, FRAMES[a.frame])
-    g.set_option(abi.RTX_OPT_SHADOW_CULL, 0 if a.no_cull else 1)
+    g.set_option(abi.RTX_OPT_SHADOW_CULL, 0 if a.no_cull else 2 if a.cull_slots else 1)
     if a.shadow_grab:
         g.set_option(abi.RTX_OPT_SHADOW_GRAB, a.shadow_grab)
     t0 = time.perf_counter()

@@ -1159,9 +1159,10 @@ int rtx_render_common(rtx_ctx *c, const rtx_frame *fr, const rtx_params *p, floa
 						  c->sorttmp_bytes, &perm, stream));
 		}
 		HIP_TRY(hipEventRecord(c->ev[4], stream));
-		DScene Ssh = c->scene; /* RTX_OPT_SHADOW_CULL off: no cull spheres */
+		DScene Ssh = c->scene; /* RTX_OPT_SHADOW_CULL: 0 no cull spheres, 2 the lane slots cull too */
 		if (!c->opt_cull)
 			Ssh.num_cull = 0;
+		Ssh.cull_slots = c->opt_cull == 2 ? 1u : 0u;
 		HIP_TRY(rtx_launch_shadow(&Ssh, &P, c->d_sp, perm, n_sp, per_wave, slot_b, c->d_contrib, c->d_ctr,
 					  p->count_traversal, (uint32_t)c->cus, stream));
 		HIP_TRY(hipEventRecord(c->ev[2], stream));
@@ -1394,9 +1395,9 @@ extern "C" int rtx_set_option(rtx_ctx *c, int option, int64_t value)
 		c->opt_sp_tile = (uint32_t)value;
 		return RTX_OK;
 	case RTX_OPT_SHADOW_CULL:
-		if (value != 0 && value != 1)
-			return fail(RTX_ERR_ARG, "shadow cull %lld is not 0 or 1", (long long)value);
-		c->opt_cull = value != 0;
+		if (value < 0 || value > 2)
+			return fail(RTX_ERR_ARG, "shadow cull %lld is not 0, 1 or 2", (long long)value);
+		c->opt_cull = (int)value;
 		return RTX_OK;
 	}
 	return fail(RTX_ERR_ARG, "unknown option %d", option);

@@ -258,6 +258,7 @@ typedef struct DScene {
 	                        * slot's own box when it is a leaf), at most RTX_CULL_MAX; every primitive of
 	                        * the tree lies in one.  Null / 0: no cull */
 	uint32_t num_cull;
+	uint32_t cull_slots;   /* RTX_OPT_SHADOW_CULL 2: the lane-slot path culls too (cone_mask_lane) */
 } DScene;
 #define RTX_CULL_MAX 64
 

@@ -131,7 +131,7 @@ struct rtx_ctx {
 	int opt_frame = RTX_FRAME_AUTO;
 	uint32_t opt_chunk = 0;   /* most tiles per chunk (0: as many as the shade-point budget allows) */
 	uint32_t opt_sp_tile = 0; /* shade points per tile a chunk is sized for (0: the estimate / last render's count) */
-	bool opt_cull = true;     /* RTX_OPT_SHADOW_CULL */
+	int opt_cull = 1;         /* RTX_OPT_SHADOW_CULL: 0 off, 1 wave-uniform packets, 2 lane slots too */
 	uint32_t mem_share = 1;   /* contexts sharing this device's HBM at once (a loopback group's n): the shade-point
 	                           * budget of a render is a third of the free HBM divided by it */
 };

@@ -803,6 +803,7 @@ const DW8 *w8;        /* 8-wide compressed BVH (WALK_W8 instances; qo / qs / qsi
 	float att_offset;
 	const float4 *cull;   /* DScene.cull: the 8-wide tree's second-level bounding spheres (cone_clear) */
 	uint32_t num_cull;    /* 0: no cull (RTX_OPT_SHADOW_CULL off, or no such tree) */
+	uint32_t cull_slots;  /* the lane-slot path culls too (RTX_OPT_SHADOW_CULL 2) */
 };
 
 __device__ __forceinline__ void reread_barrier() { asm volatile("" ::: "memory"); }
@@ -1028,13 +1029,65 @@ __device__ __forceinline__ u64 cone_mask(const KShadow &ks, f3 p, bool far)
 	return m;
 }
 
+/* The lane-slot path's cone mask (RTX_SH_SLOTCULL): each lane tests its own point's cones (emitters
+ * e < 8) against every sphere in turn, the sphere and the emitter read through the scalar cache;
+ * bit e set when no sphere meets.  A packet whose every live lane is clear for its emitter skips
+ * the walk, as a clear point's packets do on the wave-uniform path. */
+#ifndef RTX_SH_SLOTCULL
+#define RTX_SH_SLOTCULL 1
+#endif
+__device__ __forceinline__ uint32_t cone_mask_lane(const KShadow &ks, f3 p, bool own)
+{
+	const uint32_t n = uni(ks.num_cull);
+	if (!n)
+		return 0u;
+	const DEmitter *emitters = unip(ks.emitters);
+	const uint32_t ne = min(uni(ks.num_emitters), 8u);
+	const float4 *cull = unip(ks.cull);
+	uint32_t m = 0u;
+	for (uint32_t e = 0; e < ne; e++) {
+		const DEmitter E = emitter_uni(emitters + e);
+		f3 lc;
+		float lr;
+		if (E.type == RTX_SPHERE) {
+			lc = ld3(E.p0);
+			lr = E.radius;
+		} else {
+			const f3 a = ld3(E.p0), b = ld3(E.p1), c = ld3(E.p2);
+			lc = mul3s(add3(add3(a, b), c), 1.f / 3.f);
+			lr = sqrtf(fmaxf(fmaxf(magsqr3(sub3(a, lc)), magsqr3(sub3(b, lc))), magsqr3(sub3(c, lc))));
+		}
+		lr = lr * 1.0001f + 1e-6f * fmaxf(fmaxf(fabsf(lc.x), fabsf(lc.y)), fabsf(lc.z));
+		const f3 ax0 = sub3(lc, p);
+		const float L = sqrtf(magsqr3(ax0));
+		bool meets = !own || !(L > 1.01f * lr);
+		if (ballot(!meets)) {
+			const f3 ax = mul3s(ax0, 1.f / L);
+			const float sn = lr / L, cs = sqrtf(fmaxf(0.f, 1.f - sn * sn));
+			const float mag = fmaxf(fmaxf(fabsf(p.x), fabsf(p.y)), fabsf(p.z)) + fmaxf(fmaxf(fabsf(lc.x), fabsf(lc.y)), fabsf(lc.z));
+			for (uint32_t k = 0; k < n && ballot(!meets); k++) {
+				const auto *q = (const __attribute__((address_space(4))) f4v *)(cull + k);
+				const f4v sp = *q;
+				const f3 v = sub3(mk3(sp.x, sp.y, sp.z), p);
+				const float vv = magsqr3(v), t = dot3(v, ax);
+				const float e2 = sqrtf(fmaxf(0.f, vv - t * t));
+				const float br = sp.w + 2e-5f * (mag + sqrtf(vv) + L + lr);
+				meets = meets || vv <= br * br || (t >= -br && t <= L + lr + br && e2 * cs - t * sn <= br);
+			}
+		}
+		if (!meets)
+			m |= 1u << e;
+	}
+	return m;
+}
+
 /* one light sample per lane of the shade point `rec` (render.c:170-229): the light point of
  * sample idx (emitters in scene order, the hit object skipped), its shadow ray, attenuation
  * and Phong / Blinn.  Argument-block fields are read from LDS behind reread barriers. */
-template <bool COUNT, int WALK, bool UNI, bool LA>
+template <bool COUNT, int WALK, bool UNI, bool LA, bool SC = false>
 __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec_uni, uint32_t sidv, uint32_t idx, bool act, ShadowCount &sc,
 					   const uint4 *top_q, const uint32_t *top_e, lds_u32 *stk, const uint4 *t8, uint32_t wv,
-					   const uint32_t *cmask)
+					   const uint32_t *cmask, uint32_t lclr = 0u)
 {
 	reread_barrier();
 	/* the shade point's record: wave-uniform (UNI), or this lane's record sidv, whose address is
@@ -1081,6 +1134,11 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec_
 		emitter_sample(ks, E, e, j, __float_as_uint(q4.y), __float_as_uint(q4.z), p, ldir, ldist, dsq, li);
 		eobj = E.obj;
 	}
+	/* the lane-slot path: every live lane's point clear for its emitter (cone_mask_lane) */
+	if (!UNI && SC) {
+		const bool lc = e < 8u && ((lclr >> (e & 7u)) & 1u);
+		clear = ballot(act) && !ballot(act && !lc);
+	}
 	const float attf = sample_att(ks, ldist, dsq);
 	const QBvh Q = make_qbvh<WALK>(ks, top_q, top_e, stk, t8, wv);
 	const bool have_tree = uni(ks.have_tree) != 0 && !RTX_DEBUG_NOWALK && !clear;
@@ -1107,7 +1165,8 @@ __device__ __forceinline__ f3 light_sample(const KShadow &ks, const float4 *rec_
  * to LDS once; then each wave takes per_wave shade points at a time from a global queue
  * (RTX_C_SPQUEUE), in processing (Morton) order, until the points run out. */
 /* PATH: 0 both packet layouts (a runtime branch on slot_b: the counting instances), 1 only the
- * wave-uniform packets (slot_b = 64), 2 only the lane slots (slot_b < 64).  The product launches a
+ * wave-uniform packets (slot_b = 64), 2 only the lane slots (slot_b < 64), 3 the lane slots with
+ * their cone cull (RTX_OPT_SHADOW_CULL 2).  The product launches a
  * kernel of one layout, so each gets a register allocation of its own: with both in one kernel a
  * change to the slot loop moved the uniform loop's spills into its walk */
 template <bool COUNT, int OCC, int WALK, int PATH>
@@ -1131,6 +1190,8 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 		uint32_t sid[WAVE];     /* each shade point's index in the record array */
 		float Ls[3][WAVE];      /* per shade point light sum, in packet order */
 		uint32_t cm[2];         /* the current point's cone_mask (wave-uniform path) */
+		uint8_t clr[WAVE];      /* each shade point's cone_mask_lane, emitters 0..7 (lane-slot path; a byte:
+		                         * the LDS of two workgroups must still fit a CU) */
 	};
 	__shared__ WaveTables wt_w[RTX_SH_NW];
 	const uint32_t ntop = TOP ? ka.ntop : 0u;
@@ -1147,11 +1208,16 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 	__syncthreads();
 	KShadow &ks = ks_s;
 	uint32_t *off = wt_w[wv].off, *nls = wt_w[wv].nls, *sid = wt_w[wv].sid;
+	uint8_t *clr = wt_w[wv].clr;
 	float(*Ls)[WAVE] = wt_w[wv].Ls;
 	/* the lane-stack addresses: per lane, or formed from lane_id() at each access (RTX_W8_LANEADDR; 2:
 	 * the lane-slot kernel only, whose allocation spilled the per-lane address and reloaded it at
 	 * every push and pop) */
-	constexpr bool LA = RTX_W8_LANEADDR == 2 ? PATH == 2 : RTX_W8_LANEADDR != 0;
+	constexpr bool LA = RTX_W8_LANEADDR == 2 ? PATH >= 2 : RTX_W8_LANEADDR != 0;
+	/* the lane-slot path's cone cull (RTX_OPT_SHADOW_CULL 2) lives in its own instance, PATH 3, so
+	 * the default lane-slot kernel keeps its register allocation (with the code present but off,
+	 * scene6's k_shadow took 1083.4 against 1074.8 ms) */
+	constexpr bool SC = RTX_SH_SLOTCULL && WALK == WALK_W8 && (PATH == 3 || PATH == 0);
 	lds_u32 *stk = (lds_u32 *)&wstk[wv][0][LA ? 0u : lane_id()];
 	ShadowCount sc = { 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0 };
 	u64 rays_total = 0;
@@ -1222,6 +1288,17 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 		} else {
 			/* several points share a packet: each point's samples fill consecutive slots of B
 			 * (power of two) lanes, B = slot_b; a point may straddle packets */
+			if (SC) { /* each lane its own point's cone_mask_lane */
+				uint32_t m = 0u;
+				if (uni(ks.num_cull) && uni(ks.cull_slots)) {
+					const float4 *my = unip(ks.sp) + (size_t)my_sid * SPREC;
+					const float4 q0 = ldg4(my, 0), q4 = ldg4(my, 64);
+					const bool far = (__float_as_uint(q4.x) & RTX_SP_FAR) != 0;
+					m = cone_mask_lane(ks, mk3(q0.x, q0.y, q0.z), own && !far);
+				}
+				clr[lane_id()] = (uint8_t)m;
+				lds_sync();
+			}
 			uint32_t kp = 0; /* this lane's point in the previous packet (its slots only move forward) */
 			for (uint32_t base = 0;;) {
 				reread_barrier();
@@ -1242,8 +1319,9 @@ __global__ __launch_bounds__(WAVE *RTX_SH_NW, OCC) void k_shadow(KShadow ka)
 				}
 				const uint32_t idx = ((slot - off[k]) << slot_lg) + (lane_id() & (slot_b - 1));
 				const bool act = slot < tot && idx < nls[k];
-				const f3 contribution = light_sample<COUNT, WALK, false, LA>(ks, nullptr, sid[k], idx, act, sc, top_q, top_e, stk,
-											 t8, wv, nullptr);
+				const f3 contribution = light_sample<COUNT, WALK, false, LA, SC>(ks, nullptr, sid[k], idx, act, sc, top_q, top_e, stk,
+											 t8, wv, nullptr,
+											 SC ? (uint32_t)clr[k] : 0u);
 				/* per-shade-point sums.  Each slot's B lanes reduce in a fixed butterfly (masks B/2 .. 1),
 				 * then the slot sums are added to their point's total one slot at a time in slot order, so a
 				 * point whose slots straddle packets gets the same sum whatever its neighbours (with one slot
@@ -1537,6 +1615,8 @@ template <bool C, int O, int W> static hipError_t launch_shadow(const KShadow &k
 	} else {
 		if (ka.slot_b == WAVE)
 			return launch_shadow_p<C, O, W, 1>(ka, nw, cus, stream);
+		if (W == WALK_W8 && ka.cull_slots && ka.num_cull)
+			return launch_shadow_p<C, O == RTX_SHADOW_OCC_DEFAULT ? RTX_SHADOW_OCC_SLOT : O, W, 3>(ka, nw, cus, stream);
 		return launch_shadow_p<C, O == RTX_SHADOW_OCC_DEFAULT ? RTX_SHADOW_OCC_SLOT : O, W, 2>(ka, nw, cus, stream);
 	}
 }
@@ -1564,6 +1644,11 @@ extern "C" hipError_t rtx_shadow_grid_lanes(uint32_t cus, uint32_t *lanes)
 	hipError_t e = shadow_slots<false, RTX_SHADOW_OCC_DEFAULT, WALK_W8, 1>(cus, &a);
 	if (e == hipSuccess)
 		e = shadow_slots<false, RTX_SHADOW_OCC_SLOT, WALK_W8, 2>(cus, &a2);
+	if (e == hipSuccess) {
+		uint32_t a3 = 0;
+		e = shadow_slots<false, RTX_SHADOW_OCC_SLOT, WALK_W8, 3>(cus, &a3);
+		a2 = a2 > a3 ? a2 : a3;
+	}
 	a = a > a2 ? a : a2;
 	if (e == hipSuccess)
 		e = shadow_slots<true, 1, WALK_W8, 0>(cus, &b);
@@ -1642,6 +1727,7 @@ for (int a = 0; a < 3; a++) {
 	ka.lin = S->lin; /* a tiny scene: every bounded object, no walk */
 	ka.cull = (const float4 *)S->cull;
 	ka.num_cull = (walk == WALK_W8 && S->cull) ? S->num_cull : 0u;
+	ka.cull_slots = S->cull_slots;
 	ka.num_lin = S->lin ? S->num_lin : 0u;
 	if (walk == WALK_W8) { /* the 8-wide tree's own frame; the emitters it leaves out are tested linearly */
 		for (int a = 0; a < 3; a++) {

@@ -303,7 +303,9 @@ enum rtx_option {
 	RTX_OPT_SHADOW_CULL = 11      /* 1 (default): a packet of one shade point's light samples skips the 8-wide
 	                               * walk when the cone from the point around the light's bounding sphere
 	                               * meets no box of the tree's top two levels (the walk would find nothing,
-	                               * so the image is the same); 0: every packet walks */
+	                               * so the image is the same); 2: packets of several points (points with
+	                               * fewer than 64 samples) too, when every lane's point is clear for its
+	                               * emitter (emitters 0..7); 0: every packet walks */
 };
 int rtx_set_option(rtx_ctx *ctx, int option, int64_t value);
 /* The frame rtx_upload_scene builds the scene's BVHs in under RTX_FRAME_AUTO (a diagnostic; no

@@ -19,20 +19,20 @@ from test_gpu_configs import load
 pytestmark = pytest.mark.gpu
 
 
-def render_both(scene, frame, params, slot=0, frame_opt=abi.RTX_FRAME_AUTO):
+def render_both(scene, frame, params, slot=0, frame_opt=abi.RTX_FRAME_AUTO, on=1):
     out = {}
     r = rtxpy.Renderer(0)
     try:
         r.set_option(abi.RTX_OPT_TREE_FRAME, frame_opt)
         r.upload(scene)
         r.set_option(abi.RTX_OPT_SHADOW_SLOT, slot)
-        for cull in (1, 0):
+        for cull in (on, 0):
             r.set_option(abi.RTX_OPT_SHADOW_CULL, cull)
             for count in (0, 1):
                 p = rtxpy.default_params(**{f: getattr(params, f) for f, _ in abi.Params._fields_})
                 p.count_traversal = count
                 rgb, z = r.render(frame, p)
-                out[(cull, count)] = (rgb, z, r.stats())
+                out[(min(cull, 1), count)] = (rgb, z, r.stats())
     finally:
         r.close()
     return out
@@ -60,17 +60,32 @@ def test_gpu_cone_cull_is_invisible(name):
     print(name, "cleared", round(frac, 4))
 
 
-def test_gpu_cone_cull_on_the_bench_scene():
+@pytest.mark.parametrize("slot", [0, 16, 4])
+def test_gpu_cone_cull_on_the_bench_scene(slot):
     """scene5 with the dragon stand-in (bench.py's scene, a smaller frame): most floor and wall
-    points see the light past the dragon, so most packets skip the walk; the frame is the same"""
+    points see the light past the dragon, so most packets skip the walk; the frame is the same.
+    slot 0: the automatic layout (64-lane packets of one point, cone_mask); 16 / 4: lane slots of
+    several points per packet (RTX_OPT_SHADOW_CULL 2, cone_mask_lane: a packet skips when all its
+    lanes' points are clear)"""
     scene = load("scene5")
     frame = scene.frame(320, 180)
     params = rtxpy.params_from_args(["-g", "path", "-n", "4"], seed=1)
     params.rng = abi.RTX_RNG_COUNTER
-    out = render_both(scene, frame, params)
+    out = render_both(scene, frame, params, slot=slot, on=2 if slot else 1)
     frac = check(out, want_clear=True)
-    print("scene5 cleared", round(frac, 4))
+    print("scene5 slot", slot, "cleared", round(frac, 4))
     assert frac > 0.3
+    if slot:  # option 1 leaves the lane slots walking
+        r = rtxpy.Renderer(0)
+        try:
+            r.upload(scene)
+            r.set_option(abi.RTX_OPT_SHADOW_SLOT, slot)
+            p = rtxpy.default_params(**{f: getattr(params, f) for f, _ in abi.Params._fields_})
+            p.count_traversal = 1
+            r.render(frame, p)
+            assert r.stats().shadow_cone_clear == 0
+        finally:
+            r.close()
 
 
 @pytest.mark.parametrize("frame_opt", [abi.RTX_FRAME_AUTO, abi.RTX_FRAME_WORLD])
